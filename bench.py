@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X direct-sum gravity hot path (BASELINE.json config 2/4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One step = one full direct-sum force + potential solve of a synthetic
+Plummer sphere whose positions / masses are already resident in HBM:
+pack this rank's particles into 32-byte source records, all-gather the
+records of every rank over RCCL (N > 1), run the fused FP64 direct-sum
+kernel for this rank's targets against all sources.
+
+Workload: N_GPU x 1,000,000 particles (1M at N=1 = config 2; 8M at N=8 =
+config 4), targets sharded across ranks, every rank sees all sources.
+Per-GPU target count is fixed ("weak" in particles); the pair count per
+GPU grows with N, which is why the metric is the whole-job pair rate.
+
+Printed (rank 0, one JSON line): metric/value in pairs/s, the roofline of
+the direct-sum kernel against the FP64 vector peak (achieved from HIP
+events on the library stream), and the CPU baseline (oracle restatement
+of direct.rs timed on a bounded target sample on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "pynbody-extras_amd"))
+sys.path.insert(0, str(ROOT))
+
+from pynbodyext import _native as nat  # noqa: E402
+from pynbodyext.synthetic import plummer  # noqa: E402
+
+FLOP_PER_PAIR = 22            # SURVEY.md §8d, fused force + potential
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X FP64 vector, AMD spec
+N_PER_GPU = 1_000_000
+SEEDS = {1_000_000: 1002, 4_000_000: 1003, 8_000_000: 1004}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n-per-gpu", type=int, default=N_PER_GPU)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target duration of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+class Dist:
+    """Control plane (barrier, max-over-ranks) over torch.distributed gloo.
+
+    The data path never goes through torch: the source all-gather is RCCL
+    called from libpbx.so.
+    """
+
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def broadcast_bytes(self, b: bytes | None) -> bytes:
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+
+def cpu_baseline(pos, mass, seconds: float):
+    """Oracle restatement of direct.rs (per-target loop, :160-182 / :293-310)
+    on a bounded random target sample; returns pairs/s on the host cores."""
+    from oracle import gravity as og
+
+    cores = min(16, os.cpu_count() or 1)
+    og.set_num_threads(cores)
+    n = len(pos)
+    rng = np.random.default_rng(0)
+    probe = rng.choice(n, size=max(cores, 16), replace=False)
+    t0 = time.perf_counter()
+    og.direct_subset(pos, mass, probe)
+    dt = time.perf_counter() - t0
+    per_target = dt / len(probe)
+    k = int(min(n, max(len(probe), seconds / max(per_target, 1e-9))))
+    k = max(cores, (k // cores) * cores)
+    idx = rng.choice(n, size=k, replace=False)
+    t0 = time.perf_counter()
+    og.direct_subset(pos, mass, idx)
+    dt = time.perf_counter() - t0
+    return {
+        "value": k * (n - 1) / dt,
+        "unit": "pairs/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{k} random targets x {n} sources (all-particles Newtonian force+potential, "
+                  f"oracle/gravity_ref.c, OpenMP {cores} threads, {dt:.1f} s)",
+    }
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the direct-sum kernel from the committed
+    rocprofv3 PMC summary (profiles/), or None."""
+    f = ROOT / "profiles" / "pmc_direct_latest.json"
+    if not f.exists():
+        return None, None
+    try:
+        d = json.loads(f.read_text())
+        return d.get("hbm_bytes_per_launch"), str(f.relative_to(ROOT))
+    except Exception:
+        return None, None
+
+
+def main():
+    args = parse()
+    dist = Dist()
+    world, rank = dist.world, dist.rank
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    nat.load()
+    nat.set_device(dist.local_rank if world > 1 else 0)
+
+    n_loc = args.n_per_gpu
+    n_tot = n_loc * world
+    seed = SEEDS.get(n_tot, 1100 + world)
+    pos, mass = plummer(n_tot, seed=seed)
+    lo, hi = rank * n_loc, (rank + 1) * n_loc
+    pos_loc = np.ascontiguousarray(pos[lo:hi])
+    mass_loc = np.ascontiguousarray(mass[lo:hi])
+
+    d_pos = nat.DeviceArray.from_host(pos_loc)
+    d_mass = nat.DeviceArray.from_host(mass_loc)
+    d_rec = nat.DeviceArray(32 * n_tot)           # all-gathered source records
+    d_pot = nat.DeviceArray(8 * n_loc)
+    d_acc = nat.DeviceArray(24 * n_loc)
+
+    comm = None
+    if world > 1:
+        from pynbodyext.parallel import Communicator
+
+        uid = Communicator.unique_id() if rank == 0 else None
+        uid = dist.broadcast_bytes(uid)
+        comm = Communicator(world, rank, uid)
+    my_rec = d_rec.offset(32 * lo)
+
+    ev = [nat.Event(), nat.Event()]
+    kernel_ms = []
+
+    def step(timed: bool):
+        nat.call("pbx_pack_sources", d_pos.ptr, d_mass.ptr, n_loc, my_rec)
+        if comm is not None:
+            comm.allgather_inplace(d_rec.ptr, 32 * n_loc)
+        if timed:
+            ev[0].record()
+        nat.call("pbx_direct_dev", d_rec.ptr, None, n_tot, d_pos.ptr, None, n_loc, lo,
+                 nat.KERNEL_NONE, nat.WANT_POT | nat.WANT_ACC, d_pot.ptr, d_acc.ptr)
+        if timed:
+            ev[1].record()
+            kernel_ms.append(ev[0].elapsed_ms(ev[1]))
+
+    for _ in range(args.warmup):
+        step(False)
+    nat.synchronize()
+    dist.barrier()
+    nat.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    nat.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = dist.max(t1 - t0)
+    kern_avg_ms = dist.max(float(np.mean(kernel_ms)))
+
+    pairs_per_step = float(n_tot) * float(n_tot - 1)   # all ranks together
+    value = pairs_per_step * args.steps / elapsed
+    # roofline: this rank's kernel does n_loc * (n_tot - 1) pairs per launch
+    pairs_launch = float(n_loc) * float(n_tot - 1)
+    achieved_tf = pairs_launch * FLOP_PER_PAIR / (kern_avg_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic()
+
+    if rank != 0:
+        return
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(pos, mass, args.cpu_seconds)
+    out = {
+        "metric": "particle-pairs/sec (direct-sum gravity, force+potential)",
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{n_tot}-particle Plummer sphere, direct-sum force+potential "
+                        f"(Newtonian), {n_loc} targets/GPU x {n_tot} sources"
+                        + (", RCCL source all-gather" if world > 1 else ""),
+            "n_particles": n_tot,
+            "seed": seed,
+            "parallelism": f"targets sharded x{world}",
+            "device": nat.device_name(),
+        },
+        "roofline": {
+            "bound": "fp64-valu",
+            "achieved": achieved_tf,
+            "peak": FP64_VECTOR_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / FP64_VECTOR_PEAK_TFLOPS,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "kernel": "direct_kernel<Newtonian, pot+acc, self-skip>",
+            "flop_per_pair": FLOP_PER_PAIR,
+            "kernel_ms": kern_avg_ms,
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

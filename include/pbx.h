@@ -1,0 +1,133 @@
+/*
+ * pbx.h — C ABI of libpbx.so, the MI355X-native (gfx950, HIP) engine behind
+ * the pynbodyext gravity and radial-profile hot path.
+ *
+ * Every entry point takes plain pointers and sizes (no framework types) and
+ * returns an int status:
+ *     PBX_OK          0  success
+ *     PBX_ERR_VALUE   1  bad argument          -> Python ValueError
+ *     PBX_ERR_RUNTIME 2  HIP / RCCL failure     -> Python RuntimeError
+ *     PBX_ERR_NODEV   3  no usable gfx950 GPU   -> Python RuntimeError
+ * and the message of the last failure on the calling thread is returned by
+ * pbx_last_error().  Nothing here falls back to a CPU path: a missing GPU is
+ * an error.
+ *
+ * The functions below replace the reference's PyO3 boundary module
+ * `pynbodyext._rust` (crates/pynbodyext-rust/src/lib.rs:10-27) and the numpy
+ * seams of pynbodyext.profiles (profiles/bins.py:346-395,
+ * profiles/proarray.py:272-334).  Each block cites the reference interface
+ * it replaces.  Host ("h_") pointers are pageable host memory owned by the
+ * caller; device ("d_") pointers are HBM allocations (pbx_malloc) and are
+ * only used by the device-resident API (bench, multi-GPU).
+ */
+#ifndef PBX_H
+#define PBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBX_OK 0
+#define PBX_ERR_VALUE 1
+#define PBX_ERR_RUNTIME 2
+#define PBX_ERR_NODEV 3
+
+/* Softening kernel codes: the reference's Option<u8> kernel argument
+ * (crates/pynbodyext-rust/src/gravity.rs:67-82).  PBX_KERNEL_NONE is the
+ * Newtonian path taken when kernel is None (direct.rs:115-368). */
+#define PBX_KERNEL_NONE (-1)
+#define PBX_KERNEL_PLUMMER 0
+#define PBX_KERNEL_SPLINE 1
+
+/* want bitmask for the fused direct-sum entry */
+#define PBX_WANT_POT 1
+#define PBX_WANT_ACC 2
+
+/* ------------------------------------------------------------------ */
+/* runtime                                                             */
+/* ------------------------------------------------------------------ */
+const char *pbx_last_error(void);
+int pbx_version(void);                   /* returns e.g. 100 for 0.1.0 */
+int pbx_device_count(int *count);
+int pbx_set_device(int device);          /* per calling thread */
+int pbx_get_device(int *device);
+int pbx_device_synchronize(void);
+int pbx_device_name(char *buf, int buflen);
+
+int pbx_malloc(void **d_ptr, size_t bytes);
+int pbx_free(void *d_ptr);
+int pbx_memcpy_htod(void *d_dst, const void *h_src, size_t bytes);
+int pbx_memcpy_dtoh(void *h_dst, const void *d_src, size_t bytes);
+int pbx_memcpy_dtod(void *d_dst, const void *d_src, size_t bytes);
+int pbx_memset(void *d_ptr, int value, size_t bytes);
+
+/* Library-owned stream of the current device (all pbx kernels run on it)
+ * and HIP events on that stream, so callers can time kernels live. */
+int pbx_stream(void **stream);
+int pbx_event_create(void **event);
+int pbx_event_destroy(void *event);
+int pbx_event_record(void *event);
+int pbx_event_elapsed_ms(void *start, void *stop, float *ms);
+int pbx_stream_synchronize(void);
+
+/* ------------------------------------------------------------------ */
+/* gravity: direct summation, host-array boundary                      */
+/* ------------------------------------------------------------------ */
+/* Replace the four PyO3 pyfunctions of crates/pynbodyext-rust/src/gravity.rs:
+ *   direct_accelerations_py            (:448-512)
+ *   direct_accelerations_at_points_py  (:514-583)
+ *   direct_potentials_py               (:585-644)
+ *   direct_potentials_at_points_py     (:646-709)
+ * which call crates/gravity/src/direct.rs:115-658.
+ * h_pos: n x 3 doubles, C order.  h_masses / h_softenings: n doubles or NULL
+ * (NULL masses = unit masses, direct.rs:121-128).  kernel: PBX_KERNEL_*;
+ * softenings with PBX_KERNEL_NONE is a PBX_ERR_VALUE with the reference's
+ * message (gravity.rs:480-484).  Outputs are caller-allocated:
+ * h_acc n x 3, h_pot n. */
+int pbx_direct_accelerations(const double *h_pos, int64_t n,
+                             const double *h_masses, const double *h_softenings,
+                             int kernel, double *h_acc);
+int pbx_direct_potentials(const double *h_pos, int64_t n,
+                          const double *h_masses, const double *h_softenings,
+                          int kernel, double *h_pot);
+int pbx_direct_accelerations_at_points(const double *h_pos, int64_t n,
+                                       const double *h_targets, int64_t m,
+                                       const double *h_masses,
+                                       const double *h_softenings, int kernel,
+                                       double *h_acc);
+int pbx_direct_potentials_at_points(const double *h_pos, int64_t n,
+                                    const double *h_targets, int64_t m,
+                                    const double *h_masses,
+                                    const double *h_softenings, int kernel,
+                                    double *h_pot);
+
+/* ------------------------------------------------------------------ */
+/* gravity: direct summation, device-resident API (bench / multi-GPU)  */
+/* ------------------------------------------------------------------ */
+/* Pack device arrays pos (n x 3) and mass (n, or NULL = unit masses) into
+ * the 32-byte source records {x, y, z, m} the direct-sum kernel streams. */
+int pbx_pack_sources(const double *d_pos, const double *d_mass, int64_t n,
+                     double *d_records);
+/* Fused direct sum over device-resident records.
+ *   d_src      : n_src x 4 records {x,y,z,m}
+ *   d_src_h    : n_src softenings or NULL (only read when kernel >= 0)
+ *   d_tgt      : n_tgt x 3 target positions
+ *   d_tgt_h    : n_tgt target softenings or NULL (all-particles softened
+ *                form h = max(h_i, h_j), direct.rs:402,426)
+ *   self_offset: >= 0 -> target t is source (self_offset + t) and that pair
+ *                is skipped (all-particles form); -1 -> at-points form, no skip
+ *   want       : PBX_WANT_POT | PBX_WANT_ACC
+ *   d_pot      : n_tgt doubles, d_acc: n_tgt x 3 doubles (either may be NULL
+ *                when not wanted) */
+int pbx_direct_dev(const double *d_src, const double *d_src_h, int64_t n_src,
+                   const double *d_tgt, const double *d_tgt_h, int64_t n_tgt,
+                   int64_t self_offset, int kernel, int want, double *d_pot,
+                   double *d_acc);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBX_H */

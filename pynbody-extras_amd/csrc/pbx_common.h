@@ -1,0 +1,126 @@
+// pbx_common.h — shared host-side plumbing of libpbx.so: status codes,
+// thread-local error text, per-device context (stream, grow-only HBM
+// workspace), GRAVITY_TIMING instrumentation.
+//
+// The timing switch mirrors the reference's GRAVITY_TIMING env variable
+// (crates/pynbodyext-rust/src/gravity.rs:12-31): any value other than "",
+// "0" or "false" prints "[pynbodyext-timing] <label>: <ms> ms" to stderr.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/pbx.h"
+
+namespace pbx {
+
+void set_error(const char *fmt, ...);
+
+// Error carrying a pbx status code; thrown inside the library, converted to
+// a status at the extern "C" boundary by guard().
+struct Error {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void fail(int code, const char *fmt, ...);
+
+#define PBX_HIP(call)                                                        \
+  do {                                                                       \
+    hipError_t _e = (call);                                                  \
+    if (_e != hipSuccess)                                                    \
+      ::pbx::fail(PBX_ERR_RUNTIME, "%s failed: %s (%s:%d)", #call,           \
+                  hipGetErrorString(_e), __FILE__, __LINE__);                \
+  } while (0)
+
+// Run f() and translate exceptions into a status code + last-error text.
+template <class F> int guard(F &&f) {
+  try {
+    f();
+    return PBX_OK;
+  } catch (const Error &e) {
+    set_error("%s", e.msg.c_str());
+    return e.code;
+  } catch (const std::bad_alloc &) {
+    set_error("host allocation failed");
+    return PBX_ERR_RUNTIME;
+  } catch (...) {
+    set_error("unknown internal error");
+    return PBX_ERR_RUNTIME;
+  }
+}
+
+// A grow-only device buffer.  Host-array entry points reuse these across
+// calls so a profile or gravity call does not pay hipMalloc each time.
+struct DevBuf {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+  void *ensure(size_t need);
+  ~DevBuf();
+};
+
+// Per-device state.  All library kernels of a device run on `stream`.
+struct Device {
+  int id = -1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;                      // serialises host-array entry points
+  std::vector<DevBuf *> slots;        // workspace slots, indexed by enum
+  DevBuf &slot(int k);
+};
+
+// Workspace slot ids (one namespace for every module).
+enum Slot {
+  kSlotSrc = 0,
+  kSlotSrcH,
+  kSlotTgt,
+  kSlotTgtH,
+  kSlotPos,
+  kSlotMass,
+  kSlotPot,
+  kSlotAcc,
+  kSlotPart,
+  kSlotProf0,
+  kSlotProf1,
+  kSlotProf2,
+  kSlotProf3,
+  kSlotProf4,
+  kSlotProf5,
+  kSlotProf6,
+  kSlotProf7,
+  kSlotCount
+};
+
+// Device of the calling thread (initialised on first use; fails with
+// PBX_ERR_NODEV when there is no GPU).
+Device &current_device();
+
+bool timing_enabled();
+
+struct ScopedTimer {
+  const char *label;
+  std::chrono::steady_clock::time_point t0;
+  bool on;
+  explicit ScopedTimer(const char *l)
+      : label(l), t0(std::chrono::steady_clock::now()), on(timing_enabled()) {}
+  ~ScopedTimer() {
+    if (on) {
+      double ms = std::chrono::duration<double, std::milli>(
+                      std::chrono::steady_clock::now() - t0)
+                      .count();
+      std::fprintf(stderr, "[pynbodyext-timing] %s: %.3f ms\n", label, ms);
+    }
+  }
+};
+
+inline unsigned int ceil_div(int64_t a, int64_t b) {
+  return (unsigned int)((a + b - 1) / b);
+}
+
+}  // namespace pbx

@@ -1,0 +1,220 @@
+"""ctypes binding of libpbx.so, the gfx950 HIP engine (C ABI: include/pbx.h).
+
+This is the only place Python touches native code.  There is deliberately no
+CPU fallback: if the shared library is missing, or a call finds no MI355X
+(gfx950) device, the call raises.  Status codes map to exceptions the way
+the reference's PyO3 layer maps Rust errors (crates/pynbodyext-rust/src/
+gravity.rs: ValueError for argument errors).
+
+ctypes releases the GIL around every foreign call, like the reference's
+``py.allow_threads`` (gravity.rs:103-111).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_void_p
+from pathlib import Path
+
+import numpy as np
+
+PBX_OK = 0
+PBX_ERR_VALUE = 1
+PBX_ERR_RUNTIME = 2
+PBX_ERR_NODEV = 3
+
+KERNEL_NONE = -1
+KERNEL_PLUMMER = 0
+KERNEL_SPLINE = 1
+
+WANT_POT = 1
+WANT_ACC = 2
+
+_LIB_NAME = "libpbx.so"
+_lib: ctypes.CDLL | None = None
+
+_dp = POINTER(c_double)
+_i64p = POINTER(c_int64)
+
+
+class NativeLibraryMissing(ImportError):
+    """libpbx.so has not been built (run ``__graft_entry__.build()``)."""
+
+
+def lib_path() -> Path:
+    override = os.environ.get("PBX_LIBRARY")
+    if override:
+        return Path(override)
+    return Path(__file__).resolve().parent / "lib" / _LIB_NAME
+
+
+# name -> (restype, argtypes); every symbol include/pbx.h declares
+_SIGNATURES: dict[str, tuple] = {
+    "pbx_last_error": (c_char_p, []),
+    "pbx_version": (c_int, []),
+    "pbx_device_count": (c_int, [POINTER(c_int)]),
+    "pbx_set_device": (c_int, [c_int]),
+    "pbx_get_device": (c_int, [POINTER(c_int)]),
+    "pbx_device_synchronize": (c_int, []),
+    "pbx_device_name": (c_int, [c_char_p, c_int]),
+    "pbx_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
+    "pbx_free": (c_int, [c_void_p]),
+    "pbx_memcpy_htod": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "pbx_memcpy_dtoh": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "pbx_memcpy_dtod": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "pbx_memset": (c_int, [c_void_p, c_int, c_size_t]),
+    "pbx_stream": (c_int, [POINTER(c_void_p)]),
+    "pbx_event_create": (c_int, [POINTER(c_void_p)]),
+    "pbx_event_destroy": (c_int, [c_void_p]),
+    "pbx_event_record": (c_int, [c_void_p]),
+    "pbx_event_elapsed_ms": (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
+    "pbx_stream_synchronize": (c_int, []),
+    "pbx_direct_accelerations": (c_int, [_dp, c_int64, _dp, _dp, c_int, _dp]),
+    "pbx_direct_potentials": (c_int, [_dp, c_int64, _dp, _dp, c_int, _dp]),
+    "pbx_direct_accelerations_at_points": (c_int, [_dp, c_int64, _dp, c_int64, _dp, _dp, c_int, _dp]),
+    "pbx_direct_potentials_at_points": (c_int, [_dp, c_int64, _dp, c_int64, _dp, _dp, c_int, _dp]),
+    "pbx_pack_sources": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "pbx_direct_dev": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                               c_int64, c_int, c_int, c_void_p, c_void_p]),
+}
+
+
+def load() -> ctypes.CDLL:
+    """Load libpbx.so once; raise NativeLibraryMissing if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not path.exists():
+        raise NativeLibraryMissing(
+            f"{path} not found: the HIP engine is not built "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return sorted(_SIGNATURES)
+
+
+def last_error() -> str:
+    msg = load().pbx_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(status: int) -> None:
+    if status == PBX_OK:
+        return
+    msg = last_error()
+    if status == PBX_ERR_VALUE:
+        raise ValueError(msg)
+    raise RuntimeError(msg or f"libpbx error {status}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args))
+
+
+def dptr(a: np.ndarray | None):
+    """double* of a C-contiguous float64 array (or NULL)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(_dp)
+
+
+def device_count() -> int:
+    n = c_int(0)
+    call("pbx_device_count", ctypes.byref(n))
+    return n.value
+
+
+def set_device(dev: int) -> None:
+    call("pbx_set_device", int(dev))
+
+
+def device_name() -> str:
+    buf = ctypes.create_string_buffer(256)
+    call("pbx_device_name", buf, 256)
+    return buf.value.decode()
+
+
+def synchronize() -> None:
+    call("pbx_device_synchronize")
+
+
+class DeviceArray:
+    """An HBM allocation owned by Python (freed on ``free()`` / GC).
+
+    Used by the device-resident API (bench, multi-GPU sharding); the
+    host-array gravity / profile entry points manage their own workspace.
+    """
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        p = c_void_p()
+        call("pbx_malloc", ctypes.byref(p), c_size_t(max(self.nbytes, 16)))
+        self.ptr = p
+
+    @classmethod
+    def from_host(cls, a: np.ndarray) -> "DeviceArray":
+        a = np.ascontiguousarray(a)
+        d = cls(a.nbytes)
+        d.upload(a)
+        return d
+
+    def upload(self, a: np.ndarray) -> None:
+        a = np.ascontiguousarray(a)
+        if a.nbytes > self.nbytes:
+            raise ValueError("host array larger than device allocation")
+        call("pbx_memcpy_htod", self.ptr, a.ctypes.data_as(c_void_p), c_size_t(a.nbytes))
+
+    def download(self, out: np.ndarray) -> np.ndarray:
+        if not out.flags.c_contiguous or out.nbytes > self.nbytes:
+            raise ValueError("bad host output buffer")
+        call("pbx_memcpy_dtoh", out.ctypes.data_as(c_void_p), self.ptr, c_size_t(out.nbytes))
+        return out
+
+    def offset(self, nbytes: int) -> c_void_p:
+        return c_void_p(self.ptr.value + int(nbytes))
+
+    def free(self) -> None:
+        if self.ptr is not None and self.ptr.value:
+            lib = _lib
+            if lib is not None:
+                lib.pbx_free(self.ptr)
+        self.ptr = c_void_p()
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Event:
+    """A HIP event on the library stream (kernel timing on the right stream)."""
+
+    def __init__(self):
+        p = c_void_p()
+        call("pbx_event_create", ctypes.byref(p))
+        self.ptr = p
+
+    def record(self) -> None:
+        call("pbx_event_record", self.ptr)
+
+    def elapsed_ms(self, later: "Event") -> float:
+        ms = c_float(0.0)
+        call("pbx_event_elapsed_ms", self.ptr, later.ptr, ctypes.byref(ms))
+        return float(ms.value)
+
+    def __del__(self):  # pragma: no cover
+        try:
+            if _lib is not None and self.ptr.value:
+                _lib.pbx_event_destroy(self.ptr)
+        except Exception:
+            pass
