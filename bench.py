@@ -66,19 +66,22 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
+        # PBX_BENCH_FORCE_DIST=1 runs the multi-rank code path (gloo control
+        # plane + RCCL communicator) even at world size 1, as a rehearsal.
+        self.forced = os.environ.get("PBX_BENCH_FORCE_DIST") == "1"
+        self.active = self.world > 1 or self.forced
+        if self.active:
             import torch.distributed as dist
 
             dist.init_process_group("gloo")
             self.dist = dist
 
     def barrier(self):
-        if self.world > 1:
+        if self.active:
             self.dist.barrier()
 
     def max(self, x: float) -> float:
-        if self.world == 1:
+        if not self.active:
             return x
         import torch
 
@@ -87,7 +90,7 @@ class Dist:
         return float(t.item())
 
     def broadcast_bytes(self, b: bytes | None) -> bytes:
-        if self.world == 1:
+        if not self.active:
             return b
         obj = [b]
         self.dist.broadcast_object_list(obj, src=0)
@@ -103,7 +106,8 @@ def cpu_baseline(pos, mass, seconds: float):
     og.set_num_threads(cores)
     n = len(pos)
     rng = np.random.default_rng(0)
-    probe = rng.choice(n, size=max(cores, 16), replace=False)
+    og.direct_subset(pos, mass, np.arange(cores))       # spin up the thread pool
+    probe = rng.choice(n, size=4 * cores, replace=False)
     t0 = time.perf_counter()
     og.direct_subset(pos, mass, probe)
     dt = time.perf_counter() - t0
@@ -139,50 +143,43 @@ def pmc_traffic():
 
 def main():
     args = parse()
+    # Load libpbx (ROCm 7.2 HIP runtime + RCCL from /opt/rocm) BEFORE torch is
+    # imported for the gloo control plane, so torch binds to the same runtime
+    # instead of loading its bundled copies under the same sonames.
+    nat.load()
+    nat.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     dist = Dist()
     world, rank = dist.world, dist.rank
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    nat.load()
-    nat.set_device(dist.local_rank if world > 1 else 0)
 
-    n_loc = args.n_per_gpu
-    n_tot = n_loc * world
+    from pynbodyext.parallel import Communicator, ShardedDirect, shard_bounds
+
+    n_tot = args.n_per_gpu * world
     seed = SEEDS.get(n_tot, 1100 + world)
     pos, mass = plummer(n_tot, seed=seed)
-    lo, hi = rank * n_loc, (rank + 1) * n_loc
-    pos_loc = np.ascontiguousarray(pos[lo:hi])
-    mass_loc = np.ascontiguousarray(mass[lo:hi])
-
-    d_pos = nat.DeviceArray.from_host(pos_loc)
-    d_mass = nat.DeviceArray.from_host(mass_loc)
-    d_rec = nat.DeviceArray(32 * n_tot)           # all-gathered source records
-    d_pot = nat.DeviceArray(8 * n_loc)
-    d_acc = nat.DeviceArray(24 * n_loc)
+    lo, hi = shard_bounds(n_tot, world, rank)
+    n_loc = hi - lo
 
     comm = None
-    if world > 1:
-        from pynbodyext.parallel import Communicator
-
+    if dist.active:
         uid = Communicator.unique_id() if rank == 0 else None
         uid = dist.broadcast_bytes(uid)
         comm = Communicator(world, rank, uid)
-    my_rec = d_rec.offset(32 * lo)
+    solver = ShardedDirect(comm, n_tot, pos[lo:hi], mass[lo:hi])
 
-    ev = [nat.Event(), nat.Event()]
-    kernel_ms = []
+    # one event pair per timed step, read back after the timed region
+    events = [(nat.Event(), nat.Event()) for _ in range(args.steps)]
+    it = iter(events)
 
     def step(timed: bool):
-        nat.call("pbx_pack_sources", d_pos.ptr, d_mass.ptr, n_loc, my_rec)
-        if comm is not None:
-            comm.allgather_inplace(d_rec.ptr, 32 * n_loc)
+        solver.gather_sources()
         if timed:
-            ev[0].record()
-        nat.call("pbx_direct_dev", d_rec.ptr, None, n_tot, d_pos.ptr, None, n_loc, lo,
-                 nat.KERNEL_NONE, nat.WANT_POT | nat.WANT_ACC, d_pot.ptr, d_acc.ptr)
+            e0, e1 = next(it)
+            e0.record()
+        solver.solve()
         if timed:
-            ev[1].record()
-            kernel_ms.append(ev[0].elapsed_ms(ev[1]))
+            e1.record()
 
     for _ in range(args.warmup):
         step(False)
@@ -196,6 +193,7 @@ def main():
     dist.barrier()
     t1 = time.perf_counter()
     elapsed = dist.max(t1 - t0)
+    kernel_ms = [a.elapsed_ms(b) for a, b in events]
     kern_avg_ms = dist.max(float(np.mean(kernel_ms)))
 
     pairs_per_step = float(n_tot) * float(n_tot - 1)   # all ranks together

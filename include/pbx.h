@@ -127,6 +127,27 @@ int pbx_direct_dev(const double *d_src, const double *d_src_h, int64_t n_src,
                    int64_t self_offset, int kernel, int want, double *d_pot,
                    double *d_acc);
 
+/* ------------------------------------------------------------------ */
+/* multi-GPU: RCCL communicator (one process per GPU, over xGMI)       */
+/* ------------------------------------------------------------------ */
+/* No reference counterpart: the reference is single-process (rayon
+ * threads).  North-star multi-GPU design: targets are
+ * sharded across ranks, source records are all-gathered, profile partials
+ * are all-reduced.  The unique id (pbx_comm_unique_id_size() bytes) is
+ * created on rank 0 and distributed by the caller's control plane. */
+int pbx_comm_unique_id_size(void);
+int pbx_comm_unique_id(unsigned char *buf, int buflen);
+int pbx_comm_init(void **comm, int nranks, int rank, const unsigned char *uid);
+int pbx_comm_destroy(void *comm);
+/* In-place all-gather-v of byte segments: segment r is
+ * [displs[r], displs[r]+counts[r]) of d_buf, this rank's already in place. */
+int pbx_comm_allgatherv(void *comm, void *d_buf, const int64_t *counts,
+                        const int64_t *displs);
+int pbx_comm_allreduce_f64(void *comm, const double *d_send, double *d_recv,
+                           int64_t count);
+int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv,
+                           int64_t count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,117 @@
+// comm.hip — RCCL communicator of libpbx.so (one process per GPU, xGMI).
+//
+// The reference has no distributed backend (rayon threads only,
+// SURVEY.md §2); this is the MI355X multi-GPU layer of the north star:
+// the direct-sum solve shards TARGETS across ranks and all-gathers the
+// 32-byte SOURCE records (pbx_comm_allgatherv: one ncclBroadcast per
+// root inside an ncclGroup, so shards may be uneven), and per-bin profile
+// partials are summed with pbx_comm_allreduce_*.
+// All collectives run on the library stream of the calling thread's device.
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "pbx_common.h"
+
+namespace pbx {
+
+#define PBX_NCCL(call)                                                             \
+  do {                                                                             \
+    ncclResult_t _r = (call);                                                      \
+    if (_r != ncclSuccess)                                                         \
+      ::pbx::fail(PBX_ERR_RUNTIME, "%s failed: %s", #call, ncclGetErrorString(_r)); \
+  } while (0)
+
+struct Comm {
+  ncclComm_t nccl = nullptr;
+  int nranks = 0;
+  int rank = 0;
+  int device = -1;
+};
+
+}  // namespace pbx
+
+using namespace pbx;
+
+extern "C" {
+
+int pbx_comm_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int pbx_comm_unique_id(unsigned char *buf, int buflen) {
+  return guard([&] {
+    if (buflen < (int)sizeof(ncclUniqueId))
+      fail(PBX_ERR_VALUE, "unique id buffer needs %d bytes", (int)sizeof(ncclUniqueId));
+    ncclUniqueId id;
+    PBX_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(buf, &id, sizeof(id));
+  });
+}
+
+int pbx_comm_init(void **comm, int nranks, int rank, const unsigned char *uid) {
+  return guard([&] {
+    if (nranks < 1 || rank < 0 || rank >= nranks)
+      fail(PBX_ERR_VALUE, "bad rank %d / nranks %d", rank, nranks);
+    Device &d = current_device();
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    Comm *c = new Comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = d.id;
+    ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, id, rank);
+    if (r != ncclSuccess) {
+      delete c;
+      fail(PBX_ERR_RUNTIME, "ncclCommInitRank failed: %s", ncclGetErrorString(r));
+    }
+    *comm = c;
+  });
+}
+
+int pbx_comm_destroy(void *comm) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) return;
+    if (c->nccl) PBX_NCCL(ncclCommDestroy(c->nccl));
+    delete c;
+  });
+}
+
+// d_buf holds every rank's segment; segment r occupies
+// [displs[r], displs[r] + counts[r]) bytes and this rank's segment is
+// already in place.  Afterwards every rank holds all segments.
+int pbx_comm_allgatherv(void *comm, void *d_buf, const int64_t *counts, const int64_t *displs) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) fail(PBX_ERR_VALUE, "null communicator");
+    Device &d = current_device();
+    if (d.id != c->device) fail(PBX_ERR_VALUE, "communicator belongs to device %d", c->device);
+    char *base = (char *)d_buf;
+    PBX_NCCL(ncclGroupStart());
+    for (int r = 0; r < c->nranks; ++r) {
+      if (counts[r] <= 0) continue;
+      PBX_NCCL(ncclBroadcast(base + displs[r], base + displs[r], (size_t)counts[r], ncclChar, r,
+                             c->nccl, d.stream));
+    }
+    PBX_NCCL(ncclGroupEnd());
+  });
+}
+
+int pbx_comm_allreduce_f64(void *comm, const double *d_send, double *d_recv, int64_t count) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) fail(PBX_ERR_VALUE, "null communicator");
+    Device &d = current_device();
+    PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, ncclFloat64, ncclSum, c->nccl, d.stream));
+  });
+}
+
+int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv, int64_t count) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) fail(PBX_ERR_VALUE, "null communicator");
+    Device &d = current_device();
+    PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, ncclInt64, ncclSum, c->nccl, d.stream));
+  });
+}
+
+}  // extern "C"

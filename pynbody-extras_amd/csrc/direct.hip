@@ -22,6 +22,7 @@
 //  * Self-interaction (all-particles form) is excluded only on the
 //    "diagonal" source window of each block, so the main loop carries no
 //    per-pair compare.
+#include <cstdlib>
 #include <cstring>
 
 #include "pbx_common.h"
@@ -64,38 +65,44 @@ __device__ __forceinline__ double w2p_inner(double u) {
 }
 
 // One source interaction for one target.  KERN: -1 Newtonian, 0 Plummer,
-// 1 spline.  Accumulates phi += m * phi_unit and a += m * g * d.
+// 1 spline.
+//
+// Scaled accumulation: with y0 = v_rsq_f64(s) and w = y0 * (3 - s*y0^2)
+// (= 2*y1, y1 the Newton-refined 1/sqrt(s)), the kernel accumulates
+//     ph += m*w        (= -2 * m * phi_unit)
+//     a  += m*w^3 * d  (=  8 * m * g * d)
+// and the epilogue multiplies by -1/2 and 1/8 (exact powers of two).  This
+// shares m*w between potential and force and costs 10 FP64 ops after the
+// rsq instead of 11.  Only overflow moves: m*w^3 overflows for r below
+// ~1e-103 (the reference's m/r^3 a factor 8 later), i.e. for particles
+// that are already coincident to ~1e-103.
 template <int KERN, int WANT>
 __device__ __forceinline__ void pair(double dx, double dy, double dz, double m, double h,
                                      double &ph, double &ax, double &ay, double &az) {
   // s2 = r^2 + R2_TINY (direct.rs:174,305; kernel variants use r = sqrt(s2))
   double s2 = __builtin_fma(dx, dx, __builtin_fma(dy, dy, __builtin_fma(dz, dz, kR2Tiny)));
-  double phi_u, g;
-  if (KERN == 0) {
-    // Plummer: -1/sqrt(r^2 + h^2), 1/(r^2+h^2)^(3/2)  (kernel.rs:46,67-70)
-    double y = rsqrt_nr(__builtin_fma(h, h, s2));
-    phi_u = -y;
-    g = y * y * y;
-  } else {
-    double y = rsqrt_nr(s2);
-    phi_u = -y;
-    g = y * y * y;
-    if (KERN == 1) {
-      double r = s2 * y;
-      if (h > 0.0 && r < h) {  // inside the spline support (kernel.rs:47-54,71-80)
-        double hinv = 1.0 / h;
-        double u = r * hinv;
-        phi_u = w2_inner(u) * hinv;
-        g = w2p_inner(u) * (hinv * hinv) / r;
-      }
+  // Plummer: 1/sqrt(r^2 + h^2), 1/(r^2+h^2)^(3/2)  (kernel.rs:46,67-70)
+  const double s = (KERN == 0) ? __builtin_fma(h, h, s2) : s2;
+  const double y0 = __builtin_amdgcn_rsq(s);
+  const double w = y0 * __builtin_fma(-s, y0 * y0, 3.0);
+  double mw = m * w;
+  double g8 = mw * (w * w);
+  if (KERN == 1) {
+    // spline (kernel.rs:47-54,71-80): inside the support replace the
+    // Newtonian values, expressed in the same scaled units
+    double r = s2 * (0.5 * w);
+    if (h > 0.0 && r < h) {
+      double hinv = 1.0 / h;
+      double u = r * hinv;
+      mw = -2.0 * m * (w2_inner(u) * hinv);
+      g8 = 8.0 * m * (w2p_inner(u) * (hinv * hinv) / r);
     }
   }
-  if (WANT & PBX_WANT_POT) ph = __builtin_fma(m, phi_u, ph);
+  if (WANT & PBX_WANT_POT) ph += mw;
   if (WANT & PBX_WANT_ACC) {
-    double mg = m * g;
-    ax = __builtin_fma(mg, dx, ax);
-    ay = __builtin_fma(mg, dy, ay);
-    az = __builtin_fma(mg, dz, az);
+    ax = __builtin_fma(g8, dx, ax);
+    ay = __builtin_fma(g8, dy, ay);
+    az = __builtin_fma(g8, dz, az);
   }
 }
 
@@ -178,12 +185,13 @@ __global__ void __launch_bounds__(kBlock)
   for (int k = 0; k < T; ++k) {
     int64_t t = tbase + k * kBlock + threadIdx.x;
     if (t < n_tgt) {
-      if (WANT & PBX_WANT_POT) pot_out[soff + t] = ph[k];
+      // undo the scaled accumulation of pair(): exact powers of two
+      if (WANT & PBX_WANT_POT) pot_out[soff + t] = -0.5 * ph[k];
       if (WANT & PBX_WANT_ACC) {
         double *a = acc_out + 3 * (soff + t);
-        a[0] = ax[k];
-        a[1] = ay[k];
-        a[2] = az[k];
+        a[0] = 0.125 * ax[k];
+        a[1] = 0.125 * ay[k];
+        a[2] = 0.125 * az[k];
       }
     }
   }
@@ -225,16 +233,38 @@ __global__ void __launch_bounds__(kBlock)
                         mass ? mass[i] : 1.0);
 }
 
-static constexpr int kT = 2;
+// Targets per lane.  2 is the default; PBX_DIRECT_T=1|4 selects the other
+// instantiations (tuning experiments).
+static int targets_per_lane() {
+  static int t = [] {
+    const char *v = std::getenv("PBX_DIRECT_T");
+    int x = v ? std::atoi(v) : 2;
+    return (x == 1 || x == 4) ? x : 2;
+  }();
+  return t;
+}
 
 template <int KERN, int WANT, bool SELF>
 static void launch_variant(hipStream_t st, dim3 grid, const double4 *src, const double *src_h,
                            int has_h, int64_t n_src, int64_t chunk, const double *tgt,
                            const double *tgt_h, int64_t n_tgt, int64_t self_offset,
                            double *pot, double *acc, int64_t stride) {
-  hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, kT>), grid, dim3(kBlock), 0, st, src,
-                     src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
-                     stride);
+  switch (targets_per_lane()) {
+    case 1:
+      hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, 1>), grid, dim3(kBlock), 0, st, src,
+                         src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
+                         stride);
+      break;
+    case 4:
+      hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, 4>), grid, dim3(kBlock), 0, st, src,
+                         src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
+                         stride);
+      break;
+    default:
+      hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, 2>), grid, dim3(kBlock), 0, st, src,
+                         src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
+                         stride);
+  }
 }
 
 template <int KERN, int WANT>
@@ -282,7 +312,7 @@ void direct_device(Device &d, const double *src, const double *src_h, int64_t n_
     if (want & PBX_WANT_ACC) PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 3 * n_tgt, st));
     return;
   }
-  const int64_t per_block = (int64_t)kBlock * kT;
+  const int64_t per_block = (int64_t)kBlock * targets_per_lane();
   const int64_t bx = (n_tgt + per_block - 1) / per_block;
   // Aim for >= 2048 blocks (8 per CU) but keep >= 4096 sources per split.
   int64_t nsplit = (2048 + bx - 1) / bx;

@@ -76,6 +76,13 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_pack_sources": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "pbx_direct_dev": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                c_int64, c_int, c_int, c_void_p, c_void_p]),
+    "pbx_comm_unique_id_size": (c_int, []),
+    "pbx_comm_unique_id": (c_int, [c_char_p, c_int]),
+    "pbx_comm_init": (c_int, [POINTER(c_void_p), c_int, c_int, c_char_p]),
+    "pbx_comm_destroy": (c_int, [c_void_p]),
+    "pbx_comm_allgatherv": (c_int, [c_void_p, c_void_p, _i64p, _i64p]),
+    "pbx_comm_allreduce_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pbx_comm_allreduce_i64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
 }
 
 

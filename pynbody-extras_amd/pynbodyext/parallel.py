@@ -1,0 +1,128 @@
+"""Multi-GPU execution: one process per GPU, RCCL over xGMI.
+
+The reference is single-process (rayon threads over targets);
+this module is the MI355X scale-out of the same solve:
+
+* direct summation shards the TARGETS: rank r owns particles
+  [lo_r, hi_r) (contiguous, balanced); every rank packs its particles into
+  32-byte source records, one all-gather-v (RCCL broadcasts in a group)
+  gives every rank all N records, and each rank runs the direct-sum kernel
+  for its own targets with self-skip offset lo_r.  Outputs stay sharded.
+* profile partials (int64 counts, f64 per-bin sums) are summed with one
+  all-reduce.
+
+The control plane (unique-id exchange, barriers) is the caller's, e.g.
+torch.distributed with the gloo backend; the data path is RCCL only.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_int64, c_void_p
+
+import numpy as np
+
+from . import _native as nat
+
+
+def shard_bounds(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous balanced shard [lo, hi) of rank (first n % world ranks get +1)."""
+    base, extra = divmod(int(n_total), int(world))
+    lo = rank * base + min(rank, extra)
+    hi = lo + base + (1 if rank < extra else 0)
+    return lo, hi
+
+
+def all_shards(n_total: int, world: int) -> list[tuple[int, int]]:
+    return [shard_bounds(n_total, world, r) for r in range(world)]
+
+
+class Communicator:
+    """RCCL communicator of libpbx (device buffers, library stream)."""
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        self.nranks, self.rank = int(nranks), int(rank)
+        h = c_void_p()
+        nat.call("pbx_comm_init", ctypes.byref(h), self.nranks, self.rank, bytes(uid))
+        self.handle = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = nat.load()
+        size = lib.pbx_comm_unique_id_size()
+        buf = ctypes.create_string_buffer(size)
+        nat.call("pbx_comm_unique_id", buf, size)
+        return buf.raw
+
+    def allgatherv(self, d_buf, counts_bytes, displs_bytes) -> None:
+        c = np.ascontiguousarray(counts_bytes, dtype=np.int64)
+        d = np.ascontiguousarray(displs_bytes, dtype=np.int64)
+        nat.call("pbx_comm_allgatherv", self.handle, d_buf, c.ctypes.data_as(ctypes.POINTER(c_int64)),
+                 d.ctypes.data_as(ctypes.POINTER(c_int64)))
+
+    def allgather_inplace(self, d_buf, bytes_per_rank: int) -> None:
+        counts = [bytes_per_rank] * self.nranks
+        displs = [r * bytes_per_rank for r in range(self.nranks)]
+        self.allgatherv(d_buf, counts, displs)
+
+    def allreduce_sum_f64(self, d_send, d_recv, count: int) -> None:
+        nat.call("pbx_comm_allreduce_f64", self.handle, d_send, d_recv, int(count))
+
+    def allreduce_sum_i64(self, d_send, d_recv, count: int) -> None:
+        nat.call("pbx_comm_allreduce_i64", self.handle, d_send, d_recv, int(count))
+
+    def destroy(self) -> None:
+        if self.handle is not None and self.handle.value:
+            nat.call("pbx_comm_destroy", self.handle)
+        self.handle = c_void_p()
+
+
+class ShardedDirect:
+    """Direct-sum gravity over particles sharded across ranks (device-resident).
+
+    ``comm`` is a :class:`Communicator` (or None for a single rank).  The
+    local shard (positions, masses) lives in HBM; ``step`` computes the
+    potential and acceleration of the local particles due to ALL particles.
+    """
+
+    def __init__(self, comm, n_total: int, pos_local: np.ndarray, mass_local: np.ndarray | None):
+        self.comm = comm
+        world = comm.nranks if comm is not None else 1
+        rank = comm.rank if comm is not None else 0
+        self.n_total = int(n_total)
+        self.shards = all_shards(self.n_total, world)
+        self.lo, self.hi = self.shards[rank]
+        self.n_loc = self.hi - self.lo
+        if pos_local.shape != (self.n_loc, 3):
+            raise ValueError(f"rank {rank} expects {self.n_loc} local particles")
+        self.d_pos = nat.DeviceArray.from_host(np.ascontiguousarray(pos_local, dtype=np.float64))
+        self.d_mass = (nat.DeviceArray.from_host(np.ascontiguousarray(mass_local, dtype=np.float64))
+                       if mass_local is not None else None)
+        self.d_rec = nat.DeviceArray(32 * self.n_total)
+        self.d_pot = nat.DeviceArray(8 * max(self.n_loc, 1))
+        self.d_acc = nat.DeviceArray(24 * max(self.n_loc, 1))
+        self._counts = [32 * (h - lo) for lo, h in self.shards]
+        self._displs = [32 * lo for lo, _ in self.shards]
+
+    def gather_sources(self) -> None:
+        nat.call("pbx_pack_sources", self.d_pos.ptr, self.d_mass.ptr if self.d_mass else None,
+                 self.n_loc, self.d_rec.offset(32 * self.lo))
+        if self.comm is not None and self.comm.nranks > 1:
+            self.comm.allgatherv(self.d_rec.ptr, self._counts, self._displs)
+
+    def solve(self, want: int = nat.WANT_POT | nat.WANT_ACC) -> None:
+        nat.call("pbx_direct_dev", self.d_rec.ptr, None, self.n_total, self.d_pos.ptr, None,
+                 self.n_loc, self.lo, nat.KERNEL_NONE, want,
+                 self.d_pot.ptr if want & nat.WANT_POT else None,
+                 self.d_acc.ptr if want & nat.WANT_ACC else None)
+
+    def step(self, want: int = nat.WANT_POT | nat.WANT_ACC) -> None:
+        self.gather_sources()
+        self.solve(want)
+
+    def results(self) -> tuple[np.ndarray, np.ndarray]:
+        pot = np.empty(self.n_loc)
+        acc = np.empty((self.n_loc, 3))
+        if self.n_loc:
+            self.d_pot.download(pot)
+            self.d_acc.download(acc)
+        return pot, acc

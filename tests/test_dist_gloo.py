@@ -1,0 +1,100 @@
+"""N>1 host logic on CPU: world_size-2 gloo processes.
+
+Covers the multi-GPU bookkeeping of pynbodyext.parallel (balanced
+contiguous shards, all-gather-v of the 32-byte source records with uneven
+shards, self-skip offsets of the sharded solve) and the bench control plane
+(barrier, max over ranks).  The device all-gather itself is RCCL on the GPU
+box; here the same record layout is gathered with gloo and each rank's
+targets are solved by the oracle, then compared with the unsharded oracle.
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from pynbodyext.parallel import all_shards, shard_bounds
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def test_shard_bounds_cover_and_balance():
+    for n in (0, 1, 7, 10, 1_000_003):
+        for w in (1, 2, 3, 8):
+            sh = all_shards(n, w)
+            assert sh[0][0] == 0 and sh[-1][1] == n
+            assert all(sh[i][1] == sh[i + 1][0] for i in range(w - 1))
+            sizes = [h - lo for lo, h in sh]
+            assert max(sizes) - min(sizes) <= 1
+            assert shard_bounds(n, w, w - 1) == sh[-1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from oracle import gravity as og
+    from pynbodyext.parallel import all_shards, shard_bounds
+    from pynbodyext.synthetic import plummer
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pos, mass = plummer(n, seed=77)
+        lo, hi = shard_bounds(n, world, rank)
+        # pack the local shard exactly like pbx_pack_sources: {x, y, z, m}
+        rec_local = np.concatenate([pos[lo:hi], mass[lo:hi, None]], axis=1)
+        shards = all_shards(n, world)
+        maxn = max(h - l for l, h in shards)
+        buf = torch.zeros((maxn, 4), dtype=torch.float64)
+        buf[: hi - lo] = torch.from_numpy(rec_local)
+        parts = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf)
+        rec = np.concatenate([parts[r][: h - l].numpy() for r, (l, h) in enumerate(shards)])
+        assert np.array_equal(rec[:, :3], pos) and np.array_equal(rec[:, 3], mass)
+        # this rank's targets against all sources, self-skip at global index lo + t
+        pot, acc = og.direct_subset(np.ascontiguousarray(rec[:, :3]), np.ascontiguousarray(rec[:, 3]),
+                                    np.arange(lo, hi))
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        q.put((rank, lo, hi, pot, acc, float(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_direct_world2_matches_unsharded():
+    import multiprocessing as mp
+
+    from oracle import gravity as og
+    from pynbodyext.synthetic import plummer
+
+    n, world = 1003, 2          # uneven shards: 502 + 501
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    pos, mass = plummer(n, seed=77)
+    pot_ref = og.direct_potentials(pos, mass)
+    acc_ref = og.direct_accelerations(pos, mass)
+    for rank, lo, hi, pot, acc, tmax in res:
+        assert tmax == float(world)
+        np.testing.assert_array_equal(pot, pot_ref[lo:hi])
+        np.testing.assert_array_equal(acc, acc_ref[lo:hi])

@@ -1,0 +1,73 @@
+"""RCCL leg of the sharded direct sum on the GPU box (world = 1 communicator).
+
+The single-GPU box can only host one RCCL rank per GPU; the world>1 data
+path is exercised by the driver's 8-GPU bench, and its bookkeeping by
+tests/test_dist_gloo.py on CPU.
+"""
+import numpy as np
+import pytest
+
+from oracle import gravity as og
+from pynbodyext import _native as nat
+from pynbodyext.parallel import Communicator, ShardedDirect
+from pynbodyext.synthetic import plummer
+
+pytestmark = pytest.mark.gpu
+
+
+def test_rccl_world1_collectives(gpu):
+    comm = Communicator(1, 0, Communicator.unique_id())
+    try:
+        a = np.arange(10, dtype=np.float64)
+        d = nat.DeviceArray.from_host(a)
+        comm.allreduce_sum_f64(d.ptr, d.ptr, 10)
+        comm.allgather_inplace(d.ptr, 80)
+        out = np.empty(10)
+        d.download(out)
+        assert np.array_equal(out, a)
+        ai = np.arange(5, dtype=np.int64)
+        di = nat.DeviceArray.from_host(ai)
+        comm.allreduce_sum_i64(di.ptr, di.ptr, 5)
+        oi = np.empty(5, dtype=np.int64)
+        di.download(oi)
+        assert np.array_equal(oi, ai)
+    finally:
+        comm.destroy()
+
+
+def test_sharded_direct_world1(gpu):
+    pos, mass = plummer(3000, seed=4)
+    comm = Communicator(1, 0, Communicator.unique_id())
+    try:
+        s = ShardedDirect(comm, len(pos), pos, mass)
+        s.step()
+        nat.synchronize()
+        pot, acc = s.results()
+    finally:
+        comm.destroy()
+    pr = og.direct_potentials(pos, mass)
+    ar = og.direct_accelerations(pos, mass)
+    assert np.max(np.abs(pot - pr) / np.abs(pr)) < 1e-10
+    assert np.max(np.linalg.norm(acc - ar, axis=1) / np.linalg.norm(ar, axis=1)) < 1e-10
+
+
+def test_sharded_solve_of_one_shard_matches_oracle(gpu):
+    """Simulate rank 1 of 3 on one GPU: records of all ranks in place, solve
+    only the local targets with self offset lo (what each rank does)."""
+    from pynbodyext.parallel import shard_bounds
+
+    n, world, rank = 2501, 3, 1
+    pos, mass = plummer(n, seed=6)
+    lo, hi = shard_bounds(n, world, rank)
+    s = ShardedDirect(None, n, pos, mass)  # world-1 instance to hold all records
+    s.gather_sources()
+    d_tgt = nat.DeviceArray.from_host(np.ascontiguousarray(pos[lo:hi]))
+    d_pot = nat.DeviceArray(8 * (hi - lo))
+    d_acc = nat.DeviceArray(24 * (hi - lo))
+    nat.call("pbx_direct_dev", s.d_rec.ptr, None, n, d_tgt.ptr, None, hi - lo, lo,
+             nat.KERNEL_NONE, 3, d_pot.ptr, d_acc.ptr)
+    pot = d_pot.download(np.empty(hi - lo))
+    acc = d_acc.download(np.empty((hi - lo, 3)))
+    pr, ar = og.direct_subset(pos, mass, np.arange(lo, hi))
+    assert np.max(np.abs(pot - pr) / np.abs(pr)) < 1e-10
+    assert np.max(np.linalg.norm(acc - ar, axis=1) / np.linalg.norm(ar, axis=1)) < 1e-10
