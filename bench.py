@@ -56,45 +56,42 @@ def parse():
 
 
 class Dist:
-    """Control plane (barrier, max-over-ranks) over torch.distributed gloo.
+    """Control plane for one process per GPU, launched by torch.distributed.run.
 
-    The data path never goes through torch: the source all-gather is RCCL
-    called from libpbx.so.
+    Only the environment of the launcher is used (RANK / WORLD_SIZE /
+    LOCAL_RANK / MASTER_*); torch is never imported in the worker.  The RCCL
+    unique id travels through a node-local rendezvous file, and barrier /
+    max-over-ranks run on the RCCL communicator itself, which is also the
+    data path (source all-gather).
     """
 
     def __init__(self):
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        # PBX_BENCH_FORCE_DIST=1 runs the multi-rank code path (gloo control
-        # plane + RCCL communicator) even at world size 1, as a rehearsal.
-        self.forced = os.environ.get("PBX_BENCH_FORCE_DIST") == "1"
-        self.active = self.world > 1 or self.forced
+        # PBX_BENCH_FORCE_DIST=1 runs the multi-rank code path (rendezvous +
+        # RCCL communicator) even at world size 1, as a rehearsal.
+        self.active = self.world > 1 or os.environ.get("PBX_BENCH_FORCE_DIST") == "1"
+        self.comm = None
         if self.active:
-            import torch.distributed as dist
+            from pynbodyext.parallel import Communicator, FileRendezvous
 
-            dist.init_process_group("gloo")
-            self.dist = dist
+            rdzv = FileRendezvous(self.rank, self.world)
+            uid = rdzv.broadcast(Communicator.unique_id() if self.rank == 0 else None)
+            self.comm = Communicator(self.world, self.rank, uid)
+            rdzv.cleanup()
 
     def barrier(self):
-        if self.active:
-            self.dist.barrier()
+        if self.comm is not None:
+            self.comm.barrier()
 
     def max(self, x: float) -> float:
-        if not self.active:
-            return x
-        import torch
+        return self.comm.max(x) if self.comm is not None else x
 
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def broadcast_bytes(self, b: bytes | None) -> bytes:
-        if not self.active:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
-        return obj[0]
+    def close(self):
+        if self.comm is not None:
+            self.comm.destroy()
+            self.comm = None
 
 
 def cpu_baseline(pos, mass, seconds: float):
@@ -153,20 +150,14 @@ def main():
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
-    from pynbodyext.parallel import Communicator, ShardedDirect, shard_bounds
+    from pynbodyext.parallel import ShardedDirect, shard_bounds
 
     n_tot = args.n_per_gpu * world
     seed = SEEDS.get(n_tot, 1100 + world)
     pos, mass = plummer(n_tot, seed=seed)
     lo, hi = shard_bounds(n_tot, world, rank)
     n_loc = hi - lo
-
-    comm = None
-    if dist.active:
-        uid = Communicator.unique_id() if rank == 0 else None
-        uid = dist.broadcast_bytes(uid)
-        comm = Communicator(world, rank, uid)
-    solver = ShardedDirect(comm, n_tot, pos[lo:hi], mass[lo:hi])
+    solver = ShardedDirect(dist.comm, n_tot, pos[lo:hi], mass[lo:hi])
 
     # one event pair per timed step, read back after the timed region
     events = [(nat.Event(), nat.Event()) for _ in range(args.steps)]
@@ -203,6 +194,7 @@ def main():
     achieved_tf = pairs_launch * FLOP_PER_PAIR / (kern_avg_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic()
 
+    dist.close()
     if rank != 0:
         return
     cpu = None

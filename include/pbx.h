@@ -147,6 +147,11 @@ int pbx_comm_allreduce_f64(void *comm, const double *d_send, double *d_recv,
                            int64_t count);
 int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv,
                            int64_t count);
+/* Control plane on the same communicator: device barrier (returns after
+ * every rank reached it and the stream drained) and max over ranks of a
+ * host double. */
+int pbx_comm_barrier(void *comm);
+int pbx_comm_max_f64(void *comm, double value, double *out);
 
 #ifdef __cplusplus
 }

@@ -105,6 +105,32 @@ int pbx_comm_allreduce_f64(void *comm, const double *d_send, double *d_recv, int
   });
 }
 
+// Control-plane helpers on the data-plane communicator: a device barrier
+// (1-element all-reduce + stream sync) and max-over-ranks of a host scalar.
+int pbx_comm_barrier(void *comm) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) fail(PBX_ERR_VALUE, "null communicator");
+    Device &d = current_device();
+    int64_t *buf = (int64_t *)d.slot(kSlotComm).ensure(64);
+    PBX_NCCL(ncclAllReduce(buf, buf, 1, ncclInt64, ncclSum, c->nccl, d.stream));
+    PBX_HIP(hipStreamSynchronize(d.stream));
+  });
+}
+
+int pbx_comm_max_f64(void *comm, double value, double *out) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) fail(PBX_ERR_VALUE, "null communicator");
+    Device &d = current_device();
+    double *buf = (double *)d.slot(kSlotComm).ensure(64);
+    PBX_HIP(hipMemcpyAsync(buf, &value, sizeof(double), hipMemcpyHostToDevice, d.stream));
+    PBX_NCCL(ncclAllReduce(buf, buf, 1, ncclFloat64, ncclMax, c->nccl, d.stream));
+    PBX_HIP(hipMemcpyAsync(out, buf, sizeof(double), hipMemcpyDeviceToHost, d.stream));
+    PBX_HIP(hipStreamSynchronize(d.stream));
+  });
+}
+
 int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv, int64_t count) {
   return guard([&] {
     Comm *c = (Comm *)comm;

@@ -238,8 +238,8 @@ __global__ void __launch_bounds__(kBlock)
 static int targets_per_lane() {
   static int t = [] {
     const char *v = std::getenv("PBX_DIRECT_T");
-    int x = v ? std::atoi(v) : 2;
-    return (x == 1 || x == 4) ? x : 2;
+    int x = v ? std::atoi(v) : 4;
+    return (x == 1 || x == 2) ? x : 4;
   }();
   return t;
 }

@@ -94,6 +94,7 @@ enum Slot {
   kSlotProf5,
   kSlotProf6,
   kSlotProf7,
+  kSlotComm,
   kSlotCount
 };
 

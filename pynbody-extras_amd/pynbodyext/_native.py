@@ -83,6 +83,8 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_comm_allgatherv": (c_int, [c_void_p, c_void_p, _i64p, _i64p]),
     "pbx_comm_allreduce_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "pbx_comm_allreduce_i64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pbx_comm_barrier": (c_int, [c_void_p]),
+    "pbx_comm_max_f64": (c_int, [c_void_p, c_double, POINTER(c_double)]),
 }
 
 

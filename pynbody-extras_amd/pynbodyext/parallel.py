@@ -70,10 +70,73 @@ class Communicator:
     def allreduce_sum_i64(self, d_send, d_recv, count: int) -> None:
         nat.call("pbx_comm_allreduce_i64", self.handle, d_send, d_recv, int(count))
 
+    def barrier(self) -> None:
+        nat.call("pbx_comm_barrier", self.handle)
+
+    def max(self, value: float) -> float:
+        out = ctypes.c_double(0.0)
+        nat.call("pbx_comm_max_f64", self.handle, float(value), ctypes.byref(out))
+        return out.value
+
     def destroy(self) -> None:
         if self.handle is not None and self.handle.value:
             nat.call("pbx_comm_destroy", self.handle)
         self.handle = c_void_p()
+
+
+class FileRendezvous:
+    """Out-of-band exchange of the RCCL unique id between the ranks of ONE
+    node, through a file in a local directory.
+
+    The launch key is (MASTER_ADDR, MASTER_PORT, parent pid): every rank of
+    one ``torch.distributed.run`` launch is a child of the same agent, so
+    concurrent or stale launches never share a file.  No torch import is
+    needed in the worker (the launcher only sets the environment).
+    """
+
+    def __init__(self, rank: int, world: int, directory: str | None = None,
+                 key: str | None = None, timeout: float = 600.0):
+        import os
+        import tempfile
+
+        self.rank, self.world, self.timeout = int(rank), int(world), float(timeout)
+        if key is None:
+            key = "{}_{}_{}".format(os.environ.get("MASTER_ADDR", "local"),
+                                    os.environ.get("MASTER_PORT", "0"), os.getppid())
+        d = directory or os.environ.get("PBX_RDZV_DIR") or tempfile.gettempdir()
+        self.path = os.path.join(d, f"pbx_rdzv_{key}.uid")
+
+    def broadcast(self, payload: bytes | None) -> bytes:
+        import os
+        import time
+
+        if self.rank == 0:
+            tmp = f"{self.path}.tmp{os.getpid()}"
+            with open(tmp, "wb") as f:
+                f.write(payload)
+            os.replace(tmp, self.path)
+            return payload
+        t0 = time.monotonic()
+        while True:
+            try:
+                with open(self.path, "rb") as f:
+                    data = f.read()
+                if data:
+                    return data
+            except FileNotFoundError:
+                pass
+            if time.monotonic() - t0 > self.timeout:
+                raise TimeoutError(f"rank {self.rank}: no rendezvous file {self.path}")
+            time.sleep(0.05)
+
+    def cleanup(self) -> None:
+        import os
+
+        if self.rank == 0:
+            try:
+                os.remove(self.path)
+            except FileNotFoundError:
+                pass
 
 
 class ShardedDirect:

@@ -98,3 +98,27 @@ def test_sharded_direct_world2_matches_unsharded():
         assert tmax == float(world)
         np.testing.assert_array_equal(pot, pot_ref[lo:hi])
         np.testing.assert_array_equal(acc, acc_ref[lo:hi])
+
+
+def _rdzv_worker(rank, world, d, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd")]
+    from pynbodyext.parallel import FileRendezvous
+
+    r = FileRendezvous(rank, world, directory=d, key="k", timeout=60)
+    q.put((rank, r.broadcast(b"unique-id-bytes" if rank == 0 else None)))
+
+
+def test_file_rendezvous_world3(tmp_path):
+    """The out-of-band RCCL unique-id exchange of bench.py (no torch import)."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rdzv_worker, args=(r, 3, str(tmp_path), q)) for r in (2, 1, 0)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=60) for _ in range(3))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert got == {0: b"unique-id-bytes", 1: b"unique-id-bytes", 2: b"unique-id-bytes"}

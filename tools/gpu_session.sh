@@ -21,6 +21,12 @@ while read -r tmo name cmd; do
     echo "fault-like exit $rc: stopping session" | tee -a gpurun_out/session.log
     exit "$rc"
   fi
+  # a child process that aborted / segfaulted / faulted the GPU under a
+  # launcher that itself exits 1 (torchrun, pytest-xdist, ...) is fatal too
+  if grep -qE "SIGABRT|SIGSEGV|Signal 6|Signal 11|exitcode *: *-|Segmentation fault|Memory access fault|core dumped" "gpurun_out/$name.out"; then
+    echo "child fault detected in $name: stopping session" | tee -a gpurun_out/session.log
+    exit 134
+  fi
   (( rc != 0 )) && status=1
 done < "$1"
 exit $status
