@@ -128,6 +128,50 @@ int pbx_direct_dev(const double *d_src, const double *d_src_h, int64_t n_src,
                    double *d_acc);
 
 /* ------------------------------------------------------------------ */
+/* radial profiles: binning + per-bin reduction                        */
+/* ------------------------------------------------------------------ */
+/* One opaque handle per profile holds the binned quantity x (and, after a
+ * fused selection, the selection weights and original indices) in HBM.
+ * Replaces, in pynbodyext/profiles:
+ *   BinsSet._assign_particles        bins.py:346-395  (assign + csr)
+ *   equal_number_bins_algorithm      bins.py:720-746  (edges_equaln)
+ *   np.min / np.max in lin / log     bins.py:689-718  (minmax)
+ *   ProfileArray._compute sums       proarray.py:272-334 (moments)
+ * and the filter scope feeding it (Sphere & FamilyFilter + sim["r"],
+ * filters/filt.py:42-86, profiles/spatial_profile.py:30-35) (select). */
+int pbx_profile_create(void **handle);
+int pbx_profile_destroy(void *handle);
+/* x = host array of n doubles (the generic BinsSet path) */
+int pbx_profile_set_x(void *handle, const double *h_x, int64_t n);
+/* Fused selection: keep particle i when (no family ranges given, or
+ * fam[2f] <= i < fam[2f+1] for some f < nfam) and (use_sphere == 0, or
+ * ((x-cx)^2+(y-cy)^2)+(z-cz)^2 < sphere[3]) with sphere = {cx,cy,cz,R^2};
+ * x = sqrt((x*x+y*y)+z*z) (ndim 3) or sqrt(x*x+y*y) (ndim 2), weights =
+ * mass (or 1), kept in index order.  pos/mass are host (on_device = 0) or
+ * device pointers (on_device = 1). */
+int pbx_profile_select(void *handle, const double *pos, const double *mass, int64_t n,
+                       int on_device, int use_sphere, const double *sphere,
+                       const int64_t *fam, int nfam, int ndim, int64_t *n_kept);
+/* original indices (int64), x and weights of the selection (any may be NULL) */
+int pbx_profile_get_selection(void *handle, int64_t *h_idx, double *h_x, double *h_w);
+int pbx_profile_minmax(void *handle, double *mn, double *mx);
+/* equaln edges into h_edges (capacity nbins + 1); *n_edges = nbins + 1, or
+ * 2 for the reference's degenerate "< 2 values" case */
+int pbx_profile_edges_equaln(void *handle, int64_t nbins, int has_min, double bin_min,
+                             int has_max, double bin_max, double *h_edges,
+                             int64_t *n_edges);
+/* bin ids + counts (nb = n_edges - 1 int64) for ascending edges */
+int pbx_profile_assign(void *handle, const double *h_edges, int64_t n_edges,
+                       int64_t *h_counts, int64_t *n_valid);
+/* CSR of the assignment (perm: n_valid int64, offsets: nb+1); NULL = skip */
+int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets);
+/* per-bin sums h_out[nb][7] = {Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|};
+ * f_src / w_src: 0 = x, 1 = selection weights, 2 = host array (h_f / h_w,
+ * n doubles); w_src = -1: unweighted */
+int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src,
+                        const double *h_w, double *h_out);
+
+/* ------------------------------------------------------------------ */
 /* multi-GPU: RCCL communicator (one process per GPU, over xGMI)       */
 /* ------------------------------------------------------------------ */
 /* No reference counterpart: the reference is single-process (rayon

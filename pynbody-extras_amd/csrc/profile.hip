@@ -1,0 +1,953 @@
+// profile.hip — radial-profile binning and per-bin reduction on gfx950.
+//
+// Replaces the numpy hot spots of pynbodyext.profiles (SURVEY.md §8a
+// a12-a19):
+//   * Sphere & FamilyFilter mask + r = sqrt((x*x+y*y)+z*z) + sub-snapshot
+//     (filters/filt.py:42-86, core/calculate/context.py:622-641)  -> select
+//   * equaln edges = exact order statistics of the kept x
+//     (profiles/bins.py:720-746)                                   -> sort
+//   * bin = digitize(x, edges, right=True) - 1 with the extrema fix-ups and
+//     stable per-bin index lists (bins.py:346-395)                 -> assign/CSR
+//   * per-bin sums behind Mean/Sum/Sum_w/RMS/Dispersion/Abs_*
+//     (profiles/proarray.py:272-334, 632-860)                      -> moments
+//
+// All state of one profile lives in HBM behind an opaque handle; only the
+// O(nbins) results and, on request, the CSR travel back to the host.
+//
+// Building blocks (one tile = 256 threads x 16 items = 4096 elements):
+//   * stable LSD radix pass (8-bit digits): per-tile digit histogram,
+//     global exclusive scan over [digit][tile], stable scatter whose
+//     in-tile ranks come from wave ballots (the 64-lane "peer mask" of
+//     equal digits) -> the CSR is exactly numpy's stable argsort grouping.
+//   * stream compaction with the same ballot ranks (order preserving).
+//   * per-bin sums accumulated with LDS ds_add_f64 per tile, then a
+//     fixed-order reduction over tiles.
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "pbx_common.h"
+
+namespace pbx {
+namespace prof {
+
+constexpr int TPB = 256;
+constexpr int NWAVE = TPB / 64;
+constexpr int IPT = 16;
+constexpr int TILE = TPB * IPT;
+constexpr int RADIX = 256;
+constexpr int NMOM = 7;          // Σw, Σfw, Σf²w, Σf, Σf², Σ|f|w, Σ|f|
+constexpr int MAX_FAM = 16;
+constexpr int LDS_EDGES = 4096;  // edges held in LDS up to this many
+constexpr int LDS_MOM_BINS = 800;
+
+// ----------------------------------------------------------------- keys
+// Order-preserving u64 key of a double in numpy's sort order: NaN last
+// (all NaNs equal), -0.0 == +0.0.
+__host__ __device__ inline uint64_t dkey(double v) {
+  if (v != v) return ~0ull;
+  if (v == 0.0) v = 0.0;
+  uint64_t b = __builtin_bit_cast(uint64_t, v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__host__ __device__ inline double dkey_inv(uint64_t k) {
+  uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __builtin_bit_cast(double, b);
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// number of set bits of m in lanes below this lane
+__device__ __forceinline__ uint32_t rank_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// lanes (of `valid`) whose 8-bit digit equals this lane's
+__device__ __forceinline__ uint64_t peers8(uint32_t d, uint64_t valid) {
+  uint64_t m = valid;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    uint64_t bal = __ballot((d >> b) & 1u);
+    m &= ((d >> b) & 1u) ? bal : ~bal;
+  }
+  return m;
+}
+
+// ----------------------------------------------------------------- scans
+__device__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds_wave, uint32_t *total) {
+  const uint32_t lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) lds_wave[w] = x;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NWAVE; ++k) {
+    uint32_t s = lds_wave[k];
+    off += (k < w) ? s : 0u;
+    tot += s;
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return off + x - v;
+}
+
+// per-tile sums of `in` (len elements)
+__global__ void __launch_bounds__(TPB) scan_tile_sums(const uint32_t *__restrict__ in, int64_t len,
+                                                      uint32_t *__restrict__ sums) {
+  __shared__ uint32_t wsum[NWAVE];
+  int64_t base = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * IPT;
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) s += (base + k < len) ? in[base + k] : 0u;
+  uint32_t tot;
+  block_excl_scan(s, wsum, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// exclusive scan of `in` into `out` (in place allowed), adding tile_off[tile]
+__global__ void __launch_bounds__(TPB) scan_tiles(const uint32_t *in, int64_t len,
+                                                  const uint32_t *__restrict__ tile_off,
+                                                  uint32_t *out) {
+  __shared__ uint32_t wsum[NWAVE];
+  int64_t base = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * IPT;
+  uint32_t v[IPT];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    v[k] = (base + k < len) ? in[base + k] : 0u;
+    s += v[k];
+  }
+  uint32_t run = block_excl_scan(s, wsum, nullptr) + (tile_off ? tile_off[blockIdx.x] : 0u);
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    if (base + k < len) out[base + k] = run;
+    run += v[k];
+  }
+}
+
+// ----------------------------------------------------------------- radix
+template <typename K>
+__global__ void __launch_bounds__(TPB) radix_hist(const K *__restrict__ keys, int64_t n, int shift,
+                                                  uint32_t *__restrict__ hist, uint32_t ntiles) {
+  __shared__ uint32_t cnt[RADIX];
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + k * TPB + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
+}
+
+enum ValMode { VAL_NONE = 0, VAL_IOTA = 1, VAL_ARRAY = 2 };
+
+// Stable scatter of one radix pass.  Element order inside a tile is
+// (wave, iteration, lane) == index order, so ranks from per-wave running
+// counters keep the sort stable.
+template <typename K, int VM>
+__global__ void __launch_bounds__(TPB)
+    radix_scatter(const K *__restrict__ kin, const int32_t *__restrict__ vin, int64_t n, int shift,
+                  const uint32_t *__restrict__ offs, uint32_t ntiles, K *__restrict__ kout,
+                  int32_t *__restrict__ vout) {
+  __shared__ uint32_t run[NWAVE][RADIX];
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
+  __syncthreads();
+  const int64_t wbase = (int64_t)blockIdx.x * TILE + (int64_t)w * (TILE / NWAVE);
+  K key[IPT];
+  // phase 1: per-wave digit counts
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = wbase + k * 64 + lane;
+    bool ok = i < n;
+    key[k] = ok ? kin[i] : (K)0;
+    uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    uint64_t m = peers8(d, __ballot(ok));
+    if (ok && rank_below(m) == 0) run[w][d] += (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  // exclusive prefix over waves + global offset of (digit, tile)
+  {
+    const int d = threadIdx.x;  // TPB == RADIX
+    uint32_t acc = offs[(int64_t)d * ntiles + blockIdx.x];
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) {
+      uint32_t c = run[ww][d];
+      run[ww][d] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  // phase 2: positions
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = wbase + k * 64 + lane;
+    bool ok = i < n;
+    uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    uint64_t m = peers8(d, __ballot(ok));
+    uint32_t r = rank_below(m);
+    uint32_t base = ok ? run[w][d] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (ok && r == 0) run[w][d] = base + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    if (ok) {
+      uint32_t pos = base + r;
+      kout[pos] = key[k];
+      if (VM == VAL_IOTA) vout[pos] = (int32_t)i;
+      if (VM == VAL_ARRAY) vout[pos] = vin[i];
+    }
+  }
+}
+
+// ----------------------------------------------------------------- select
+struct SelectParams {
+  int use_sphere;
+  int ndim;  // 3 -> r, 2 -> rxy
+  int nfam;  // 0 -> no family filter
+  double cx, cy, cz, r2max;
+  int64_t fam_lo[MAX_FAM];
+  int64_t fam_hi[MAX_FAM];
+};
+
+// mask and x of particle i (no FMA contraction: numpy evaluates these as
+// separate multiplies and adds; sqrt is correctly rounded)
+__device__ __forceinline__ bool select_one(const double *__restrict__ pos, int64_t i,
+                                          const SelectParams &p, double &x) {
+#pragma clang fp contract(off)
+  const double px = pos[3 * i + 0], py = pos[3 * i + 1], pz = pos[3 * i + 2];
+  bool keep = true;
+  if (p.nfam > 0) {
+    bool in = false;
+    for (int f = 0; f < p.nfam; ++f) in |= (i >= p.fam_lo[f]) & (i < p.fam_hi[f]);
+    keep = in;
+  }
+  if (p.use_sphere) {
+    double dx = px - p.cx, dy = py - p.cy, dz = pz - p.cz;
+    keep = keep && (((dx * dx + dy * dy) + dz * dz) < p.r2max);
+  }
+  x = (p.ndim == 2) ? __builtin_sqrt(px * px + py * py)
+                    : __builtin_sqrt((px * px + py * py) + pz * pz);
+  return keep;
+}
+
+__global__ void __launch_bounds__(TPB) select_count(const double *__restrict__ pos, int64_t n,
+                                                    SelectParams p, uint32_t *__restrict__ tile_cnt) {
+  __shared__ uint32_t wsum[NWAVE];
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  const int64_t wbase = (int64_t)blockIdx.x * TILE + (int64_t)w * (TILE / NWAVE);
+  uint32_t c = 0;
+#pragma unroll 4
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = wbase + k * 64 + lane;
+    double x;
+    bool keep = (i < n) && select_one(pos, i, p, x);
+    c += keep;
+  }
+  uint32_t tot;
+  block_excl_scan(c, wsum, &tot);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+// writes the kept x, weight, original index in index order; also the key
+// min / max of the kept x (NaN-aware: NaN keys are the maximum key)
+__global__ void __launch_bounds__(TPB)
+    select_write(const double *__restrict__ pos, const double *__restrict__ mass, int64_t n,
+                 SelectParams p, const uint32_t *__restrict__ tile_off, double *__restrict__ xo,
+                 double *__restrict__ wo, int32_t *__restrict__ io,
+                 unsigned long long *__restrict__ minmax) {
+  __shared__ uint32_t wcnt[NWAVE];
+  __shared__ unsigned long long wmin[NWAVE], wmax[NWAVE];
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  const int64_t wbase = (int64_t)blockIdx.x * TILE + (int64_t)w * (TILE / NWAVE);
+  double xv[IPT];
+  uint32_t keepbits = 0, c = 0;
+  unsigned long long kmin = ~0ull, kmax = 0ull;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = wbase + k * 64 + lane;
+    bool keep = (i < n) && select_one(pos, i, p, xv[k]);
+    keepbits |= (uint32_t)keep << k;
+    uint64_t b = __ballot(keep);
+    c += (uint32_t)__popcll(b);
+    if (keep) {
+      unsigned long long kk = dkey(xv[k]);
+      kmin = kk < kmin ? kk : kmin;
+      kmax = kk > kmax ? kk : kmax;
+    }
+  }
+  // wave min / max
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long a = __shfl_xor(kmin, o, 64);
+    unsigned long long b = __shfl_xor(kmax, o, 64);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if (lane == 0) {
+    wcnt[w] = c;
+    wmin[w] = kmin;
+    wmax[w] = kmax;
+  }
+  __syncthreads();
+  uint32_t run = tile_off[blockIdx.x];
+  for (int ww = 0; ww < w; ++ww) run += wcnt[ww];
+  if (threadIdx.x == 0) {
+    unsigned long long a = wmin[0], b = wmax[0];
+    for (int ww = 1; ww < NWAVE; ++ww) {
+      a = wmin[ww] < a ? wmin[ww] : a;
+      b = wmax[ww] > b ? wmax[ww] : b;
+    }
+    if (a != ~0ull) atomicMin(&minmax[0], a);
+    if (b != 0ull) atomicMax(&minmax[1], b);
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    bool keep = (keepbits >> k) & 1u;
+    uint64_t b = __ballot(keep);
+    if (keep) {
+      int64_t i = wbase + k * 64 + lane;
+      uint32_t pos_out = run + rank_below(b);
+      xo[pos_out] = xv[k];
+      if (wo) wo[pos_out] = mass ? mass[i] : 1.0;
+      io[pos_out] = (int32_t)i;
+    }
+    run += (uint32_t)__popcll(b);
+  }
+}
+
+// min / max key of an x array (generic path)
+__global__ void __launch_bounds__(TPB) minmax_keys(const double *__restrict__ x, int64_t n,
+                                                   unsigned long long *__restrict__ minmax) {
+  unsigned long long kmin = ~0ull, kmax = 0ull;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    unsigned long long k = dkey(x[i]);
+    kmin = k < kmin ? k : kmin;
+    kmax = k > kmax ? k : kmax;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long a = __shfl_xor(kmin, o, 64);
+    unsigned long long b = __shfl_xor(kmax, o, 64);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if (lane_id() == 0) {
+    if (kmin != ~0ull) atomicMin(&minmax[0], kmin);
+    if (kmax != 0ull) atomicMax(&minmax[1], kmax);
+  }
+}
+
+__global__ void __launch_bounds__(TPB) make_keys(const double *__restrict__ x, int64_t n,
+                                                 uint64_t *__restrict__ keys) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+    keys[i] = dkey(x[i]);
+}
+
+// In a sorted key array: out[0] = first key >= a, out[1] = first key > b,
+// out[2] = first NaN key (lanes 0..2 each do one binary search).
+__global__ void count_bounds(const uint64_t *__restrict__ keys, int64_t n, uint64_t a, uint64_t b,
+                             int64_t *__restrict__ out) {
+  const int t = threadIdx.x;
+  if (blockIdx.x != 0 || t > 2) return;
+  const uint64_t probe = (t == 0) ? a : (t == 1 ? b : ~0ull);
+  const bool strict = (t == 1);  // first key > probe, else first key >= probe
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    bool left = strict ? (keys[mid] <= probe) : (keys[mid] < probe);
+    if (left) lo = mid + 1; else hi = mid;
+  }
+  out[t] = lo;
+}
+
+__global__ void gather_keys(const uint64_t *__restrict__ keys, const int64_t *__restrict__ ranks,
+                            int64_t m, double *__restrict__ out) {
+  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t < m) out[t] = dkey_inv(keys[ranks[t]]);
+}
+
+// ----------------------------------------------------------------- assign
+// bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
+// x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379)
+__device__ __forceinline__ uint32_t bin_of(double v, const double *e, int nb) {
+  int lo = 0, hi = nb + 1;  // first k with e[k] >= v  (NaN: never -> nb+1)
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (e[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  int b = lo - 1;
+  if (v == e[0]) b = 0;
+  if (v == e[nb]) b = nb - 1;
+  if (v != v) b = nb;  // searchsorted puts NaN past every edge
+  return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
+}
+
+__global__ void __launch_bounds__(TPB)
+    assign_bins(const double *__restrict__ x, int64_t n, const double *__restrict__ edges, int nb,
+                uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double *e = (double *)smem;
+  const bool lds_edges = (nb + 1) <= LDS_EDGES;
+  uint32_t *cnt = (uint32_t *)(smem + (lds_edges ? sizeof(double) * (nb + 1) : 0));
+  if (lds_edges)
+    for (int k = threadIdx.x; k <= nb; k += TPB) e[k] = edges[k];
+  for (int k = threadIdx.x; k <= nb; k += TPB) cnt[k] = 0;
+  __syncthreads();
+  const double *ee = lds_edges ? e : edges;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+#pragma unroll 4
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + k * TPB + threadIdx.x;
+    if (i < n) {
+      uint32_t b = bin_of(x[i], ee, nb);
+      bins[i] = b;
+      atomicAdd(&cnt[b], 1u);
+    }
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < nb; k += TPB)
+    if (cnt[k]) atomicAdd(&counts[k], (unsigned long long)cnt[k]);
+}
+
+// ----------------------------------------------------------------- moments
+template <int WMODE>  // 0: no weights, 1: weights
+__global__ void __launch_bounds__(TPB)
+    moments_kernel(const uint32_t *__restrict__ bins, const double *__restrict__ f,
+                   const double *__restrict__ wt, int64_t n, int nb, double *__restrict__ slab,
+                   double *__restrict__ global_acc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double *acc = (double *)smem;
+  const bool in_lds = nb <= LDS_MOM_BINS;
+  if (in_lds) {
+    for (int k = threadIdx.x; k < nb * NMOM; k += TPB) acc[k] = 0.0;
+    __syncthreads();
+  }
+  double *tgt = in_lds ? acc : global_acc;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+#pragma unroll 4
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + k * TPB + threadIdx.x;
+    if (i >= n) continue;
+    uint32_t b = bins[i];
+    if (b >= (uint32_t)nb) continue;
+    double v = f[i];
+    double a = __builtin_fabs(v);
+    double ww = WMODE ? wt[i] : 1.0;
+    double *t = tgt + (int64_t)b * NMOM;
+    if (WMODE) {
+      atomicAdd(&t[0], ww);
+      atomicAdd(&t[1], v * ww);
+      atomicAdd(&t[2], (v * v) * ww);
+      atomicAdd(&t[5], a * ww);
+    }
+    atomicAdd(&t[3], v);
+    atomicAdd(&t[4], v * v);
+    atomicAdd(&t[6], a);
+  }
+  if (in_lds) {
+    __syncthreads();
+    double *dst = slab + (int64_t)blockIdx.x * nb * NMOM;
+    for (int k = threadIdx.x; k < nb * NMOM; k += TPB) dst[k] = acc[k];
+  }
+}
+
+__global__ void __launch_bounds__(TPB) reduce_slab(const double *__restrict__ slab, int64_t ntiles,
+                                                   int64_t len, double *__restrict__ out) {
+  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t >= len) return;
+  double s = 0.0;
+  for (int64_t b = 0; b < ntiles; ++b) s += slab[b * len + t];
+  out[t] = s;
+}
+
+__global__ void widen_perm(const int32_t *__restrict__ p, int64_t n, int64_t *__restrict__ out) {
+  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t < n) out[t] = p[t];
+}
+
+// ----------------------------------------------------------------- handle
+struct Buf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  void *get(size_t need) {
+    if (need <= bytes) return p;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t want = need < 256 ? 256 : need;
+    PBX_HIP(hipMalloc(&p, want));
+    bytes = want;
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+struct Profile {
+  int device = -1;
+  int64_t n = 0;          // elements in the binned space
+  int64_t nb = -1;        // bins of the last assignment
+  int64_t n_valid = 0;
+  bool has_w = false;
+  bool has_idx = false;
+  bool csr_ready = false;
+  Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
+      field, weight, ranks, bounds;
+};
+
+static inline uint32_t ntiles_of(int64_t n) { return (uint32_t)((n + TILE - 1) / TILE); }
+
+// exclusive scan of len u32 in place (len <= TILE*TILE)
+static void scan_u32(Profile &P, hipStream_t st, uint32_t *a, int64_t len) {
+  if (len <= 0) return;
+  int64_t nt = (len + TILE - 1) / TILE;
+  if (nt == 1) {
+    hipLaunchKernelGGL(scan_tiles, dim3(1), dim3(TPB), 0, st, a, len, nullptr, a);
+  } else {
+    if (nt > TILE) fail(PBX_ERR_VALUE, "scan too long (%lld)", (long long)len);
+    uint32_t *sums = (uint32_t *)P.tsum.get(sizeof(uint32_t) * (size_t)nt);
+    hipLaunchKernelGGL(scan_tile_sums, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, sums);
+    hipLaunchKernelGGL(scan_tiles, dim3(1), dim3(TPB), 0, st, sums, nt, nullptr, sums);
+    hipLaunchKernelGGL(scan_tiles, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, sums, a);
+  }
+  PBX_HIP(hipGetLastError());
+}
+
+// one stable radix pass: kin -> kout (+ values)
+template <typename K>
+static void radix_pass(Profile &P, hipStream_t st, const K *kin, const int32_t *vin, int vm,
+                       int64_t n, int shift, K *kout, int32_t *vout) {
+  uint32_t nt = ntiles_of(n);
+  uint32_t *hist = (uint32_t *)P.hist.get(sizeof(uint32_t) * (size_t)nt * RADIX);
+  hipLaunchKernelGGL(radix_hist<K>, dim3(nt), dim3(TPB), 0, st, kin, n, shift, hist, nt);
+  scan_u32(P, st, hist, (int64_t)nt * RADIX);
+  if (vm == VAL_NONE)
+    hipLaunchKernelGGL((radix_scatter<K, VAL_NONE>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout);
+  else if (vm == VAL_IOTA)
+    hipLaunchKernelGGL((radix_scatter<K, VAL_IOTA>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout);
+  else
+    hipLaunchKernelGGL((radix_scatter<K, VAL_ARRAY>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout);
+  PBX_HIP(hipGetLastError());
+}
+
+static void check_n(int64_t n) {
+  if (n < 0) fail(PBX_ERR_VALUE, "negative length");
+  if (n >= (int64_t)1 << 31) fail(PBX_ERR_VALUE, "profiles are limited to < 2^31 particles");
+}
+
+static Profile &as_profile(void *h) {
+  if (!h) fail(PBX_ERR_VALUE, "null profile handle");
+  Profile *p = (Profile *)h;
+  int dev = current_device().id;
+  if (p->device != dev) fail(PBX_ERR_VALUE, "profile belongs to device %d", p->device);
+  return *p;
+}
+
+}  // namespace prof
+}  // namespace pbx
+
+using namespace pbx;
+using namespace pbx::prof;
+
+extern "C" {
+
+int pbx_profile_create(void **handle) {
+  return guard([&] {
+    Device &d = current_device();
+    Profile *p = new Profile();
+    p->device = d.id;
+    *handle = p;
+  });
+}
+
+int pbx_profile_destroy(void *handle) {
+  return guard([&] {
+    if (!handle) return;
+    Profile *p = (Profile *)handle;
+    current_device();
+    Buf *all[] = {&p->x, &p->w, &p->idx, &p->bins, &p->perm, &p->keys0, &p->keys1, &p->vtmp,
+                  &p->hist, &p->tsum, &p->edges, &p->counts, &p->minmax, &p->slab, &p->acc,
+                  &p->field, &p->weight, &p->ranks, &p->bounds};
+    for (Buf *b : all) b->release();
+    delete p;
+  });
+}
+
+int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    check_n(n);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    double *x = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
+    if (n) PBX_HIP(hipMemcpyAsync(x, h_x, sizeof(double) * n, hipMemcpyHostToDevice, d.stream));
+    P.n = n;
+    P.has_w = false;
+    P.has_idx = false;
+    P.csr_ready = false;
+    P.nb = -1;
+  });
+}
+
+int pbx_profile_select(void *handle, const double *pos, const double *mass, int64_t n,
+                       int on_device, int use_sphere, const double *sphere, const int64_t *fam,
+                       int nfam, int ndim, int64_t *n_kept) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    check_n(n);
+    if (ndim != 2 && ndim != 3) fail(PBX_ERR_VALUE, "ndim must be either 2 or 3");
+    if (nfam < 0 || nfam > MAX_FAM) fail(PBX_ERR_VALUE, "at most %d family ranges", MAX_FAM);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.select");
+    SelectParams sp{};
+    sp.use_sphere = use_sphere;
+    sp.ndim = ndim;
+    sp.nfam = nfam;
+    if (use_sphere) {
+      sp.cx = sphere[0];
+      sp.cy = sphere[1];
+      sp.cz = sphere[2];
+      sp.r2max = sphere[3];
+    }
+    for (int f = 0; f < nfam; ++f) {
+      sp.fam_lo[f] = fam[2 * f];
+      sp.fam_hi[f] = fam[2 * f + 1];
+    }
+    const double *d_pos = pos, *d_mass = mass;
+    if (!on_device && n) {
+      double *tp = (double *)P.keys0.get(sizeof(double) * 3 * (size_t)n);
+      PBX_HIP(hipMemcpyAsync(tp, pos, sizeof(double) * 3 * n, hipMemcpyHostToDevice, st));
+      d_pos = tp;
+      if (mass) {
+        double *tm2 = (double *)P.keys1.get(sizeof(double) * (size_t)n);
+        PBX_HIP(hipMemcpyAsync(tm2, mass, sizeof(double) * n, hipMemcpyHostToDevice, st));
+        d_mass = tm2;
+      }
+    }
+    uint32_t nt = ntiles_of(n);
+    // tile counts live in the (idle) radix histogram buffer; scan_u32 uses
+    // P.tsum as its own scratch
+    uint32_t *tc = (uint32_t *)P.hist.get(sizeof(uint32_t) * (size_t)(nt + 1));
+    double *xo = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
+    double *wo = (double *)P.w.get(sizeof(double) * (size_t)(n ? n : 1));
+    int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(n ? n : 1));
+    unsigned long long *mm = (unsigned long long *)P.minmax.get(16);
+    unsigned long long init[2] = {~0ull, 0ull};
+    PBX_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, st));
+    int64_t kept = 0;
+    if (n) {
+      // tile counts -> exclusive scan (tile offsets) -> order-preserving write
+      hipLaunchKernelGGL(select_count, dim3(nt), dim3(TPB), 0, st, d_pos, n, sp, tc);
+      PBX_HIP(hipGetLastError());
+      uint32_t last = 0;
+      PBX_HIP(hipMemcpyAsync(&last, tc + nt - 1, 4, hipMemcpyDeviceToHost, st));
+      scan_u32(P, st, tc, nt);
+      uint32_t off_last = 0;
+      PBX_HIP(hipMemcpyAsync(&off_last, tc + nt - 1, 4, hipMemcpyDeviceToHost, st));
+      hipLaunchKernelGGL(select_write, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, tc, xo,
+                         wo, io, mm);
+      PBX_HIP(hipGetLastError());
+      PBX_HIP(hipStreamSynchronize(st));
+      kept = (int64_t)off_last + last;
+    }
+    P.n = kept;
+    P.has_w = true;
+    P.has_idx = true;
+    P.csr_ready = false;
+    P.nb = -1;
+    *n_kept = kept;
+  });
+}
+
+int pbx_profile_get_selection(void *handle, int64_t *h_idx, double *h_x, double *h_w) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    if (!P.has_idx) fail(PBX_ERR_VALUE, "profile has no selection");
+    const int64_t n = P.n;
+    if (n == 0) return;
+    if (h_idx) {
+      int64_t *tmp = (int64_t *)P.vtmp.get(sizeof(int64_t) * (size_t)n);
+      hipLaunchKernelGGL(widen_perm, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st,
+                         (const int32_t *)P.idx.p, n, tmp);
+      PBX_HIP(hipMemcpyAsync(h_idx, tmp, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+    }
+    if (h_x) PBX_HIP(hipMemcpyAsync(h_x, P.x.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    if (h_w && P.has_w)
+      PBX_HIP(hipMemcpyAsync(h_w, P.w.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+  });
+}
+
+// np.min / np.max of x (NaN propagates to both, like numpy)
+int pbx_profile_minmax(void *handle, double *mn, double *mx) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    if (P.n == 0) fail(PBX_ERR_VALUE, "zero-size array to reduction operation minimum which has no identity");
+    unsigned long long *mm = (unsigned long long *)P.minmax.get(16);
+    unsigned long long h[2] = {~0ull, 0ull};
+    PBX_HIP(hipMemcpyAsync(mm, h, 16, hipMemcpyHostToDevice, st));
+    unsigned grid = (unsigned)std::min<int64_t>(2048, (P.n + TPB - 1) / TPB);
+    hipLaunchKernelGGL(minmax_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, P.n, mm);
+    PBX_HIP(hipGetLastError());
+    PBX_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    double lo = dkey_inv(h[0]), hi = dkey_inv(h[1]);
+    if (hi != hi) lo = hi;  // any NaN -> both NaN
+    *mn = lo;
+    *mx = hi;
+  });
+}
+
+// equaln edges (bins.py:720-746): order statistics of the x values inside
+// [bin_min, bin_max]; returns the number of edges written (nbins+1, or 2
+// for the degenerate < 2 case; 0 with status VALUE for empty input).
+int pbx_profile_edges_equaln(void *handle, int64_t nbins, int has_min, double bin_min,
+                             int has_max, double bin_max, double *h_edges, int64_t *n_edges) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (nbins < 1) fail(PBX_ERR_VALUE, "nbins must be >= 1");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.equaln");
+    const int64_t n = P.n;
+    if (n == 0) fail(PBX_ERR_VALUE, "Cannot create bins: input array is empty");
+    uint64_t *k0 = (uint64_t *)P.keys0.get(sizeof(uint64_t) * (size_t)n);
+    uint64_t *k1 = (uint64_t *)P.keys1.get(sizeof(uint64_t) * (size_t)n);
+    unsigned grid = (unsigned)std::min<int64_t>(4096, (n + TPB - 1) / TPB);
+    hipLaunchKernelGGL(make_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n, k0);
+    PBX_HIP(hipGetLastError());
+    // only the bits where min and max keys differ need sorting
+    unsigned long long *mm = (unsigned long long *)P.minmax.get(16);
+    unsigned long long h[2] = {~0ull, 0ull};
+    PBX_HIP(hipMemcpyAsync(mm, h, 16, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(minmax_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n, mm);
+    PBX_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    uint64_t diff = h[0] ^ h[1];
+    int hb = diff ? 63 - __builtin_clzll(diff) : -1;
+    uint64_t *a = k0, *b = k1;
+    for (int shift = 0; shift <= hb; shift += 8) {
+      radix_pass<uint64_t>(P, st, a, nullptr, VAL_NONE, n, shift, b, nullptr);
+      std::swap(a, b);
+    }
+    // clip window [lo, hi) of the sorted keys: sorted_x[sorted_x >= bin_min]
+    // then [sorted_x <= bin_max] (bins.py:734-737).  A NaN x fails both
+    // comparisons and NaN keys sort last; a NaN bound keeps nothing.
+    int64_t lo = 0, hi = n;
+    if (has_min || has_max) {
+      uint64_t ka = has_min ? dkey(bin_min) : 0ull;
+      uint64_t kb = has_max ? dkey(bin_max) : ~0ull;
+      int64_t *bd = (int64_t *)P.bounds.get(32);
+      hipLaunchKernelGGL(count_bounds, dim3(1), dim3(64), 0, st, a, n, ka, kb, bd);
+      PBX_HIP(hipGetLastError());
+      int64_t b3[3];
+      PBX_HIP(hipMemcpyAsync(b3, bd, 24, hipMemcpyDeviceToHost, st));
+      PBX_HIP(hipStreamSynchronize(st));
+      hi = b3[2];  // drop the NaN block
+      if (has_min) lo = (bin_min != bin_min) ? hi : b3[0];
+      if (has_max) hi = (bin_max != bin_max) ? lo : std::min<int64_t>(hi, b3[1]);
+      if (hi < lo) hi = lo;
+    }
+    const int64_t m = hi - lo;
+    std::vector<int64_t> ranks;
+    if (m < 2) {
+      if (m == 0) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
+      ranks = {lo, lo};
+    } else {
+      ranks.push_back(lo);
+      for (int64_t i = 1; i < nbins; ++i)
+        ranks.push_back(lo + (int64_t)((double)(i * m) / (double)nbins));
+      ranks.push_back(lo + m - 1);
+    }
+    const int64_t ne = (int64_t)ranks.size();
+    int64_t *dr = (int64_t *)P.ranks.get(sizeof(int64_t) * (size_t)ne);
+    double *de = (double *)P.edges.get(sizeof(double) * (size_t)ne);
+    PBX_HIP(hipMemcpyAsync(dr, ranks.data(), sizeof(int64_t) * ne, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(gather_keys, dim3(ceil_div(ne, TPB)), dim3(TPB), 0, st, a, dr, ne, de);
+    PBX_HIP(hipGetLastError());
+    PBX_HIP(hipMemcpyAsync(h_edges, de, sizeof(double) * ne, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    *n_edges = ne;
+  });
+}
+
+// bins + per-bin counts for explicit edges (ascending); builds the bin ids
+// the CSR and moments use.  counts: nb int64 (host).
+int pbx_profile_assign(void *handle, const double *h_edges, int64_t n_edges, int64_t *h_counts,
+                       int64_t *n_valid) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (n_edges < 2) fail(PBX_ERR_VALUE, "Explicit bin_edges must be a 1D array of length >= 2");
+    const int64_t nb = n_edges - 1;
+    if (nb >= (int64_t)1 << 24) fail(PBX_ERR_VALUE, "too many bins");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.assign");
+    const int64_t n = P.n;
+    double *de = (double *)P.edges.get(sizeof(double) * (size_t)n_edges);
+    PBX_HIP(hipMemcpyAsync(de, h_edges, sizeof(double) * n_edges, hipMemcpyHostToDevice, st));
+    unsigned long long *cnt = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
+    PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint64_t) * (nb + 1), st));
+    uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n ? n : 1));
+    if (n) {
+      size_t lds = ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
+                   sizeof(uint32_t) * (nb + 1);
+      if (lds > 150 * 1024) fail(PBX_ERR_VALUE, "too many bins for the device histogram (%lld)", (long long)nb);
+      hipLaunchKernelGGL(assign_bins, dim3(ntiles_of(n)), dim3(TPB), lds, st,
+                         (const double *)P.x.p, n, (const double *)de, (int)nb, bins, cnt);
+      PBX_HIP(hipGetLastError());
+    }
+    PBX_HIP(hipMemcpyAsync(h_counts, cnt, sizeof(int64_t) * nb, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    int64_t s = 0;
+    for (int64_t k = 0; k < nb; ++k) s += h_counts[k];
+    P.nb = nb;
+    P.n_valid = s;
+    P.csr_ready = false;
+    *n_valid = s;
+  });
+}
+
+// CSR of the last assignment: perm (n_valid int64, ascending indices inside
+// each bin = the reference's binind lists concatenated) and offsets (nb+1).
+// Either output may be NULL (then the CSR stays on the device only).
+int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (P.nb < 0) fail(PBX_ERR_VALUE, "call pbx_profile_assign first");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.csr");
+    const int64_t n = P.n, nb = P.nb;
+    if (!P.csr_ready && n) {
+      // stable counting sort of the bin ids (nb = dropped) carrying indices
+      int bits = 0;
+      while (((int64_t)1 << bits) <= nb) ++bits;
+      uint32_t *ka = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n);
+      uint32_t *kb = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n);
+      int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n);
+      int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n);
+      const uint32_t *kin = (const uint32_t *)P.bins.p;
+      bool first = true;
+      for (int shift = 0; shift < bits; shift += 8) {
+        if (first) {
+          radix_pass<uint32_t>(P, st, kin, nullptr, VAL_IOTA, n, shift, ka, va);
+          first = false;
+        } else {
+          radix_pass<uint32_t>(P, st, ka, va, VAL_ARRAY, n, shift, kb, vb);
+          std::swap(ka, kb);
+          std::swap(va, vb);
+        }
+      }
+      if ((void *)va != P.perm.p)
+        PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+      P.csr_ready = true;
+    }
+    if (h_offsets) {
+      std::vector<int64_t> c((size_t)nb);
+      PBX_HIP(hipMemcpyAsync(c.data(), P.counts.p, sizeof(int64_t) * nb, hipMemcpyDeviceToHost, st));
+      PBX_HIP(hipStreamSynchronize(st));
+      h_offsets[0] = 0;
+      for (int64_t k = 0; k < nb; ++k) h_offsets[k + 1] = h_offsets[k] + c[(size_t)k];
+    }
+    if (h_perm && P.n_valid) {
+      int64_t *tmp = (int64_t *)P.field.get(sizeof(int64_t) * (size_t)P.n_valid);
+      hipLaunchKernelGGL(widen_perm, dim3(ceil_div(P.n_valid, TPB)), dim3(TPB), 0, st,
+                         (const int32_t *)P.perm.p, P.n_valid, tmp);
+      PBX_HIP(hipMemcpyAsync(h_perm, tmp, sizeof(int64_t) * P.n_valid, hipMemcpyDeviceToHost, st));
+    }
+    PBX_HIP(hipStreamSynchronize(st));
+  });
+}
+
+// Per-bin sums of the last assignment:
+//   out[bin*7 + k], k = Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|
+// f_src / w_src: 0 = the profile's x, 1 = its weights (selection mass),
+// 2 = a host array of n doubles (h_f / h_w); w_src -1 = unweighted (the
+// weighted columns are then left 0).
+int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, const double *h_w,
+                        double *h_out) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (P.nb < 0) fail(PBX_ERR_VALUE, "call pbx_profile_assign first");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.moments");
+    const int64_t n = P.n, nb = P.nb;
+    auto src = [&](int which, const double *hp, Buf &stage) -> const double * {
+      if (which == 0) return (const double *)P.x.p;
+      if (which == 1) {
+        if (!P.has_w) fail(PBX_ERR_VALUE, "profile has no selection weights");
+        return (const double *)P.w.p;
+      }
+      if (which == 2) {
+        if (!hp && n) fail(PBX_ERR_VALUE, "host array is NULL");
+        double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
+        if (n) PBX_HIP(hipMemcpyAsync(dp, hp, sizeof(double) * n, hipMemcpyHostToDevice, st));
+        return dp;
+      }
+      fail(PBX_ERR_VALUE, "bad source selector %d", which);
+    };
+    const double *f = src(f_src, h_f, P.field);
+    const double *w = (w_src < 0) ? nullptr : src(w_src, h_w, P.weight);
+    const int64_t len = nb * NMOM;
+    double *acc = (double *)P.acc.get(sizeof(double) * (size_t)len);
+    PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * len, st));
+    if (n && nb > 0) {
+      uint32_t nt = ntiles_of(n);
+      const bool in_lds = nb <= LDS_MOM_BINS;
+      double *slab = in_lds ? (double *)P.slab.get(sizeof(double) * (size_t)nt * len) : nullptr;
+      size_t lds = in_lds ? sizeof(double) * (size_t)len : 0;
+      if (w)
+        hipLaunchKernelGGL(moments_kernel<1>, dim3(nt), dim3(TPB), lds, st,
+                           (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab, acc);
+      else
+        hipLaunchKernelGGL(moments_kernel<0>, dim3(nt), dim3(TPB), lds, st,
+                           (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab, acc);
+      PBX_HIP(hipGetLastError());
+      if (in_lds) {
+        hipLaunchKernelGGL(reduce_slab, dim3(ceil_div(len, TPB)), dim3(TPB), 0, st, slab,
+                           (int64_t)nt, len, acc);
+        PBX_HIP(hipGetLastError());
+      }
+    }
+    PBX_HIP(hipMemcpyAsync(h_out, acc, sizeof(double) * len, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+  });
+}
+
+}  // extern "C"

@@ -76,6 +76,18 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_pack_sources": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "pbx_direct_dev": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                c_int64, c_int, c_int, c_void_p, c_void_p]),
+    "pbx_profile_create": (c_int, [POINTER(c_void_p)]),
+    "pbx_profile_destroy": (c_int, [c_void_p]),
+    "pbx_profile_set_x": (c_int, [c_void_p, _dp, c_int64]),
+    "pbx_profile_select": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, _dp, _i64p,
+                                   c_int, c_int, _i64p]),
+    "pbx_profile_get_selection": (c_int, [c_void_p, _i64p, _dp, _dp]),
+    "pbx_profile_minmax": (c_int, [c_void_p, _dp, _dp]),
+    "pbx_profile_edges_equaln": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double, _dp,
+                                         _i64p]),
+    "pbx_profile_assign": (c_int, [c_void_p, _dp, c_int64, _i64p, _i64p]),
+    "pbx_profile_csr": (c_int, [c_void_p, _i64p, _i64p]),
+    "pbx_profile_moments": (c_int, [c_void_p, c_int, _dp, c_int, _dp, _dp]),
     "pbx_comm_unique_id_size": (c_int, []),
     "pbx_comm_unique_id": (c_int, [c_char_p, c_int]),
     "pbx_comm_init": (c_int, [POINTER(c_void_p), c_int, c_int, c_char_p]),

@@ -1,0 +1,189 @@
+"""Device state of one binning (libpbx profile handle, HBM-resident).
+
+Thin ctypes wrapper of the pbx_profile_* entry points (include/pbx.h):
+the binned quantity x (and, after a fused selection, the selection mass
+and original indices) stays in HBM; edges, counts, CSR and per-bin sums are
+computed by the HIP kernels of csrc/profile.hip.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_double, c_int64, c_void_p
+
+import numpy as np
+
+from .. import _native as nat
+
+NMOM = 7  # Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|
+SRC_X, SRC_W, SRC_HOST, SRC_NONE = 0, 1, 2, -1
+
+_i64p = ctypes.POINTER(c_int64)
+
+
+def _i64(a: np.ndarray):
+    return a.ctypes.data_as(_i64p)
+
+
+class DeviceBins:
+    """One binned quantity on the GPU and the results derived from it."""
+
+    def __init__(self):
+        h = c_void_p()
+        nat.call("pbx_profile_create", byref(h))
+        self._h = h
+        self.n = 0
+        self.nbins = None
+        self.n_valid = 0
+        self.has_selection = False
+        self._csr = None
+
+    # -- construction -------------------------------------------------------
+    @classmethod
+    def from_x(cls, x) -> "DeviceBins":
+        d = cls()
+        d.set_x(x)
+        return d
+
+    def set_x(self, x) -> None:
+        a = np.ascontiguousarray(np.asarray(x), dtype=np.float64).reshape(-1)
+        nat.call("pbx_profile_set_x", self._h, nat.dptr(a), a.shape[0])
+        self.n = a.shape[0]
+        self.has_selection = False
+        self.nbins = None
+        self._csr = None
+
+    @classmethod
+    def select(cls, pos, mass=None, *, sphere=None, families=None, ndim: int = 3,
+               on_device: bool = False, n: int | None = None) -> "DeviceBins":
+        """Fused mask + x + compaction.
+
+        pos / mass: host (N,3) / (N,) float64 arrays, or device pointers
+        (``on_device=True``, then ``n`` is required).  sphere: (cen, radius)
+        or None.  families: list of (start, stop) index ranges or None.
+        """
+        d = cls()
+        if on_device:
+            p_pos, p_mass, n_part = pos, mass, int(n)
+            keep = ()
+        else:
+            pos = np.ascontiguousarray(pos, dtype=np.float64)
+            if pos.ndim != 2 or pos.shape[1] != 3:
+                raise ValueError("pos must be (N,3)")
+            n_part = pos.shape[0]
+            mass = None if mass is None else np.ascontiguousarray(mass, dtype=np.float64)
+            p_pos = pos.ctypes.data_as(c_void_p)
+            p_mass = None if mass is None else mass.ctypes.data_as(c_void_p)
+            keep = (pos, mass)  # noqa: F841 - keep alive during the call
+        sph = np.zeros(4)
+        if sphere is not None:
+            cen, radius = sphere
+            radius = float(radius)
+            sph[:3] = np.asarray(cen, dtype=np.float64).reshape(3)
+            sph[3] = radius * radius
+        fam = np.zeros(2, dtype=np.int64)
+        nfam = 0
+        if families is not None:
+            fam = np.ascontiguousarray(np.asarray(families, dtype=np.int64).reshape(-1, 2))
+            nfam = fam.shape[0]
+            if nfam == 0:  # an empty family set keeps nothing
+                fam = np.array([[0, 0]], dtype=np.int64)
+                nfam = 1
+        kept = c_int64(0)
+        nat.call("pbx_profile_select", d._h, p_pos, p_mass, n_part, int(on_device),
+                 int(sphere is not None), nat.dptr(sph), _i64(fam), nfam, int(ndim), byref(kept))
+        del keep
+        d.n = kept.value
+        d.has_selection = True
+        return d
+
+    def selection(self, idx=True, x=True, w=True):
+        """(original indices int64, x, weights) of the fused selection."""
+        oi = np.empty(self.n, dtype=np.int64) if idx else None
+        ox = np.empty(self.n) if x else None
+        ow = np.empty(self.n) if w else None
+        nat.call("pbx_profile_get_selection", self._h, None if oi is None else _i64(oi),
+                 nat.dptr(ox), nat.dptr(ow))
+        return oi, ox, ow
+
+    # -- edges --------------------------------------------------------------
+    def minmax(self) -> tuple[float, float]:
+        lo, hi = c_double(), c_double()
+        nat.call("pbx_profile_minmax", self._h, byref(lo), byref(hi))
+        return lo.value, hi.value
+
+    def edges_equaln(self, nbins: int, bin_min=None, bin_max=None) -> np.ndarray:
+        out = np.empty(int(nbins) + 1)
+        ne = c_int64(0)
+        try:
+            nat.call("pbx_profile_edges_equaln", self._h, int(nbins), int(bin_min is not None),
+                     float(bin_min) if bin_min is not None else 0.0, int(bin_max is not None),
+                     float(bin_max) if bin_max is not None else 0.0, nat.dptr(out), byref(ne))
+        except ValueError as e:
+            if str(e).startswith("index 0 is out of bounds"):
+                raise IndexError(str(e)) from None
+            raise
+        return out[: ne.value].copy()
+
+    # -- assignment ---------------------------------------------------------
+    def assign(self, edges) -> np.ndarray:
+        e = np.ascontiguousarray(np.asarray(edges), dtype=np.float64).reshape(-1)
+        nb = e.shape[0] - 1
+        counts = np.zeros(max(nb, 0), dtype=np.int64)
+        nv = c_int64(0)
+        nat.call("pbx_profile_assign", self._h, nat.dptr(e), e.shape[0], _i64(counts), byref(nv))
+        self.nbins = nb
+        self.n_valid = nv.value
+        self._csr = None
+        self.counts = counts
+        return counts
+
+    def csr(self) -> tuple[np.ndarray, np.ndarray]:
+        """(perm, offsets): the per-bin ascending index lists, concatenated."""
+        if self._csr is None:
+            perm = np.empty(self.n_valid, dtype=np.int64)
+            offs = np.empty(self.nbins + 1, dtype=np.int64)
+            nat.call("pbx_profile_csr", self._h, _i64(perm), _i64(offs))
+            self._csr = (perm, offs)
+        return self._csr
+
+    def build_csr_on_device(self) -> None:
+        """Build the CSR in HBM without downloading it."""
+        nat.call("pbx_profile_csr", self._h, None, None)
+
+    # -- reductions ---------------------------------------------------------
+    def moments(self, field=SRC_X, weights=SRC_NONE) -> np.ndarray:
+        """Per-bin sums (nbins, 7): Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|.
+
+        field / weights: SRC_X, SRC_W (selection mass), a host array of
+        length n, or (weights only) SRC_NONE.
+        """
+        if self.nbins is None:
+            raise ValueError("assign() first")
+
+        def src(v):
+            if isinstance(v, (int, np.integer)) and not isinstance(v, bool):
+                return int(v), None
+            a = np.ascontiguousarray(np.asarray(v), dtype=np.float64).reshape(-1)
+            if a.shape[0] != self.n:
+                raise ValueError(f"array length {a.shape[0]} != {self.n}")
+            return SRC_HOST, a
+
+        fs, fa = src(field)
+        ws, wa = src(weights) if weights is not None else (SRC_NONE, None)
+        out = np.zeros((self.nbins, NMOM))
+        nat.call("pbx_profile_moments", self._h, fs, nat.dptr(fa), ws, nat.dptr(wa), nat.dptr(out))
+        return out
+
+    def close(self) -> None:
+        if self._h is not None and self._h.value and nat._lib is not None:
+            try:
+                nat.call("pbx_profile_destroy", self._h)
+            except Exception:
+                pass
+        self._h = c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
