@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="skip the radial-profile leg (config 3)")
+    ap.add_argument("--profile-sizes", default="1000000,16000000,64000000",
+                    help="comma-separated particle counts of the profile size sweep")
     return ap.parse_args()
 
 
@@ -123,6 +127,80 @@ def cpu_baseline(pos, mass, seconds: float):
         "sample": f"{k} random targets x {n} sources (all-particles Newtonian force+potential, "
                   f"oracle/gravity_ref.c, OpenMP {cores} threads, {dt:.1f} s)",
     }
+
+
+PROFILE_BYTES_PER_PARTICLE = 49  # equaln profile, algorithmic HBM bytes / input particle
+HBM_PEAK_GBS = 8000.0
+
+
+def bench_profile(sizes, steps: int, warmup: int, cpu: bool):
+    """Config 3: RadialProfileBuilder(ndim=3, weight='mass', equaln, 128 bins)
+    behind Sphere(R=10) & FamilyFilter('dm'), positions / masses resident in
+    HBM.  One step = fused select (mask + r + compaction) -> equaln edges ->
+    bin assignment + counts -> CSR (binind) built in HBM -> per-bin Σ mass and
+    mass-weighted <r>.  particles/s counts every INPUT particle."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X, DeviceBins
+    from pynbodyext.synthetic import family_slices
+
+    out = []
+    for n in sizes:
+        pos, mass = plummer(n, seed=SEEDS.get(n, 1002))
+        dm = family_slices(n)["dm"]
+        d_pos = nat.DeviceArray.from_host(pos)
+        d_mass = nat.DeviceArray.from_host(mass)
+        dev = DeviceBins()
+        e0, e1 = nat.Event(), nat.Event()
+
+        def step():
+            DeviceBins.select(d_pos.ptr, d_mass.ptr, sphere=((0.0, 0.0, 0.0), 10.0),
+                              families=[(dm.start, dm.stop)], ndim=3, on_device=True, n=n, into=dev)
+            edges = dev.edges_equaln(128)
+            dev.assign(edges)
+            dev.build_csr_on_device()
+            msum = dev.moments(SRC_W, SRC_NONE)[:, 3]
+            rmean = dev.moments(SRC_X, SRC_W)
+            return edges, msum, rmean
+
+        for _ in range(warmup):
+            step()
+        nat.synchronize()
+        times, dev_ms = [], []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            e0.record()
+            res = step()
+            e1.record()
+            nat.synchronize()
+            times.append(time.perf_counter() - t0)
+            dev_ms.append(e0.elapsed_ms(e1))
+        t = float(np.median(times))
+        td = float(np.median(dev_ms)) * 1e-3
+        row = {"n": n, "n_kept": dev.n, "ms": t * 1e3, "particles_per_s": n / t,
+               "hbm_gbs_algorithmic": n * PROFILE_BYTES_PER_PARTICLE / td / 1e9,
+               "stream_ms": td * 1e3}
+        out.append(row)
+        if cpu and n == sizes[0]:
+            from oracle import profile_ref as pr
+
+            mask = pr.sphere_mask(pos, 10.0)
+            mask[dm.stop:] = False
+            t0 = time.perf_counter()
+            ref = pr.radial_profile(pos, mass, mask, "equaln", 128)
+            tc = time.perf_counter() - t0
+            row["cpu_baseline"] = {
+                "value": n / tc, "unit": "particles/s", "cores": 1, "kind": "port",
+                "sample": f"full {n}-particle workload, oracle/profile_ref.py (numpy restatement "
+                          f"of bins.py/proarray.py), 1 thread, {tc:.3f} s"}
+            edges, msum, _ = res
+            row["parity_vs_oracle"] = {
+                "edges_bit_exact": bool(np.array_equal(edges, ref["edges"])),
+                "counts_bit_exact": bool(np.array_equal(dev.counts, ref["counts"])),
+                "mass_sum_max_rel": float(np.nanmax(np.abs(msum - ref["mass_sum"]) /
+                                                    np.abs(ref["mass_sum"])))}
+        dev.close()
+        d_pos.free()
+        d_mass.free()
+    return out
 
 
 def pmc_traffic():
@@ -236,6 +314,28 @@ def main():
         },
         "cpu_baseline": cpu,
     }
+    if not args.no_profile and world == 1:
+        sizes = [int(s) for s in args.profile_sizes.split(",") if s]
+        sweep = bench_profile(sizes, steps=max(3, args.steps), warmup=1,
+                              cpu=not args.no_cpu_baseline)
+        head = sweep[0]
+        big = max(sweep, key=lambda r: r["hbm_gbs_algorithmic"])
+        out["profile"] = {
+            "metric": "particles/sec (RadialProfileBuilder equaln 128, Sphere&FamilyFilter, "
+                      "weight=mass)",
+            "value": head["particles_per_s"],
+            "unit": "particles/s",
+            "config": {"workload": f"{head['n']}-particle Plummer sphere, Sphere(R=10) & "
+                                   "FamilyFilter('dm'), equaln 128 bins, mass sum + mean r",
+                       "kept": head["n_kept"]},
+            "roofline": {"bound": "hbm", "achieved": big["hbm_gbs_algorithmic"],
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": big["hbm_gbs_algorithmic"] / HBM_PEAK_GBS,
+                         "at_n": big["n"], "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE,
+                         "traffic": None},
+            "sweep": sweep,
+            "cpu_baseline": head.get("cpu_baseline"),
+        }
     print(json.dumps(out), flush=True)
 
 

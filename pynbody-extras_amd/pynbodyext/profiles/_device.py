@@ -54,14 +54,17 @@ class DeviceBins:
 
     @classmethod
     def select(cls, pos, mass=None, *, sphere=None, families=None, ndim: int = 3,
-               on_device: bool = False, n: int | None = None) -> "DeviceBins":
+               on_device: bool = False, n: int | None = None,
+               into: "DeviceBins | None" = None) -> "DeviceBins":
         """Fused mask + x + compaction.
 
         pos / mass: host (N,3) / (N,) float64 arrays, or device pointers
         (``on_device=True``, then ``n`` is required).  sphere: (cen, radius)
         or None.  families: list of (start, stop) index ranges or None.
+        ``into`` reuses an existing handle (and its HBM buffers).
         """
-        d = cls()
+        d = into if into is not None else cls()
+        d.nbins, d._csr = None, None
         if on_device:
             p_pos, p_mass, n_part = pos, mass, int(n)
             keep = ()
