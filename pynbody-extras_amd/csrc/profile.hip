@@ -331,9 +331,11 @@ __global__ void __launch_bounds__(TPB)
   }
 }
 
-// min / max key of an x array (generic path)
+// min / max key of an x array (generic path): grid-stride, block reduce,
+// one atomic pair per block
 __global__ void __launch_bounds__(TPB) minmax_keys(const double *__restrict__ x, int64_t n,
                                                    unsigned long long *__restrict__ minmax) {
+  __shared__ unsigned long long smin[NWAVE], smax[NWAVE];
   unsigned long long kmin = ~0ull, kmax = 0ull;
   for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
     unsigned long long k = dkey(x[i]);
@@ -347,7 +349,17 @@ __global__ void __launch_bounds__(TPB) minmax_keys(const double *__restrict__ x,
     kmin = a < kmin ? a : kmin;
     kmax = b > kmax ? b : kmax;
   }
+  const int w = threadIdx.x >> 6;
   if (lane_id() == 0) {
+    smin[w] = kmin;
+    smax[w] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < NWAVE; ++k) {
+      kmin = smin[k] < kmin ? smin[k] : kmin;
+      kmax = smax[k] > kmax ? smax[k] : kmax;
+    }
     if (kmin != ~0ull) atomicMin(&minmax[0], kmin);
     if (kmax != 0ull) atomicMax(&minmax[1], kmax);
   }
@@ -439,26 +451,28 @@ __global__ void __launch_bounds__(TPB)
     __syncthreads();
   }
   double *tgt = in_lds ? acc : global_acc;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  // grid-stride over tiles: at most gridDim.x slabs to reduce afterwards
+  for (int64_t base = (int64_t)blockIdx.x * TILE; base < n; base += (int64_t)gridDim.x * TILE) {
 #pragma unroll 4
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + k * TPB + threadIdx.x;
-    if (i >= n) continue;
-    uint32_t b = bins[i];
-    if (b >= (uint32_t)nb) continue;
-    double v = f[i];
-    double a = __builtin_fabs(v);
-    double ww = WMODE ? wt[i] : 1.0;
-    double *t = tgt + (int64_t)b * NMOM;
-    if (WMODE) {
-      atomicAdd(&t[0], ww);
-      atomicAdd(&t[1], v * ww);
-      atomicAdd(&t[2], (v * v) * ww);
-      atomicAdd(&t[5], a * ww);
+    for (int k = 0; k < IPT; ++k) {
+      int64_t i = base + k * TPB + threadIdx.x;
+      if (i >= n) continue;
+      uint32_t b = bins[i];
+      if (b >= (uint32_t)nb) continue;
+      double v = f[i];
+      double a = __builtin_fabs(v);
+      double ww = WMODE ? wt[i] : 1.0;
+      double *t = tgt + (int64_t)b * NMOM;
+      if (WMODE) {
+        atomicAdd(&t[0], ww);
+        atomicAdd(&t[1], v * ww);
+        atomicAdd(&t[2], (v * v) * ww);
+        atomicAdd(&t[5], a * ww);
+      }
+      atomicAdd(&t[3], v);
+      atomicAdd(&t[4], v * v);
+      atomicAdd(&t[6], a);
     }
-    atomicAdd(&t[3], v);
-    atomicAdd(&t[4], v * v);
-    atomicAdd(&t[6], a);
   }
   if (in_lds) {
     __syncthreads();
@@ -467,13 +481,25 @@ __global__ void __launch_bounds__(TPB)
   }
 }
 
+// Sum slab[tile][len] over tiles in a fixed order: each block owns 64
+// outputs, its 4 waves take every 4th tile, then wave partials are added in
+// wave order (deterministic).
 __global__ void __launch_bounds__(TPB) reduce_slab(const double *__restrict__ slab, int64_t ntiles,
                                                    int64_t len, double *__restrict__ out) {
-  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (t >= len) return;
+  __shared__ double part[NWAVE][64];
+  const int w = threadIdx.x >> 6;
+  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
   double s = 0.0;
-  for (int64_t b = 0; b < ntiles; ++b) s += slab[b * len + t];
-  out[t] = s;
+  if (col < len)
+    for (int64_t b = w; b < ntiles; b += NWAVE) s += slab[b * len + col];
+  part[w][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (w == 0 && col < len) {
+    double t = part[0][threadIdx.x];
+#pragma unroll
+    for (int k = 1; k < NWAVE; ++k) t += part[k][threadIdx.x];
+    out[col] = t;
+  }
 }
 
 __global__ void widen_perm(const int32_t *__restrict__ p, int64_t n, int64_t *__restrict__ out) {
@@ -510,6 +536,8 @@ struct Profile {
   bool has_w = false;
   bool has_idx = false;
   bool csr_ready = false;
+  bool mm_valid = false;   // mm = min / max key of x, cached on the host
+  uint64_t mm[2] = {0, 0};
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
 };
@@ -555,6 +583,28 @@ static void radix_pass(Profile &P, hipStream_t st, const K *kin, const int32_t *
 static void check_n(int64_t n) {
   if (n < 0) fail(PBX_ERR_VALUE, "negative length");
   if (n >= (int64_t)1 << 31) fail(PBX_ERR_VALUE, "profiles are limited to < 2^31 particles");
+}
+
+// min / max key of the current x (cached: the fused selection produces it
+// for free; otherwise one grid-stride reduction)
+static void minmax_of(Profile &P, hipStream_t st, uint64_t out[2]) {
+  if (!P.mm_valid) {
+    unsigned long long *mm = (unsigned long long *)P.minmax.get(16);
+    unsigned long long h[2] = {~0ull, 0ull};
+    PBX_HIP(hipMemcpyAsync(mm, h, 16, hipMemcpyHostToDevice, st));
+    if (P.n) {
+      unsigned grid = (unsigned)std::min<int64_t>(1024, (P.n + TPB - 1) / TPB);
+      hipLaunchKernelGGL(minmax_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, P.n, mm);
+      PBX_HIP(hipGetLastError());
+    }
+    PBX_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    P.mm[0] = h[0];
+    P.mm[1] = h[1];
+    P.mm_valid = true;
+  }
+  out[0] = P.mm[0];
+  out[1] = P.mm[1];
 }
 
 static Profile &as_profile(void *h) {
@@ -607,6 +657,7 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
     P.has_w = false;
     P.has_idx = false;
     P.csr_ready = false;
+    P.mm_valid = false;
     P.nb = -1;
   });
 }
@@ -671,9 +722,14 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
       hipLaunchKernelGGL(select_write, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, tc, xo,
                          wo, io, mm);
       PBX_HIP(hipGetLastError());
+      unsigned long long hm[2];
+      PBX_HIP(hipMemcpyAsync(hm, mm, 16, hipMemcpyDeviceToHost, st));
       PBX_HIP(hipStreamSynchronize(st));
       kept = (int64_t)off_last + last;
+      P.mm[0] = hm[0];
+      P.mm[1] = hm[1];
     }
+    P.mm_valid = true;
     P.n = kept;
     P.has_w = true;
     P.has_idx = true;
@@ -713,14 +769,8 @@ int pbx_profile_minmax(void *handle, double *mn, double *mx) {
     std::lock_guard<std::mutex> lk(d.mu);
     hipStream_t st = d.stream;
     if (P.n == 0) fail(PBX_ERR_VALUE, "zero-size array to reduction operation minimum which has no identity");
-    unsigned long long *mm = (unsigned long long *)P.minmax.get(16);
-    unsigned long long h[2] = {~0ull, 0ull};
-    PBX_HIP(hipMemcpyAsync(mm, h, 16, hipMemcpyHostToDevice, st));
-    unsigned grid = (unsigned)std::min<int64_t>(2048, (P.n + TPB - 1) / TPB);
-    hipLaunchKernelGGL(minmax_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, P.n, mm);
-    PBX_HIP(hipGetLastError());
-    PBX_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
-    PBX_HIP(hipStreamSynchronize(st));
+    uint64_t h[2];
+    minmax_of(P, st, h);
     double lo = dkey_inv(h[0]), hi = dkey_inv(h[1]);
     if (hi != hi) lo = hi;  // any NaN -> both NaN
     *mn = lo;
@@ -748,12 +798,8 @@ int pbx_profile_edges_equaln(void *handle, int64_t nbins, int has_min, double bi
     hipLaunchKernelGGL(make_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n, k0);
     PBX_HIP(hipGetLastError());
     // only the bits where min and max keys differ need sorting
-    unsigned long long *mm = (unsigned long long *)P.minmax.get(16);
-    unsigned long long h[2] = {~0ull, 0ull};
-    PBX_HIP(hipMemcpyAsync(mm, h, 16, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(minmax_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n, mm);
-    PBX_HIP(hipMemcpyAsync(h, mm, 16, hipMemcpyDeviceToHost, st));
-    PBX_HIP(hipStreamSynchronize(st));
+    uint64_t h[2];
+    minmax_of(P, st, h);
     uint64_t diff = h[0] ^ h[1];
     int hb = diff ? 63 - __builtin_clzll(diff) : -1;
     uint64_t *a = k0, *b = k1;
@@ -928,7 +974,8 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, c
     double *acc = (double *)P.acc.get(sizeof(double) * (size_t)len);
     PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * len, st));
     if (n && nb > 0) {
-      uint32_t nt = ntiles_of(n);
+      // <= 512 resident blocks (2 per CU) stride over the tiles
+      uint32_t nt = std::min<uint32_t>(ntiles_of(n), 512u);
       const bool in_lds = nb <= LDS_MOM_BINS;
       double *slab = in_lds ? (double *)P.slab.get(sizeof(double) * (size_t)nt * len) : nullptr;
       size_t lds = in_lds ? sizeof(double) * (size_t)len : 0;
@@ -940,7 +987,7 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, c
                            (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab, acc);
       PBX_HIP(hipGetLastError());
       if (in_lds) {
-        hipLaunchKernelGGL(reduce_slab, dim3(ceil_div(len, TPB)), dim3(TPB), 0, st, slab,
+        hipLaunchKernelGGL(reduce_slab, dim3(ceil_div(len, 64)), dim3(TPB), 0, st, slab,
                            (int64_t)nt, len, acc);
         PBX_HIP(hipGetLastError());
       }
