@@ -128,6 +128,54 @@ int pbx_direct_dev(const double *d_src, const double *d_src_h, int64_t n_src,
                    double *d_acc);
 
 /* ------------------------------------------------------------------ */
+/* gravity: Barnes-Hut octree                                          */
+/* ------------------------------------------------------------------ */
+/* Replaces the PyO3 class `Octree` (crates/pynbodyext-rust/src/gravity.rs:
+ * 114-445) over crates/gravity/src/tree.rs + multipole.rs.  The tree lives
+ * in HBM behind an opaque handle; it reproduces the reference octree node
+ * for node (root box, octants, split rule, payload order), so the opening
+ * decisions of every target equal the reference's.
+ * pos/masses/softenings/points/outputs are host arrays when on_device == 0,
+ * device arrays when on_device == 1.  kernel: PBX_KERNEL_PLUMMER or
+ * PBX_KERNEL_SPLINE (the PyO3 layer maps None to Plummer, gravity.rs:77-82).
+ * want: PBX_WANT_POT | PBX_WANT_ACC. */
+typedef struct pbx_octree pbx_octree;
+/* Octree::new (gravity.rs:123-226): structure; mass payload iff masses */
+int pbx_octree_create(const double *pos, int64_t n, const double *masses,
+                      const double *softenings, int64_t leaf_capacity,
+                      int multipole_order, int kernel, int on_device,
+                      pbx_octree **out);
+int pbx_octree_destroy(pbx_octree *tree);
+/* build_mass(masses=None) (gravity.rs:228-239): NULL keeps current masses */
+int pbx_octree_build_mass(pbx_octree *tree, const double *masses, int on_device);
+/* set_softenings (gravity.rs:241-258; h_max is not rebuilt, tree.rs:777) */
+int pbx_octree_set_softenings(pbx_octree *tree, const double *softenings, int on_device);
+/* set_kernel (gravity.rs:260-265) */
+int pbx_octree_set_kernel(pbx_octree *tree, int kernel);
+/* compute_potentials / compute_accelerations (gravity.rs:267-346,
+ * tree.rs:1415-1496): every particle, self pair skipped, outputs in the
+ * caller's particle order (pot n, acc n x 3) */
+int pbx_octree_compute(pbx_octree *tree, double theta, int want, double *pot,
+                       double *acc, int on_device);
+/* potentials_at_points / accelerations_at_points (gravity.rs:348-445,
+ * tree.rs:1498-1558): m query points (m x 3), no self skip */
+int pbx_octree_at_points(pbx_octree *tree, const double *points, int64_t m,
+                         double theta, int want, double *pot, double *acc,
+                         int on_device);
+/* out[8] = {n, nodes, levels, has_mass_payload, has_hmax,
+ *           accepted node interactions and leaf pairs of the last walk,
+ *           path words} */
+int pbx_octree_info(pbx_octree *tree, int64_t *out);
+/* Node arrays for parity tests (any pointer may be NULL), node ids in the
+ * device's breadth-first numbering:
+ *   center nodes x 4 {cx, cy, cz, half}; com nodes x 4 {x, y, z, mass};
+ *   hmax nodes; links nodes x 3 {first (-1 for a leaf), next, n_children};
+ *   leaf nodes x 2 {start, count} into perm; perm n (leaf order -> index);
+ *   moments nodes x ncoef(order) (order >= 2). */
+int pbx_octree_export(pbx_octree *tree, double *center, double *com, double *hmax,
+                      int64_t *links, int64_t *leaf, int64_t *perm, double *moments);
+
+/* ------------------------------------------------------------------ */
 /* radial profiles: binning + per-bin reduction                        */
 /* ------------------------------------------------------------------ */
 /* One opaque handle per profile holds the binned quantity x (and, after a

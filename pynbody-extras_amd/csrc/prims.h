@@ -1,0 +1,269 @@
+// prims.h — device primitives shared by the profile and octree engines:
+// wave-ballot ranks, block/tile exclusive scans of u32, and one stable LSD
+// radix pass (8-bit digit) over u32/u64 keys with optional int32 values.
+//
+// One tile = 256 threads x 16 items = 4096 elements.  A radix pass is:
+// per-tile digit histogram -> exclusive scan over [digit][tile] -> stable
+// scatter whose in-tile ranks come from 64-lane "peer masks" of equal
+// digits (the scatter preserves input order within a digit, so a sequence
+// of passes is a stable sort).
+#pragma once
+
+#include <algorithm>
+
+#include "pbx_common.h"
+
+namespace pbx {
+namespace prim {
+
+constexpr int TPB = 256;
+constexpr int NWAVE = TPB / 64;
+constexpr int IPT = 16;
+constexpr int TILE = TPB * IPT;
+constexpr int RADIX = 256;
+
+// Order-preserving u64 key of a double in numpy's sort order: NaN last
+// (all NaNs equal), -0.0 == +0.0.
+__host__ __device__ inline uint64_t dkey(double v) {
+  if (v != v) return ~0ull;
+  if (v == 0.0) v = 0.0;
+  uint64_t b = __builtin_bit_cast(uint64_t, v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__host__ __device__ inline double dkey_inv(uint64_t k) {
+  uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __builtin_bit_cast(double, b);
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// number of set bits of m in lanes below this lane
+__device__ __forceinline__ uint32_t rank_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// lanes (of `valid`) whose 8-bit digit equals this lane's
+__device__ __forceinline__ uint64_t peers8(uint32_t d, uint64_t valid) {
+  uint64_t m = valid;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    uint64_t bal = __ballot((d >> b) & 1u);
+    m &= ((d >> b) & 1u) ? bal : ~bal;
+  }
+  return m;
+}
+
+// exclusive scan of one u32 per thread over the block
+__device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t *lds_wave, uint32_t *total) {
+  const uint32_t lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) lds_wave[w] = x;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NWAVE; ++k) {
+    uint32_t s = lds_wave[k];
+    off += (k < w) ? s : 0u;
+    tot += s;
+  }
+  __syncthreads();
+  if (total) *total = tot;
+  return off + x - v;
+}
+
+namespace {
+
+// per-tile sums of `in` (len elements)
+__global__ void __launch_bounds__(TPB) scan_tile_sums(const uint32_t *__restrict__ in, int64_t len,
+                                                      uint32_t *__restrict__ sums) {
+  __shared__ uint32_t wsum[NWAVE];
+  int64_t base = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * IPT;
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) s += (base + k < len) ? in[base + k] : 0u;
+  uint32_t tot;
+  block_excl_scan(s, wsum, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// exclusive scan of `in` into `out` (in place allowed), adding tile_off[tile]
+__global__ void __launch_bounds__(TPB) scan_tiles(const uint32_t *in, int64_t len,
+                                                  const uint32_t *__restrict__ tile_off,
+                                                  uint32_t *out) {
+  __shared__ uint32_t wsum[NWAVE];
+  int64_t base = (int64_t)blockIdx.x * TILE + (int64_t)threadIdx.x * IPT;
+  uint32_t v[IPT];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    v[k] = (base + k < len) ? in[base + k] : 0u;
+    s += v[k];
+  }
+  uint32_t run = block_excl_scan(s, wsum, nullptr) + (tile_off ? tile_off[blockIdx.x] : 0u);
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    if (base + k < len) out[base + k] = run;
+    run += v[k];
+  }
+}
+
+}  // namespace
+
+template <typename K>
+__global__ void __launch_bounds__(TPB) radix_hist(const K *__restrict__ keys, int64_t n, int shift,
+                                                  uint32_t *__restrict__ hist, uint32_t ntiles) {
+  __shared__ uint32_t cnt[RADIX];
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = base + k * TPB + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
+}
+
+enum ValMode { VAL_NONE = 0, VAL_IOTA = 1, VAL_ARRAY = 2 };
+
+// Stable scatter of one radix pass.  Element order inside a tile is
+// (wave, iteration, lane) == index order, so ranks from per-wave running
+// counters keep the sort stable.
+template <typename K, int VM>
+__global__ void __launch_bounds__(TPB)
+    radix_scatter(const K *__restrict__ kin, const int32_t *__restrict__ vin, int64_t n, int shift,
+                  const uint32_t *__restrict__ offs, uint32_t ntiles, K *__restrict__ kout,
+                  int32_t *__restrict__ vout) {
+  __shared__ uint32_t run[NWAVE][RADIX];
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
+  __syncthreads();
+  const int64_t wbase = (int64_t)blockIdx.x * TILE + (int64_t)w * (TILE / NWAVE);
+  K key[IPT];
+  // phase 1: per-wave digit counts
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = wbase + k * 64 + lane;
+    bool ok = i < n;
+    key[k] = ok ? kin[i] : (K)0;
+    uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    uint64_t m = peers8(d, __ballot(ok));
+    if (ok && rank_below(m) == 0) run[w][d] += (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  // exclusive prefix over waves + global offset of (digit, tile)
+  {
+    const int d = threadIdx.x;  // TPB == RADIX
+    uint32_t acc = offs[(int64_t)d * ntiles + blockIdx.x];
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) {
+      uint32_t c = run[ww][d];
+      run[ww][d] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  // phase 2: positions
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    int64_t i = wbase + k * 64 + lane;
+    bool ok = i < n;
+    uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    uint64_t m = peers8(d, __ballot(ok));
+    uint32_t r = rank_below(m);
+    uint32_t base = ok ? run[w][d] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (ok && r == 0) run[w][d] = base + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    if (ok) {
+      uint32_t pos = base + r;
+      kout[pos] = key[k];
+      if (VM == VAL_IOTA) vout[pos] = (int32_t)i;
+      if (VM == VAL_ARRAY) vout[pos] = vin[i];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host
+// A grow-only device allocation owned by one engine object.
+struct Buf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  void *get(size_t need) {
+    if (need <= bytes) return p;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t want = need < 256 ? 256 : need;
+    PBX_HIP(hipMalloc(&p, want));
+    bytes = want;
+    return p;
+  }
+  template <typename T> T *as() const { return (T *)p; }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+static inline uint32_t ntiles_of(int64_t n) { return (uint32_t)((n + TILE - 1) / TILE); }
+
+// Exclusive scan of len u32 in place, any length (recursive over tile sums).
+// `tsum` holds the per-level tile sums (grown on demand, one region per
+// recursion level).
+static inline void scan_u32(Buf &tsum, hipStream_t st, uint32_t *a, int64_t len,
+                            size_t tsum_off = 0) {
+  if (len <= 0) return;
+  int64_t nt = (len + TILE - 1) / TILE;
+  if (nt == 1) {
+    hipLaunchKernelGGL(scan_tiles, dim3(1), dim3(TPB), 0, st, a, len, nullptr, a);
+  } else {
+    // room for this level's sums plus every deeper level's
+    size_t need = tsum_off + sizeof(uint32_t) * (size_t)(nt + nt / TILE + 64);
+    if (tsum.bytes < need) {
+      if (tsum_off != 0) fail(PBX_ERR_RUNTIME, "scan workspace too small");
+      tsum.get(need);
+    }
+    uint32_t *sums = (uint32_t *)((char *)tsum.p + tsum_off);
+    hipLaunchKernelGGL(scan_tile_sums, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, sums);
+    scan_u32(tsum, st, sums, nt, tsum_off + sizeof(uint32_t) * (size_t)nt);
+    hipLaunchKernelGGL(scan_tiles, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, sums, a);
+  }
+  PBX_HIP(hipGetLastError());
+}
+
+// one stable radix pass: kin -> kout (+ values)
+template <typename K>
+static void radix_pass(Buf &hist_buf, Buf &tsum, hipStream_t st, const K *kin, const int32_t *vin,
+                       int vm, int64_t n, int shift, K *kout, int32_t *vout) {
+  uint32_t nt = ntiles_of(n);
+  uint32_t *hist = (uint32_t *)hist_buf.get(sizeof(uint32_t) * (size_t)nt * RADIX);
+  hipLaunchKernelGGL(radix_hist<K>, dim3(nt), dim3(TPB), 0, st, kin, n, shift, hist, nt);
+  scan_u32(tsum, st, hist, (int64_t)nt * RADIX);
+  if (vm == VAL_NONE)
+    hipLaunchKernelGGL((radix_scatter<K, VAL_NONE>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout);
+  else if (vm == VAL_IOTA)
+    hipLaunchKernelGGL((radix_scatter<K, VAL_IOTA>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout);
+  else
+    hipLaunchKernelGGL((radix_scatter<K, VAL_ARRAY>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout);
+  PBX_HIP(hipGetLastError());
+}
+
+}  // namespace prim
+}  // namespace pbx

@@ -1,0 +1,1428 @@
+// tree.hip — Barnes–Hut octree gravity on gfx950: device build, payloads
+// and a wave-coherent stackless walk.
+//
+// Replaces crates/gravity/src/tree.rs (Octree, Tree3D) and the multipole
+// machinery of crates/gravity/src/multipole.rs behind the C ABI of
+// include/pbx.h (the PyO3 class it replaces is
+// crates/pynbodyext-rust/src/gravity.rs:114-445).
+//
+// Parity contract (DESIGN.md "octree"): the device tree is the reference's
+// tree — same cubic root box (tree.rs:628-654), same `>=`-centre octant
+// rule and child centres c +- half/2 (tree.rs:804-845), same split rule
+// count > leaf_capacity (tree.rs:847-864), leaf particle lists in ascending
+// index order, same BH payload summation order (tree.rs:866-932), same
+// opening test size2 < theta^2 (|com - t|^2 + tiny) with the mul_add of
+// tree.rs:1117 and the h_max guard (tree.rs:56-71), and each target visits
+// the nodes of the reference's DFS in the same order.  Acceptance
+// decisions are therefore identical to the reference; only the arithmetic
+// inside an accepted interaction (v_rsq_f64 + Newton, FMA, recurrence for
+// the derivative tensor, binomial M2M) differs, at the 1e-15 level.
+//
+// Build (all on the device):
+//   1. bounding box (ordered-key atomics), root centre/half on the host
+//      with the reference's expressions;
+//   2. per particle, its octant path through the reference's node centres
+//      (centre updates are the same sequential additions as tree.rs:834-838)
+//      packed 21 levels per u64 word;
+//   3. stable LSD radix sort of the paths (stable => equal paths stay in
+//      index order);
+//   4. level-synchronous split: every node that must split finds its
+//      children's ranges by binary search on the next digit; children are
+//      allocated contiguously (breadth-first ids) and threaded with
+//      first/next links like tree.rs:736-776;
+//   5. leaf lists re-sorted by original index (the Rust Vec order), then
+//      particles are packed as 32-byte records {x, y, z, m} in leaf order;
+//   6. payloads bottom-up level by level: mass/COM, h_max, P2M at the COM
+//      for leaves and M2M (binomial translation) for internal nodes.
+//
+// Walk: one target per lane, 64 spatially adjacent targets per wave.  The
+// wave walks the UNION of its lanes' walks: a wave-uniform node index w
+// (node records and leaf particles are scalar loads), each lane keeps the
+// next node of ITS OWN reference walk in p and is active at w iff p == w.
+// After an internal node the wave descends iff some active lane opened it.
+// Every lane therefore sees exactly its own sequence of nodes, in the
+// reference's order, and makes the reference's decision at each of them.
+#include <algorithm>
+#include <cstdlib>
+#include <utility>
+#include <cstring>
+#include <vector>
+
+#include "prims.h"
+
+namespace pbx {
+namespace tree {
+
+using namespace prim;
+
+static constexpr double kR2Tiny = 2.2250738585072014e-308;  // tree.rs:36
+constexpr int LPW = 21;                                      // octree levels per key word
+constexpr int MAX_WORDS = 53;  // 1113 levels: half underflows to 0 before that
+constexpr int WALK_TPB = 64;   // one wave per block
+
+// --------------------------------------------------------------- moments
+// Cartesian slots in graded order (the field order of MultipoleMoment,
+// multipole.rs:11-74): slot s <-> (l, m, n), l + m + n <= 5.
+struct Slot3 {
+  int l, m, n;
+};
+constexpr Slot3 kSlots[56] = {
+    {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {2, 0, 0}, {0, 2, 0}, {0, 0, 2}, {1, 1, 0},
+    {1, 0, 1}, {0, 1, 1}, {3, 0, 0}, {0, 3, 0}, {0, 0, 3}, {2, 1, 0}, {2, 0, 1}, {1, 2, 0},
+    {1, 0, 2}, {0, 2, 1}, {0, 1, 2}, {1, 1, 1}, {4, 0, 0}, {0, 4, 0}, {0, 0, 4}, {3, 1, 0},
+    {3, 0, 1}, {1, 3, 0}, {1, 0, 3}, {0, 3, 1}, {0, 1, 3}, {2, 2, 0}, {2, 0, 2}, {0, 2, 2},
+    {2, 1, 1}, {1, 2, 1}, {1, 1, 2}, {5, 0, 0}, {0, 5, 0}, {0, 0, 5}, {4, 1, 0}, {4, 0, 1},
+    {1, 4, 0}, {1, 0, 4}, {0, 4, 1}, {0, 1, 4}, {3, 2, 0}, {3, 0, 2}, {2, 3, 0}, {2, 0, 3},
+    {0, 3, 2}, {0, 2, 3}, {2, 2, 1}, {2, 1, 2}, {1, 2, 2}, {3, 1, 1}, {1, 3, 1}, {1, 1, 3}};
+
+__host__ __device__ constexpr int ncoef(int order) {
+  return (order + 1) * (order + 2) * (order + 3) / 6;
+}
+
+__host__ __device__ constexpr int slot_of(int l, int m, int n) {
+  for (int s = 0; s < 56; ++s)
+    if (kSlots[s].l == l && kSlots[s].m == m && kSlots[s].n == n) return s;
+  return -1;
+}
+
+
+// slot index as a guaranteed constant expression
+template <int L, int M, int N> constexpr int kSlot = slot_of(L, M, N);
+
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double e = __builtin_fma(-x * y, y, 1.0);
+  return __builtin_fma(0.5 * y, e, y);
+}
+
+// Derivative tensor D[s] = d^(l+m+n)/dx^l dy^m dz^n of 1/|R| at R = (x, y, z)
+// up to order P, from the recurrence obtained by differentiating
+// r^2 dphi/dx + x phi = 0 (Leibniz):
+//   r^2 D(l,m,n) = -(2l-1) x D(l-1,m,n) - (l-1)^2 D(l-2,m,n)
+//                  - 2m y D(l,m-1,n) - m(m-1) D(l,m-2,n)
+//                  - 2n z D(l,m,n-1) - n(n-1) D(l,m,n-2),   l >= 1
+// (and the same with the roles of the axes exchanged when l = 0).
+// compile-time loop: f(std::integral_constant<int, 0..N-1>) in order
+template <class F, int... S>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+template <int N, class F> __device__ __forceinline__ void static_for(F &&f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int P>
+__device__ __forceinline__ void derivs(double x, double y, double z, double inv_r,
+                                       double (&D)[ncoef(P)]) {
+  const double q = inv_r * inv_r;  // 1/r^2
+  D[0] = inv_r;
+  static_for<ncoef(P)>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    if constexpr (s > 0) {
+      constexpr int l = kSlots[s].l, m = kSlots[s].m, n = kSlots[s].n;
+      constexpr int a = l > 0 ? 0 : (m > 0 ? 1 : 2);  // recurse along axis a
+      double acc = 0.0;
+      if constexpr (l > 0) {
+        acc = __builtin_fma((a == 0 ? 2.0 * l - 1.0 : 2.0 * l) * x, D[kSlot<l - 1, m, n>], acc);
+        if constexpr (l > 1)
+          acc = __builtin_fma(a == 0 ? (l - 1.0) * (l - 1.0) : l * (l - 1.0),
+                              D[kSlot<l - 2, m, n>], acc);
+      }
+      if constexpr (m > 0) {
+        acc = __builtin_fma((a == 1 ? 2.0 * m - 1.0 : 2.0 * m) * y, D[kSlot<l, m - 1, n>], acc);
+        if constexpr (m > 1)
+          acc = __builtin_fma(a == 1 ? (m - 1.0) * (m - 1.0) : m * (m - 1.0),
+                              D[kSlot<l, m - 2, n>], acc);
+      }
+      if constexpr (n > 0) {
+        acc = __builtin_fma((a == 2 ? 2.0 * n - 1.0 : 2.0 * n) * z, D[kSlot<l, m, n - 1>], acc);
+        if constexpr (n > 1)
+          acc = __builtin_fma(a == 2 ? (n - 1.0) * (n - 1.0) : n * (n - 1.0),
+                              D[kSlot<l, m, n - 2>], acc);
+      }
+      D[s] = -acc * q;
+    }
+  });
+}
+
+// phi and a from moments M (about the node COM) and D at R = COM - target,
+// with the reference's term selection (multipole.rs:1352-1528): phi drops
+// the dipole (M about the COM), a_i = -sum_{|s|<=P-1} M[s] D[s + e_i].
+template <int P, int WANT>
+__device__ __forceinline__ void eval_multipole(const double *__restrict__ M,
+                                               const double (&D)[ncoef(P)], double &ph,
+                                               double &ax, double &ay, double &az) {
+  if (WANT & PBX_WANT_POT) {
+    double sum = 0.0;
+    static_for<ncoef(P)>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (k == 0 || k > 3) sum = __builtin_fma(M[k], D[k], sum);
+    });
+    ph -= sum;
+  }
+  if (WANT & PBX_WANT_ACC) {
+    constexpr int PA = P >= 2 ? P - 1 : 0;
+    double gx = 0.0, gy = 0.0, gz = 0.0;
+    static_for<ncoef(PA)>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int l = kSlots[k].l, m = kSlots[k].m, n = kSlots[k].n;
+      const double mk = M[k];
+      gx = __builtin_fma(mk, D[kSlot<l + 1, m, n>], gx);
+      gy = __builtin_fma(mk, D[kSlot<l, m + 1, n>], gy);
+      gz = __builtin_fma(mk, D[kSlot<l, m, n + 1>], gz);
+    });
+    ax -= gx;
+    ay -= gy;
+    az -= gz;
+  }
+}
+
+// ---------------------------------------------------------- softening
+// kernel.rs:41-82 (Plummer 0, W2 spline 1); r is sqrt(r^2 + tiny).
+__device__ __forceinline__ double w2_pot(double u) {
+  double u2 = u * u;
+  if (u < 0.5) {
+    double u4 = u2 * u2;
+    return (16.0 / 3.0) * u2 - (48.0 / 5.0) * u4 + (32.0 / 5.0) * (u4 * u) - 14.0 / 5.0;
+  }
+  if (u < 1.0) {
+    double u3 = u2 * u, u4 = u2 * u2;
+    return (1.0 / 15.0) / u + (32.0 / 3.0) * u2 - 16.0 * u3 + (48.0 / 5.0) * u4 -
+           (32.0 / 15.0) * (u4 * u) - 16.0 / 5.0;
+  }
+  return -1.0 / u;
+}
+
+__device__ __forceinline__ double w2_der(double u) {
+  double u2 = u * u, u3 = u2 * u, u4 = u2 * u2;
+  if (u < 0.5) return (32.0 / 3.0) * u - (192.0 / 5.0) * u3 + 32.0 * u4;
+  if (u < 1.0)
+    return -(1.0 / 15.0) / u2 + (64.0 / 3.0) * u - 48.0 * u2 + (192.0 / 5.0) * u3 -
+           (32.0 / 3.0) * u4;
+  return 1.0 / u2;
+}
+
+__device__ __forceinline__ double kern_pot(int kind, double r, double h) {
+  if (r == 0.0) return 0.0;
+  if (kind == 0) return -1.0 / __builtin_sqrt(r * r + h * h);
+  if (h <= 0.0) return -1.0 / r;
+  return w2_pot(r / h) / h;
+}
+
+__device__ __forceinline__ double kern_acc(int kind, double r, double h) {
+  if (r == 0.0) return 0.0;
+  if (kind == 0) {
+    double s2 = r * r + h * h;
+    return 1.0 / (__builtin_sqrt(s2) * s2);
+  }
+  if (h <= 0.0) return 1.0 / (r * r * r);
+  return w2_der(r / h) / (h * h) / r;
+}
+
+// squared distance with the reference's mul_add nesting (tree.rs:139,1117)
+__device__ __forceinline__ double dist2_fma(double dx, double dy, double dz) {
+#pragma clang fp contract(off)
+  return __builtin_fma(dx, dx, __builtin_fma(dy, dy, dz * dz));
+}
+
+// ------------------------------------------------------------------ build
+// bounding box: ordered keys of min x,y,z and max x,y,z (NaN ignored like
+// the `<` / `>` updates of tree.rs:631-640)
+__global__ void __launch_bounds__(TPB) bbox_kernel(const double *__restrict__ pos, int64_t n,
+                                                   unsigned long long *__restrict__ out) {
+  __shared__ unsigned long long red[6][NWAVE];
+  unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0ull, 0ull, 0ull};
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      double v = pos[3 * i + d];
+      if (v != v) continue;
+      unsigned long long k = dkey(v);
+      mn[d] = k < mn[d] ? k : mn[d];
+      mx[d] = k > mx[d] ? k : mx[d];
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      unsigned long long a = __shfl_xor(mn[d], o, 64), b = __shfl_xor(mx[d], o, 64);
+      mn[d] = a < mn[d] ? a : mn[d];
+      mx[d] = b > mx[d] ? b : mx[d];
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    for (int d = 0; d < 3; ++d) {
+      red[d][w] = mn[d];
+      red[3 + d][w] = mx[d];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    int d = threadIdx.x;
+    unsigned long long a = red[d][0], b = red[3 + d][0];
+    for (int k = 1; k < NWAVE; ++k) {
+      a = red[d][k] < a ? red[d][k] : a;
+      b = red[3 + d][k] > b ? red[3 + d][k] : b;
+    }
+    atomicMin(&out[d], a);
+    atomicMax(&out[3 + d], b);
+  }
+}
+
+// Octant path of every particle through the reference's node centres,
+// LPW levels per word (level 0 in the top bits of word 0).
+__global__ void __launch_bounds__(TPB)
+    path_keys(const double *__restrict__ pos, int64_t n, double cx0, double cy0, double cz0,
+              double half0, int nwords, uint64_t *__restrict__ keys) {
+#pragma clang fp contract(off)
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const double x = pos[3 * i], y = pos[3 * i + 1], z = pos[3 * i + 2];
+  double cx = cx0, cy = cy0, cz = cz0, h = half0;
+  for (int w = 0; w < nwords; ++w) {
+    uint64_t word = 0;
+    for (int l = 0; l < LPW; ++l) {
+      uint32_t o = (x >= cx ? 1u : 0u) | (y >= cy ? 2u : 0u) | (z >= cz ? 4u : 0u);
+      word = (word << 3) | o;
+      double off = h / 2.0;
+      cx += (o & 1u) ? off : -off;
+      cy += (o & 2u) ? off : -off;
+      cz += (o & 4u) ? off : -off;
+      h = off;
+    }
+    keys[(int64_t)w * n + i] = word;
+  }
+}
+
+__global__ void gather_u64(const uint64_t *__restrict__ src, const int32_t *__restrict__ perm,
+                           int64_t n, uint64_t *__restrict__ dst) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) dst[i] = perm ? src[perm[i]] : src[i];
+}
+
+__global__ void key_or_and(const uint64_t *__restrict__ k, int64_t n,
+                           unsigned long long *__restrict__ out) {
+  unsigned long long o = 0, a = ~0ull;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    o |= k[i];
+    a &= k[i];
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    o |= __shfl_xor(o, s, 64);
+    a &= __shfl_xor(a, s, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicOr(&out[0], o);
+    atomicAnd(&out[1], a);
+  }
+}
+
+struct BuildView {
+  const uint64_t *keys;  // sorted paths, nwords x n
+  const int32_t *perm;   // sorted -> original
+  const double *pos;     // original order
+  int64_t n;
+  int nwords;
+  int64_t cap;           // leaf capacity
+  int32_t *nstart, *ncount, *nfirst, *nnext, *nchild;
+  double4 *ncen;         // centre xyz + half
+};
+
+__device__ __forceinline__ uint32_t digit_at(const BuildView &v, int64_t i, int d) {
+  const uint64_t k = v.keys[(int64_t)(d / LPW) * v.n + i];
+  return (uint32_t)(k >> (3 * (LPW - 1 - d % LPW))) & 7u;
+}
+
+// A node with more than leaf_capacity particles that all sit on one point
+// never separates (tree.rs:847-864 recurses forever); it stays a leaf here.
+__device__ bool all_identical(const BuildView &v, int64_t a, int64_t b) {
+  for (int w = 0; w < v.nwords; ++w)
+    if (v.keys[(int64_t)w * v.n + a] != v.keys[(int64_t)w * v.n + b - 1]) return false;
+  const int64_t p0 = v.perm[a];
+  const uint64_t *q0 = (const uint64_t *)(v.pos + 3 * p0);
+  for (int64_t i = a + 1; i < b; ++i) {
+    const uint64_t *q = (const uint64_t *)(v.pos + 3 * (int64_t)v.perm[i]);
+    if (q[0] != q0[0] || q[1] != q0[1] || q[2] != q0[2]) return false;
+  }
+  return true;
+}
+
+__global__ void root_init(BuildView v, double cx, double cy, double cz, double half,
+                          int32_t *__restrict__ frontier, uint32_t *__restrict__ nfront) {
+  v.nstart[0] = 0;
+  v.ncount[0] = (int32_t)v.n;
+  v.nfirst[0] = -1;
+  v.nnext[0] = -1;
+  v.nchild[0] = 0;
+  v.ncen[0] = make_double4(cx, cy, cz, half);
+  bool split = v.n > v.cap && half != 0.0 && !all_identical(v, 0, v.n);
+  if (split) frontier[0] = 0;
+  *nfront = split ? 1u : 0u;
+}
+
+// children ranges of every frontier node: lb[f*9 + o] = first particle with
+// digit >= o at level d (digits are sorted inside a node's range)
+__global__ void split_count(BuildView v, const int32_t *__restrict__ frontier, int64_t F, int d,
+                            int32_t *__restrict__ lb, uint32_t *__restrict__ cnt) {
+  int64_t f = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (f >= F) return;
+  const int32_t node = frontier[f];
+  const int64_t s = v.nstart[node], e = s + v.ncount[node];
+  int64_t lo = s;
+  uint32_t c = 0;
+  int64_t prev = s;
+  for (uint32_t o = 0; o < 8; ++o) {
+    int64_t a = lo, b = e;  // first index in [lo, e) with digit >= o
+    while (a < b) {
+      int64_t mid = (a + b) >> 1;
+      if (digit_at(v, mid, d) < o) a = mid + 1;
+      else b = mid;
+    }
+    lb[f * 9 + o] = (int32_t)a;
+    if (o > 0 && a > prev) ++c;
+    prev = a;
+    lo = a;
+  }
+  lb[f * 9 + 8] = (int32_t)e;
+  if (e > prev) ++c;
+  cnt[f] = c;
+}
+
+// create the children of every frontier node (ids base + exclusive scan);
+// flag the ones that must split at the next level
+__global__ void split_make(BuildView v, const int32_t *__restrict__ frontier, int64_t F,
+                           const int32_t *__restrict__ lb, const uint32_t *__restrict__ cbase,
+                           int32_t level_base, uint32_t *__restrict__ flags) {
+#pragma clang fp contract(off)
+  int64_t f = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (f >= F) return;
+  const int32_t node = frontier[f];
+  const double4 pc = v.ncen[node];
+  const double off = pc.w / 2.0;  // tree.rs:835
+  int32_t k = level_base + (int32_t)cbase[f];
+  int last = -1, nkid = 0;
+  for (int o = 0; o < 8; ++o)
+    if (lb[f * 9 + o + 1] > lb[f * 9 + o]) {
+      last = o;
+      ++nkid;
+    }
+  v.nfirst[node] = k;
+  v.nchild[node] = nkid;
+  const int32_t parent_next = v.nnext[node];
+  for (int o = 0; o < 8; ++o) {
+    const int32_t a = lb[f * 9 + o], b = lb[f * 9 + o + 1];
+    if (b <= a) continue;
+    const int32_t c = k++;
+    double4 cc;
+    cc.x = pc.x + ((o & 1) ? off : -off);
+    cc.y = pc.y + ((o & 2) ? off : -off);
+    cc.z = pc.z + ((o & 4) ? off : -off);
+    cc.w = off;
+    v.ncen[c] = cc;
+    v.nstart[c] = a;
+    v.ncount[c] = b - a;
+    v.nfirst[c] = -1;
+    v.nchild[c] = 0;
+    v.nnext[c] = (o == last) ? parent_next : c + 1;
+    bool split = (int64_t)(b - a) > v.cap && off != 0.0 && !all_identical(v, a, b);
+    flags[c - level_base] = split ? 1u : 0u;
+  }
+}
+
+__global__ void compact_frontier(const uint32_t *__restrict__ scanned, int64_t C,
+                                 int32_t level_base, int32_t *__restrict__ out) {
+  int64_t c = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (c >= C) return;
+  if (scanned[c + 1] != scanned[c]) out[scanned[c]] = level_base + (int32_t)c;
+}
+
+// leaf lists in ascending original index (the Rust Vec order of
+// tree.rs:815-828), then the records of every particle in leaf order
+__global__ void leaf_sort(const int32_t *__restrict__ nchild, const int32_t *__restrict__ nstart,
+                          const int32_t *__restrict__ ncount, int64_t nn,
+                          int32_t *__restrict__ perm) {
+  int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k >= nn || nchild[k] != 0) return;
+  const int32_t s = nstart[k], c = ncount[k];
+  for (int32_t i = s + 1; i < s + c; ++i) {
+    int32_t v = perm[i];
+    int32_t j = i - 1;
+    while (j >= s && perm[j] > v) {
+      perm[j + 1] = perm[j];
+      --j;
+    }
+    perm[j + 1] = v;
+  }
+}
+
+__global__ void pack_records(const double *__restrict__ pos, const double *__restrict__ mass,
+                             const int32_t *__restrict__ perm, int64_t n,
+                             double4 *__restrict__ rec) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = perm[i];
+  rec[i] = make_double4(pos[3 * p], pos[3 * p + 1], pos[3 * p + 2], mass ? mass[p] : 1.0);
+}
+
+__global__ void gather_f64(const double *__restrict__ src, const int32_t *__restrict__ perm,
+                           int64_t n, double *__restrict__ dst) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) dst[i] = src[perm[i]];
+}
+
+// P2M of one particle at (x, y, z) relative to the expansion centre:
+// M[l,m,n] += mass x^l y^m z^n / (l! m! n!)
+template <int P>
+__device__ __forceinline__ void p2m_add(double (&M)[ncoef(P)], double m, double x, double y,
+                                        double z) {
+  double px[P + 1], py[P + 1], pz[P + 1];
+  px[0] = m;
+  py[0] = 1.0;
+  pz[0] = 1.0;
+  static_for<P>([&](auto ac) {
+    constexpr int a = decltype(ac)::value + 1;
+    px[a] = px[a - 1] * x * (1.0 / a);
+    py[a] = py[a - 1] * y * (1.0 / a);
+    pz[a] = pz[a - 1] * z * (1.0 / a);
+  });
+  static_for<ncoef(P)>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    M[s] += px[kSlots[s].l] * (py[kSlots[s].m] * pz[kSlots[s].n]);
+  });
+}
+
+// M2M: moments C about the child COM shifted by t = parent COM - child COM
+// (multipole.rs:1536-1595 in binomial form):
+//   M[l,m,n] += sum_{i<=l, j<=m, k<=n} C[i,j,k] (-t)^(l-i,m-j,n-k) / (l-i)!(m-j)!(n-k)!
+template <int P>
+__device__ __forceinline__ void m2m_add(double (&M)[ncoef(P)], const double *__restrict__ C,
+                                        double tx, double ty, double tz) {
+  double ex[P + 1], ey[P + 1], ez[P + 1];
+  ex[0] = ey[0] = ez[0] = 1.0;
+  static_for<P>([&](auto ac) {
+    constexpr int a = decltype(ac)::value + 1;
+    ex[a] = ex[a - 1] * (-tx) * (1.0 / a);
+    ey[a] = ey[a - 1] * (-ty) * (1.0 / a);
+    ez[a] = ez[a - 1] * (-tz) * (1.0 / a);
+  });
+  double c[ncoef(P)];
+  static_for<ncoef(P)>([&](auto sc) { c[decltype(sc)::value] = C[decltype(sc)::value]; });
+  static_for<ncoef(P)>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    constexpr int l = kSlots[s].l, m = kSlots[s].m, n = kSlots[s].n;
+    double acc = 0.0;
+    static_for<l + 1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      static_for<m + 1>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        static_for<n + 1>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          acc = __builtin_fma(c[kSlot<i, j, k>], ex[l - i] * (ey[m - j] * ez[n - k]), acc);
+        });
+      });
+    });
+    M[s] += acc;
+  });
+}
+
+struct PayloadView {
+  const int32_t *nstart, *ncount, *nfirst, *nchild;
+  const double4 *rec;
+  const double *soft;  // sorted softenings or null
+  double4 *com;        // com xyz + mass
+  double *hmax;        // or null
+  double *mom;         // ncoef(P) per node (P >= 2) or null
+};
+
+// one level of the bottom-up payload pass (tree.rs:866-1067)
+template <int P>
+__global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, int32_t b) {
+  int32_t k = a + (int32_t)(blockIdx.x * TPB + threadIdx.x);
+  if (k >= b) return;
+  double mass = 0.0, cx = 0.0, cy = 0.0, cz = 0.0, hm = 0.0;
+  const int32_t nc = v.nchild[k];
+  if (nc == 0) {
+    const int32_t s = v.nstart[k], c = v.ncount[k];
+    {
+#pragma clang fp contract(off)
+      for (int32_t j = s; j < s + c; ++j) {
+        const double4 r = v.rec[j];
+        mass += r.w;
+        cx += r.x * r.w;
+        cy += r.y * r.w;
+        cz += r.z * r.w;
+      }
+      if (mass > 0.0) {
+        cx /= mass;
+        cy /= mass;
+        cz /= mass;
+      }
+    }
+    if (v.hmax)
+      for (int32_t j = s; j < s + c; ++j) hm = __builtin_fmax(hm, __builtin_fmax(v.soft[j], 0.0));
+    if (P >= 2 && mass != 0.0) {
+      double M[ncoef(P)];
+      static_for<ncoef(P)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
+      for (int32_t j = s; j < s + c; ++j) {
+        const double4 r = v.rec[j];
+        p2m_add<P>(M, r.w, r.x - cx, r.y - cy, r.z - cz);
+      }
+      static_for<ncoef(P)>(
+          [&](auto qc) { v.mom[(int64_t)k * ncoef(P) + decltype(qc)::value] = M[decltype(qc)::value]; });
+    }
+  } else {
+    const int32_t f = v.nfirst[k];
+    {
+#pragma clang fp contract(off)
+      for (int32_t ch = f; ch < f + nc; ++ch) {
+        const double4 q = v.com[ch];
+        if (q.w == 0.0) continue;
+        mass += q.w;
+        cx += q.x * q.w;
+        cy += q.y * q.w;
+        cz += q.z * q.w;
+      }
+      if (mass > 0.0) {
+        cx /= mass;
+        cy /= mass;
+        cz /= mass;
+      }
+    }
+    if (v.hmax)
+      for (int32_t ch = f; ch < f + nc; ++ch) hm = __builtin_fmax(hm, v.hmax[ch]);
+    if (P >= 2 && mass != 0.0) {
+      double M[ncoef(P)];
+      static_for<ncoef(P)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
+      for (int32_t ch = f; ch < f + nc; ++ch) {
+        const double4 q = v.com[ch];
+        if (q.w == 0.0) continue;
+        m2m_add<P>(M, v.mom + (int64_t)ch * ncoef(P), cx - q.x, cy - q.y, cz - q.z);
+      }
+      static_for<ncoef(P)>(
+          [&](auto qc) { v.mom[(int64_t)k * ncoef(P) + decltype(qc)::value] = M[decltype(qc)::value]; });
+    } else if (P >= 2) {
+#pragma unroll
+      for (int q = 0; q < ncoef(P); ++q) v.mom[(int64_t)k * ncoef(P) + q] = 0.0;
+    }
+  }
+  if (P >= 2 && nc == 0 && mass == 0.0) {
+#pragma unroll
+    for (int q = 0; q < ncoef(P); ++q) v.mom[(int64_t)k * ncoef(P) + q] = 0.0;
+  }
+  v.com[k] = make_double4(cx, cy, cz, mass);
+  if (v.hmax) v.hmax[k] = hm;
+}
+
+// ------------------------------------------------------------------- walk
+struct alignas(16) WalkNode {  // 64 bytes, read with scalar loads
+  double cx, cy, cz, mass;     // centre of mass, mass
+  double size2, hmax;          // (2 half)^2, max softening below (0 if none)
+  int32_t next, first;         // threaded links; first = -1 for a leaf
+  int32_t leaf_start, leaf_count;
+};
+
+__global__ void pack_walk(const double4 *__restrict__ com, const double4 *__restrict__ ncen,
+                          const double *__restrict__ hmax, const int32_t *__restrict__ nnext,
+                          const int32_t *__restrict__ nfirst, const int32_t *__restrict__ nchild,
+                          const int32_t *__restrict__ nstart, const int32_t *__restrict__ ncount,
+                          int64_t nn, WalkNode *__restrict__ out) {
+#pragma clang fp contract(off)
+  int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k >= nn) return;
+  WalkNode w;
+  const double4 c = com[k];
+  w.cx = c.x;
+  w.cy = c.y;
+  w.cz = c.z;
+  w.mass = c.w;
+  const double s = ncen[k].w * 2.0;  // tree.rs:794-798
+  w.size2 = s * s;
+  w.hmax = hmax ? hmax[k] : 0.0;
+  w.next = nnext[k];
+  const bool leaf = nchild[k] == 0;
+  w.first = leaf ? -1 : nfirst[k];
+  w.leaf_start = leaf ? nstart[k] : 0;
+  w.leaf_count = leaf ? ncount[k] : 0;
+  out[k] = w;
+}
+
+struct WalkParams {
+  const WalkNode *nodes;
+  const double *mom;        // ncoef(P) per node (P >= 2)
+  const double4 *rec;       // sources in leaf order
+  const double *soft;       // sorted softenings (softenings set) or null
+  const double *tgt;        // (m, 3) query points; null => targets are the sources
+  const int32_t *perm;      // leaf order -> original index (self mode)
+  int64_t m;                // number of targets
+  double theta2;
+  double sep;               // multipole_min_separation_factor (kernel.rs:20-37)
+  int kernel;
+  int has_hmax;
+  double *pot, *acc;
+  unsigned long long *counters;  // [accepted nodes, leaf pairs] or null
+  int64_t max_steps;             // > number of nodes
+  unsigned int *fault;           // set when a wave exceeds max_steps
+};
+
+// SOFT: h_max guard and/or softened leaf sums are live
+template <int P, int WANT, bool SOFT>
+__global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
+  const int64_t t = (int64_t)blockIdx.x * WALK_TPB + threadIdx.x;
+  const bool valid = t < wp.m;
+  const bool self_mode = wp.tgt == nullptr;
+  double tx = 0.0, ty = 0.0, tz = 0.0, th = 0.0;
+  int64_t self = -1;
+  if (valid) {
+    if (self_mode) {
+      const double4 r = wp.rec[t];
+      tx = r.x;
+      ty = r.y;
+      tz = r.z;
+      self = t;
+      if (SOFT && wp.soft) th = __builtin_fmax(wp.soft[t], 0.0);
+    } else {
+      tx = wp.tgt[3 * t];
+      ty = wp.tgt[3 * t + 1];
+      tz = wp.tgt[3 * t + 2];
+    }
+  }
+  const bool has_th = SOFT && self_mode && wp.soft != nullptr;
+  double ph = 0.0, ax = 0.0, ay = 0.0, az = 0.0;
+  unsigned long long n_node = 0, n_pp = 0;
+  int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
+  int32_t w = 0;               // the wave's node (uniform)
+  int64_t steps = 0;           // the wave moves strictly forward in DFS order
+  while (w >= 0) {
+    if (++steps > wp.max_steps) {  // corrupted links: stop instead of hanging
+      if (threadIdx.x == 0) atomicOr(wp.fault, 1u);
+      break;
+    }
+    const WalkNode nd = wp.nodes[w];
+    const bool act = (p == w);
+    if (nd.mass == 0.0) {  // tree.rs:1087-1090
+      if (act) p = nd.next;
+      w = nd.next;
+      continue;
+    }
+    if (nd.first < 0) {  // leaf: direct sum in ascending index order
+      if (act) {
+        const int32_t s = nd.leaf_start, e = nd.leaf_start + nd.leaf_count;
+        n_pp += (unsigned long long)nd.leaf_count;
+        for (int32_t j = s; j < e; ++j) {
+          const double4 r = wp.rec[j];
+          double dx = r.x - tx, dy = r.y - ty, dz = r.z - tz, m = r.w;
+          const bool me = (j == self);  // skip_self (tree.rs:129-131)
+          m = me ? 0.0 : m;
+          dx = me ? 1.0 : dx;
+          const double r2 = dist2_fma(dx, dy, dz);
+          double h = 0.0;
+          if (SOFT) {
+            h = th;
+            if (wp.soft) h = __builtin_fmax(__builtin_fmax(wp.soft[j], 0.0), th);
+          }
+          if (!SOFT || h <= 0.0 || (wp.kernel == 1 && r2 >= h * h)) {
+            const double y = rsqrt_nr(r2 + kR2Tiny);
+            if (WANT & PBX_WANT_POT) ph = __builtin_fma(-m, y, ph);
+            if (WANT & PBX_WANT_ACC) {
+              const double g = m * (y * y * y);
+              ax = __builtin_fma(g, dx, ax);
+              ay = __builtin_fma(g, dy, ay);
+              az = __builtin_fma(g, dz, az);
+            }
+          } else {
+            const double rr = __builtin_sqrt(r2 + kR2Tiny);
+            if (WANT & PBX_WANT_POT) ph = __builtin_fma(m, kern_pot(wp.kernel, rr, h), ph);
+            if (WANT & PBX_WANT_ACC) {
+              const double g = m * kern_acc(wp.kernel, rr, h);
+              ax = __builtin_fma(g, dx, ax);
+              ay = __builtin_fma(g, dy, ay);
+              az = __builtin_fma(g, dz, az);
+            }
+          }
+        }
+        p = nd.next;
+      }
+      w = nd.next;
+      continue;
+    }
+    bool open = false;
+    if (act) {
+      const double dx = nd.cx - tx, dy = nd.cy - ty, dz = nd.cz - tz;
+      const double dist2 = dist2_fma(dx, dy, dz) + kR2Tiny;  // tree.rs:1117
+      bool soft_ok = true;
+      if (SOFT && wp.has_hmax) {  // node_soft_ok, tree.rs:56-71
+        double h = __builtin_fmax(nd.hmax, 0.0);
+        if (has_th) h = __builtin_fmax(h, th);
+        if (h > 0.0) {
+          const double ch = wp.sep * h;
+          soft_ok = dist2 > ch * ch;
+        }
+      }
+      if (soft_ok && nd.size2 < wp.theta2 * dist2) {
+        ++n_node;
+        if constexpr (P == 0) {  // monopole without multipoles (tree.rs:1126-1129, 1284-1291)
+          const double y = rsqrt_nr(dist2 + kR2Tiny);
+          if (WANT & PBX_WANT_POT) ph = __builtin_fma(-nd.mass, y, ph);
+          if (WANT & PBX_WANT_ACC) {
+            const double g = nd.mass * (y * y * y);
+            ax = __builtin_fma(g, dx, ax);
+            ay = __builtin_fma(g, dy, ay);
+            az = __builtin_fma(g, dz, az);
+          }
+        } else {
+          // derivative builders add eps2 = R2_TINY and R2_TINY again
+          // (multipole.rs:594, tree.rs:1429)
+          const double r2 = dx * dx + dy * dy + dz * dz + 2.0 * kR2Tiny;
+          const double inv_r = rsqrt_nr(r2);
+          if constexpr (P == 1) {  // stored as O0: monopole with the D1 tensor (multipole.rs:272)
+            double D[4];
+            derivs<1>(dx, dy, dz, inv_r, D);
+            if (WANT & PBX_WANT_POT) ph = __builtin_fma(-nd.mass, D[0], ph);
+            if (WANT & PBX_WANT_ACC) {
+              ax = __builtin_fma(-nd.mass, D[1], ax);
+              ay = __builtin_fma(-nd.mass, D[2], ay);
+              az = __builtin_fma(-nd.mass, D[3], az);
+            }
+          } else {
+            double D[ncoef(P)];
+            derivs<P>(dx, dy, dz, inv_r, D);
+            eval_multipole<P, WANT>(wp.mom + (int64_t)w * ncoef(P), D, ph, ax, ay, az);
+          }
+        }
+        p = nd.next;
+      } else {
+        open = true;
+        p = nd.first;
+      }
+    }
+    w = (__ballot(open) != 0ull) ? nd.first : nd.next;
+  }
+  if (!valid) return;
+  const int64_t o = self_mode ? (int64_t)wp.perm[t] : t;
+  if (WANT & PBX_WANT_POT) wp.pot[o] = ph;
+  if (WANT & PBX_WANT_ACC) {
+    wp.acc[3 * o] = ax;
+    wp.acc[3 * o + 1] = ay;
+    wp.acc[3 * o + 2] = az;
+  }
+  if (wp.counters) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+      n_node += __shfl_xor(n_node, s, 64);
+      n_pp += __shfl_xor(n_pp, s, 64);
+    }
+    if (threadIdx.x == 0) {
+      atomicAdd(&wp.counters[0], n_node);
+      atomicAdd(&wp.counters[1], n_pp);
+    }
+  }
+}
+
+// ------------------------------------------------------------------- host
+struct Octree {
+  int device = -1;
+  int64_t n = 0;
+  int64_t leaf_capacity = 32;
+  int order = 0;   // multipole_order as given
+  int kernel = 0;  // 0 Plummer, 1 spline
+  bool user_mass = false;
+  bool soft_set = false;
+  bool has_bh = false;
+  bool has_hmax = false;
+  int nwords = 2;
+  double root[4] = {0, 0, 0, 0};
+  int64_t nn = 0, cap = 0;
+  std::vector<int32_t> lvl;  // first node id of every level (+ end)
+  Buf pos, mass, soft;       // original order (device copies)
+  Buf perm, rec, soft_s;     // leaf order
+  Buf nstart, ncount, nfirst, nnext, nchild, ncen;
+  Buf com, hmax, mom, walk;
+  Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
+  unsigned long long last_counts[3] = {0, 0, 0};  // nodes, leaf pairs, fault
+  int moment_order() const { return order < 5 ? order : 5; }
+};
+
+static inline unsigned nblk(int64_t n) { return (unsigned)((n + TPB - 1) / TPB); }
+
+// grow a node array to `ncap` elements of `esize` bytes keeping `keep` elements
+static void grow_keep(Buf &b, size_t esize, int64_t ncap, int64_t keep, hipStream_t st) {
+  size_t need = esize * (size_t)ncap;
+  if (need <= b.bytes) return;
+  void *np = nullptr;
+  PBX_HIP(hipMalloc(&np, need));
+  if (keep > 0 && b.p) PBX_HIP(hipMemcpyAsync(np, b.p, esize * (size_t)keep, hipMemcpyDeviceToDevice, st));
+  if (b.p) {
+    PBX_HIP(hipStreamSynchronize(st));
+    (void)hipFree(b.p);
+  }
+  b.p = np;
+  b.bytes = need;
+}
+
+static void ensure_nodes(Octree &T, int64_t need, hipStream_t st) {
+  if (need <= T.cap) return;
+  int64_t c = std::max<int64_t>(need, T.cap * 2);
+  grow_keep(T.nstart, 4, c, T.nn, st);
+  grow_keep(T.ncount, 4, c, T.nn, st);
+  grow_keep(T.nfirst, 4, c, T.nn, st);
+  grow_keep(T.nnext, 4, c, T.nn, st);
+  grow_keep(T.nchild, 4, c, T.nn, st);
+  grow_keep(T.ncen, sizeof(double4), c, T.nn, st);
+  T.cap = c;
+}
+
+static uint32_t read_u32(const void *dptr, hipStream_t st) {
+  uint32_t v = 0;
+  PBX_HIP(hipMemcpyAsync(&v, dptr, 4, hipMemcpyDeviceToHost, st));
+  PBX_HIP(hipStreamSynchronize(st));
+  return v;
+}
+
+// sort perm by the multi-word paths (LSD over words, last word first)
+static void sort_paths(Octree &T, hipStream_t st) {
+  const int64_t n = T.n;
+  uint64_t *keys = T.keys.as<uint64_t>();
+  uint64_t *k0 = (uint64_t *)T.ktmp0.get(8 * (size_t)n);
+  uint64_t *k1 = (uint64_t *)T.ktmp1.get(8 * (size_t)n);
+  int32_t *v0 = T.perm.as<int32_t>();
+  int32_t *v1 = (int32_t *)T.vtmp.get(4 * (size_t)n);
+  unsigned long long *oa = (unsigned long long *)T.small.get(64);
+  bool have_perm = false;
+  for (int w = T.nwords - 1; w >= 0; --w) {
+    // bits that vary across all paths of this word
+    unsigned long long h[2] = {0ull, ~0ull};
+    PBX_HIP(hipMemcpyAsync(oa, h, 16, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(key_or_and, dim3(std::min<unsigned>(1024, nblk(n))), dim3(TPB), 0, st,
+                       keys + (int64_t)w * n, n, oa);
+    PBX_HIP(hipMemcpyAsync(h, oa, 16, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    const uint64_t vary = h[0] ^ h[1];
+    if (!vary) continue;
+    hipLaunchKernelGGL(gather_u64, dim3(nblk(n)), dim3(TPB), 0, st, keys + (int64_t)w * n,
+                       have_perm ? v0 : (const int32_t *)nullptr, n, k0);
+    for (int shift = 0; shift < 64; shift += 8) {
+      if (!((vary >> shift) & 0xffull)) continue;
+      radix_pass<uint64_t>(T.hist, T.tsum, st, k0, v0, have_perm ? VAL_ARRAY : VAL_IOTA, n,
+                           shift, k1, v1);
+      std::swap(k0, k1);
+      std::swap(v0, v1);
+      have_perm = true;
+    }
+  }
+  if (!have_perm) {  // every path equal: identity order
+    std::vector<int32_t> iota(n);
+    for (int64_t i = 0; i < n; ++i) iota[i] = (int32_t)i;
+    PBX_HIP(hipMemcpyAsync(v0, iota.data(), 4 * (size_t)n, hipMemcpyHostToDevice, st));
+    PBX_HIP(hipStreamSynchronize(st));
+  }
+  if (v0 != T.perm.as<int32_t>()) {
+    // result landed in the scratch buffer: swap the allocations
+    std::swap(T.perm, T.vtmp);
+  }
+  // sorted paths (structure pass reads them in leaf order)
+  uint64_t *sorted = (uint64_t *)T.ktmp1.get(8 * (size_t)n * T.nwords);
+  for (int w = 0; w < T.nwords; ++w)
+    hipLaunchKernelGGL(gather_u64, dim3(nblk(n)), dim3(TPB), 0, st, keys + (int64_t)w * n,
+                       T.perm.as<int32_t>(), n, sorted + (int64_t)w * n);
+  PBX_HIP(hipGetLastError());
+  std::swap(T.keys, T.ktmp1);
+}
+
+// levels of the tree; returns false when the paths are too short
+static bool split_levels(Octree &T, hipStream_t st) {
+  const int64_t n = T.n;
+  T.nn = 0;
+  ensure_nodes(T, std::max<int64_t>(64, n / 2 + 64), st);
+  BuildView v;
+  v.keys = T.keys.as<uint64_t>();
+  v.perm = T.perm.as<int32_t>();
+  v.pos = T.pos.as<double>();
+  v.n = n;
+  v.nwords = T.nwords;
+  v.cap = T.leaf_capacity;
+  auto bind = [&] {
+    v.nstart = T.nstart.as<int32_t>();
+    v.ncount = T.ncount.as<int32_t>();
+    v.nfirst = T.nfirst.as<int32_t>();
+    v.nnext = T.nnext.as<int32_t>();
+    v.nchild = T.nchild.as<int32_t>();
+    v.ncen = T.ncen.as<double4>();
+  };
+  bind();
+  int32_t *fr = (int32_t *)T.front0.get(4 * 64);
+  uint32_t *sm = (uint32_t *)T.small.get(64);
+  hipLaunchKernelGGL(root_init, dim3(1), dim3(1), 0, st, v, T.root[0], T.root[1], T.root[2],
+                     T.root[3], fr, sm);
+  int64_t F = read_u32(sm, st);
+  T.nn = 1;
+  T.lvl.assign({0, 1});
+  int d = 0;
+  while (F > 0) {
+    if (d >= LPW * T.nwords) return false;
+    int32_t *front = T.front0.as<int32_t>();
+    int32_t *lb = (int32_t *)T.lb.get(4 * 9 * (size_t)F);
+    uint32_t *cnt = (uint32_t *)T.cnt.get(4 * (size_t)(F + 1));
+    PBX_HIP(hipMemsetAsync(cnt + F, 0, 4, st));
+    hipLaunchKernelGGL(split_count, dim3(nblk(F)), dim3(TPB), 0, st, v, front, F, d, lb, cnt);
+    scan_u32(T.tsum, st, cnt, F + 1);
+    const int64_t C = read_u32(cnt + F, st);
+    if (T.nn + C >= ((int64_t)1 << 31)) fail(PBX_ERR_VALUE, "octree too large (%lld nodes)", (long long)(T.nn + C));
+    ensure_nodes(T, T.nn + C, st);
+    bind();
+    uint32_t *flags = (uint32_t *)T.flags.get(4 * (size_t)(C + 1));
+    PBX_HIP(hipMemsetAsync(flags + C, 0, 4, st));
+    hipLaunchKernelGGL(split_make, dim3(nblk(F)), dim3(TPB), 0, st, v, front, F, lb, cnt,
+                       (int32_t)T.nn, flags);
+    scan_u32(T.tsum, st, flags, C + 1);
+    const int64_t F2 = read_u32(flags + C, st);
+    int32_t *front2 = (int32_t *)T.front1.get(4 * (size_t)std::max<int64_t>(F2, 1));
+    if (F2 > 0)
+      hipLaunchKernelGGL(compact_frontier, dim3(nblk(C)), dim3(TPB), 0, st, flags, C,
+                         (int32_t)T.nn, front2);
+    PBX_HIP(hipGetLastError());
+    T.nn += C;
+    T.lvl.push_back((int32_t)T.nn);
+    std::swap(T.front0, T.front1);
+    F = F2;
+    ++d;
+  }
+  return true;
+}
+
+static void build_structure(Octree &T, hipStream_t st) {
+  ScopedTimer tm("octree.build_structure");
+  const int64_t n = T.n;
+  // root box (tree.rs:628-654)
+  double mn[3], mx[3];
+  {
+    unsigned long long *bb = (unsigned long long *)T.small.get(64);
+    unsigned long long h[6] = {~0ull, ~0ull, ~0ull, 0ull, 0ull, 0ull};
+    PBX_HIP(hipMemcpyAsync(bb, h, 48, hipMemcpyHostToDevice, st));
+    if (n > 0)
+      hipLaunchKernelGGL(bbox_kernel, dim3(std::min<unsigned>(1024, nblk(n))), dim3(TPB), 0, st,
+                         T.pos.as<double>(), n, bb);
+    PBX_HIP(hipMemcpyAsync(h, bb, 48, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    for (int d = 0; d < 3; ++d) {
+      // no finite value seen: the reference's +inf / -inf initial bounds
+      mn[d] = h[d] == ~0ull ? INFINITY : dkey_inv(h[d]);
+      mx[d] = h[3 + d] == 0ull ? -INFINITY : dkey_inv(h[3 + d]);
+    }
+  }
+  {
+#pragma clang fp contract(off)
+    for (int d = 0; d < 3; ++d) T.root[d] = (mn[d] + mx[d]) / 2.0;
+    double half = 0.0;
+    for (int d = 0; d < 3; ++d) half = std::fmax(half, (mx[d] - mn[d]) / 2.0);
+    if (half == 0.0) half = 1e-6;
+    T.root[3] = half;
+  }
+  T.perm.get(4 * (size_t)std::max<int64_t>(n, 1));
+  if (n == 0) {
+    T.nn = 0;
+    ensure_nodes(T, 64, st);
+    int32_t z[2] = {0, 0};
+    int32_t neg = -1;
+    PBX_HIP(hipMemcpyAsync(T.nstart.p, &z[0], 4, hipMemcpyHostToDevice, st));
+    PBX_HIP(hipMemcpyAsync(T.ncount.p, &z[1], 4, hipMemcpyHostToDevice, st));
+    PBX_HIP(hipMemcpyAsync(T.nfirst.p, &neg, 4, hipMemcpyHostToDevice, st));
+    PBX_HIP(hipMemcpyAsync(T.nnext.p, &neg, 4, hipMemcpyHostToDevice, st));
+    PBX_HIP(hipMemcpyAsync(T.nchild.p, &z[0], 4, hipMemcpyHostToDevice, st));
+    double4 c = make_double4(T.root[0], T.root[1], T.root[2], T.root[3]);
+    PBX_HIP(hipMemcpyAsync(T.ncen.p, &c, sizeof(c), hipMemcpyHostToDevice, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    T.nn = 1;
+    T.lvl.assign({0, 1});
+    T.rec.get(64);
+    return;
+  }
+  for (T.nwords = 2;; ++T.nwords) {
+    if (T.nwords > MAX_WORDS) fail(PBX_ERR_RUNTIME, "octree deeper than %d levels", LPW * MAX_WORDS);
+    uint64_t *keys = (uint64_t *)T.keys.get(8 * (size_t)n * T.nwords);
+    hipLaunchKernelGGL(path_keys, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(), n,
+                       T.root[0], T.root[1], T.root[2], T.root[3], T.nwords, keys);
+    PBX_HIP(hipGetLastError());
+    sort_paths(T, st);
+    if (split_levels(T, st)) break;
+  }
+  hipLaunchKernelGGL(leaf_sort, dim3(nblk(T.nn)), dim3(TPB), 0, st, T.nchild.as<int32_t>(),
+                     T.nstart.as<int32_t>(), T.ncount.as<int32_t>(), T.nn, T.perm.as<int32_t>());
+  PBX_HIP(hipGetLastError());
+}
+
+static void pack_particles(Octree &T, hipStream_t st) {
+  const int64_t n = T.n;
+  double4 *rec = (double4 *)T.rec.get(sizeof(double4) * (size_t)std::max<int64_t>(n, 1));
+  if (n > 0) {
+    hipLaunchKernelGGL(pack_records, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(),
+                       T.user_mass ? T.mass.as<double>() : (const double *)nullptr,
+                       T.perm.as<int32_t>(), n, rec);
+    if (T.soft_set)
+      hipLaunchKernelGGL(gather_f64, dim3(nblk(n)), dim3(TPB), 0, st, T.soft.as<double>(),
+                         T.perm.as<int32_t>(), n, (double *)T.soft_s.get(8 * (size_t)n));
+  }
+  PBX_HIP(hipGetLastError());
+}
+
+template <int P>
+static void run_payload(Octree &T, hipStream_t st, PayloadView v) {
+  for (int L = (int)T.lvl.size() - 2; L >= 0; --L) {
+    const int32_t a = T.lvl[L], b = T.lvl[L + 1];
+    if (b > a) hipLaunchKernelGGL(payload_level<P>, dim3(nblk(b - a)), dim3(TPB), 0, st, v, a, b);
+  }
+  PBX_HIP(hipGetLastError());
+}
+
+// build_mass_payload (tree.rs:968-1012)
+static void build_payload(Octree &T, hipStream_t st) {
+  ScopedTimer tm("octree.build_mass_payload");
+  pack_particles(T, st);
+  T.has_hmax = T.soft_set;
+  PayloadView v;
+  v.nstart = T.nstart.as<int32_t>();
+  v.ncount = T.ncount.as<int32_t>();
+  v.nfirst = T.nfirst.as<int32_t>();
+  v.nchild = T.nchild.as<int32_t>();
+  v.rec = T.rec.as<double4>();
+  v.soft = T.soft_set ? T.soft_s.as<double>() : nullptr;
+  v.com = (double4 *)T.com.get(sizeof(double4) * (size_t)T.nn);
+  v.hmax = T.has_hmax ? (double *)T.hmax.get(8 * (size_t)T.nn) : nullptr;
+  const int P = T.moment_order();
+  v.mom = P >= 2 ? (double *)T.mom.get(8 * (size_t)T.nn * ncoef(P)) : nullptr;
+  switch (P) {
+    case 0:
+    case 1: run_payload<0>(T, st, v); break;
+    case 2: run_payload<2>(T, st, v); break;
+    case 3: run_payload<3>(T, st, v); break;
+    case 4: run_payload<4>(T, st, v); break;
+    default: run_payload<5>(T, st, v); break;
+  }
+  hipLaunchKernelGGL(pack_walk, dim3(nblk(T.nn)), dim3(TPB), 0, st, T.com.as<double4>(),
+                     T.ncen.as<double4>(), v.hmax, T.nnext.as<int32_t>(), T.nfirst.as<int32_t>(),
+                     T.nchild.as<int32_t>(), T.nstart.as<int32_t>(), T.ncount.as<int32_t>(), T.nn,
+                     (WalkNode *)T.walk.get(sizeof(WalkNode) * (size_t)T.nn));
+  PBX_HIP(hipGetLastError());
+  T.has_bh = true;
+}
+
+template <int P, int WANT>
+static void launch_walk_pw(const WalkParams &wp, bool soft, hipStream_t st) {
+  const unsigned grid = (unsigned)((wp.m + WALK_TPB - 1) / WALK_TPB);
+  if (soft)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, true>), dim3(grid), dim3(WALK_TPB), 0, st, wp);
+  else
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false>), dim3(grid), dim3(WALK_TPB), 0, st, wp);
+}
+
+template <int P>
+static void launch_walk_p(const WalkParams &wp, int want, bool soft, hipStream_t st) {
+  if (want == PBX_WANT_POT) launch_walk_pw<P, PBX_WANT_POT>(wp, soft, st);
+  else if (want == PBX_WANT_ACC) launch_walk_pw<P, PBX_WANT_ACC>(wp, soft, st);
+  else launch_walk_pw<P, PBX_WANT_POT | PBX_WANT_ACC>(wp, soft, st);
+}
+
+// walk for m targets (tgt == null: all particles, skip_self) into device
+// outputs in original / query order
+static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t m, double *d_pot,
+                 double *d_acc, hipStream_t st) {
+  unsigned long long *ctr = (unsigned long long *)T.counters.get(32);
+  PBX_HIP(hipMemsetAsync(ctr, 0, 32, st));
+  if (m == 0) return;
+  WalkParams wp;
+  wp.nodes = T.walk.as<WalkNode>();
+  wp.mom = T.mom.as<double>();
+  wp.rec = T.rec.as<double4>();
+  wp.tgt = d_tgt;
+
+  wp.soft = T.soft_set ? T.soft_s.as<double>() : nullptr;
+  wp.perm = T.perm.as<int32_t>();
+  wp.m = m;
+  {
+#pragma clang fp contract(off)
+    wp.theta2 = theta * theta;  // tree.rs:1428
+  }
+  wp.sep = T.kernel == 0 ? 2.8 : 1.0;
+  wp.kernel = T.kernel;
+  wp.has_hmax = T.has_hmax ? 1 : 0;
+  wp.pot = d_pot;
+  wp.acc = d_acc;
+  wp.counters = ctr;
+  wp.max_steps = T.nn + 16;
+  wp.fault = (unsigned int *)(ctr + 2);
+  // softened leaves need softenings; the guard needs h_max; at query points
+  // there is no target softening (tree.rs:1516,1547)
+  const bool soft = T.has_hmax || T.soft_set;
+  if (T.n == 0) {
+    if (d_pot) PBX_HIP(hipMemsetAsync(d_pot, 0, 8 * (size_t)m, st));
+    if (d_acc) PBX_HIP(hipMemsetAsync(d_acc, 0, 24 * (size_t)m, st));
+    return;
+  }
+  switch (T.moment_order()) {
+    case 0: launch_walk_p<0>(wp, want, soft, st); break;
+    case 1: launch_walk_p<1>(wp, want, soft, st); break;
+    case 2: launch_walk_p<2>(wp, want, soft, st); break;
+    case 3: launch_walk_p<3>(wp, want, soft, st); break;
+    case 4: launch_walk_p<4>(wp, want, soft, st); break;
+    default: launch_walk_p<5>(wp, want, soft, st); break;
+  }
+  PBX_HIP(hipGetLastError());
+}
+
+static Octree &as_tree(pbx_octree *h) {
+  if (!h) fail(PBX_ERR_VALUE, "null octree handle");
+  Octree *t = (Octree *)h;
+  if (t->device != current_device().id) fail(PBX_ERR_VALUE, "octree belongs to device %d", t->device);
+  return *t;
+}
+
+static void upload(Buf &b, const double *src, int64_t count, int on_device, hipStream_t st) {
+  double *d = (double *)b.get(8 * (size_t)std::max<int64_t>(count, 1));
+  if (count > 0)
+    PBX_HIP(hipMemcpyAsync(d, src, 8 * (size_t)count,
+                           on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+}
+
+static const char *method_name(int want, bool at_points) {
+  if (at_points) return want == PBX_WANT_POT ? "potentials_at_points" : "accelerations_at_points";
+  return want == PBX_WANT_POT ? "compute_potentials" : "compute_accelerations";
+}
+
+}  // namespace tree
+}  // namespace pbx
+
+using namespace pbx;
+using namespace pbx::tree;
+
+extern "C" {
+
+int pbx_octree_create(const double *pos, int64_t n, const double *masses,
+                      const double *softenings, int64_t leaf_capacity, int multipole_order,
+                      int kernel, int on_device, pbx_octree **out) {
+  return guard([&] {
+    if (!out) fail(PBX_ERR_VALUE, "null output handle");
+    *out = nullptr;
+    if (n < 0) fail(PBX_ERR_VALUE, "negative particle count");
+    if (n >= ((int64_t)1 << 31) - 1) fail(PBX_ERR_VALUE, "octrees are limited to < 2^31 particles");
+    if (n > 0 && !pos) fail(PBX_ERR_VALUE, "positions must not be null");
+    if (kernel != 0 && kernel != 1) fail(PBX_ERR_VALUE, "kernel must be 0 (Plummer) or 1 (CubicSplineW2)");
+    if (multipole_order < 0 || multipole_order > 255) fail(PBX_ERR_VALUE, "multipole_order must fit in u8");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    hipStream_t st = dev.stream;
+    Octree *T = new Octree();
+    try {
+      T->device = dev.id;
+      T->n = n;
+      T->leaf_capacity = leaf_capacity < 1 ? 1 : leaf_capacity;  // tree.rs:701
+      T->order = multipole_order;
+      T->kernel = kernel;
+      upload(T->pos, pos, 3 * n, on_device, st);
+      if (masses) {
+        upload(T->mass, masses, n, on_device, st);
+        T->user_mass = true;
+      }
+      if (softenings) {
+        upload(T->soft, softenings, n, on_device, st);
+        T->soft_set = true;
+      }
+      build_structure(*T, st);
+      if (masses) build_payload(*T, st);  // gravity.rs:210-220
+      PBX_HIP(hipStreamSynchronize(st));
+    } catch (...) {
+      delete T;
+      throw;
+    }
+    *out = (pbx_octree *)T;
+  });
+}
+
+int pbx_octree_destroy(pbx_octree *t) {
+  return guard([&] {
+    if (!t) return;
+    Octree *T = (Octree *)t;
+    Buf *bufs[] = {&T->pos, &T->mass, &T->soft, &T->perm, &T->rec, &T->soft_s, &T->nstart,
+                   &T->ncount, &T->nfirst, &T->nnext, &T->nchild, &T->ncen, &T->com, &T->hmax,
+                   &T->mom, &T->walk, &T->keys, &T->ktmp0, &T->ktmp1, &T->vtmp, &T->hist,
+                   &T->tsum, &T->front0, &T->front1, &T->lb, &T->cnt, &T->flags, &T->small,
+                   &T->counters};
+    for (Buf *b : bufs) b->release();
+    delete T;
+  });
+}
+
+int pbx_octree_build_mass(pbx_octree *t, const double *masses, int on_device) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    if (masses) {
+      upload(T.mass, masses, T.n, on_device, dev.stream);
+      T.user_mass = true;
+    }
+    build_payload(T, dev.stream);
+    PBX_HIP(hipStreamSynchronize(dev.stream));
+  });
+}
+
+int pbx_octree_set_softenings(pbx_octree *t, const double *softenings, int on_device) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    if (softenings) {
+      upload(T.soft, softenings, T.n, on_device, dev.stream);
+      T.soft_set = true;
+      if (T.n > 0)
+        hipLaunchKernelGGL(gather_f64, dim3(nblk(T.n)), dim3(TPB), 0, dev.stream,
+                           T.soft.as<double>(), T.perm.as<int32_t>(), T.n,
+                           (double *)T.soft_s.get(8 * (size_t)T.n));
+    } else {
+      T.soft_set = false;  // h_max keeps its build-time value (tree.rs:777-782)
+    }
+    PBX_HIP(hipStreamSynchronize(dev.stream));
+  });
+}
+
+int pbx_octree_set_kernel(pbx_octree *t, int kernel) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (kernel != 0 && kernel != 1) fail(PBX_ERR_VALUE, "kernel must be 0 (Plummer) or 1 (CubicSplineW2)");
+    T.kernel = kernel;
+  });
+}
+
+int pbx_octree_compute(pbx_octree *t, double theta, int want, double *pot, double *acc,
+                       int on_device) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (want < 1 || want > 3) fail(PBX_ERR_VALUE, "want must be 1, 2 or 3");
+    if (!T.has_bh)
+      fail(PBX_ERR_VALUE, "mass payload not built; call build_mass() before %s",
+           method_name(want, false));
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    hipStream_t st = dev.stream;
+    ScopedTimer tm("octree.compute");
+    const int64_t n = T.n;
+    double *dp = nullptr, *da = nullptr;
+    if (on_device) {
+      dp = (want & PBX_WANT_POT) ? pot : nullptr;
+      da = (want & PBX_WANT_ACC) ? acc : nullptr;
+    } else {
+      if (want & PBX_WANT_POT) dp = (double *)dev.slot(kSlotPot).ensure(8 * (size_t)std::max<int64_t>(n, 1));
+      if (want & PBX_WANT_ACC) da = (double *)dev.slot(kSlotAcc).ensure(24 * (size_t)std::max<int64_t>(n, 1));
+    }
+    walk(T, theta, want, nullptr, n, dp, da, st);
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 24, hipMemcpyDeviceToHost, st));
+    if (!on_device) {
+      if (dp && n) PBX_HIP(hipMemcpyAsync(pot, dp, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
+      if (da && n) PBX_HIP(hipMemcpyAsync(acc, da, 24 * (size_t)n, hipMemcpyDeviceToHost, st));
+    }
+    PBX_HIP(hipStreamSynchronize(st));
+    if (T.last_counts[2] & 0xffffffffull) fail(PBX_ERR_RUNTIME, "octree walk exceeded its step bound");
+  });
+}
+
+int pbx_octree_at_points(pbx_octree *t, const double *points, int64_t m, double theta, int want,
+                         double *pot, double *acc, int on_device) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (want < 1 || want > 3) fail(PBX_ERR_VALUE, "want must be 1, 2 or 3");
+    if (!T.has_bh)
+      fail(PBX_ERR_VALUE, "mass payload not built; call build_mass() before %s",
+           method_name(want, true));
+    if (m < 0) fail(PBX_ERR_VALUE, "negative point count");
+    if (m >= ((int64_t)1 << 31)) fail(PBX_ERR_VALUE, "too many query points");
+    if (m > 0 && !points) fail(PBX_ERR_VALUE, "points must not be null");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    hipStream_t st = dev.stream;
+    const double *dt = points;
+    double *dp = nullptr, *da = nullptr;
+    if (on_device) {
+      dp = (want & PBX_WANT_POT) ? pot : nullptr;
+      da = (want & PBX_WANT_ACC) ? acc : nullptr;
+    } else {
+      double *tb = (double *)dev.slot(kSlotTgt).ensure(24 * (size_t)std::max<int64_t>(m, 1));
+      if (m) PBX_HIP(hipMemcpyAsync(tb, points, 24 * (size_t)m, hipMemcpyHostToDevice, st));
+      dt = tb;
+      if (want & PBX_WANT_POT) dp = (double *)dev.slot(kSlotPot).ensure(8 * (size_t)std::max<int64_t>(m, 1));
+      if (want & PBX_WANT_ACC) da = (double *)dev.slot(kSlotAcc).ensure(24 * (size_t)std::max<int64_t>(m, 1));
+    }
+    // at points there is no target softening and no self skip
+    walk(T, theta, want, dt, m, dp, da, st);
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 24, hipMemcpyDeviceToHost, st));
+    if (!on_device) {
+      if (dp && m) PBX_HIP(hipMemcpyAsync(pot, dp, 8 * (size_t)m, hipMemcpyDeviceToHost, st));
+      if (da && m) PBX_HIP(hipMemcpyAsync(acc, da, 24 * (size_t)m, hipMemcpyDeviceToHost, st));
+    }
+    PBX_HIP(hipStreamSynchronize(st));
+    if (T.last_counts[2] & 0xffffffffull) fail(PBX_ERR_RUNTIME, "octree walk exceeded its step bound");
+  });
+}
+
+int pbx_octree_info(pbx_octree *t, int64_t *out) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (!out) fail(PBX_ERR_VALUE, "null output");
+    out[0] = T.n;
+    out[1] = T.nn;
+    out[2] = (int64_t)T.lvl.size() - 1;  // levels (root = 1)
+    out[3] = T.has_bh;
+    out[4] = T.has_hmax;
+    out[5] = (int64_t)T.last_counts[0];
+    out[6] = (int64_t)T.last_counts[1];
+    out[7] = T.nwords;
+  });
+}
+
+int pbx_octree_export(pbx_octree *t, double *center, double *com, double *hmax, int64_t *links,
+                      int64_t *leaf, int64_t *perm, double *moments) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    hipStream_t st = dev.stream;
+    const int64_t nn = T.nn, n = T.n;
+    auto dl = [&](void *dst, const void *src, size_t bytes) {
+      if (dst && bytes) PBX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    };
+    dl(center, T.ncen.p, sizeof(double4) * nn);
+    if (com) {
+      if (!T.has_bh) fail(PBX_ERR_VALUE, "mass payload not built");
+      dl(com, T.com.p, sizeof(double4) * nn);
+    }
+    if (hmax && T.has_hmax) dl(hmax, T.hmax.p, 8 * nn);
+    std::vector<int32_t> a(nn), b(nn), c(nn), s(nn), k(nn);
+    if (links || leaf) {
+      dl(a.data(), T.nfirst.p, 4 * nn);
+      dl(b.data(), T.nnext.p, 4 * nn);
+      dl(c.data(), T.nchild.p, 4 * nn);
+      dl(s.data(), T.nstart.p, 4 * nn);
+      dl(k.data(), T.ncount.p, 4 * nn);
+    }
+    std::vector<int32_t> pm(n);
+    if (perm) dl(pm.data(), T.perm.p, 4 * n);
+    if (moments && T.has_bh && T.moment_order() >= 2)
+      dl(moments, T.mom.p, 8 * (size_t)nn * ncoef(T.moment_order()));
+    PBX_HIP(hipStreamSynchronize(st));
+    for (int64_t i = 0; i < nn; ++i) {
+      if (links) {
+        links[3 * i] = c[i] ? a[i] : -1;
+        links[3 * i + 1] = b[i];
+        links[3 * i + 2] = c[i];
+      }
+      if (leaf) {
+        leaf[2 * i] = s[i];
+        leaf[2 * i + 1] = k[i];
+      }
+    }
+    if (perm)
+      for (int64_t i = 0; i < n; ++i) perm[i] = pm[i];
+  });
+}
+
+}  // extern "C"

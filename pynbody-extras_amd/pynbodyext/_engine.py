@@ -19,6 +19,8 @@ Argument handling restated from gravity.rs:
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import _native as nat
@@ -145,7 +147,168 @@ def direct_potentials_at_points_py(positions, targets, masses=None, threads=0,
     return out
 
 
+def _usize(v, argname: str) -> int:
+    if isinstance(v, bool) or not isinstance(v, (int, np.integer)):
+        raise TypeError(f"argument '{argname}': '{type(v).__name__}' object cannot be "
+                        "interpreted as an integer")
+    v = int(v)
+    if v < 0:
+        raise OverflowError("can't convert negative int to unsigned")
+    return v
+
+
+def _u8(v, argname: str) -> int:
+    v = _usize(v, argname)
+    if v > 255:
+        raise OverflowError("can't convert to u8")
+    return v
+
+
+def _kernel_opt(kernel) -> int:
+    """parse_kernel_opt (gravity.rs:77-82): None -> Plummer."""
+    if kernel is None:
+        return nat.KERNEL_PLUMMER
+    return _kernel_code(kernel)
+
+
+class Octree:
+    """Barnes–Hut octree with the PyO3 class surface of the reference
+    (crates/pynbodyext-rust/src/gravity.rs:114-445); the tree and every walk
+    live on the GPU (include/pbx.h ``pbx_octree_*``).
+
+    ``Octree(positions, masses=None, leaf_capacity=32, multipole_order=0,
+    softenings=None, kernel=None)`` copies its inputs, builds the octree, and
+    builds the mass payload only when masses are given (gravity.rs:210-220).
+    """
+
+    def __init__(self, positions, masses=None, leaf_capacity=32, multipole_order=0,
+                 softenings=None, kernel=None):
+        leaf_capacity = _usize(leaf_capacity, "leaf_capacity")
+        multipole_order = _u8(multipole_order, "multipole_order")
+        if kernel is not None:
+            _u8(kernel, "kernel")
+        self._h = None
+        pos = extract_vec3(positions, "positions")
+        n = pos.shape[0]
+        m = _extract_vec1(masses, n, "masses", "masses")
+        h = _extract_vec1(softenings, n, "softenings", "softenings")
+        if kernel is None and h is not None:
+            raise ValueError(
+                "softenings require an explicit kernel; pass kernel=0/1 (or omit softenings)")
+        k = _kernel_opt(kernel)
+        handle = ctypes.c_void_p()
+        nat.call("pbx_octree_create", nat.vptr(pos), n, nat.vptr(m), nat.vptr(h),
+                 leaf_capacity, multipole_order, k, 0, ctypes.byref(handle))
+        self._h = handle
+        self._n = n
+
+    @classmethod
+    def _from_device(cls, d_pos, n, d_mass=None, leaf_capacity=8, multipole_order=3,
+                     d_soft=None, kernel=0) -> "Octree":
+        """Build from HBM-resident arrays (device pointers; bench / multi-GPU)."""
+        self = cls.__new__(cls)
+        self._h = None
+        handle = ctypes.c_void_p()
+        nat.call("pbx_octree_create", d_pos, int(n), d_mass, d_soft, int(leaf_capacity),
+                 int(multipole_order), int(kernel), 1, ctypes.byref(handle))
+        self._h = handle
+        self._n = int(n)
+        return self
+
+    def __del__(self):  # pragma: no cover - GC timing
+        self.close()
+
+    def close(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and nat._lib is not None:
+            try:
+                nat.call("pbx_octree_destroy", h)
+            except Exception:
+                pass
+        self._h = None
+
+    # -- mutation (gravity.rs:228-265) ------------------------------------
+    def build_mass(self, masses=None):
+        m = _extract_vec1(masses, self._n, "masses", "masses")
+        nat.call("pbx_octree_build_mass", self._h, nat.vptr(m), 0)
+
+    def set_softenings(self, softenings=None):
+        h = _extract_vec1(softenings, self._n, "softenings", "softenings")
+        nat.call("pbx_octree_set_softenings", self._h, nat.vptr(h), 0)
+
+    def set_kernel(self, kernel=None):
+        if kernel is not None:
+            _u8(kernel, "kernel")
+        nat.call("pbx_octree_set_kernel", self._h, _kernel_opt(kernel))
+
+    # -- queries (gravity.rs:267-445) --------------------------------------
+    def compute_accelerations(self, theta, threads=0):
+        _threads(threads)
+        out = np.zeros((self._n, 3), dtype=np.float64)
+        nat.call("pbx_octree_compute", self._h, float(theta), nat.WANT_ACC, None,
+                 nat.vptr(out), 0)
+        return out
+
+    def compute_potentials(self, theta, threads=0):
+        _threads(threads)
+        out = np.zeros(self._n, dtype=np.float64)
+        nat.call("pbx_octree_compute", self._h, float(theta), nat.WANT_POT, nat.vptr(out),
+                 None, 0)
+        return out
+
+    def _at_points(self, points, theta, threads, want, method):
+        _threads(threads)
+        if not self.info()["has_mass_payload"]:
+            raise ValueError(f"mass payload not built; call build_mass() before {method}")
+        pts = extract_vec3(points, "points")
+        m = pts.shape[0]
+        pot = np.zeros(m, dtype=np.float64) if want == nat.WANT_POT else None
+        acc = np.zeros((m, 3), dtype=np.float64) if want == nat.WANT_ACC else None
+        nat.call("pbx_octree_at_points", self._h, nat.vptr(pts), m, float(theta), want,
+                 nat.vptr(pot), nat.vptr(acc), 0)
+        return pot if want == nat.WANT_POT else acc
+
+    def accelerations_at_points(self, points, theta, threads=0):
+        return self._at_points(points, theta, threads, nat.WANT_ACC, "accelerations_at_points")
+
+    def potentials_at_points(self, points, theta, threads=0):
+        return self._at_points(points, theta, threads, nat.WANT_POT, "potentials_at_points")
+
+    # -- device-resident form (bench) --------------------------------------
+    def _compute_device(self, theta, want, d_pot=None, d_acc=None):
+        nat.call("pbx_octree_compute", self._h, float(theta), int(want), d_pot, d_acc, 1)
+
+    # -- introspection -----------------------------------------------------
+    def info(self) -> dict:
+        out = np.zeros(8, dtype=np.int64)
+        nat.call("pbx_octree_info", self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+        keys = ("n", "nodes", "levels", "has_mass_payload", "has_hmax", "node_interactions",
+                "leaf_pairs", "path_words")
+        return {k: int(v) for k, v in zip(keys, out)}
+
+    def export(self) -> dict:
+        """Node arrays (device breadth-first numbering) for parity tests."""
+        inf = self.info()
+        nn, n = inf["nodes"], inf["n"]
+        i64 = ctypes.POINTER(ctypes.c_int64)
+        d = dict(center=np.zeros((nn, 4)), com=np.zeros((nn, 4)) if inf["has_mass_payload"] else None,
+                 hmax=np.zeros(nn) if inf["has_hmax"] else None,
+                 links=np.zeros((nn, 3), dtype=np.int64), leaf=np.zeros((nn, 2), dtype=np.int64),
+                 perm=np.zeros(n, dtype=np.int64))
+        nat.call("pbx_octree_export", self._h, nat.dptr(d["center"]), nat.dptr(d["com"]),
+                 nat.dptr(d["hmax"]), d["links"].ctypes.data_as(i64),
+                 d["leaf"].ctypes.data_as(i64), d["perm"].ctypes.data_as(i64), None)
+        return d
+
+    def export_moments(self, ncoef: int) -> np.ndarray:
+        nn = self.info()["nodes"]
+        out = np.zeros((nn, ncoef))
+        nat.call("pbx_octree_export", self._h, None, None, None, None, None, None, nat.dptr(out))
+        return out
+
+
 __all__ = [
+    "Octree",
     "direct_accelerations_py",
     "direct_potentials_py",
     "direct_accelerations_at_points_py",

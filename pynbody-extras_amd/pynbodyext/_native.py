@@ -76,6 +76,17 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_pack_sources": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "pbx_direct_dev": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                c_int64, c_int, c_int, c_void_p, c_void_p]),
+    "pbx_octree_create": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                  c_int, POINTER(c_void_p)]),
+    "pbx_octree_destroy": (c_int, [c_void_p]),
+    "pbx_octree_build_mass": (c_int, [c_void_p, c_void_p, c_int]),
+    "pbx_octree_set_softenings": (c_int, [c_void_p, c_void_p, c_int]),
+    "pbx_octree_set_kernel": (c_int, [c_void_p, c_int]),
+    "pbx_octree_compute": (c_int, [c_void_p, c_double, c_int, c_void_p, c_void_p, c_int]),
+    "pbx_octree_at_points": (c_int, [c_void_p, c_void_p, c_int64, c_double, c_int, c_void_p,
+                                     c_void_p, c_int]),
+    "pbx_octree_info": (c_int, [c_void_p, _i64p]),
+    "pbx_octree_export": (c_int, [c_void_p, _dp, _dp, _dp, _i64p, _i64p, _i64p, _dp]),
     "pbx_profile_create": (c_int, [POINTER(c_void_p)]),
     "pbx_profile_destroy": (c_int, [c_void_p]),
     "pbx_profile_set_x": (c_int, [c_void_p, _dp, c_int64]),
@@ -146,6 +157,13 @@ def dptr(a: np.ndarray | None):
     if a is None:
         return None
     return a.ctypes.data_as(_dp)
+
+
+def vptr(a: np.ndarray | None):
+    """void* of a C-contiguous array (or NULL)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(c_void_p)
 
 
 def device_count() -> int:

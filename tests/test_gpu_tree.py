@@ -1,0 +1,264 @@
+"""GPU parity of the Barnes–Hut octree (csrc/tree.hip) against the oracle
+restatement of tree.rs / multipole.rs (oracle/tree_ref.c).
+
+What is checked, per case:
+  * geometry: the device tree equals the reference tree node for node in
+    DFS order — bit-exact centres/half sizes, identical leaf index lists
+    (ascending), bit-exact BH payload (mass, COM) and h_max;
+  * moments: multipole moments within 1e-12 of the oracle's (P2M/M2M are
+    computed with different (binomial) formulas);
+  * decisions: the accepted-node and leaf-pair totals of the walk equal the
+    oracle's, i.e. every target made the reference's opening decisions;
+  * values: per particle |dphi|/|phi| <= 1e-5 and ||da||/||a|| <= 1e-5 (the
+    contract), plus a tight 1e-9 bound (decisions identical => only
+    rounding differs).
+"""
+import numpy as np
+import pytest
+
+from oracle import gravity as og
+from oracle import tree as ot
+from pynbodyext import _engine
+from pynbodyext.gravity import Gravity
+from pynbodyext.synthetic import plummer
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+TIGHT = 1e-9
+NCOEF = {2: 10, 3: 20, 4: 35, 5: 56}
+
+
+def rel_pot(a, b):
+    return float(np.max(np.abs(a - b) / np.abs(b))) if len(b) else 0.0
+
+
+def rel_acc(a, b):
+    if not len(b):
+        return 0.0
+    return float(np.max(np.linalg.norm(a - b, axis=1) / np.linalg.norm(b, axis=1)))
+
+
+def preorder(first, nxt):
+    out, k = [], 0
+    while k != -1:
+        out.append(k)
+        k = first[k] if first[k] != -1 else nxt[k]
+    return np.array(out, dtype=np.int64)
+
+
+def check_structure(dev: _engine.Octree, ref: ot.RefOctree, order: int, masses=True):
+    d, r = dev.export(), ref.export()
+    do = preorder(d["links"][:, 0], d["links"][:, 1])
+    ro = preorder(r["first"], r["next"])
+    assert len(do) == len(ro) == dev.info()["nodes"] == ref.num_nodes
+    assert np.array_equal(d["center"][do, :3], r["center"][ro])
+    assert np.array_equal(d["center"][do, 3], r["half"][ro])
+    dleaf = d["links"][do, 0] == -1
+    rleaf = r["leaf_off"][ro] >= 0
+    assert np.array_equal(dleaf, rleaf)
+    for a, b in zip(do[dleaf], ro[rleaf]):
+        s, c = d["leaf"][a]
+        ids_d = d["perm"][s:s + c]
+        ids_r = r["perm"][r["leaf_off"][b]:r["leaf_off"][b] + r["leaf_len"][b]]
+        assert np.array_equal(ids_d, ids_r)
+    if d["com"] is not None:
+        assert np.array_equal(d["com"][do, 3], r["mass"][ro])
+        assert np.array_equal(d["com"][do, :3], r["com"][ro])
+    if r["hmax"] is not None:
+        assert np.array_equal(d["hmax"][do], r["hmax"][ro])
+    P = min(order, 5)
+    if P >= 2 and d["com"] is not None:
+        md = dev.export_moments(NCOEF[P])[do]
+        mr = r["mom"][ro][:, :NCOEF[P]]
+        # each moment is a sum of products of masses and |x|^k: scale by the
+        # node's mass * size^k
+        size = (2 * r["half"][ro])[:, None]
+        deg = np.array([[0, 1, 1, 1, 2, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3] + [4] * 15 +
+                        [5] * 21][0][:NCOEF[P]])
+        scale = np.abs(r["mass"][ro])[:, None] * size ** deg[None, :] + 1e-300
+        assert np.max(np.abs(md - mr) / scale) < 1e-12
+
+
+def check_walk(dev, ref, theta, n):
+    pot_d = dev.compute_potentials(theta)
+    cnt_d = dev.info()
+    acc_d = dev.compute_accelerations(theta)
+    pot_r, acc_r, nn_r, np_r = ref.compute_subset(np.arange(n), theta)
+    assert cnt_d["node_interactions"] == int(nn_r.sum())
+    assert cnt_d["leaf_pairs"] == int(np_r.sum())
+    rp, ra = rel_pot(pot_d, pot_r), rel_acc(acc_d, acc_r)
+    assert rp < TOL and ra < TOL
+    assert rp < TIGHT and ra < TIGHT, (rp, ra)
+
+
+def uniform(n, seed):
+    return np.random.default_rng(seed).random((n, 3)) - 0.5
+
+
+@pytest.mark.parametrize("order", [0, 1, 2, 3, 4, 5])
+def test_plummer_orders(gpu, order):
+    pos, mass = plummer(20_000, seed=70 + order)
+    dev = _engine.Octree(pos, mass, 8, order)
+    ref = ot.RefOctree(pos, mass, 8, order)
+    check_structure(dev, ref, order)
+    check_walk(dev, ref, 0.5, len(pos))
+
+
+@pytest.mark.parametrize("leaf", [1, 3, 32, 100])
+def test_leaf_capacities(gpu, leaf):
+    pos = uniform(6000, leaf)
+    mass = 0.5 + np.random.default_rng(leaf).random(6000)
+    dev = _engine.Octree(pos, mass, leaf, 3)
+    ref = ot.RefOctree(pos, mass, leaf, 3)
+    check_structure(dev, ref, 3)
+    check_walk(dev, ref, 0.7, len(pos))
+
+
+def test_unit_masses_build_mass_later(gpu):
+    pos = uniform(5000, 9)
+    dev = _engine.Octree(pos, None, 16, 2)
+    with pytest.raises(ValueError, match="call build_mass\\(\\) before compute_potentials"):
+        dev.compute_potentials(0.5)
+    with pytest.raises(ValueError, match="before accelerations_at_points"):
+        dev.accelerations_at_points(pos[:3].copy(), 0.5)
+    dev.build_mass()
+    ref = ot.RefOctree(pos, None, 16, 2, tree3d=True)
+    check_structure(dev, ref, 2)
+    check_walk(dev, ref, 0.6, len(pos))
+    # new masses through build_mass(masses)
+    m2 = np.random.default_rng(3).random(5000)
+    dev.build_mass(m2)
+    ref.build_mass(m2)
+    check_structure(dev, ref, 2)
+    check_walk(dev, ref, 0.6, len(pos))
+
+
+@pytest.mark.parametrize("kernel", [0, 1])
+def test_softened(gpu, kernel):
+    pos, mass = plummer(12_000, seed=11)
+    h = 0.005 + 0.02 * np.random.default_rng(12).random(len(pos))
+    dev = _engine.Octree(pos, mass, 8, 3, h, kernel)
+    ref = ot.RefOctree(pos, mass, 8, 3, softenings=h, kernel=kernel)
+    check_structure(dev, ref, 3)
+    check_walk(dev, ref, 0.5, len(pos))
+    # set_kernel keeps h_max, changes the kernel (tree.rs:784-786)
+    dev.set_kernel(1 - kernel)
+    ref.set_kernel(1 - kernel)
+    check_walk(dev, ref, 0.5, len(pos))
+    # set_softenings(None) keeps the build-time h_max guard (tree.rs:777-782)
+    dev.set_softenings(None)
+    ref.set_softenings(None)
+    check_walk(dev, ref, 0.5, len(pos))
+    # and new softenings without a rebuild
+    h2 = 0.5 * h
+    dev.set_softenings(h2)
+    ref.set_softenings(h2)
+    check_walk(dev, ref, 0.5, len(pos))
+
+
+def test_at_points(gpu):
+    pos, mass = plummer(15_000, seed=21)
+    q = plummer(3000, seed=22)[0] * 1.3
+    q[:10] = pos[:10]  # coincident with particles: no self skip at points
+    dev = _engine.Octree(pos, mass, 8, 3)
+    ref = ot.RefOctree(pos, mass, 8, 3)
+    pd, pr = dev.potentials_at_points(q, 0.5), ref.potentials_at_points(q, 0.5)
+    ad, ar = dev.accelerations_at_points(q, 0.5), ref.accelerations_at_points(q, 0.5)
+    finite = np.arange(len(q)) >= 10
+    assert rel_pot(pd[finite], pr[finite]) < TIGHT
+    assert rel_acc(ad[finite], ar[finite]) < TIGHT
+    # coincident: -m/sqrt(R2_TINY) ~ -6.7e153 m dominates the potential and the
+    # force term is (m*0)*inf = NaN, in the reference (tree.rs:313-318) as here
+    assert np.all(pd[:10] < -1e140) and np.allclose(pd[:10], pr[:10], rtol=1e-9)
+    assert np.array_equal(np.isnan(ad[:10]), np.isnan(ar[:10]))
+
+
+def test_theta0_equals_direct(gpu):
+    pos, mass = plummer(3000, seed=31)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    assert rel_pot(dev.compute_potentials(0.0), og.direct_potentials(pos, mass)) < 1e-12
+    assert rel_acc(dev.compute_accelerations(0.0), og.direct_accelerations(pos, mass)) < 1e-12
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 8, 9])
+def test_small_n(gpu, n):
+    pos = uniform(n, 40 + n)
+    mass = np.ones(n)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    pot = dev.compute_potentials(0.5)
+    acc = dev.compute_accelerations(0.5)
+    assert pot.shape == (n,) and acc.shape == (n, 3)
+    if n >= 2:
+        ref = ot.RefOctree(pos, mass, 8, 3)
+        check_structure(dev, ref, 3)
+        check_walk(dev, ref, 0.5, n)
+    elif n == 1:
+        assert pot.tolist() == [0.0] and acc.tolist() == [[0.0, 0.0, 0.0]]
+    assert dev.potentials_at_points(np.zeros((2, 3)), 0.5).shape == (2,)
+
+
+def test_coincident_cluster(gpu):
+    # 30 particles on one point (> leaf capacity): the reference recurses
+    # forever; oracle and device both stop splitting there.
+    pos = uniform(2000, 50)
+    pos[100:130] = pos[100]
+    mass = np.ones(2000)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    ref = ot.RefOctree(pos, mass, 8, 3)
+    check_structure(dev, ref, 3)
+    pd, pr = dev.compute_potentials(0.5), ref.compute_potentials(0.5)
+    assert rel_pot(pd, pr) < TIGHT
+
+
+def test_deep_tree_needs_more_path_words(gpu):
+    # two clusters 1e-14 apart at O(1) coordinates: > 42 levels
+    pos = uniform(400, 60)
+    pos[:20] = 0.25 + 1e-15 * np.arange(20)[:, None]
+    mass = np.ones(400)
+    dev = _engine.Octree(pos, mass, 4, 3)
+    ref = ot.RefOctree(pos, mass, 4, 3)
+    assert dev.info()["path_words"] >= 3
+    check_structure(dev, ref, 3)
+    assert rel_pot(dev.compute_potentials(0.5), ref.compute_potentials(0.5)) < TIGHT
+
+
+def test_errors(gpu):
+    pos = uniform(10, 1)
+    with pytest.raises(ValueError, match="masses must be length N"):
+        _engine.Octree(pos, np.ones(3))
+    with pytest.raises(ValueError, match="softenings require an explicit kernel"):
+        _engine.Octree(pos, np.ones(10), 8, 3, np.ones(10))
+    with pytest.raises(ValueError, match="kernel must be 0"):
+        _engine.Octree(pos, np.ones(10), 8, 3, None, 2)
+    with pytest.raises(TypeError):
+        _engine.Octree(pos.astype(np.float32))
+    with pytest.raises(OverflowError):
+        _engine.Octree(pos, None, 8, 300)
+    t = _engine.Octree(pos, np.ones(10))
+    with pytest.raises(ValueError, match="points must be \\(N,3\\) float64 array"):
+        t.potentials_at_points(np.zeros(4).reshape(2, 2), 0.5)
+
+
+def test_gravity_front_end(gpu):
+    pos, mass = plummer(8000, seed=81)
+    g = Gravity(pos, mass)
+    pot = g.tree_potentials(theta=0.5)
+    acc = g.tree_accelerations(theta=0.5)
+    ref = ot.RefOctree(pos, mass, 8, 3)  # TreeOptions defaults (base.py:82-100)
+    assert rel_pot(pot, ref.compute_potentials(0.5)) < TIGHT
+    assert rel_acc(acc, ref.compute_accelerations(0.5)) < TIGHT
+
+
+def test_1m_subset(gpu):
+    """1M Plummer, theta 0.5, leaf 8, order 3: full structure + 8192 targets."""
+    pos, mass = plummer(1_000_000, seed=1002)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    ref = ot.RefOctree(pos, mass, 8, 3)
+    check_structure(dev, ref, 3)
+    pot = dev.compute_potentials(0.5)
+    acc = dev.compute_accelerations(0.5)
+    idx = np.random.default_rng(0).choice(len(pos), 8192, replace=False)
+    idx = np.concatenate([idx, np.argsort((pos * pos).sum(1))[:64]])
+    pr, ar, _, _ = ref.compute_subset(idx, 0.5)
+    assert rel_pot(pot[idx], pr) < TIGHT and rel_acc(acc[idx], ar) < TIGHT
