@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Benchmark of the MI355X direct-sum gravity hot path (BASELINE.json config 2/4).
+"""Benchmark of the MI355X gravity + profile hot path (BASELINE.json configs 2-5).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -56,6 +56,8 @@ def parse():
                     help="skip the radial-profile leg (config 3)")
     ap.add_argument("--profile-sizes", default="1000000,16000000,64000000",
                     help="comma-separated particle counts of the profile size sweep")
+    ap.add_argument("--no-tree", action="store_true", help="skip the Barnes-Hut leg (config 5)")
+    ap.add_argument("--tree-n", type=int, default=4_000_000)
     return ap.parse_args()
 
 
@@ -203,6 +205,132 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool):
     return out
 
 
+TREE_FLOP_NODE = 231  # order-3 force+potential node interaction incl. opening test (ISA count, FMA = 2)
+TREE_FLOP_PP = 22     # leaf pair, same algorithmic count as the direct sum
+
+
+def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc):
+    """Oracle restatement of tree.rs (serial build + payload like the
+    reference, OpenMP walk over a bounded random target sample); returns the
+    extrapolated full-solve rate in effective pairs/s and the parity of the
+    GPU values on the sampled targets."""
+    from oracle import gravity as og
+    from oracle import tree as ot
+
+    cores = min(16, os.cpu_count() or 1)
+    og.set_num_threads(cores)
+    n = len(pos)
+    rng = np.random.default_rng(0)
+    t0 = time.perf_counter()
+    ref = ot.RefOctree(pos, mass, 8, 3)
+    t_build = time.perf_counter() - t0
+    probe = rng.choice(n, size=64 * cores, replace=False)
+    t0 = time.perf_counter()
+    ref.compute_subset(probe, theta)
+    per_target = (time.perf_counter() - t0) / len(probe)
+    k = int(min(n, max(len(probe), max(seconds - t_build, 1.0) / max(per_target, 1e-12))))
+    idx = rng.choice(n, size=k, replace=False)
+    t0 = time.perf_counter()
+    pot, acc, _, _ = ref.compute_subset(idx, theta)
+    t_walk = time.perf_counter() - t0
+    t_full = t_build + t_walk * n / k
+    rp = float(np.max(np.abs(gpu_pot[idx] - pot) / np.abs(pot)))
+    ra = float(np.max(np.linalg.norm(gpu_acc[idx] - acc, axis=1) / np.linalg.norm(acc, axis=1)))
+    return {
+        "value": float(n) * float(n - 1) / t_full,
+        "unit": "effective pairs/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"oracle/tree_ref.c: serial build+payload of all {n} particles ({t_build:.1f} s) + "
+                  f"walk of {k} random targets on {cores} OpenMP threads ({t_walk:.1f} s), "
+                  f"full solve extrapolated to {t_full:.1f} s",
+    }, {"targets_checked": k, "pot_max_rel": rp, "acc_max_rel": ra}
+
+
+def bench_tree(n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: float):
+    """Config 5: Barnes-Hut tree (theta=0.5, leaf 8, order 3 = Gravity's
+    TreeOptions defaults, base.py:82-100) force + potential of an n-particle
+    Plummer sphere resident in HBM, then the 256-bin log radial profile
+    (0.01..50) of the mass-weighted potential.  One step = device octree build
+    + mass/multipole payload + walk (all particles, self skipped) + profile
+    (r, bin assignment, per-bin sums of m and m*phi)."""
+    from pynbodyext._engine import Octree
+    from pynbodyext.profiles._device import SRC_W, DeviceBins
+
+    theta = 0.5
+    pos, mass = plummer(n, seed=SEEDS.get(n, 1003))
+    d_pos = nat.DeviceArray.from_host(pos)
+    d_mass = nat.DeviceArray.from_host(mass)
+    d_pot = nat.DeviceArray(8 * n)
+    d_acc = nat.DeviceArray(24 * n)
+    edges = np.logspace(np.log10(0.01), np.log10(50.0), 257)
+    prof = DeviceBins()
+    ev = [nat.Event() for _ in range(4)]
+
+    def step():
+        ev[0].record()
+        tree = Octree._from_device(d_pos.ptr, n, d_mass.ptr, 8, 3)
+        ev[1].record()
+        tree._compute_device(theta, nat.WANT_POT | nat.WANT_ACC, d_pot.ptr, d_acc.ptr)
+        ev[2].record()
+        DeviceBins.select(d_pos.ptr, d_mass.ptr, ndim=3, on_device=True, n=n, into=prof)
+        prof.assign(edges)
+        mom = prof.moments(d_pot, SRC_W)
+        ev[3].record()
+        info = tree.info()
+        tree.close()
+        return mom, info
+
+    for _ in range(warmup):
+        step()
+    nat.synchronize()
+    wall, parts = [], []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        mom, info = step()
+        nat.synchronize()
+        wall.append(time.perf_counter() - t0)
+        parts.append([ev[i].elapsed_ms(ev[i + 1]) for i in range(3)])
+    t = float(np.median(wall))
+    build_ms, walk_ms, prof_ms = (float(np.median([p[i] for p in parts])) for i in range(3))
+    flops = info["node_interactions"] * TREE_FLOP_NODE + info["leaf_pairs"] * TREE_FLOP_PP
+    achieved = flops / (walk_ms * 1e-3) / 1e12
+    pot = np.empty(n)
+    acc = np.empty((n, 3))
+    d_pot.download(pot)
+    d_acc.download(acc)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        phi_profile = mom[:, 1] / mom[:, 0]
+    out = {
+        "metric": "effective particle-pairs/sec (Barnes-Hut force+potential + 256-bin potential profile)",
+        "value": float(n) * float(n - 1) / t,
+        "unit": "effective pairs/s",
+        "ms_per_step": t * 1e3,
+        "config": {"workload": f"{n}-particle Plummer sphere, octree theta=0.5 leaf 8 multipole "
+                               "order 3 (Newtonian), force+potential at every particle, then "
+                               "RadialProfile log 256 bins [0.01, 50] of the mass-weighted potential",
+                   "n_particles": n, "nodes": info["nodes"], "levels": info["levels"]},
+        "phases_ms": {"build_and_payload": build_ms, "walk": walk_ms, "profile": prof_ms},
+        "interactions": {"node": info["node_interactions"], "leaf_pairs": info["leaf_pairs"],
+                         "per_particle": (info["node_interactions"] + info["leaf_pairs"]) / n},
+        "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_VECTOR_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
+                     "traffic": None, "kernel": "walk_kernel<order 3, pot+acc>",
+                     "flop_per_node": TREE_FLOP_NODE, "flop_per_leaf_pair": TREE_FLOP_PP,
+                     "kernel_ms": walk_ms},
+        "profile_check": {"bins_nonempty": int(np.sum(mom[:, 0] > 0)),
+                          "phi_innermost_bin": float(phi_profile[mom[:, 0] > 0][0]),
+                          "phi_outermost_bin": float(phi_profile[mom[:, 0] > 0][-1])},
+    }
+    if cpu:
+        out["cpu_baseline"], out["parity_vs_oracle"] = tree_cpu_baseline(
+            pos, mass, cpu_seconds, theta, pot, acc)
+    prof.close()
+    for a in (d_pos, d_mass, d_pot, d_acc):
+        a.free()
+    return out
+
+
 def pmc_traffic():
     """HBM bytes per launch of the direct-sum kernel from the committed
     rocprofv3 PMC summary (profiles/), or None."""
@@ -336,6 +464,9 @@ def main():
             "sweep": sweep,
             "cpu_baseline": head.get("cpu_baseline"),
         }
+    if not args.no_tree and world == 1:
+        out["tree"] = bench_tree(args.tree_n, steps=max(3, args.steps), warmup=1,
+                                 cpu=not args.no_cpu_baseline, cpu_seconds=args.cpu_seconds)
     print(json.dumps(out), flush=True)
 
 

@@ -215,7 +215,9 @@ int pbx_profile_assign(void *handle, const double *h_edges, int64_t n_edges,
 int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets);
 /* per-bin sums h_out[nb][7] = {Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|};
  * f_src / w_src: 0 = x, 1 = selection weights, 2 = host array (h_f / h_w,
- * n doubles); w_src = -1: unweighted */
+ * n doubles in selection order), 3 = device array indexed by ORIGINAL
+ * particle (gathered through the selection, e.g. a tree potential left in
+ * HBM by pbx_octree_compute); w_src = -1: unweighted */
 int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src,
                         const double *h_w, double *h_out);
 

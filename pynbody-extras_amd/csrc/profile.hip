@@ -330,6 +330,12 @@ __global__ void __launch_bounds__(TPB) reduce_slab(const double *__restrict__ sl
   }
 }
 
+__global__ void gather_by_idx(const double *__restrict__ src, const int32_t *__restrict__ idx,
+                              int64_t n, double *__restrict__ dst) {
+  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t < n) dst[t] = src[idx[t]];
+}
+
 __global__ void widen_perm(const int32_t *__restrict__ p, int64_t n, int64_t *__restrict__ out) {
   int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (t < n) out[t] = p[t];
@@ -746,6 +752,15 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, c
         if (!hp && n) fail(PBX_ERR_VALUE, "host array is NULL");
         double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
         if (n) PBX_HIP(hipMemcpyAsync(dp, hp, sizeof(double) * n, hipMemcpyHostToDevice, st));
+        return dp;
+      }
+      if (which == 3) {  // device array per ORIGINAL particle (e.g. a tree potential)
+        if (!hp && n) fail(PBX_ERR_VALUE, "device array is NULL");
+        if (!P.has_idx) return hp;
+        double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
+        if (n)
+          hipLaunchKernelGGL(gather_by_idx, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st, hp,
+                             (const int32_t *)P.idx.p, n, dp);
         return dp;
       }
       fail(PBX_ERR_VALUE, "bad source selector %d", which);

@@ -98,7 +98,7 @@ _SIGNATURES: dict[str, tuple] = {
                                          _i64p]),
     "pbx_profile_assign": (c_int, [c_void_p, _dp, c_int64, _i64p, _i64p]),
     "pbx_profile_csr": (c_int, [c_void_p, _i64p, _i64p]),
-    "pbx_profile_moments": (c_int, [c_void_p, c_int, _dp, c_int, _dp, _dp]),
+    "pbx_profile_moments": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, _dp]),
     "pbx_comm_unique_id_size": (c_int, []),
     "pbx_comm_unique_id": (c_int, [c_char_p, c_int]),
     "pbx_comm_init": (c_int, [POINTER(c_void_p), c_int, c_int, c_char_p]),

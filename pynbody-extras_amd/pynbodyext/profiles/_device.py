@@ -15,7 +15,7 @@ import numpy as np
 from .. import _native as nat
 
 NMOM = 7  # Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|
-SRC_X, SRC_W, SRC_HOST, SRC_NONE = 0, 1, 2, -1
+SRC_X, SRC_W, SRC_HOST, SRC_DEVICE, SRC_NONE = 0, 1, 2, 3, -1
 
 _i64p = ctypes.POINTER(c_int64)
 
@@ -166,6 +166,8 @@ class DeviceBins:
         def src(v):
             if isinstance(v, (int, np.integer)) and not isinstance(v, bool):
                 return int(v), None
+            if isinstance(v, nat.DeviceArray):  # per original particle, in HBM
+                return SRC_DEVICE, v.ptr
             a = np.ascontiguousarray(np.asarray(v), dtype=np.float64).reshape(-1)
             if a.shape[0] != self.n:
                 raise ValueError(f"array length {a.shape[0]} != {self.n}")
@@ -174,7 +176,10 @@ class DeviceBins:
         fs, fa = src(field)
         ws, wa = src(weights) if weights is not None else (SRC_NONE, None)
         out = np.zeros((self.nbins, NMOM))
-        nat.call("pbx_profile_moments", self._h, fs, nat.dptr(fa), ws, nat.dptr(wa), nat.dptr(out))
+        def ptr(a):
+            return a if isinstance(a, ctypes.c_void_p) else nat.vptr(a)
+
+        nat.call("pbx_profile_moments", self._h, fs, ptr(fa), ws, ptr(wa), nat.dptr(out))
         return out
 
     def close(self) -> None:
