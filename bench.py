@@ -205,7 +205,7 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool):
     return out
 
 
-TREE_FLOP_NODE = 231  # order-3 force+potential node interaction incl. opening test (ISA count, FMA = 2)
+TREE_FLOP_NODE = 94   # order-3 force+potential node interaction incl. opening test (ISA count, FMA = 2)
 TREE_FLOP_PP = 22     # leaf pair, same algorithmic count as the direct sum
 
 
@@ -312,7 +312,9 @@ def bench_tree(n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: float):
                    "n_particles": n, "nodes": info["nodes"], "levels": info["levels"]},
         "phases_ms": {"build_and_payload": build_ms, "walk": walk_ms, "profile": prof_ms},
         "interactions": {"node": info["node_interactions"], "leaf_pairs": info["leaf_pairs"],
-                         "per_particle": (info["node_interactions"] + info["leaf_pairs"]) / n},
+                         "per_particle": (info["node_interactions"] + info["leaf_pairs"]) / n,
+                         "simd_lane_efficiency": info["active_lane_steps"] /
+                         max(1, 64 * info["wave_steps"])},
         "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_VECTOR_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
                      "traffic": None, "kernel": "walk_kernel<order 3, pot+acc>",

@@ -162,9 +162,10 @@ int pbx_octree_compute(pbx_octree *tree, double theta, int want, double *pot,
 int pbx_octree_at_points(pbx_octree *tree, const double *points, int64_t m,
                          double theta, int want, double *pot, double *acc,
                          int on_device);
-/* out[8] = {n, nodes, levels, has_mass_payload, has_hmax,
- *           accepted node interactions and leaf pairs of the last walk,
- *           path words} */
+/* out[10] = {n, nodes, levels, has_mass_payload, has_hmax,
+ *            accepted node interactions and leaf pairs of the last walk,
+ *            path words, wave steps and active-lane steps of the last walk
+ *            (SIMD efficiency = active / (64 * steps))} */
 int pbx_octree_info(pbx_octree *tree, int64_t *out);
 /* Node arrays for parity tests (any pointer may be NULL), node ids in the
  * device's breadth-first numbering:

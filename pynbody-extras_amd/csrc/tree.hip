@@ -616,6 +616,56 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
   if (v.hmax) v.hmax[k] = hm;
 }
 
+// Detraced evaluation coefficients (orders 2 and 3).  With raw moments
+// M_lmn = sum m x^l y^m z^n / (l! m! n!) and S^(n) = sum m x^(n-fold), the
+// order-n part of the reference's sum_k M_k D_k(R) is
+//   (1/n!) S^(n) : grad^n (1/r) = (1/n!) (-1)^n (2n-1)!! r^-(2n+1) T[S^(n)] : R^n
+// because grad^n (1/r) is the detraced tensor (-1)^n (2n-1)!! T[R^n] / r^(2n+1)
+// and T is an orthogonal projection.  Per node we store
+//   Q' = 3/2 T[S2]           (xx, yy, zz, xy, xz, yz)
+//   K' = 5/2 T[S3] with each component times its multinomial weight
+//        (x^3, x^2y, x^2z, xy^2, xyz, xz^2, y^3, y^2z, yz^2, z^3)
+// so phi = -M/r - q2'/r^5 + q3'/r^7 with q2' = R.Q'.R and q3' = K'(R).
+__host__ __device__ constexpr int ncoef_fast(int P) { return P == 3 ? 16 : (P == 2 ? 6 : 0); }
+
+template <int P>
+__global__ void pack_coef(const double *__restrict__ mom, int64_t nn, double *__restrict__ coef) {
+  int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k >= nn) return;
+  const double *M = mom + k * ncoef(P);
+  double *C = coef + k * ncoef_fast(P);
+  const double sxx = 2.0 * M[4], syy = 2.0 * M[5], szz = 2.0 * M[6];
+  const double tr3 = (sxx + syy + szz) * (1.0 / 3.0);
+  C[0] = 1.5 * (sxx - tr3);
+  C[1] = 1.5 * (syy - tr3);
+  C[2] = 1.5 * (szz - tr3);
+  C[3] = 1.5 * M[7];  // xy
+  C[4] = 1.5 * M[8];  // xz
+  C[5] = 1.5 * M[9];  // yz
+  if constexpr (P == 3) {
+    // S_ijk = l! m! n! M_lmn
+    const double sxxx = 6.0 * M[10], syyy = 6.0 * M[11], szzz = 6.0 * M[12];
+    const double sxxy = 2.0 * M[13], sxxz = 2.0 * M[14], sxyy = 2.0 * M[15];
+    const double sxzz = 2.0 * M[16], syyz = 2.0 * M[17], syzz = 2.0 * M[18];
+    const double sxyz = M[19];
+    const double tx = sxxx + sxyy + sxzz, ty = sxxy + syyy + syzz, tz = sxxz + syyz + szzz;
+    // T[S3]_ijk = S_ijk - (d_ij t_k + d_ik t_j + d_jk t_i) / 5
+    const double oxxx = sxxx - 0.6 * tx, oyyy = syyy - 0.6 * ty, ozzz = szzz - 0.6 * tz;
+    const double oxxy = sxxy - 0.2 * ty, oxxz = sxxz - 0.2 * tz, oxyy = sxyy - 0.2 * tx;
+    const double oxzz = sxzz - 0.2 * tx, oyyz = syyz - 0.2 * tz, oyzz = syzz - 0.2 * ty;
+    C[6] = 2.5 * oxxx;         // x^3
+    C[7] = 2.5 * 3.0 * oxxy;   // x^2 y
+    C[8] = 2.5 * 3.0 * oxxz;   // x^2 z
+    C[9] = 2.5 * 3.0 * oxyy;   // x y^2
+    C[10] = 2.5 * 6.0 * sxyz;  // x y z
+    C[11] = 2.5 * 3.0 * oxzz;  // x z^2
+    C[12] = 2.5 * oyyy;        // y^3
+    C[13] = 2.5 * 3.0 * oyyz;  // y^2 z
+    C[14] = 2.5 * 3.0 * oyzz;  // y z^2
+    C[15] = 2.5 * ozzz;        // z^3
+  }
+}
+
 // ------------------------------------------------------------------- walk
 struct alignas(16) WalkNode {  // 64 bytes, read with scalar loads
   double cx, cy, cz, mass;     // centre of mass, mass
@@ -651,7 +701,8 @@ __global__ void pack_walk(const double4 *__restrict__ com, const double4 *__rest
 
 struct WalkParams {
   const WalkNode *nodes;
-  const double *mom;        // ncoef(P) per node (P >= 2)
+  const double *mom;        // ncoef(P) per node (P >= 4)
+  const double *coef;       // ncoef_fast(P) detraced coefficients per node (P = 2, 3)
   const double4 *rec;       // sources in leaf order
   const double *soft;       // sorted softenings (softenings set) or null
   const double *tgt;        // (m, 3) query points; null => targets are the sources
@@ -691,7 +742,7 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
   }
   const bool has_th = SOFT && self_mode && wp.soft != nullptr;
   double ph = 0.0, ax = 0.0, ay = 0.0, az = 0.0;
-  unsigned long long n_node = 0, n_pp = 0;
+  unsigned long long n_node = 0, n_pp = 0, n_active = 0;
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
   int64_t steps = 0;           // the wave moves strictly forward in DFS order
@@ -702,6 +753,7 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
     }
     const WalkNode nd = wp.nodes[w];
     const bool act = (p == w);
+    n_active += (unsigned long long)__popcll(__ballot(act));  // SIMD efficiency counter
     if (nd.mass == 0.0) {  // tree.rs:1087-1090
       if (act) p = nd.next;
       w = nd.next;
@@ -786,6 +838,42 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
               ay = __builtin_fma(-nd.mass, D[2], ay);
               az = __builtin_fma(-nd.mass, D[3], az);
             }
+          } else if constexpr (P == 2 || P == 3) {
+            // detraced evaluation (see pack_coef): u = 1/r,
+            //   phi = -M u - u^5 q2' + u^7 q3',  q2' = R.Q'.R, q3' = K'(R)
+            //   a   = (M u^3 + 5 q2' u^7) R - 2 u^5 Q'.R
+            const double *C = wp.coef + (int64_t)w * ncoef_fast(P);
+            const double u = inv_r, u2 = u * u, u3 = u2 * u, u5 = u3 * u2;
+            const double qx = __builtin_fma(C[0], dx, __builtin_fma(C[3], dy, C[4] * dz));
+            const double qy = __builtin_fma(C[3], dx, __builtin_fma(C[1], dy, C[5] * dz));
+            const double qz = __builtin_fma(C[4], dx, __builtin_fma(C[5], dy, C[2] * dz));
+            const double q2 = __builtin_fma(dx, qx, __builtin_fma(dy, qy, dz * qz));
+            if (WANT & PBX_WANT_POT) {
+              double t = __builtin_fma(-u5, q2, -nd.mass * u);
+              if constexpr (P == 3) {
+                const double zz = dz * dz;
+                const double A = __builtin_fma(C[6], dx, __builtin_fma(C[7], dy, C[8] * dz));
+                const double B = __builtin_fma(C[9], dy, C[10] * dz);
+                const double X = __builtin_fma(dx, A, __builtin_fma(dy, B, C[11] * zz));
+                const double G = __builtin_fma(C[12], dy, C[13] * dz);
+                const double Y = __builtin_fma(dy, G, C[14] * zz);
+                const double q3 = __builtin_fma(dx, X, __builtin_fma(dy, Y, (C[15] * dz) * zz));
+                t = __builtin_fma(u5 * u2, q3, t);
+              }
+              ph += t;
+            }
+            if (WANT & PBX_WANT_ACC) {
+              // the order-P force uses moments up to P-1 (multipole.rs:1408-1528):
+              // order 2 -> monopole (+ the dipole, zero about the COM)
+              double c = nd.mass * u3, s = 0.0;
+              if constexpr (P == 3) {
+                c = __builtin_fma(5.0 * q2, u5 * u2, c);
+                s = -2.0 * u5;
+              }
+              ax = __builtin_fma(c, dx, __builtin_fma(s, qx, ax));
+              ay = __builtin_fma(c, dy, __builtin_fma(s, qy, ay));
+              az = __builtin_fma(c, dz, __builtin_fma(s, qz, az));
+            }
           } else {
             double D[ncoef(P)];
             derivs<P>(dx, dy, dz, inv_r, D);
@@ -817,6 +905,8 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
     if (threadIdx.x == 0) {
       atomicAdd(&wp.counters[0], n_node);
       atomicAdd(&wp.counters[1], n_pp);
+      atomicAdd(&wp.counters[3], (unsigned long long)steps);
+      atomicAdd(&wp.counters[4], n_active);
     }
   }
 }
@@ -839,9 +929,10 @@ struct Octree {
   Buf pos, mass, soft;       // original order (device copies)
   Buf perm, rec, soft_s;     // leaf order
   Buf nstart, ncount, nfirst, nnext, nchild, ncen;
-  Buf com, hmax, mom, walk;
+  Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
-  unsigned long long last_counts[3] = {0, 0, 0};  // nodes, leaf pairs, fault
+  // accepted nodes, leaf pairs, fault flag, wave steps, active-lane steps
+  unsigned long long last_counts[5] = {0, 0, 0, 0, 0};
   int moment_order() const { return order < 5 ? order : 5; }
 };
 
@@ -1100,6 +1191,11 @@ static void build_payload(Octree &T, hipStream_t st) {
     case 4: run_payload<4>(T, st, v); break;
     default: run_payload<5>(T, st, v); break;
   }
+  if (P == 2 || P == 3) {
+    double *cf = (double *)T.coef.get(8 * (size_t)T.nn * ncoef_fast(P));
+    if (P == 2) hipLaunchKernelGGL(pack_coef<2>, dim3(nblk(T.nn)), dim3(TPB), 0, st, v.mom, T.nn, cf);
+    else hipLaunchKernelGGL(pack_coef<3>, dim3(nblk(T.nn)), dim3(TPB), 0, st, v.mom, T.nn, cf);
+  }
   hipLaunchKernelGGL(pack_walk, dim3(nblk(T.nn)), dim3(TPB), 0, st, T.com.as<double4>(),
                      T.ncen.as<double4>(), v.hmax, T.nnext.as<int32_t>(), T.nfirst.as<int32_t>(),
                      T.nchild.as<int32_t>(), T.nstart.as<int32_t>(), T.ncount.as<int32_t>(), T.nn,
@@ -1128,12 +1224,13 @@ static void launch_walk_p(const WalkParams &wp, int want, bool soft, hipStream_t
 // outputs in original / query order
 static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t m, double *d_pot,
                  double *d_acc, hipStream_t st) {
-  unsigned long long *ctr = (unsigned long long *)T.counters.get(32);
-  PBX_HIP(hipMemsetAsync(ctr, 0, 32, st));
+  unsigned long long *ctr = (unsigned long long *)T.counters.get(64);
+  PBX_HIP(hipMemsetAsync(ctr, 0, 64, st));
   if (m == 0) return;
   WalkParams wp;
   wp.nodes = T.walk.as<WalkNode>();
   wp.mom = T.mom.as<double>();
+  wp.coef = T.coef.as<double>();
   wp.rec = T.rec.as<double4>();
   wp.tgt = d_tgt;
 
@@ -1245,7 +1342,7 @@ int pbx_octree_destroy(pbx_octree *t) {
     Octree *T = (Octree *)t;
     Buf *bufs[] = {&T->pos, &T->mass, &T->soft, &T->perm, &T->rec, &T->soft_s, &T->nstart,
                    &T->ncount, &T->nfirst, &T->nnext, &T->nchild, &T->ncen, &T->com, &T->hmax,
-                   &T->mom, &T->walk, &T->keys, &T->ktmp0, &T->ktmp1, &T->vtmp, &T->hist,
+                   &T->mom, &T->coef, &T->walk, &T->keys, &T->ktmp0, &T->ktmp1, &T->vtmp, &T->hist,
                    &T->tsum, &T->front0, &T->front1, &T->lb, &T->cnt, &T->flags, &T->small,
                    &T->counters};
     for (Buf *b : bufs) b->release();
@@ -1316,7 +1413,7 @@ int pbx_octree_compute(pbx_octree *t, double theta, int want, double *pot, doubl
       if (want & PBX_WANT_ACC) da = (double *)dev.slot(kSlotAcc).ensure(24 * (size_t)std::max<int64_t>(n, 1));
     }
     walk(T, theta, want, nullptr, n, dp, da, st);
-    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 24, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 40, hipMemcpyDeviceToHost, st));
     if (!on_device) {
       if (dp && n) PBX_HIP(hipMemcpyAsync(pot, dp, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
       if (da && n) PBX_HIP(hipMemcpyAsync(acc, da, 24 * (size_t)n, hipMemcpyDeviceToHost, st));
@@ -1354,7 +1451,7 @@ int pbx_octree_at_points(pbx_octree *t, const double *points, int64_t m, double 
     }
     // at points there is no target softening and no self skip
     walk(T, theta, want, dt, m, dp, da, st);
-    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 24, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 40, hipMemcpyDeviceToHost, st));
     if (!on_device) {
       if (dp && m) PBX_HIP(hipMemcpyAsync(pot, dp, 8 * (size_t)m, hipMemcpyDeviceToHost, st));
       if (da && m) PBX_HIP(hipMemcpyAsync(acc, da, 24 * (size_t)m, hipMemcpyDeviceToHost, st));
@@ -1376,6 +1473,8 @@ int pbx_octree_info(pbx_octree *t, int64_t *out) {
     out[5] = (int64_t)T.last_counts[0];
     out[6] = (int64_t)T.last_counts[1];
     out[7] = T.nwords;
+    out[8] = (int64_t)T.last_counts[3];
+    out[9] = (int64_t)T.last_counts[4];
   });
 }
 

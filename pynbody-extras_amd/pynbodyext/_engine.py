@@ -280,10 +280,10 @@ class Octree:
 
     # -- introspection -----------------------------------------------------
     def info(self) -> dict:
-        out = np.zeros(8, dtype=np.int64)
+        out = np.zeros(10, dtype=np.int64)
         nat.call("pbx_octree_info", self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
         keys = ("n", "nodes", "levels", "has_mass_payload", "has_hmax", "node_interactions",
-                "leaf_pairs", "path_words")
+                "leaf_pairs", "path_words", "wave_steps", "active_lane_steps")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def export(self) -> dict:
