@@ -627,13 +627,15 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
 //        (x^3, x^2y, x^2z, xy^2, xyz, xz^2, y^3, y^2z, yz^2, z^3)
 // so phi = -M/r - q2'/r^5 + q3'/r^7 with q2' = R.Q'.R and q3' = K'(R).
 __host__ __device__ constexpr int ncoef_fast(int P) { return P == 3 ? 16 : (P == 2 ? 6 : 0); }
+template <int P> __host__ __device__ constexpr int rec_stride();
 
 template <int P>
-__global__ void pack_coef(const double *__restrict__ mom, int64_t nn, double *__restrict__ coef) {
+__global__ void pack_coef(const double *__restrict__ mom, const int32_t *__restrict__ pre,
+                          int64_t nn, double *__restrict__ coef) {
   int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (k >= nn) return;
   const double *M = mom + k * ncoef(P);
-  double *C = coef + k * ncoef_fast(P);
+  double *C = coef + (int64_t)pre[k] * rec_stride<P>() + 8;
   const double sxx = 2.0 * M[4], syy = 2.0 * M[5], szz = 2.0 * M[6];
   const double tr3 = (sxx + syy + szz) * (1.0 / 3.0);
   C[0] = 1.5 * (sxx - tr3);
@@ -667,43 +669,82 @@ __global__ void pack_coef(const double *__restrict__ mom, int64_t nn, double *__
 }
 
 // ------------------------------------------------------------------- walk
-struct alignas(16) WalkNode {  // 64 bytes, read with scalar loads
-  double cx, cy, cz, mass;     // centre of mass, mass
-  double size2, hmax;          // (2 half)^2, max softening below (0 if none)
-  int32_t next, first;         // threaded links; first = -1 for a leaf
-  int32_t leaf_start, leaf_count;
-};
+// One record per node in DFS preorder, read by a wave with a single burst of
+// scalar loads:  [cx cy cz mass | size2 hmax | next first | leaf_start count]
+// (64 B) followed by the node's evaluation coefficients (orders 2-3: the
+// detraced Q', K'; orders 4-5: raw moments).
+template <int P> __host__ __device__ constexpr int rec_stride() {
+  return P <= 1 ? 8 : (P == 2 ? 16 : (P == 3 ? 24 : (P == 4 ? 48 : 64)));
+}
 
+template <int P>
 __global__ void pack_walk(const double4 *__restrict__ com, const double4 *__restrict__ ncen,
-                          const double *__restrict__ hmax, const int32_t *__restrict__ nnext,
-                          const int32_t *__restrict__ nfirst, const int32_t *__restrict__ nchild,
+                          const double *__restrict__ hmax, const int32_t *__restrict__ nchild,
                           const int32_t *__restrict__ nstart, const int32_t *__restrict__ ncount,
-                          int64_t nn, WalkNode *__restrict__ out) {
+                          const int32_t *__restrict__ pre, const int32_t *__restrict__ size,
+                          int64_t nn, double *__restrict__ walk) {
 #pragma clang fp contract(off)
   int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (k >= nn) return;
-  WalkNode w;
+  const int32_t pk = pre[k];
+  double *r = walk + (int64_t)pk * rec_stride<P>();
   const double4 c = com[k];
-  w.cx = c.x;
-  w.cy = c.y;
-  w.cz = c.z;
-  w.mass = c.w;
+  r[0] = c.x;
+  r[1] = c.y;
+  r[2] = c.z;
+  r[3] = c.w;
   const double s = ncen[k].w * 2.0;  // tree.rs:794-798
-  w.size2 = s * s;
-  w.hmax = hmax ? hmax[k] : 0.0;
-  w.next = nnext[k];
+  r[4] = s * s;
+  r[5] = hmax ? hmax[k] : 0.0;
+  // DFS preorder ids: first child = k + 1, next_branch = k + subtree size
+  // (the same threading as tree.rs:736-776, renumbered)
+  const int64_t after = (int64_t)pk + size[k];
   const bool leaf = nchild[k] == 0;
-  w.first = leaf ? -1 : nfirst[k];
-  w.leaf_start = leaf ? nstart[k] : 0;
-  w.leaf_count = leaf ? ncount[k] : 0;
-  out[k] = w;
+  int32_t *ir = (int32_t *)(r + 6);
+  ir[0] = after < nn ? (int32_t)after : -1;
+  ir[1] = leaf ? -1 : pk + 1;
+  ir[2] = leaf ? nstart[k] : 0;
+  ir[3] = leaf ? ncount[k] : 0;
+}
+
+// subtree sizes, one level bottom-up
+__global__ void subtree_size(const int32_t *__restrict__ nfirst, const int32_t *__restrict__ nchild,
+                             int32_t a, int32_t b, int32_t *__restrict__ size) {
+  int32_t k = a + (int32_t)(blockIdx.x * TPB + threadIdx.x);
+  if (k >= b) return;
+  int32_t s = 1;
+  const int32_t f = nfirst[k], nc = nchild[k];
+  for (int32_t c = f; c < f + nc; ++c) s += size[c];
+  size[k] = s;
+}
+
+// DFS preorder ids of the children of one level's nodes, top-down
+__global__ void preorder_ids(const int32_t *__restrict__ nfirst, const int32_t *__restrict__ nchild,
+                             const int32_t *__restrict__ size, int32_t a, int32_t b,
+                             int32_t *__restrict__ pre) {
+  int32_t k = a + (int32_t)(blockIdx.x * TPB + threadIdx.x);
+  if (k >= b) return;
+  int32_t run = pre[k] + 1;
+  const int32_t f = nfirst[k], nc = nchild[k];
+  for (int32_t c = f; c < f + nc; ++c) {
+    pre[c] = run;
+    run += size[c];
+  }
+}
+
+// raw moments in preorder (orders >= 4 evaluate them directly)
+template <int P>
+__global__ void pack_moments(const double *__restrict__ mom, const int32_t *__restrict__ pre,
+                             int64_t nn, double *__restrict__ walk) {
+  int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k >= nn) return;
+  double *out = walk + (int64_t)pre[k] * rec_stride<P>() + 8;
+  for (int q = 0; q < ncoef(P); ++q) out[q] = mom[k * ncoef(P) + q];
 }
 
 struct WalkParams {
-  const WalkNode *nodes;
-  const double *mom;        // ncoef(P) per node (P >= 4)
-  const double *coef;       // ncoef_fast(P) detraced coefficients per node (P = 2, 3)
-  const double4 *rec;       // sources in leaf order
+  const double *walk;       // node records in DFS preorder, rec_stride<P>() doubles each
+  const double4 *rec;       // sources in leaf order (+ 4 zero records of padding)
   const double *soft;       // sorted softenings (softenings set) or null
   const double *tgt;        // (m, 3) query points; null => targets are the sources
   const int32_t *perm;      // leaf order -> original index (self mode)
@@ -713,14 +754,84 @@ struct WalkParams {
   int kernel;
   int has_hmax;
   double *pot, *acc;
-  unsigned long long *counters;  // [accepted nodes, leaf pairs] or null
+  unsigned long long *counters;  // [accepted nodes, leaf pairs, fault, wave steps, active lanes]
   int64_t max_steps;             // > number of nodes
   unsigned int *fault;           // set when a wave exceeds max_steps
 };
 
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+// 64-byte scalar chunk -> the i-th double / int of it (i compile-time)
+__device__ __forceinline__ double chunk_d(const u32x16 &c, int i) {
+  return __builtin_bit_cast(double, (uint64_t)c[2 * i] | ((uint64_t)c[2 * i + 1] << 32));
+}
+__device__ __forceinline__ int32_t chunk_i(const u32x16 &c, int i) { return (int32_t)c[i]; }
+
+// the chunks of one node record (or of 4 leaf records) with all scalar
+// loads in flight together: one memory round trip (the compiler would sink
+// the coefficient loads into the accept branch and serialise them)
+template <int NCH>
+__device__ __forceinline__ void load_chunks(const double *ptr, u32x16 (&c)[NCH]) {
+  // the address is wave-uniform; make sure it sits in SGPRs
+  const uint64_t a = (uint64_t)ptr;
+  // (readfirstlane returns a signed int: go through uint32_t so the low
+  // word is zero-extended, not sign-extended)
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const double *base = (const double *)(((uint64_t)hi << 32) | (uint64_t)lo);
+  if constexpr (NCH == 1) {
+    asm volatile("s_load_dwordx16 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(c[0]) : "s"(base) : "memory");
+  } else if constexpr (NCH == 2) {
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(c[0]), "=&s"(c[1]) : "s"(base) : "memory");
+  } else {
+    static_assert(NCH == 3, "node records are 1-3 chunks");
+    asm volatile("s_load_dwordx16 %0, %3, 0x0\n\ts_load_dwordx16 %1, %3, 0x40\n\t"
+                 "s_load_dwordx16 %2, %3, 0x80\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(c[0]), "=&s"(c[1]), "=&s"(c[2]) : "s"(base) : "memory");
+  }
+}
+
+// one source pair of a leaf (tree.rs:98-417), self pair neutralised
+template <int WANT, bool SOFT>
+__device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, double sy, double sz,
+                                          double sm, double sh, bool me, double tx, double ty,
+                                          double tz, double th, double &ph, double &ax,
+                                          double &ay, double &az) {
+  double dx = sx - tx, dy = sy - ty, dz = sz - tz;
+  const double m = me ? 0.0 : sm;
+  dx = me ? 1.0 : dx;
+  const double r2 = dist2_fma(dx, dy, dz);
+  double h = 0.0;
+  if (SOFT) h = wp.soft ? __builtin_fmax(__builtin_fmax(sh, 0.0), th) : th;
+  if (!SOFT || h <= 0.0 || (wp.kernel == 1 && r2 >= h * h)) {
+    const double y = rsqrt_nr(r2 + kR2Tiny);
+    if (WANT & PBX_WANT_POT) ph = __builtin_fma(-m, y, ph);
+    if (WANT & PBX_WANT_ACC) {
+      const double g = m * (y * y * y);
+      ax = __builtin_fma(g, dx, ax);
+      ay = __builtin_fma(g, dy, ay);
+      az = __builtin_fma(g, dz, az);
+    }
+  } else {
+    const double rr = __builtin_sqrt(r2 + kR2Tiny);
+    if (WANT & PBX_WANT_POT) ph = __builtin_fma(m, kern_pot(wp.kernel, rr, h), ph);
+    if (WANT & PBX_WANT_ACC) {
+      const double g = m * kern_acc(wp.kernel, rr, h);
+      ax = __builtin_fma(g, dx, ax);
+      ay = __builtin_fma(g, dy, ay);
+      az = __builtin_fma(g, dz, az);
+    }
+  }
+}
+
 // SOFT: h_max guard and/or softened leaf sums are live
 template <int P, int WANT, bool SOFT>
 __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
+  constexpr int RS = rec_stride<P>();
+  constexpr int NCH = (P == 2 || P == 3) ? RS / 8 : 1;  // chunks loaded eagerly
   const int64_t t = (int64_t)blockIdx.x * WALK_TPB + threadIdx.x;
   const bool valid = t < wp.m;
   const bool self_mode = wp.tgt == nullptr;
@@ -751,75 +862,63 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
       if (threadIdx.x == 0) atomicOr(wp.fault, 1u);
       break;
     }
-    const WalkNode nd = wp.nodes[w];
+    u32x16 c[NCH];
+    load_chunks<NCH>(wp.walk + (int64_t)w * RS, c);
+    const double mass = chunk_d(c[0], 3);
+    const int32_t next = chunk_i(c[0], 12), first = chunk_i(c[0], 13);
     const bool act = (p == w);
     n_active += (unsigned long long)__popcll(__ballot(act));  // SIMD efficiency counter
-    if (nd.mass == 0.0) {  // tree.rs:1087-1090
-      if (act) p = nd.next;
-      w = nd.next;
+    if (mass == 0.0) {  // tree.rs:1087-1090
+      if (act) p = next;
+      w = next;
       continue;
     }
-    if (nd.first < 0) {  // leaf: direct sum in ascending index order
+    if (first < 0) {  // leaf: direct sum in ascending index order
       if (act) {
-        const int32_t s = nd.leaf_start, e = nd.leaf_start + nd.leaf_count;
-        n_pp += (unsigned long long)nd.leaf_count;
-        for (int32_t j = s; j < e; ++j) {
-          const double4 r = wp.rec[j];
-          double dx = r.x - tx, dy = r.y - ty, dz = r.z - tz, m = r.w;
-          const bool me = (j == self);  // skip_self (tree.rs:129-131)
-          m = me ? 0.0 : m;
-          dx = me ? 1.0 : dx;
-          const double r2 = dist2_fma(dx, dy, dz);
-          double h = 0.0;
-          if (SOFT) {
-            h = th;
-            if (wp.soft) h = __builtin_fmax(__builtin_fmax(wp.soft[j], 0.0), th);
-          }
-          if (!SOFT || h <= 0.0 || (wp.kernel == 1 && r2 >= h * h)) {
-            const double y = rsqrt_nr(r2 + kR2Tiny);
-            if (WANT & PBX_WANT_POT) ph = __builtin_fma(-m, y, ph);
-            if (WANT & PBX_WANT_ACC) {
-              const double g = m * (y * y * y);
-              ax = __builtin_fma(g, dx, ax);
-              ay = __builtin_fma(g, dy, ay);
-              az = __builtin_fma(g, dz, az);
-            }
-          } else {
-            const double rr = __builtin_sqrt(r2 + kR2Tiny);
-            if (WANT & PBX_WANT_POT) ph = __builtin_fma(m, kern_pot(wp.kernel, rr, h), ph);
-            if (WANT & PBX_WANT_ACC) {
-              const double g = m * kern_acc(wp.kernel, rr, h);
-              ax = __builtin_fma(g, dx, ax);
-              ay = __builtin_fma(g, dy, ay);
-              az = __builtin_fma(g, dz, az);
-            }
+        const int32_t s = chunk_i(c[0], 14), e = s + chunk_i(c[0], 15);
+        n_pp += (unsigned long long)(e - s);
+        for (int32_t j = s; j < e; j += 4) {  // 4 records (128 B) per round trip
+          u32x16 r[2];
+          load_chunks<2>((const double *)(wp.rec + j), r);
+          double4 hs = make_double4(0.0, 0.0, 0.0, 0.0);
+          if (SOFT && wp.soft) hs = *(const double4 *)(wp.soft + j);
+          const double hv[4] = {hs.x, hs.y, hs.z, hs.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (j + q < e)
+              leaf_pair<WANT, SOFT>(wp, chunk_d(r[q / 2], 4 * (q & 1)),
+                                    chunk_d(r[q / 2], 4 * (q & 1) + 1),
+                                    chunk_d(r[q / 2], 4 * (q & 1) + 2),
+                                    chunk_d(r[q / 2], 4 * (q & 1) + 3), hv[q], j + q == self, tx,
+                                    ty, tz, th, ph, ax, ay, az);
           }
         }
-        p = nd.next;
+        p = next;
       }
-      w = nd.next;
+      w = next;
       continue;
     }
     bool open = false;
     if (act) {
-      const double dx = nd.cx - tx, dy = nd.cy - ty, dz = nd.cz - tz;
+      const double dx = chunk_d(c[0], 0) - tx, dy = chunk_d(c[0], 1) - ty,
+                   dz = chunk_d(c[0], 2) - tz;
       const double dist2 = dist2_fma(dx, dy, dz) + kR2Tiny;  // tree.rs:1117
       bool soft_ok = true;
       if (SOFT && wp.has_hmax) {  // node_soft_ok, tree.rs:56-71
-        double h = __builtin_fmax(nd.hmax, 0.0);
+        double h = __builtin_fmax(chunk_d(c[0], 5), 0.0);
         if (has_th) h = __builtin_fmax(h, th);
         if (h > 0.0) {
           const double ch = wp.sep * h;
           soft_ok = dist2 > ch * ch;
         }
       }
-      if (soft_ok && nd.size2 < wp.theta2 * dist2) {
+      if (soft_ok && chunk_d(c[0], 4) < wp.theta2 * dist2) {
         ++n_node;
         if constexpr (P == 0) {  // monopole without multipoles (tree.rs:1126-1129, 1284-1291)
           const double y = rsqrt_nr(dist2 + kR2Tiny);
-          if (WANT & PBX_WANT_POT) ph = __builtin_fma(-nd.mass, y, ph);
+          if (WANT & PBX_WANT_POT) ph = __builtin_fma(-mass, y, ph);
           if (WANT & PBX_WANT_ACC) {
-            const double g = nd.mass * (y * y * y);
+            const double g = mass * (y * y * y);
             ax = __builtin_fma(g, dx, ax);
             ay = __builtin_fma(g, dy, ay);
             az = __builtin_fma(g, dz, az);
@@ -827,66 +926,65 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
         } else {
           // derivative builders add eps2 = R2_TINY and R2_TINY again
           // (multipole.rs:594, tree.rs:1429)
-          const double r2 = dx * dx + dy * dy + dz * dz + 2.0 * kR2Tiny;
-          const double inv_r = rsqrt_nr(r2);
+          const double inv_r = rsqrt_nr(dist2 + kR2Tiny);
           if constexpr (P == 1) {  // stored as O0: monopole with the D1 tensor (multipole.rs:272)
             double D[4];
             derivs<1>(dx, dy, dz, inv_r, D);
-            if (WANT & PBX_WANT_POT) ph = __builtin_fma(-nd.mass, D[0], ph);
+            if (WANT & PBX_WANT_POT) ph = __builtin_fma(-mass, D[0], ph);
             if (WANT & PBX_WANT_ACC) {
-              ax = __builtin_fma(-nd.mass, D[1], ax);
-              ay = __builtin_fma(-nd.mass, D[2], ay);
-              az = __builtin_fma(-nd.mass, D[3], az);
+              ax = __builtin_fma(-mass, D[1], ax);
+              ay = __builtin_fma(-mass, D[2], ay);
+              az = __builtin_fma(-mass, D[3], az);
             }
           } else if constexpr (P == 2 || P == 3) {
             // detraced evaluation (see pack_coef): u = 1/r,
             //   phi = -M u - u^5 q2' + u^7 q3',  q2' = R.Q'.R, q3' = K'(R)
             //   a   = (M u^3 + 5 q2' u^7) R - 2 u^5 Q'.R
-            const double *C = wp.coef + (int64_t)w * ncoef_fast(P);
+            auto C = [&](int i) { return chunk_d(c[1 + (i >> 3)], i & 7); };
             const double u = inv_r, u2 = u * u, u3 = u2 * u, u5 = u3 * u2;
-            const double qx = __builtin_fma(C[0], dx, __builtin_fma(C[3], dy, C[4] * dz));
-            const double qy = __builtin_fma(C[3], dx, __builtin_fma(C[1], dy, C[5] * dz));
-            const double qz = __builtin_fma(C[4], dx, __builtin_fma(C[5], dy, C[2] * dz));
+            const double qx = __builtin_fma(C(0), dx, __builtin_fma(C(3), dy, C(4) * dz));
+            const double qy = __builtin_fma(C(3), dx, __builtin_fma(C(1), dy, C(5) * dz));
+            const double qz = __builtin_fma(C(4), dx, __builtin_fma(C(5), dy, C(2) * dz));
             const double q2 = __builtin_fma(dx, qx, __builtin_fma(dy, qy, dz * qz));
             if (WANT & PBX_WANT_POT) {
-              double t = __builtin_fma(-u5, q2, -nd.mass * u);
+              double tp = __builtin_fma(-u5, q2, -mass * u);
               if constexpr (P == 3) {
                 const double zz = dz * dz;
-                const double A = __builtin_fma(C[6], dx, __builtin_fma(C[7], dy, C[8] * dz));
-                const double B = __builtin_fma(C[9], dy, C[10] * dz);
-                const double X = __builtin_fma(dx, A, __builtin_fma(dy, B, C[11] * zz));
-                const double G = __builtin_fma(C[12], dy, C[13] * dz);
-                const double Y = __builtin_fma(dy, G, C[14] * zz);
-                const double q3 = __builtin_fma(dx, X, __builtin_fma(dy, Y, (C[15] * dz) * zz));
-                t = __builtin_fma(u5 * u2, q3, t);
+                const double A = __builtin_fma(C(6), dx, __builtin_fma(C(7), dy, C(8) * dz));
+                const double B = __builtin_fma(C(9), dy, C(10) * dz);
+                const double X = __builtin_fma(dx, A, __builtin_fma(dy, B, C(11) * zz));
+                const double G = __builtin_fma(C(12), dy, C(13) * dz);
+                const double Y = __builtin_fma(dy, G, C(14) * zz);
+                const double q3 = __builtin_fma(dx, X, __builtin_fma(dy, Y, (C(15) * dz) * zz));
+                tp = __builtin_fma(u5 * u2, q3, tp);
               }
-              ph += t;
+              ph += tp;
             }
             if (WANT & PBX_WANT_ACC) {
               // the order-P force uses moments up to P-1 (multipole.rs:1408-1528):
               // order 2 -> monopole (+ the dipole, zero about the COM)
-              double c = nd.mass * u3, s = 0.0;
+              double cc = mass * u3, sq = 0.0;
               if constexpr (P == 3) {
-                c = __builtin_fma(5.0 * q2, u5 * u2, c);
-                s = -2.0 * u5;
+                cc = __builtin_fma(5.0 * q2, u5 * u2, cc);
+                sq = -2.0 * u5;
               }
-              ax = __builtin_fma(c, dx, __builtin_fma(s, qx, ax));
-              ay = __builtin_fma(c, dy, __builtin_fma(s, qy, ay));
-              az = __builtin_fma(c, dz, __builtin_fma(s, qz, az));
+              ax = __builtin_fma(cc, dx, __builtin_fma(sq, qx, ax));
+              ay = __builtin_fma(cc, dy, __builtin_fma(sq, qy, ay));
+              az = __builtin_fma(cc, dz, __builtin_fma(sq, qz, az));
             }
           } else {
             double D[ncoef(P)];
             derivs<P>(dx, dy, dz, inv_r, D);
-            eval_multipole<P, WANT>(wp.mom + (int64_t)w * ncoef(P), D, ph, ax, ay, az);
+            eval_multipole<P, WANT>(wp.walk + (int64_t)w * RS + 8, D, ph, ax, ay, az);
           }
         }
-        p = nd.next;
+        p = next;
       } else {
         open = true;
-        p = nd.first;
+        p = first;
       }
     }
-    w = (__ballot(open) != 0ull) ? nd.first : nd.next;
+    w = (__ballot(open) != 0ull) ? first : next;
   }
   if (!valid) return;
   const int64_t o = self_mode ? (int64_t)wp.perm[t] : t;
@@ -898,9 +996,9 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
   }
   if (wp.counters) {
 #pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-      n_node += __shfl_xor(n_node, s, 64);
-      n_pp += __shfl_xor(n_pp, s, 64);
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+      n_node += __shfl_xor(n_node, sh, 64);
+      n_pp += __shfl_xor(n_pp, sh, 64);
     }
     if (threadIdx.x == 0) {
       atomicAdd(&wp.counters[0], n_node);
@@ -928,7 +1026,7 @@ struct Octree {
   std::vector<int32_t> lvl;  // first node id of every level (+ end)
   Buf pos, mass, soft;       // original order (device copies)
   Buf perm, rec, soft_s;     // leaf order
-  Buf nstart, ncount, nfirst, nnext, nchild, ncen;
+  Buf nstart, ncount, nfirst, nnext, nchild, ncen, pre, size;
   Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
   // accepted nodes, leaf pairs, fault flag, wave steps, active-lane steps
@@ -1083,6 +1181,25 @@ static bool split_levels(Octree &T, hipStream_t st) {
   return true;
 }
 
+// subtree sizes (bottom-up) and DFS preorder ids (top-down) of every node
+static void preorder(Octree &T, hipStream_t st) {
+  int32_t *size = (int32_t *)T.size.get(4 * (size_t)std::max<int64_t>(T.nn, 1));
+  int32_t *pre = (int32_t *)T.pre.get(4 * (size_t)std::max<int64_t>(T.nn, 1));
+  const int L = (int)T.lvl.size() - 1;
+  for (int l = L - 1; l >= 0; --l) {
+    const int32_t a = T.lvl[l], b = T.lvl[l + 1];
+    hipLaunchKernelGGL(subtree_size, dim3(nblk(b - a)), dim3(TPB), 0, st, T.nfirst.as<int32_t>(),
+                       T.nchild.as<int32_t>(), a, b, size);
+  }
+  PBX_HIP(hipMemsetAsync(pre, 0, 4, st));
+  for (int l = 0; l < L; ++l) {
+    const int32_t a = T.lvl[l], b = T.lvl[l + 1];
+    hipLaunchKernelGGL(preorder_ids, dim3(nblk(b - a)), dim3(TPB), 0, st, T.nfirst.as<int32_t>(),
+                       T.nchild.as<int32_t>(), size, a, b, pre);
+  }
+  PBX_HIP(hipGetLastError());
+}
+
 static void build_structure(Octree &T, hipStream_t st) {
   ScopedTimer tm("octree.build_structure");
   const int64_t n = T.n;
@@ -1128,6 +1245,7 @@ static void build_structure(Octree &T, hipStream_t st) {
     T.nn = 1;
     T.lvl.assign({0, 1});
     T.rec.get(64);
+    preorder(T, st);
     return;
   }
   for (T.nwords = 2;; ++T.nwords) {
@@ -1142,18 +1260,27 @@ static void build_structure(Octree &T, hipStream_t st) {
   hipLaunchKernelGGL(leaf_sort, dim3(nblk(T.nn)), dim3(TPB), 0, st, T.nchild.as<int32_t>(),
                      T.nstart.as<int32_t>(), T.ncount.as<int32_t>(), T.nn, T.perm.as<int32_t>());
   PBX_HIP(hipGetLastError());
+  preorder(T, st);
+}
+
+// softenings in leaf order (+ 4 zero pad entries, read 4 at a time)
+static void gather_softenings(Octree &T, hipStream_t st) {
+  double *d = (double *)T.soft_s.get(8 * (size_t)(T.n + 4));
+  PBX_HIP(hipMemsetAsync(d + T.n, 0, 32, st));
+  hipLaunchKernelGGL(gather_f64, dim3(nblk(T.n)), dim3(TPB), 0, st, T.soft.as<double>(),
+                     T.perm.as<int32_t>(), T.n, d);
 }
 
 static void pack_particles(Octree &T, hipStream_t st) {
   const int64_t n = T.n;
-  double4 *rec = (double4 *)T.rec.get(sizeof(double4) * (size_t)std::max<int64_t>(n, 1));
+  // 4 zero records of padding: the walk reads leaves 4 records at a time
+  double4 *rec = (double4 *)T.rec.get(sizeof(double4) * (size_t)(n + 4));
+  PBX_HIP(hipMemsetAsync(rec + n, 0, sizeof(double4) * 4, st));
   if (n > 0) {
     hipLaunchKernelGGL(pack_records, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(),
                        T.user_mass ? T.mass.as<double>() : (const double *)nullptr,
                        T.perm.as<int32_t>(), n, rec);
-    if (T.soft_set)
-      hipLaunchKernelGGL(gather_f64, dim3(nblk(n)), dim3(TPB), 0, st, T.soft.as<double>(),
-                         T.perm.as<int32_t>(), n, (double *)T.soft_s.get(8 * (size_t)n));
+    if (T.soft_set) gather_softenings(T, st);
   }
   PBX_HIP(hipGetLastError());
 }
@@ -1191,15 +1318,27 @@ static void build_payload(Octree &T, hipStream_t st) {
     case 4: run_payload<4>(T, st, v); break;
     default: run_payload<5>(T, st, v); break;
   }
-  if (P == 2 || P == 3) {
-    double *cf = (double *)T.coef.get(8 * (size_t)T.nn * ncoef_fast(P));
-    if (P == 2) hipLaunchKernelGGL(pack_coef<2>, dim3(nblk(T.nn)), dim3(TPB), 0, st, v.mom, T.nn, cf);
-    else hipLaunchKernelGGL(pack_coef<3>, dim3(nblk(T.nn)), dim3(TPB), 0, st, v.mom, T.nn, cf);
+  const int32_t *pre = T.pre.as<int32_t>();
+  const dim3 g(nblk(T.nn)), b(TPB);
+  auto pack = [&](auto pc) {
+    constexpr int PP = decltype(pc)::value;
+    double *wk = (double *)T.walk.get(8 * (size_t)T.nn * rec_stride<PP>());
+    hipLaunchKernelGGL(pack_walk<PP>, g, b, 0, st, T.com.as<double4>(), T.ncen.as<double4>(),
+                       v.hmax, T.nchild.as<int32_t>(), T.nstart.as<int32_t>(),
+                       T.ncount.as<int32_t>(), pre, T.size.as<int32_t>(), T.nn, wk);
+    if constexpr (PP == 2 || PP == 3)
+      hipLaunchKernelGGL(pack_coef<PP>, g, b, 0, st, v.mom, pre, T.nn, wk);
+    else if constexpr (PP >= 4)
+      hipLaunchKernelGGL(pack_moments<PP>, g, b, 0, st, v.mom, pre, T.nn, wk);
+  };
+  switch (P) {
+    case 0: pack(std::integral_constant<int, 0>{}); break;
+    case 1: pack(std::integral_constant<int, 1>{}); break;
+    case 2: pack(std::integral_constant<int, 2>{}); break;
+    case 3: pack(std::integral_constant<int, 3>{}); break;
+    case 4: pack(std::integral_constant<int, 4>{}); break;
+    default: pack(std::integral_constant<int, 5>{}); break;
   }
-  hipLaunchKernelGGL(pack_walk, dim3(nblk(T.nn)), dim3(TPB), 0, st, T.com.as<double4>(),
-                     T.ncen.as<double4>(), v.hmax, T.nnext.as<int32_t>(), T.nfirst.as<int32_t>(),
-                     T.nchild.as<int32_t>(), T.nstart.as<int32_t>(), T.ncount.as<int32_t>(), T.nn,
-                     (WalkNode *)T.walk.get(sizeof(WalkNode) * (size_t)T.nn));
   PBX_HIP(hipGetLastError());
   T.has_bh = true;
 }
@@ -1228,9 +1367,7 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   PBX_HIP(hipMemsetAsync(ctr, 0, 64, st));
   if (m == 0) return;
   WalkParams wp;
-  wp.nodes = T.walk.as<WalkNode>();
-  wp.mom = T.mom.as<double>();
-  wp.coef = T.coef.as<double>();
+  wp.walk = T.walk.as<double>();
   wp.rec = T.rec.as<double4>();
   wp.tgt = d_tgt;
 
@@ -1341,7 +1478,7 @@ int pbx_octree_destroy(pbx_octree *t) {
     if (!t) return;
     Octree *T = (Octree *)t;
     Buf *bufs[] = {&T->pos, &T->mass, &T->soft, &T->perm, &T->rec, &T->soft_s, &T->nstart,
-                   &T->ncount, &T->nfirst, &T->nnext, &T->nchild, &T->ncen, &T->com, &T->hmax,
+                   &T->ncount, &T->nfirst, &T->nnext, &T->nchild, &T->ncen, &T->pre, &T->size, &T->com, &T->hmax,
                    &T->mom, &T->coef, &T->walk, &T->keys, &T->ktmp0, &T->ktmp1, &T->vtmp, &T->hist,
                    &T->tsum, &T->front0, &T->front1, &T->lb, &T->cnt, &T->flags, &T->small,
                    &T->counters};
@@ -1372,10 +1509,7 @@ int pbx_octree_set_softenings(pbx_octree *t, const double *softenings, int on_de
     if (softenings) {
       upload(T.soft, softenings, T.n, on_device, dev.stream);
       T.soft_set = true;
-      if (T.n > 0)
-        hipLaunchKernelGGL(gather_f64, dim3(nblk(T.n)), dim3(TPB), 0, dev.stream,
-                           T.soft.as<double>(), T.perm.as<int32_t>(), T.n,
-                           (double *)T.soft_s.get(8 * (size_t)T.n));
+      if (T.n > 0) gather_softenings(T, dev.stream);
     } else {
       T.soft_set = false;  // h_max keeps its build-time value (tree.rs:777-782)
     }

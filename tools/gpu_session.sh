@@ -23,7 +23,7 @@ while read -r tmo name cmd; do
   fi
   # a child process that aborted / segfaulted / faulted the GPU under a
   # launcher that itself exits 1 (torchrun, pytest-xdist, ...) is fatal too
-  if grep -qE "SIGABRT|SIGSEGV|Signal 6|Signal 11|exitcode *: *-|Segmentation fault|Memory access fault|core dumped" "gpurun_out/$name.out"; then
+  if grep -qE "SIGABRT|SIGSEGV|Signal 6|Signal 11|exitcode *: *-|Segmentation fault|Memory access fault|illegal memory access|core dumped" "gpurun_out/$name.out"; then
     echo "child fault detected in $name: stopping session" | tee -a gpurun_out/session.log
     exit 134
   fi

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of bench.py.
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  Per MI355X_MICROARCH.md
+("HBM"), gfx950's FETCH_SIZE counts exactly half of the bytes of wide
+coalesced streaming reads, so the corrected read traffic is 2 x FETCH_SIZE;
+WRITE_SIZE is exact for 16-B-per-lane stores.  Both are memory-side (L2
+fabric) requests, Infinity-Cache hits included.
+
+usage: tools/pmc_summary.py FETCH_CSV WRITE_CSV OUT_DIR
+writes OUT_DIR/pmc_summary.csv (per kernel) and the per-launch traffic of the
+bench's dominant kernels as profiles/pmc_{direct,tree,profile}_latest.json.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def load(path):
+    per = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            per[row["Kernel_Name"]].append(float(row["Counter_Value"]) * 1024.0)
+    return per
+
+
+def main():
+    fetch, write, out = load(sys.argv[1]), load(sys.argv[2]), Path(sys.argv[3]).resolve()
+    out.mkdir(parents=True, exist_ok=True)
+    rows = []
+    for name in sorted(set(fetch) | set(write), key=lambda k: -sum(fetch.get(k, [0]))):
+        f, w = fetch.get(name, []), write.get(name, [])
+        rows.append({
+            "kernel": name, "dispatches": max(len(f), len(w)),
+            "fetch_bytes_raw_avg": sum(f) / len(f) if f else None,
+            "read_bytes_corrected_avg": 2 * sum(f) / len(f) if f else None,
+            "write_bytes_avg": sum(w) / len(w) if w else None,
+        })
+    with open(out / "pmc_summary.csv", "w", newline="") as fh:
+        wr = csv.DictWriter(fh, fieldnames=list(rows[0]))
+        wr.writeheader()
+        wr.writerows(rows)
+
+    def pick(sub):
+        return [r for r in rows if sub in r["kernel"]]
+
+    root = Path(__file__).resolve().parent.parent / "profiles"
+    src = str((out / "pmc_summary.csv").relative_to(root.parent))
+    d = pick("direct_kernel")
+    if d:
+        r = d[0]
+        (root / "pmc_direct_latest.json").write_text(json.dumps({
+            "kernel": r["kernel"], "hbm_bytes_per_launch": r["read_bytes_corrected_avg"] + (r["write_bytes_avg"] or 0),
+            "read_bytes_per_launch": r["read_bytes_corrected_avg"], "write_bytes_per_launch": r["write_bytes_avg"],
+            "note": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); sources are scalar loads, "
+                    "memory-side requests incl. Infinity-Cache hits", "source": src}, indent=1))
+    t = pick("walk_kernel<3, 3")
+    if t:
+        r = t[0]
+        (root / "pmc_tree_latest.json").write_text(json.dumps({
+            "kernel": r["kernel"], "hbm_bytes_per_launch": r["read_bytes_corrected_avg"] + (r["write_bytes_avg"] or 0),
+            "read_bytes_per_launch": r["read_bytes_corrected_avg"], "write_bytes_per_launch": r["write_bytes_avg"],
+            "note": "2 x FETCH_SIZE + WRITE_SIZE; node records / leaf particles are scalar loads",
+            "source": src}, indent=1))
+    prof = [r for r in rows if "pbx::prof::" in r["kernel"] or "radix_" in r["kernel"] or "scan_t" in r["kernel"]]
+    if prof:
+        (root / "pmc_profile_latest.json").write_text(json.dumps({
+            "kernels": [r["kernel"] for r in prof],
+            "note": "per-dispatch averages of every profile-path kernel in the 64M run "
+                    "(radix/scan kernels are shared with the octree build)",
+            "per_kernel": prof, "source": src}, indent=1))
+    for r in rows[:25]:
+        print(f"{r['dispatches']:5d}  read {r['read_bytes_corrected_avg'] or 0:14.0f}  "
+              f"write {r['write_bytes_avg'] or 0:14.0f}  {r['kernel'][:110]}")
+
+
+if __name__ == "__main__":
+    main()
