@@ -247,96 +247,118 @@ def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc)
     }, {"targets_checked": k, "pot_max_rel": rp, "acc_max_rel": ra}
 
 
-def bench_tree(n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: float):
+def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: float):
     """Config 5: Barnes-Hut tree (theta=0.5, leaf 8, order 3 = Gravity's
     TreeOptions defaults, base.py:82-100) force + potential of an n-particle
     Plummer sphere resident in HBM, then the 256-bin log radial profile
     (0.01..50) of the mass-weighted potential.  One step = device octree build
     + mass/multipole payload + walk (all particles, self skipped) + profile
-    (r, bin assignment, per-bin sums of m and m*phi)."""
-    from pynbodyext._engine import Octree
-    from pynbodyext.profiles._device import SRC_W, DeviceBins
+    (r, bin assignment, per-bin sums of m and m*phi).  With N ranks (strong
+    scaling, n fixed): every rank builds the tree, walks its cost-balanced
+    range of the leaf-ordered targets and the profile partials are summed by
+    one RCCL all-reduce (pynbodyext.parallel.ShardedTree)."""
+    from pynbodyext.parallel import ShardedTree
+    from pynbodyext.profiles._device import DeviceBins
 
     theta = 0.5
     pos, mass = plummer(n, seed=SEEDS.get(n, 1003))
     d_pos = nat.DeviceArray.from_host(pos)
     d_mass = nat.DeviceArray.from_host(mass)
-    d_pot = nat.DeviceArray(8 * n)
-    d_acc = nat.DeviceArray(24 * n)
     edges = np.logspace(np.log10(0.01), np.log10(50.0), 257)
     prof = DeviceBins()
+    solver = ShardedTree(dist.comm, n, d_pos, d_mass, 8, 3, theta)
+    solver.build()
+    if dist.active:
+        solver.balance()
     ev = [nat.Event() for _ in range(4)]
 
     def step():
         ev[0].record()
-        tree = Octree._from_device(d_pos.ptr, n, d_mass.ptr, 8, 3)
+        solver.build()
         ev[1].record()
-        tree._compute_device(theta, nat.WANT_POT | nat.WANT_ACC, d_pot.ptr, d_acc.ptr)
+        solver.walk()
         ev[2].record()
-        DeviceBins.select(d_pos.ptr, d_mass.ptr, ndim=3, on_device=True, n=n, into=prof)
-        prof.assign(edges)
-        mom = prof.moments(d_pot, SRC_W)
+        mom = solver.profile(prof, edges)
         ev[3].record()
-        info = tree.info()
-        tree.close()
-        return mom, info
+        return mom
 
     for _ in range(warmup):
         step()
     nat.synchronize()
+    dist.barrier()
     wall, parts = [], []
     for _ in range(steps):
         t0 = time.perf_counter()
-        mom, info = step()
+        mom = step()
         nat.synchronize()
-        wall.append(time.perf_counter() - t0)
+        dist.barrier()
+        wall.append(dist.max(time.perf_counter() - t0))
         parts.append([ev[i].elapsed_ms(ev[i + 1]) for i in range(3)])
     t = float(np.median(wall))
     build_ms, walk_ms, prof_ms = (float(np.median([p[i] for p in parts])) for i in range(3))
+    info = solver.info
+    first, count = solver.ranges[dist.rank] if solver.ranges else (0, n)
     flops = info["node_interactions"] * TREE_FLOP_NODE + info["leaf_pairs"] * TREE_FLOP_PP
     achieved = flops / (walk_ms * 1e-3) / 1e12
-    pot = np.empty(n)
-    acc = np.empty((n, 3))
-    d_pot.download(pot)
-    d_acc.download(acc)
+    walk_max = dist.max(walk_ms)
     with np.errstate(invalid="ignore", divide="ignore"):
         phi_profile = mom[:, 1] / mom[:, 0]
     out = {
         "metric": "effective particle-pairs/sec (Barnes-Hut force+potential + 256-bin potential profile)",
         "value": float(n) * float(n - 1) / t,
         "unit": "effective pairs/s",
+        "n_gpus": dist.world,
+        "scaling": "strong",
         "ms_per_step": t * 1e3,
         "config": {"workload": f"{n}-particle Plummer sphere, octree theta=0.5 leaf 8 multipole "
                                "order 3 (Newtonian), force+potential at every particle, then "
                                "RadialProfile log 256 bins [0.01, 50] of the mass-weighted potential",
-                   "n_particles": n, "nodes": info["nodes"], "levels": info["levels"]},
-        "phases_ms": {"build_and_payload": build_ms, "walk": walk_ms, "profile": prof_ms},
+                   "n_particles": n, "nodes": info["nodes"], "levels": info["levels"],
+                   "parallelism": f"tree replicated, leaf-ordered targets cost-balanced x{dist.world}"
+                                  + (", RCCL all-reduce of profile partials" if dist.world > 1 else "")},
+        "phases_ms": {"build_and_payload": build_ms, "walk": walk_ms, "walk_max_over_ranks": walk_max,
+                      "profile": prof_ms},
         "interactions": {"node": info["node_interactions"], "leaf_pairs": info["leaf_pairs"],
-                         "per_particle": (info["node_interactions"] + info["leaf_pairs"]) / n,
+                         "per_target": (info["node_interactions"] + info["leaf_pairs"]) / max(count, 1),
                          "simd_lane_efficiency": info["active_lane_steps"] /
-                         max(1, 64 * info["wave_steps"])},
+                         max(1, 64 * info["wave_steps"]), "targets_rank0": count},
         "roofline": {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_VECTOR_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
-                     "traffic": None, "kernel": "walk_kernel<order 3, pot+acc>",
+                     "traffic": pmc_traffic("tree")[0], "kernel": "walk_kernel<order 3, pot+acc>",
                      "flop_per_node": TREE_FLOP_NODE, "flop_per_leaf_pair": TREE_FLOP_PP,
                      "kernel_ms": walk_ms},
         "profile_check": {"bins_nonempty": int(np.sum(mom[:, 0] > 0)),
                           "phi_innermost_bin": float(phi_profile[mom[:, 0] > 0][0]),
                           "phi_outermost_bin": float(phi_profile[mom[:, 0] > 0][-1])},
     }
-    if cpu:
+    if cpu and dist.world == 1 and dist.rank == 0:
+        pot = np.empty(n)
+        acc = np.empty((n, 3))
+        # compact leaf-order outputs -> original order
+        idx = nat.DeviceArray(8 * n)
+        solver.tree._leaf_particles_device(0, n, None, None, idx.ptr)
+        order = np.empty(n, dtype=np.int64)
+        idx.download(order)
+        tmp = np.empty(n)
+        solver.d_pot.download(tmp)
+        pot[order] = tmp
+        tmp3 = np.empty((n, 3))
+        solver.d_acc.download(tmp3)
+        acc[order] = tmp3
+        idx.free()
         out["cpu_baseline"], out["parity_vs_oracle"] = tree_cpu_baseline(
             pos, mass, cpu_seconds, theta, pot, acc)
+    solver.close()
     prof.close()
-    for a in (d_pos, d_mass, d_pot, d_acc):
-        a.free()
+    d_pos.free()
+    d_mass.free()
     return out
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the direct-sum kernel from the committed
-    rocprofv3 PMC summary (profiles/), or None."""
-    f = ROOT / "profiles" / "pmc_direct_latest.json"
+def pmc_traffic(which: str = "direct"):
+    """HBM bytes per launch of a bench kernel from the committed rocprofv3
+    PMC summary (profiles/pmc_<which>_latest.json, tools/pmc_summary.py), or None."""
+    f = ROOT / "profiles" / f"pmc_{which}_latest.json"
     if not f.exists():
         return None, None
     try:
@@ -400,8 +422,12 @@ def main():
     # roofline: this rank's kernel does n_loc * (n_tot - 1) pairs per launch
     pairs_launch = float(n_loc) * float(n_tot - 1)
     achieved_tf = pairs_launch * FLOP_PER_PAIR / (kern_avg_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic()
+    traffic, traffic_src = pmc_traffic("direct")
 
+    tree = None
+    if not args.no_tree:
+        tree = bench_tree(dist, args.tree_n, steps=max(3, args.steps), warmup=1,
+                          cpu=not args.no_cpu_baseline, cpu_seconds=args.cpu_seconds)
     dist.close()
     if rank != 0:
         return
@@ -466,9 +492,8 @@ def main():
             "sweep": sweep,
             "cpu_baseline": head.get("cpu_baseline"),
         }
-    if not args.no_tree and world == 1:
-        out["tree"] = bench_tree(args.tree_n, steps=max(3, args.steps), warmup=1,
-                                 cpu=not args.no_cpu_baseline, cpu_seconds=args.cpu_seconds)
+    if tree is not None:
+        out["tree"] = tree
     print(json.dumps(out), flush=True)
 
 

@@ -146,6 +146,11 @@ int pbx_octree_create(const double *pos, int64_t n, const double *masses,
                       int multipole_order, int kernel, int on_device,
                       pbx_octree **out);
 int pbx_octree_destroy(pbx_octree *tree);
+/* Octree::new semantics on new particles (same leaf_capacity / order /
+ * kernel), reusing the handle's HBM buffers (a time step of a simulation,
+ * the next snapshot); mass payload iff masses */
+int pbx_octree_rebuild(pbx_octree *tree, const double *pos, int64_t n, const double *masses,
+                       const double *softenings, int on_device);
 /* build_mass(masses=None) (gravity.rs:228-239): NULL keeps current masses */
 int pbx_octree_build_mass(pbx_octree *tree, const double *masses, int on_device);
 /* set_softenings (gravity.rs:241-258; h_max is not rebuilt, tree.rs:777) */
@@ -162,6 +167,19 @@ int pbx_octree_compute(pbx_octree *tree, double theta, int want, double *pot,
 int pbx_octree_at_points(pbx_octree *tree, const double *points, int64_t m,
                          double theta, int want, double *pot, double *acc,
                          int on_device);
+/* One rank's shard of compute_*: the targets are the particles
+ * [first, first + count) of the tree's leaf (DFS) order, self pairs skipped.
+ * compact = 0: outputs at the particles' original indices (full-length
+ * device arrays); compact = 1: count entries in leaf order.  d_cost
+ * (optional, count int32): accepted nodes + leaf pairs per target, to
+ * balance the next split.  Device pointers only. */
+int pbx_octree_compute_range(pbx_octree *tree, double theta, int want, int64_t first,
+                             int64_t count, int compact, double *d_pot, double *d_acc,
+                             int32_t *d_cost);
+/* positions (count x 3), masses and original indices (int64) of the leaf-order
+ * particles [first, first + count), into device buffers (any may be NULL) */
+int pbx_octree_leaf_particles(pbx_octree *tree, int64_t first, int64_t count, double *d_pos,
+                              double *d_mass, int64_t *d_idx);
 /* out[10] = {n, nodes, levels, has_mass_payload, has_hmax,
  *            accepted node interactions and leaf pairs of the last walk,
  *            path words, wave steps and active-lane steps of the last walk

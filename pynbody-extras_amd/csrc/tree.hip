@@ -302,8 +302,9 @@ __global__ void gather_u64(const uint64_t *__restrict__ src, const int32_t *__re
   if (i < n) dst[i] = perm ? src[perm[i]] : src[i];
 }
 
-__global__ void key_or_and(const uint64_t *__restrict__ k, int64_t n,
-                           unsigned long long *__restrict__ out) {
+__global__ void __launch_bounds__(TPB) key_or_and(const uint64_t *__restrict__ k, int64_t n,
+                                                  unsigned long long *__restrict__ out) {
+  __shared__ unsigned long long so[NWAVE], sa[NWAVE];
   unsigned long long o = 0, a = ~0ull;
   for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
     o |= k[i];
@@ -315,6 +316,15 @@ __global__ void key_or_and(const uint64_t *__restrict__ k, int64_t n,
     a &= __shfl_xor(a, s, 64);
   }
   if ((threadIdx.x & 63) == 0) {
+    so[threadIdx.x >> 6] = o;
+    sa[threadIdx.x >> 6] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < NWAVE; ++w) {
+      o |= so[w];
+      a &= sa[w];
+    }
     atomicOr(&out[0], o);
     atomicAnd(&out[1], a);
   }
@@ -749,6 +759,9 @@ struct WalkParams {
   const double *tgt;        // (m, 3) query points; null => targets are the sources
   const int32_t *perm;      // leaf order -> original index (self mode)
   int64_t m;                // number of targets
+  int64_t first;            // self mode: targets are leaf-order particles first .. first+m-1
+  int compact;              // self mode: 1 -> outputs at t (leaf order), 0 -> original index
+  int32_t *cost;            // optional per-target interaction count (nodes + leaf pairs)
   double theta2;
   double sep;               // multipole_min_separation_factor (kernel.rs:20-37)
   int kernel;
@@ -839,12 +852,13 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
   int64_t self = -1;
   if (valid) {
     if (self_mode) {
-      const double4 r = wp.rec[t];
+      const int64_t ts = wp.first + t;
+      const double4 r = wp.rec[ts];
       tx = r.x;
       ty = r.y;
       tz = r.z;
-      self = t;
-      if (SOFT && wp.soft) th = __builtin_fmax(wp.soft[t], 0.0);
+      self = ts;
+      if (SOFT && wp.soft) th = __builtin_fmax(wp.soft[ts], 0.0);
     } else {
       tx = wp.tgt[3 * t];
       ty = wp.tgt[3 * t + 1];
@@ -987,7 +1001,8 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
     w = (__ballot(open) != 0ull) ? first : next;
   }
   if (!valid) return;
-  const int64_t o = self_mode ? (int64_t)wp.perm[t] : t;
+  const int64_t o = (self_mode && !wp.compact) ? (int64_t)wp.perm[wp.first + t] : t;
+  if (wp.cost) wp.cost[t] = (int32_t)(n_node + n_pp);
   if (WANT & PBX_WANT_POT) wp.pot[o] = ph;
   if (WANT & PBX_WANT_ACC) {
     wp.acc[3 * o] = ax;
@@ -1009,6 +1024,21 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
   }
 }
 
+__global__ void leaf_particles_kernel(const double4 *__restrict__ rec, const int32_t *__restrict__ perm,
+                                      int64_t first, int64_t count, double *__restrict__ pos,
+                                      double *__restrict__ mass, int64_t *__restrict__ idx) {
+  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t >= count) return;
+  const double4 r = rec[first + t];
+  if (pos) {
+    pos[3 * t] = r.x;
+    pos[3 * t + 1] = r.y;
+    pos[3 * t + 2] = r.z;
+  }
+  if (mass) mass[t] = r.w;
+  if (idx) idx[t] = perm[first + t];
+}
+
 // ------------------------------------------------------------------- host
 struct Octree {
   int device = -1;
@@ -1020,7 +1050,7 @@ struct Octree {
   bool soft_set = false;
   bool has_bh = false;
   bool has_hmax = false;
-  int nwords = 2;
+  int nwords = 1;
   double root[4] = {0, 0, 0, 0};
   int64_t nn = 0, cap = 0;
   std::vector<int32_t> lvl;  // first node id of every level (+ end)
@@ -1029,6 +1059,13 @@ struct Octree {
   Buf nstart, ncount, nfirst, nnext, nchild, ncen, pre, size;
   Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
+  ~Octree() {
+    Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
+                   &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &keys, &ktmp0,
+                   &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
+                   &counters};
+    for (Buf *b : bufs) b->release();
+  }
   // accepted nodes, leaf pairs, fault flag, wave steps, active-lane steps
   unsigned long long last_counts[5] = {0, 0, 0, 0, 0};
   int moment_order() const { return order < 5 ? order : 5; }
@@ -1248,7 +1285,7 @@ static void build_structure(Octree &T, hipStream_t st) {
     preorder(T, st);
     return;
   }
-  for (T.nwords = 2;; ++T.nwords) {
+  for (T.nwords = 1;; ++T.nwords) {
     if (T.nwords > MAX_WORDS) fail(PBX_ERR_RUNTIME, "octree deeper than %d levels", LPW * MAX_WORDS);
     uint64_t *keys = (uint64_t *)T.keys.get(8 * (size_t)n * T.nwords);
     hipLaunchKernelGGL(path_keys, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(), n,
@@ -1362,7 +1399,8 @@ static void launch_walk_p(const WalkParams &wp, int want, bool soft, hipStream_t
 // walk for m targets (tgt == null: all particles, skip_self) into device
 // outputs in original / query order
 static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t m, double *d_pot,
-                 double *d_acc, hipStream_t st) {
+                 double *d_acc, hipStream_t st, int64_t first = 0, int compact = 0,
+                 int32_t *d_cost = nullptr) {
   unsigned long long *ctr = (unsigned long long *)T.counters.get(64);
   PBX_HIP(hipMemsetAsync(ctr, 0, 64, st));
   if (m == 0) return;
@@ -1374,6 +1412,9 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   wp.soft = T.soft_set ? T.soft_s.as<double>() : nullptr;
   wp.perm = T.perm.as<int32_t>();
   wp.m = m;
+  wp.first = first;
+  wp.compact = compact;
+  wp.cost = d_cost;
   {
 #pragma clang fp contract(off)
     wp.theta2 = theta * theta;  // tree.rs:1428
@@ -1419,6 +1460,27 @@ static void upload(Buf &b, const double *src, int64_t count, int on_device, hipS
                            on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
 }
 
+// Octree::new on (new) particles (gravity.rs:123-226): copies, structure,
+// mass payload iff masses; HBM buffers are grow-only and reused
+static void init_tree(Octree &T, const double *pos, int64_t n, const double *masses,
+                      const double *softenings, int on_device, hipStream_t st) {
+  T.n = n;
+  T.has_bh = T.has_hmax = false;
+  T.user_mass = T.soft_set = false;
+  upload(T.pos, pos, 3 * n, on_device, st);
+  if (masses) {
+    upload(T.mass, masses, n, on_device, st);
+    T.user_mass = true;
+  }
+  if (softenings) {
+    upload(T.soft, softenings, n, on_device, st);
+    T.soft_set = true;
+  }
+  build_structure(T, st);
+  if (masses) build_payload(T, st);  // gravity.rs:210-220
+  PBX_HIP(hipStreamSynchronize(st));
+}
+
 static const char *method_name(int want, bool at_points) {
   if (at_points) return want == PBX_WANT_POT ? "potentials_at_points" : "accelerations_at_points";
   return want == PBX_WANT_POT ? "compute_potentials" : "compute_accelerations";
@@ -1445,26 +1507,13 @@ int pbx_octree_create(const double *pos, int64_t n, const double *masses,
     if (multipole_order < 0 || multipole_order > 255) fail(PBX_ERR_VALUE, "multipole_order must fit in u8");
     Device &dev = current_device();
     std::lock_guard<std::mutex> lk(dev.mu);
-    hipStream_t st = dev.stream;
     Octree *T = new Octree();
     try {
       T->device = dev.id;
-      T->n = n;
       T->leaf_capacity = leaf_capacity < 1 ? 1 : leaf_capacity;  // tree.rs:701
       T->order = multipole_order;
       T->kernel = kernel;
-      upload(T->pos, pos, 3 * n, on_device, st);
-      if (masses) {
-        upload(T->mass, masses, n, on_device, st);
-        T->user_mass = true;
-      }
-      if (softenings) {
-        upload(T->soft, softenings, n, on_device, st);
-        T->soft_set = true;
-      }
-      build_structure(*T, st);
-      if (masses) build_payload(*T, st);  // gravity.rs:210-220
-      PBX_HIP(hipStreamSynchronize(st));
+      init_tree(*T, pos, n, masses, softenings, on_device, dev.stream);
     } catch (...) {
       delete T;
       throw;
@@ -1473,18 +1522,21 @@ int pbx_octree_create(const double *pos, int64_t n, const double *masses,
   });
 }
 
-int pbx_octree_destroy(pbx_octree *t) {
+int pbx_octree_rebuild(pbx_octree *t, const double *pos, int64_t n, const double *masses,
+                       const double *softenings, int on_device) {
   return guard([&] {
-    if (!t) return;
-    Octree *T = (Octree *)t;
-    Buf *bufs[] = {&T->pos, &T->mass, &T->soft, &T->perm, &T->rec, &T->soft_s, &T->nstart,
-                   &T->ncount, &T->nfirst, &T->nnext, &T->nchild, &T->ncen, &T->pre, &T->size, &T->com, &T->hmax,
-                   &T->mom, &T->coef, &T->walk, &T->keys, &T->ktmp0, &T->ktmp1, &T->vtmp, &T->hist,
-                   &T->tsum, &T->front0, &T->front1, &T->lb, &T->cnt, &T->flags, &T->small,
-                   &T->counters};
-    for (Buf *b : bufs) b->release();
-    delete T;
+    Octree &T = as_tree(t);
+    if (n < 0) fail(PBX_ERR_VALUE, "negative particle count");
+    if (n >= ((int64_t)1 << 31) - 1) fail(PBX_ERR_VALUE, "octrees are limited to < 2^31 particles");
+    if (n > 0 && !pos) fail(PBX_ERR_VALUE, "positions must not be null");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    init_tree(T, pos, n, masses, softenings, on_device, dev.stream);
   });
+}
+
+int pbx_octree_destroy(pbx_octree *t) {
+  return guard([&] { delete (Octree *)t; });
 }
 
 int pbx_octree_build_mass(pbx_octree *t, const double *masses, int on_device) {
@@ -1592,6 +1644,46 @@ int pbx_octree_at_points(pbx_octree *t, const double *points, int64_t m, double 
     }
     PBX_HIP(hipStreamSynchronize(st));
     if (T.last_counts[2] & 0xffffffffull) fail(PBX_ERR_RUNTIME, "octree walk exceeded its step bound");
+  });
+}
+
+int pbx_octree_compute_range(pbx_octree *t, double theta, int want, int64_t first, int64_t count,
+                             int compact, double *d_pot, double *d_acc, int32_t *d_cost) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (want < 1 || want > 3) fail(PBX_ERR_VALUE, "want must be 1, 2 or 3");
+    if (!T.has_bh)
+      fail(PBX_ERR_VALUE, "mass payload not built; call build_mass() before %s",
+           method_name(want, false));
+    if (first < 0 || count < 0 || first + count > T.n)
+      fail(PBX_ERR_VALUE, "target range [%lld, %lld) outside [0, %lld)", (long long)first,
+           (long long)(first + count), (long long)T.n);
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    hipStream_t st = dev.stream;
+    ScopedTimer tm("octree.compute_range");
+    walk(T, theta, want, nullptr, count, (want & PBX_WANT_POT) ? d_pot : nullptr,
+         (want & PBX_WANT_ACC) ? d_acc : nullptr, st, first, compact, d_cost);
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 40, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    if (T.last_counts[2] & 0xffffffffull) fail(PBX_ERR_RUNTIME, "octree walk exceeded its step bound");
+  });
+}
+
+int pbx_octree_leaf_particles(pbx_octree *t, int64_t first, int64_t count, double *d_pos,
+                              double *d_mass, int64_t *d_idx) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (first < 0 || count < 0 || first + count > T.n) fail(PBX_ERR_VALUE, "range outside the tree");
+    if (!T.has_bh) fail(PBX_ERR_VALUE, "mass payload not built; call build_mass() first");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    if (count > 0)
+      hipLaunchKernelGGL(leaf_particles_kernel, dim3(nblk(count)), dim3(TPB), 0, dev.stream,
+                         T.rec.as<double4>(), T.perm.as<int32_t>(), first, count, d_pos, d_mass,
+                         d_idx);
+    PBX_HIP(hipGetLastError());
+    PBX_HIP(hipStreamSynchronize(dev.stream));
   });
 }
 

@@ -215,6 +215,11 @@ class Octree:
         self._n = int(n)
         return self
 
+    def _rebuild_device(self, d_pos, n, d_mass=None, d_soft=None) -> None:
+        """Rebuild on new HBM-resident particles, reusing this tree's buffers."""
+        nat.call("pbx_octree_rebuild", self._h, d_pos, int(n), d_mass, d_soft, 1)
+        self._n = int(n)
+
     def __del__(self):  # pragma: no cover - GC timing
         self.close()
 
@@ -277,6 +282,16 @@ class Octree:
     # -- device-resident form (bench) --------------------------------------
     def _compute_device(self, theta, want, d_pot=None, d_acc=None):
         nat.call("pbx_octree_compute", self._h, float(theta), int(want), d_pot, d_acc, 1)
+
+    def _compute_range_device(self, theta, want, first, count, compact, d_pot=None, d_acc=None,
+                              d_cost=None):
+        """Walk the leaf-order targets [first, first+count) (multi-GPU shard)."""
+        nat.call("pbx_octree_compute_range", self._h, float(theta), int(want), int(first),
+                 int(count), int(compact), d_pot, d_acc, d_cost)
+
+    def _leaf_particles_device(self, first, count, d_pos=None, d_mass=None, d_idx=None):
+        nat.call("pbx_octree_leaf_particles", self._h, int(first), int(count), d_pos, d_mass,
+                 d_idx)
 
     # -- introspection -----------------------------------------------------
     def info(self) -> dict:

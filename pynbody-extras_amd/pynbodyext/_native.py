@@ -79,12 +79,17 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_octree_create": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int,
                                   c_int, POINTER(c_void_p)]),
     "pbx_octree_destroy": (c_int, [c_void_p]),
+    "pbx_octree_rebuild": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int]),
     "pbx_octree_build_mass": (c_int, [c_void_p, c_void_p, c_int]),
     "pbx_octree_set_softenings": (c_int, [c_void_p, c_void_p, c_int]),
     "pbx_octree_set_kernel": (c_int, [c_void_p, c_int]),
     "pbx_octree_compute": (c_int, [c_void_p, c_double, c_int, c_void_p, c_void_p, c_int]),
     "pbx_octree_at_points": (c_int, [c_void_p, c_void_p, c_int64, c_double, c_int, c_void_p,
                                      c_void_p, c_int]),
+    "pbx_octree_compute_range": (c_int, [c_void_p, c_double, c_int, c_int64, c_int64, c_int,
+                                         c_void_p, c_void_p, c_void_p]),
+    "pbx_octree_leaf_particles": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p,
+                                          c_void_p]),
     "pbx_octree_info": (c_int, [c_void_p, _i64p]),
     "pbx_octree_export": (c_int, [c_void_p, _dp, _dp, _dp, _i64p, _i64p, _i64p, _dp]),
     "pbx_profile_create": (c_int, [POINTER(c_void_p)]),

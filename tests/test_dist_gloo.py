@@ -122,3 +122,87 @@ def test_file_rendezvous_world3(tmp_path):
         p.join(timeout=30)
         assert p.exitcode == 0
     assert got == {0: b"unique-id-bytes", 1: b"unique-id-bytes", 2: b"unique-id-bytes"}
+
+
+# --- Barnes-Hut: replicated tree, cost-balanced leaf-order target ranges ---
+def test_balanced_ranges():
+    from pynbodyext.parallel import balanced_ranges
+
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 5, 1000):
+        cost = rng.integers(1, 5000, n)
+        for w in (1, 2, 3, 8):
+            rr = balanced_ranges(cost, w)
+            assert len(rr) == w
+            assert sum(c for _, c in rr) == n
+            assert all(rr[i][0] + rr[i][1] == rr[i + 1][0] for i in range(w - 1))
+            if n >= 100 and w > 1:
+                loads = [cost[f:f + c].sum() for f, c in rr]
+                assert max(loads) <= cost.sum() / w + cost.max()
+
+
+def _tree_worker(rank, world, port, n, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from oracle import tree as ot
+    from pynbodyext.parallel import balanced_ranges
+    from pynbodyext.synthetic import plummer
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pos, mass = plummer(n, seed=91)
+        ref = ot.RefOctree(pos, mass, 8, 3)       # every rank builds the tree
+        e = ref.export()
+        order = e["perm"]                          # leaf order -> original index
+        # costs of a first walk, then this rank's balanced leaf-order range
+        _, _, nn, npp = ref.compute_subset(order, 0.5)
+        first, count = balanced_ranges(nn + npp, world)[rank]
+        idx = order[first:first + count]
+        pot, _, _, _ = ref.compute_subset(idx, 0.5)
+        r = np.sqrt((pos[idx] ** 2).sum(1))
+        edges = np.logspace(np.log10(0.01), np.log10(50.0), 33)
+        b = np.searchsorted(edges, r, side="left") - 1
+        ok = (b >= 0) & (b < 32)
+        part = np.zeros((32, 2))
+        np.add.at(part[:, 0], b[ok], mass[idx][ok])
+        np.add.at(part[:, 1], b[ok], mass[idx][ok] * pot[ok])
+        t = torch.from_numpy(part)
+        dist.all_reduce(t)                         # RCCL all-reduce on the GPU box
+        q.put((rank, first, count, t.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_tree_world2_profile_matches_unsharded():
+    import multiprocessing as mp
+
+    from oracle import tree as ot
+    from pynbodyext.synthetic import plummer
+
+    n, world = 3000, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tree_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert res[0][1] == 0 and res[0][2] + res[1][2] == n and res[1][1] == res[0][2]
+    pos, mass = plummer(n, seed=91)
+    pot = ot.RefOctree(pos, mass, 8, 3).compute_potentials(0.5)
+    r = np.sqrt((pos ** 2).sum(1))
+    edges = np.logspace(np.log10(0.01), np.log10(50.0), 33)
+    b = np.searchsorted(edges, r, side="left") - 1
+    ok = (b >= 0) & (b < 32)
+    full = np.zeros((32, 2))
+    np.add.at(full[:, 0], b[ok], mass[ok])
+    np.add.at(full[:, 1], b[ok], mass[ok] * pot[ok])
+    for _, _, _, part in res:
+        np.testing.assert_allclose(part, full, rtol=1e-12, atol=1e-15)

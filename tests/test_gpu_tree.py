@@ -262,3 +262,65 @@ def test_1m_subset(gpu):
     idx = np.concatenate([idx, np.argsort((pos * pos).sum(1))[:64]])
     pr, ar, _, _ = ref.compute_subset(idx, 0.5)
     assert rel_pot(pot[idx], pr) < TIGHT and rel_acc(acc[idx], ar) < TIGHT
+
+
+def test_range_walk_shards_equal_full(gpu):
+    """Multi-GPU shard path on one GPU: 3 cost-balanced leaf-order ranges
+    (compact outputs) reassemble the full compute_*; costs add up to the
+    interaction counters; profile partials add up to the full profile."""
+    from pynbodyext import _native as nat
+    from pynbodyext.parallel import balanced_ranges
+    from pynbodyext.profiles._device import SRC_W, DeviceBins
+
+    n = 30_000
+    pos, mass = plummer(n, seed=97)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    pot_full = dev.compute_potentials(0.5)
+    acc_full = dev.compute_accelerations(0.5)
+    totals = dev.info()
+    d_pot, d_acc = nat.DeviceArray(8 * n), nat.DeviceArray(24 * n)
+    d_cost, d_idx = nat.DeviceArray(4 * n), nat.DeviceArray(8 * n)
+    dev._compute_range_device(0.5, nat.WANT_POT, 0, n, 1, d_pot.ptr, None, d_cost.ptr)
+    cost = np.empty(n, dtype=np.int32)
+    d_cost.download(cost)
+    assert int(cost.astype(np.int64).sum()) == totals["node_interactions"] + totals["leaf_pairs"]
+    order = np.empty(n, dtype=np.int64)
+    dev._leaf_particles_device(0, n, None, None, d_idx.ptr)
+    d_idx.download(order)
+    assert np.array_equal(np.sort(order), np.arange(n))
+    edges = np.logspace(np.log10(0.01), np.log10(50.0), 65)
+    full = DeviceBins.select(pos, mass, ndim=3)
+    full.assign(edges)
+    mom_full = full.moments(pot_full, SRC_W)
+    mom_sum = np.zeros_like(mom_full)
+    d_spos, d_smass = nat.DeviceArray(24 * n), nat.DeviceArray(8 * n)
+    for first, count in balanced_ranges(cost, 3):
+        dev._compute_range_device(0.5, nat.WANT_POT | nat.WANT_ACC, first, count, 1, d_pot.ptr,
+                                  d_acc.ptr, None)
+        p = np.empty(count)
+        a = np.empty((count, 3))
+        d_pot.download(p)
+        d_acc.download(a)
+        ids = order[first:first + count]
+        assert np.array_equal(p, pot_full[ids]) and np.array_equal(a, acc_full[ids])
+        dev._leaf_particles_device(first, count, d_spos.ptr, d_smass.ptr, None)
+        part = DeviceBins.select(d_spos.ptr, d_smass.ptr, ndim=3, on_device=True, n=count)
+        part.assign(edges)
+        mom_sum += part.moments(d_pot, SRC_W)
+    np.testing.assert_array_equal(mom_sum[:, 0] > 0, mom_full[:, 0] > 0)
+    np.testing.assert_allclose(mom_sum, mom_full, rtol=1e-12, atol=1e-300)
+    with pytest.raises(ValueError, match="outside"):
+        dev._compute_range_device(0.5, nat.WANT_POT, n - 5, 10, 1, d_pot.ptr, None, None)
+
+
+def test_rebuild_reuses_handle(gpu):
+    from pynbodyext import _native as nat
+
+    pos1, m1 = plummer(5000, seed=3)
+    pos2, m2 = plummer(7000, seed=4)
+    t = _engine.Octree(pos1, m1, 8, 3)
+    d_pos, d_m = nat.DeviceArray.from_host(pos2), nat.DeviceArray.from_host(m2)
+    t._rebuild_device(d_pos.ptr, len(pos2), d_m.ptr)
+    ref = ot.RefOctree(pos2, m2, 8, 3)
+    check_structure(t, ref, 3)
+    check_walk(t, ref, 0.5, len(pos2))
