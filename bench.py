@@ -464,7 +464,7 @@ def main():
             "frac": achieved_tf / FP64_VECTOR_PEAK_TFLOPS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "direct_kernel<Newtonian, pot+acc, self-skip>",
+            "kernel": "sym_kernel<pot+acc> (each unordered pair once)" if solver.symmetric else "direct_kernel<Newtonian, pot+acc, self-skip>",
             "flop_per_pair": FLOP_PER_PAIR,
             "kernel_ms": kern_avg_ms,
         },

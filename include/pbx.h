@@ -127,6 +127,20 @@ int pbx_direct_dev(const double *d_src, const double *d_src_h, int64_t n_src,
                    int64_t self_offset, int kernel, int want, double *d_pot,
                    double *d_acc);
 
+/* All-particles Newtonian direct sum with each unordered pair evaluated
+ * once (Newton's third law; pbx_direct_dev and the host entry points use it
+ * by themselves for n >= 8192), split into work units so that ranks can
+ * share one solve: every rank runs its units into a per-particle
+ * accumulator d_acc4 (npad x 4 doubles, zeroed by the caller), the ranks sum
+ * the accumulators (pbx_comm_allreduce_f64), and each rank converts its own
+ * particles [lo, hi) into potentials / accelerations.  h_weights (optional,
+ * n_units) = relative cost of each unit, for balancing. */
+int pbx_direct_sym_plan(int64_t n, int64_t *npad, int64_t *n_units, int64_t *h_weights);
+int pbx_direct_sym_accumulate(const double *d_src, int64_t n, int64_t u0, int64_t u1, int want,
+                              double *d_acc4);
+int pbx_direct_sym_finish(const double *d_acc4, int64_t lo, int64_t hi, int want, double *d_pot,
+                          double *d_acc);
+
 /* ------------------------------------------------------------------ */
 /* gravity: Barnes-Hut octree                                          */
 /* ------------------------------------------------------------------ */

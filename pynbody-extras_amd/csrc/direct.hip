@@ -301,12 +301,42 @@ static void launch_want(int want, bool self, hipStream_t st, dim3 grid, const do
   }
 }
 
+// direct_sym.hip
+int64_t sym_padded(int64_t n);
+int64_t sym_unit_count(int64_t n);
+void sym_accumulate(Device &d, double4 *rec, int64_t n, int64_t u0, int64_t u1, int want,
+                    double *acc4, DevBuf &unit_buf);
+void sym_finish(Device &d, const double *acc4, int64_t lo, int64_t hi, int want, double *pot,
+                double *acc);
+
+// All-particles Newtonian sums of at least this many particles evaluate each
+// unordered pair once (direct_sym.hip); PBX_DIRECT_SYM=0 disables it.
+static constexpr int64_t kSymMinN = 8192;
+static bool sym_enabled() {
+  static bool on = [] {
+    const char *v = std::getenv("PBX_DIRECT_SYM");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 // Launch the direct sum on device-resident data (all pointers device).
 void direct_device(Device &d, const double *src, const double *src_h, int64_t n_src,
                    const double *tgt, const double *tgt_h, int64_t n_tgt, int64_t self_offset,
                    int kernel, int want, double *pot, double *acc) {
   if (n_tgt <= 0) return;
   hipStream_t st = d.stream;
+  if (kernel == PBX_KERNEL_NONE && self_offset == 0 && n_tgt == n_src && n_src >= kSymMinN &&
+      sym_enabled()) {
+    const int64_t npad = sym_padded(n_src);
+    double4 *rec = (double4 *)d.slot(kSlotSymRec).ensure(sizeof(double4) * npad);
+    double *acc4 = (double *)d.slot(kSlotSymAcc).ensure(sizeof(double) * 4 * npad);
+    PBX_HIP(hipMemcpyAsync(rec, src, sizeof(double4) * n_src, hipMemcpyDeviceToDevice, st));
+    PBX_HIP(hipMemsetAsync(acc4, 0, sizeof(double) * 4 * npad, st));
+    sym_accumulate(d, rec, n_src, 0, sym_unit_count(n_src), want, acc4, d.slot(kSlotSymUnits));
+    sym_finish(d, acc4, 0, n_src, want, pot, acc);
+    return;
+  }
   if (n_src <= 0) {
     if (want & PBX_WANT_POT) PBX_HIP(hipMemsetAsync(pot, 0, sizeof(double) * n_tgt, st));
     if (want & PBX_WANT_ACC) PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 3 * n_tgt, st));

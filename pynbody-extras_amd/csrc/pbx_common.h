@@ -95,6 +95,9 @@ enum Slot {
   kSlotProf6,
   kSlotProf7,
   kSlotComm,
+  kSlotSymRec,
+  kSlotSymAcc,
+  kSlotSymUnits,
   kSlotCount
 };
 

@@ -76,6 +76,9 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_pack_sources": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "pbx_direct_dev": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
                                c_int64, c_int, c_int, c_void_p, c_void_p]),
+    "pbx_direct_sym_plan": (c_int, [c_int64, _i64p, _i64p, _i64p]),
+    "pbx_direct_sym_accumulate": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p]),
+    "pbx_direct_sym_finish": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     "pbx_octree_create": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int,
                                   c_int, POINTER(c_void_p)]),
     "pbx_octree_destroy": (c_int, [c_void_p]),

@@ -24,6 +24,9 @@ import numpy as np
 from . import _native as nat
 
 
+SYM_MIN_N = 8192  # all-particles solves of at least this size use direct_sym.hip
+
+
 def shard_bounds(n_total: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous balanced shard [lo, hi) of rank (first n % world ranks get +1)."""
     base, extra = divmod(int(n_total), int(world))
@@ -147,10 +150,15 @@ class ShardedDirect:
     potential and acceleration of the local particles due to ALL particles.
     """
 
-    def __init__(self, comm, n_total: int, pos_local: np.ndarray, mass_local: np.ndarray | None):
+    def __init__(self, comm, n_total: int, pos_local: np.ndarray, mass_local: np.ndarray | None,
+                 symmetric: bool | None = None):
         self.comm = comm
         world = comm.nranks if comm is not None else 1
         rank = comm.rank if comm is not None else 0
+        # each unordered pair once (csrc/direct_sym.hip): the work units of the
+        # pair triangle are split across ranks by weight, one RCCL all-reduce
+        # of the per-particle accumulator, each rank converts its own shard
+        self.symmetric = (n_total >= SYM_MIN_N) if symmetric is None else bool(symmetric)
         self.n_total = int(n_total)
         self.shards = all_shards(self.n_total, world)
         self.lo, self.hi = self.shards[rank]
@@ -165,6 +173,17 @@ class ShardedDirect:
         self.d_acc = nat.DeviceArray(24 * max(self.n_loc, 1))
         self._counts = [32 * (h - lo) for lo, h in self.shards]
         self._displs = [32 * lo for lo, _ in self.shards]
+        if self.symmetric:
+            npad, nunits = ctypes.c_int64(), ctypes.c_int64()
+            nat.call("pbx_direct_sym_plan", self.n_total, ctypes.byref(npad), ctypes.byref(nunits),
+                     None)
+            w = np.zeros(nunits.value, dtype=np.int64)
+            nat.call("pbx_direct_sym_plan", self.n_total, None, None,
+                     w.ctypes.data_as(ctypes.POINTER(c_int64)))
+            first, count = balanced_ranges(w, world)[rank]
+            self.units = (first, first + count)
+            self.npad = npad.value
+            self.d_acc4 = nat.DeviceArray(32 * self.npad)
 
     def gather_sources(self) -> None:
         nat.call("pbx_pack_sources", self.d_pos.ptr, self.d_mass.ptr if self.d_mass else None,
@@ -173,10 +192,18 @@ class ShardedDirect:
             self.comm.allgatherv(self.d_rec.ptr, self._counts, self._displs)
 
     def solve(self, want: int = nat.WANT_POT | nat.WANT_ACC) -> None:
-        nat.call("pbx_direct_dev", self.d_rec.ptr, None, self.n_total, self.d_pos.ptr, None,
-                 self.n_loc, self.lo, nat.KERNEL_NONE, want,
-                 self.d_pot.ptr if want & nat.WANT_POT else None,
-                 self.d_acc.ptr if want & nat.WANT_ACC else None)
+        pot = self.d_pot.ptr if want & nat.WANT_POT else None
+        acc = self.d_acc.ptr if want & nat.WANT_ACC else None
+        if not self.symmetric:
+            nat.call("pbx_direct_dev", self.d_rec.ptr, None, self.n_total, self.d_pos.ptr, None,
+                     self.n_loc, self.lo, nat.KERNEL_NONE, want, pot, acc)
+            return
+        nat.call("pbx_memset", self.d_acc4.ptr, 0, ctypes.c_size_t(32 * self.npad))
+        nat.call("pbx_direct_sym_accumulate", self.d_rec.ptr, self.n_total, self.units[0],
+                 self.units[1], want, self.d_acc4.ptr)
+        if self.comm is not None:
+            self.comm.allreduce_sum_f64(self.d_acc4.ptr, self.d_acc4.ptr, 4 * self.npad)
+        nat.call("pbx_direct_sym_finish", self.d_acc4.ptr, self.lo, self.hi, want, pot, acc)
 
     def step(self, want: int = nat.WANT_POT | nat.WANT_ACC) -> None:
         self.gather_sources()

@@ -71,3 +71,56 @@ def test_sharded_solve_of_one_shard_matches_oracle(gpu):
     pr, ar = og.direct_subset(pos, mass, np.arange(lo, hi))
     assert np.max(np.abs(pot - pr) / np.abs(pr)) < 1e-10
     assert np.max(np.linalg.norm(acc - ar, axis=1) / np.linalg.norm(ar, axis=1)) < 1e-10
+
+
+def test_symmetric_units_split_across_ranks(gpu):
+    """Multi-GPU symmetric direct sum on one GPU: the unit triangle split into
+    3 weight-balanced ranges (what 3 ranks run), accumulators summed (what the
+    RCCL all-reduce does), each rank's shard finished."""
+    import ctypes
+
+    from pynbodyext.parallel import balanced_ranges, shard_bounds
+
+    n, world = 20_000, 3
+    pos, mass = plummer(n, seed=8)
+    s = ShardedDirect(None, n, pos, mass, symmetric=True)
+    s.gather_sources()
+    npad, nunits = ctypes.c_int64(), ctypes.c_int64()
+    nat.call("pbx_direct_sym_plan", n, ctypes.byref(npad), ctypes.byref(nunits), None)
+    w = np.zeros(nunits.value, dtype=np.int64)
+    nat.call("pbx_direct_sym_plan", n, None, None, w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    total = np.zeros(4 * npad.value)
+    d_acc4 = nat.DeviceArray(32 * npad.value)
+    for first, count in balanced_ranges(w, world):
+        nat.call("pbx_memset", d_acc4.ptr, 0, ctypes.c_size_t(32 * npad.value))
+        nat.call("pbx_direct_sym_accumulate", s.d_rec.ptr, n, first, first + count, 3, d_acc4.ptr)
+        part = np.empty(4 * npad.value)
+        d_acc4.download(part)
+        total += part
+    d_acc4.upload(total)
+    pr = og.direct_potentials(pos, mass)
+    ar = og.direct_accelerations(pos, mass)
+    for rank in range(world):
+        lo, hi = shard_bounds(n, world, rank)
+        d_pot, d_acc = nat.DeviceArray(8 * (hi - lo)), nat.DeviceArray(24 * (hi - lo))
+        nat.call("pbx_direct_sym_finish", d_acc4.ptr, lo, hi, 3, d_pot.ptr, d_acc.ptr)
+        pot = d_pot.download(np.empty(hi - lo))
+        acc = d_acc.download(np.empty((hi - lo, 3)))
+        assert np.max(np.abs(pot - pr[lo:hi]) / np.abs(pr[lo:hi])) < 1e-10
+        assert np.max(np.linalg.norm(acc - ar[lo:hi], axis=1) /
+                      np.linalg.norm(ar[lo:hi], axis=1)) < 1e-10
+
+
+def test_sharded_direct_symmetric_world1(gpu):
+    pos, mass = plummer(12_000, seed=9)
+    comm = Communicator(1, 0, Communicator.unique_id())
+    try:
+        s = ShardedDirect(comm, len(pos), pos, mass)
+        assert s.symmetric
+        s.step()
+        nat.synchronize()
+        pot, acc = s.results()
+    finally:
+        comm.destroy()
+    pr = og.direct_potentials(pos, mass)
+    assert np.max(np.abs(pot - pr) / np.abs(pr)) < 1e-10
