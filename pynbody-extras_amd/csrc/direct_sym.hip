@@ -89,20 +89,18 @@ __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t j
             __builtin_fma(dx, dx, __builtin_fma(dy, dy, __builtin_fma(dz, dz, kR2Tiny)));
         const double y0 = __builtin_amdgcn_rsq(s2);
         const double w = y0 * __builtin_fma(-s2, y0 * y0, 3.0);  // 2/r
-        const double w2 = w * w;
-        const double mw = ms * w;
-        if (WANT & PBX_WANT_POT) tp[kt] += mw;
+        const double q = w * (w * w);                              // 8/r^3
+        if (WANT & PBX_WANT_POT) tp[kt] = __builtin_fma(ms, w, tp[kt]);
         if (WANT & PBX_WANT_ACC) {
-          const double g = mw * w2;
+          const double g = ms * q;
           ta[kt] = __builtin_fma(g, dx, ta[kt]);
           tb[kt] = __builtin_fma(g, dy, tb[kt]);
           tc[kt] = __builtin_fma(g, dz, tc[kt]);
         }
         if (SYMM) {
-          const double mt = tm[kt] * w;
-          if (WANT & PBX_WANT_POT) sp[ks] += mt;
+          if (WANT & PBX_WANT_POT) sp[ks] = __builtin_fma(tm[kt], w, sp[ks]);
           if (WANT & PBX_WANT_ACC) {
-            const double g = mt * w2;
+            const double g = tm[kt] * q;
             sa[ks] = __builtin_fma(-g, dx, sa[ks]);
             sb[ks] = __builtin_fma(-g, dy, sb[ks]);
             sc[ks] = __builtin_fma(-g, dz, sc[ks]);
