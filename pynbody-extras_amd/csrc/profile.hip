@@ -222,6 +222,165 @@ __global__ void gather_keys(const uint64_t *__restrict__ keys, const int64_t *__
   if (t < m) out[t] = dkey_inv(keys[ranks[t]]);
 }
 
+// ------------------------------------------------ equaln by radix select
+// The nbins+1 order statistics of the window keys, found together by an MSD
+// radix select on 12-bit digits of (key - base): per level one read of x
+// and a digit histogram per active prefix group; each rank picks its digit
+// from its group's prefix sums and narrows its residual rank.  No sort, no
+// host round trip until the edges are done.
+constexpr int MS_BITS = 12;
+constexpr int MS_DIG = 1 << MS_BITS;
+constexpr int MS_MAXQ = 1025;  // nbins <= 1024 (more bins: the radix-sort path)
+
+struct MsRank {
+  uint64_t prefix;  // digits chosen so far
+  int64_t rr;       // rank inside the current prefix group
+  int32_t group;    // index of the group (sorted unique prefixes)
+  int32_t pad;
+};
+
+__global__ void __launch_bounds__(TPB)
+    msel_hist(const double *__restrict__ x, int64_t n, uint64_t ka, uint64_t kb, uint64_t base,
+              int s, int w, int first, const uint64_t *__restrict__ groups,
+              const int32_t *__restrict__ ng_ptr, uint32_t *__restrict__ H) {
+  __shared__ uint32_t lh[MS_DIG];    // level 0: one group, privatised histogram
+  __shared__ uint64_t gs[MS_MAXQ];   // later levels: the active prefixes (sorted)
+  const int ng = first ? 1 : *ng_ptr;
+  if (first)
+    for (int i = threadIdx.x; i < MS_DIG; i += TPB) lh[i] = 0;
+  else
+    for (int i = threadIdx.x; i < ng; i += TPB) gs[i] = groups[i];
+  __syncthreads();
+  const uint64_t dmask = (1ull << w) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const uint64_t k = dkey(x[i]);
+    if (k < ka || k > kb) continue;
+    const uint64_t off = k - base;
+    const uint32_t d = (uint32_t)((off >> s) & dmask);
+    if (first) {
+      atomicAdd(&lh[d], 1u);
+      continue;
+    }
+    const uint64_t pref = off >> (s + w);
+    int a = 0, b = ng;
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (gs[mid] < pref) a = mid + 1; else b = mid;
+    }
+    if (a < ng && gs[a] == pref) atomicAdd(&H[(int64_t)a * MS_DIG + d], 1u);
+  }
+  if (first) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < MS_DIG; i += TPB)
+      if (lh[i]) atomicAdd(&H[i], lh[i]);
+  }
+}
+
+// one block per active group: prefix sums of its histogram (the row is
+// zeroed for the next level), then every rank of the group picks its digit
+__global__ void __launch_bounds__(TPB)
+    msel_resolve(uint32_t *__restrict__ H, const int32_t *__restrict__ ng_ptr,
+                 MsRank *__restrict__ R, int nq, int first, int64_t nbins, int w,
+                 int64_t *__restrict__ m_out) {
+  const int g = blockIdx.x;
+  const int ng = first ? 1 : *ng_ptr;
+  if (g >= ng) return;
+  __shared__ uint32_t incl[MS_DIG];
+  __shared__ uint32_t wsum[NWAVE];
+  uint32_t *row = H + (int64_t)g * MS_DIG;
+  uint32_t v[MS_DIG / TPB];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int k = 0; k < MS_DIG / TPB; ++k) {
+    v[k] = row[threadIdx.x * (MS_DIG / TPB) + k];
+    tot += v[k];
+  }
+  uint32_t run = block_excl_scan(tot, wsum, nullptr);
+#pragma unroll
+  for (int k = 0; k < MS_DIG / TPB; ++k) {
+    run += v[k];
+    incl[threadIdx.x * (MS_DIG / TPB) + k] = run;
+    row[threadIdx.x * (MS_DIG / TPB) + k] = 0;
+  }
+  __syncthreads();
+  if (first) {  // the window size m and the reference's ranks (bins.py:738-744)
+    const int64_t m = (int64_t)incl[MS_DIG - 1];
+    if (threadIdx.x == 0) *m_out = m;
+    for (int q = threadIdx.x; q < nq; q += TPB) {
+      int64_t r = 0;
+      if (m >= 2) r = (q == nq - 1) ? m - 1 : (int64_t)((double)(q * m) / (double)nbins);
+      R[q].prefix = 0;
+      R[q].rr = r;
+      R[q].group = 0;
+    }
+    __syncthreads();
+  }
+  for (int q = threadIdx.x; q < nq; q += TPB) {
+    if (R[q].group != g) continue;
+    const int64_t rr = R[q].rr;
+    int a = 0, b = MS_DIG - 1;  // first digit whose inclusive count exceeds rr
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if ((int64_t)incl[mid] <= rr) a = mid + 1; else b = mid;
+    }
+    R[q].rr = rr - (a ? (int64_t)incl[a - 1] : 0);
+    R[q].prefix = (R[q].prefix << w) | (uint64_t)a;
+  }
+}
+
+// the active groups of the next level: sorted unique prefixes (one block)
+__global__ void __launch_bounds__(1024)
+    msel_groups(MsRank *__restrict__ R, int nq, uint64_t *__restrict__ groups,
+                int32_t *__restrict__ ng_out) {
+  __shared__ uint64_t key[2048];
+  __shared__ int32_t cnt[2048];
+  for (int i = threadIdx.x; i < 2048; i += 1024) key[i] = i < nq ? R[i].prefix : ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= 2048; size <<= 1)  // bitonic sort
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < 2048; i += 1024) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const uint64_t a = key[i], b = key[j];
+          if ((a > b) == up) {
+            key[i] = b;
+            key[j] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = threadIdx.x; i < 2048; i += 1024)
+    cnt[i] = (i < nq && (i == 0 || key[i] != key[i - 1])) ? 1 : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // compact the unique prefixes (nq <= 1025: serial is fine)
+    int u = 0;
+    for (int i = 0; i < nq; ++i)
+      if (cnt[i]) key[u++] = key[i];
+    *ng_out = u;
+    cnt[0] = u;
+  }
+  __syncthreads();
+  const int ng = cnt[0];
+  for (int i = threadIdx.x; i < ng; i += 1024) groups[i] = key[i];
+  for (int q = threadIdx.x; q < nq; q += 1024) {
+    const uint64_t p = R[q].prefix;
+    int a = 0, b = ng;
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if (key[mid] < p) a = mid + 1; else b = mid;
+    }
+    R[q].group = a;
+  }
+}
+
+__global__ void msel_edges(const MsRank *__restrict__ R, int nq, uint64_t base,
+                           double *__restrict__ out) {
+  const int q = blockIdx.x * TPB + threadIdx.x;
+  if (q < nq) out[q] = dkey_inv(base + R[q].prefix);
+}
+
 // ----------------------------------------------------------------- assign
 // bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
 // x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379)
@@ -352,6 +511,7 @@ struct Profile {
   bool csr_ready = false;
   bool mm_valid = false;   // mm = min / max key of x, cached on the host
   uint64_t mm[2] = {0, 0};
+  Buf msH, msR, msG, msNg, msM;
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
 };
@@ -395,6 +555,72 @@ static void minmax_of(Profile &P, hipStream_t st, uint64_t out[2]) {
   out[1] = P.mm[1];
 }
 
+// PBX_EQUALN=sort selects the radix-sort path (kept for large nbins / A/B)
+static bool select_enabled() {
+  static bool on = [] {
+    const char *v = std::getenv("PBX_EQUALN");
+    return !(v && std::strcmp(v, "sort") == 0);
+  }();
+  return on;
+}
+
+// equaln edges by multi-rank radix select (see msel_* kernels).  Window and
+// rank semantics are those of the sort path: sorted_x[sorted_x >= bin_min],
+// then [sorted_x <= bin_max] (bins.py:734-737; NaN fails both and a NaN
+// bound keeps nothing; without bounds NaN sorts last and stays), then
+// edges = s[0], s[int(i*m/nb)], s[m-1] (bins.py:738-744).
+static void equaln_select(Profile &P, hipStream_t st, int64_t nbins, int has_min, double bin_min,
+                          int has_max, double bin_max, double *h_edges, int64_t *n_edges) {
+  const int nq = (int)nbins + 1;
+  uint64_t mm[2];
+  minmax_of(P, st, mm);
+  bool empty = false;
+  uint64_t ka = 0ull, kb = ~0ull;
+  if (has_min || has_max) {
+    kb = ~0ull - 1;  // NaN keys never pass a comparison
+    if (has_min) {
+      if (bin_min != bin_min) empty = true;
+      else ka = dkey(bin_min);
+    }
+    if (has_max) {
+      if (bin_max != bin_max) empty = true;
+      else kb = std::min<uint64_t>(kb, dkey(bin_max));
+    }
+  }
+  const uint64_t lo = std::max<uint64_t>(ka, mm[0]);
+  const uint64_t hi = std::min<uint64_t>(kb, mm[1]);
+  if (empty || lo > hi) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
+  const uint64_t span = hi - lo;
+  const int B = span ? 64 - __builtin_clzll(span) : 1;
+  const int L = (B + MS_BITS - 1) / MS_BITS;
+  uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * (size_t)nq * MS_DIG);
+  MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
+  uint64_t *G = (uint64_t *)P.msG.get(sizeof(uint64_t) * (size_t)nq);
+  int32_t *ng = (int32_t *)P.msNg.get(16);
+  int64_t *m_dev = (int64_t *)P.msM.get(16);
+  double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
+  PBX_HIP(hipMemsetAsync(H, 0, sizeof(uint32_t) * (size_t)nq * MS_DIG, st));
+  const int64_t n = P.n;
+  const unsigned grid = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (n + TPB - 1) / TPB));
+  for (int l = 0; l < L; ++l) {
+    const int w = (l == 0) ? B - MS_BITS * (L - 1) : MS_BITS;
+    const int sh = MS_BITS * (L - 1 - l);
+    hipLaunchKernelGGL(msel_hist, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n, ka, kb,
+                       lo, sh, w, l == 0 ? 1 : 0, G, ng, H);
+    hipLaunchKernelGGL(msel_resolve, dim3(l == 0 ? 1 : nq), dim3(TPB), 0, st, H, ng, R, nq,
+                       l == 0 ? 1 : 0, nbins, w, m_dev);
+    if (l + 1 < L) hipLaunchKernelGGL(msel_groups, dim3(1), dim3(1024), 0, st, R, nq, G, ng);
+  }
+  hipLaunchKernelGGL(msel_edges, dim3(ceil_div(nq, TPB)), dim3(TPB), 0, st, R, nq, lo, de);
+  PBX_HIP(hipGetLastError());
+  int64_t m = 0;
+  PBX_HIP(hipMemcpyAsync(&m, m_dev, 8, hipMemcpyDeviceToHost, st));
+  PBX_HIP(hipMemcpyAsync(h_edges, de, sizeof(double) * nq, hipMemcpyDeviceToHost, st));
+  PBX_HIP(hipStreamSynchronize(st));
+  if (m == 0) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
+  *n_edges = (m < 2) ? 2 : nq;
+}
+
 static Profile &as_profile(void *h) {
   if (!h) fail(PBX_ERR_VALUE, "null profile handle");
   Profile *p = (Profile *)h;
@@ -427,7 +653,8 @@ int pbx_profile_destroy(void *handle) {
     current_device();
     Buf *all[] = {&p->x, &p->w, &p->idx, &p->bins, &p->perm, &p->keys0, &p->keys1, &p->vtmp,
                   &p->hist, &p->tsum, &p->edges, &p->counts, &p->minmax, &p->slab, &p->acc,
-                  &p->field, &p->weight, &p->ranks, &p->bounds};
+                  &p->field, &p->weight, &p->ranks, &p->bounds, &p->msH, &p->msR, &p->msG,
+                  &p->msNg, &p->msM};
     for (Buf *b : all) b->release();
     delete p;
   });
@@ -580,6 +807,10 @@ int pbx_profile_edges_equaln(void *handle, int64_t nbins, int has_min, double bi
     ScopedTimer tm("pbx.profile.equaln");
     const int64_t n = P.n;
     if (n == 0) fail(PBX_ERR_VALUE, "Cannot create bins: input array is empty");
+    if (nbins + 1 <= MS_MAXQ && select_enabled()) {
+      equaln_select(P, st, nbins, has_min, bin_min, has_max, bin_max, h_edges, n_edges);
+      return;
+    }
     uint64_t *k0 = (uint64_t *)P.keys0.get(sizeof(uint64_t) * (size_t)n);
     uint64_t *k1 = (uint64_t *)P.keys1.get(sizeof(uint64_t) * (size_t)n);
     unsigned grid = (unsigned)std::min<int64_t>(4096, (n + TPB - 1) / TPB);
