@@ -139,18 +139,27 @@ enum ValMode { VAL_NONE = 0, VAL_IOTA = 1, VAL_ARRAY = 2 };
 
 // Stable scatter of one radix pass.  Element order inside a tile is
 // (wave, iteration, lane) == index order, so ranks from per-wave running
-// counters keep the sort stable.
+// counters keep the sort stable.  The tile is first sorted by digit in LDS
+// and then written out run by run: consecutive threads store consecutive
+// addresses of one digit's output run (a direct scatter would store 64
+// lanes into up to 64 different runs).  kout may be null (values only).
 template <typename K, int VM>
 __global__ void __launch_bounds__(TPB)
     radix_scatter(const K *__restrict__ kin, const int32_t *__restrict__ vin, int64_t n, int shift,
                   const uint32_t *__restrict__ offs, uint32_t ntiles, K *__restrict__ kout,
                   int32_t *__restrict__ vout) {
   __shared__ uint32_t run[NWAVE][RADIX];
+  __shared__ uint32_t dstart[RADIX];  // tile-local start of each digit
+  __shared__ uint32_t gofs[RADIX];    // global start of each digit's run of this tile
+  __shared__ uint32_t wsum[NWAVE];
+  __shared__ K sk[TILE];
+  __shared__ int32_t sv[VM == VAL_NONE ? 1 : TILE];
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
   __syncthreads();
-  const int64_t wbase = (int64_t)blockIdx.x * TILE + (int64_t)w * (TILE / NWAVE);
+  const int64_t tbase = (int64_t)blockIdx.x * TILE;
+  const int64_t wbase = tbase + (int64_t)w * (TILE / NWAVE);
   K key[IPT];
   // phase 1: per-wave digit counts
 #pragma unroll
@@ -163,10 +172,16 @@ __global__ void __launch_bounds__(TPB)
     if (ok && rank_below(m) == 0) run[w][d] += (uint32_t)__popcll(m);
   }
   __syncthreads();
-  // exclusive prefix over waves + global offset of (digit, tile)
+  // tile-local digit starts, per-wave starts inside them, global run starts
   {
     const int d = threadIdx.x;  // TPB == RADIX
-    uint32_t acc = offs[(int64_t)d * ntiles + blockIdx.x];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) tot += run[ww][d];
+    const uint32_t st = block_excl_scan(tot, wsum, nullptr);
+    dstart[d] = st;
+    gofs[d] = offs[(int64_t)d * ntiles + blockIdx.x];
+    uint32_t acc = st;
 #pragma unroll
     for (int ww = 0; ww < NWAVE; ++ww) {
       uint32_t c = run[ww][d];
@@ -175,7 +190,7 @@ __global__ void __launch_bounds__(TPB)
     }
   }
   __syncthreads();
-  // phase 2: positions
+  // phase 2: tile-local positions -> LDS
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     int64_t i = wbase + k * 64 + lane;
@@ -188,11 +203,21 @@ __global__ void __launch_bounds__(TPB)
     if (ok && r == 0) run[w][d] = base + (uint32_t)__popcll(m);
     __builtin_amdgcn_wave_barrier();
     if (ok) {
-      uint32_t pos = base + r;
-      kout[pos] = key[k];
-      if (VM == VAL_IOTA) vout[pos] = (int32_t)i;
-      if (VM == VAL_ARRAY) vout[pos] = vin[i];
+      const uint32_t pos = base + r;
+      sk[pos] = key[k];
+      if (VM == VAL_IOTA) sv[pos] = (int32_t)i;
+      if (VM == VAL_ARRAY) sv[pos] = vin[i];
     }
+  }
+  __syncthreads();
+  // phase 3: runs out, coalesced
+  const int tn = (int)((n - tbase) < TILE ? (n - tbase) : TILE);
+  for (int j = threadIdx.x; j < tn; j += TPB) {
+    const K kk = sk[j];
+    const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+    const uint32_t p = gofs[d] + ((uint32_t)j - dstart[d]);
+    if (kout) kout[p] = kk;
+    if (VM != VAL_NONE) vout[p] = sv[j];
   }
 }
 
@@ -247,11 +272,13 @@ static inline void scan_u32(Buf &tsum, hipStream_t st, uint32_t *a, int64_t len,
 
 // one stable radix pass: kin -> kout (+ values)
 template <typename K>
+// (prehist: hist_buf already holds this pass's [digit][tile] counts)
 static void radix_pass(Buf &hist_buf, Buf &tsum, hipStream_t st, const K *kin, const int32_t *vin,
-                       int vm, int64_t n, int shift, K *kout, int32_t *vout) {
+                       int vm, int64_t n, int shift, K *kout, int32_t *vout, bool prehist = false) {
   uint32_t nt = ntiles_of(n);
   uint32_t *hist = (uint32_t *)hist_buf.get(sizeof(uint32_t) * (size_t)nt * RADIX);
-  hipLaunchKernelGGL(radix_hist<K>, dim3(nt), dim3(TPB), 0, st, kin, n, shift, hist, nt);
+  if (!prehist)
+    hipLaunchKernelGGL(radix_hist<K>, dim3(nt), dim3(TPB), 0, st, kin, n, shift, hist, nt);
   scan_u32(tsum, st, hist, (int64_t)nt * RADIX);
   if (vm == VAL_NONE)
     hipLaunchKernelGGL((radix_scatter<K, VAL_NONE>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,

@@ -224,13 +224,21 @@ __global__ void gather_keys(const uint64_t *__restrict__ keys, const int64_t *__
 
 // ------------------------------------------------ equaln by radix select
 // The nbins+1 order statistics of the window keys, found together by an MSD
-// radix select on 12-bit digits of (key - base): per level one read of x
-// and a digit histogram per active prefix group; each rank picks its digit
-// from its group's prefix sums and narrows its residual rank.  No sort, no
-// host round trip until the edges are done.
+// radix select on the bits of (key - base).  Level 0 takes the top 14 bits
+// with a privatised LDS histogram per block (rows reduced afterwards); each
+// rank then picks its digit from the prefix sums and narrows its residual
+// rank.  Level 1 reads x once more, keeps only keys whose level-0 digit some
+// rank chose (an LDS bitmap test, then a search of the sorted active groups)
+// and appends them to a compact list; deeper levels work on that list only,
+// compacting again as they go.  No sort, no host round trip until the edges
+// are done.
+constexpr int MS0_BITS = 14;
+constexpr int MS0_DIG = 1 << MS0_BITS;
+constexpr int MS0_TPB = 1024;
 constexpr int MS_BITS = 12;
 constexpr int MS_DIG = 1 << MS_BITS;
 constexpr int MS_MAXQ = 1025;  // nbins <= 1024 (more bins: the radix-sort path)
+constexpr int MS_MAXL = 8;
 
 struct MsRank {
   uint64_t prefix;  // digits chosen so far
@@ -239,72 +247,180 @@ struct MsRank {
   int32_t pad;
 };
 
-__global__ void __launch_bounds__(TPB)
-    msel_hist(const double *__restrict__ x, int64_t n, uint64_t ka, uint64_t kb, uint64_t base,
-              int s, int w, int first, const uint64_t *__restrict__ groups,
-              const int32_t *__restrict__ ng_ptr, uint32_t *__restrict__ H) {
-  __shared__ uint32_t lh[MS_DIG];    // level 0: one group, privatised histogram
-  __shared__ uint64_t gs[MS_MAXQ];   // later levels: the active prefixes (sorted)
-  const int ng = first ? 1 : *ng_ptr;
-  if (first)
-    for (int i = threadIdx.x; i < MS_DIG; i += TPB) lh[i] = 0;
-  else
-    for (int i = threadIdx.x; i < ng; i += TPB) gs[i] = groups[i];
+// level 0: one 2^w0-bin histogram per block in LDS, written out as a row
+__global__ void __launch_bounds__(MS0_TPB)
+    msel_hist0(const double *__restrict__ x, int64_t n, uint64_t ka, uint64_t kb, uint64_t base,
+               int s, uint32_t *__restrict__ rows) {
+  __shared__ uint32_t lh[MS0_DIG];
+  for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
   __syncthreads();
-  const uint64_t dmask = (1ull << w) - 1;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
-    const uint64_t k = dkey(x[i]);
-    if (k < ka || k > kb) continue;
-    const uint64_t off = k - base;
-    const uint32_t d = (uint32_t)((off >> s) & dmask);
-    if (first) {
-      atomicAdd(&lh[d], 1u);
-      continue;
+  // window keys satisfy base <= k <= base + span < base + 2^B, so the digit
+  // (k - base) >> s is below 2^w0 without masking
+  constexpr int U = 8;  // loads in flight per thread
+  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * U; i0 < n; i0 += (int64_t)gridDim.x * MS0_TPB * U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+      v[u] = i < n ? x[i] : 0.0;
     }
-    const uint64_t pref = off >> (s + w);
-    int a = 0, b = ng;
-    while (a < b) {
-      const int mid = (a + b) >> 1;
-      if (gs[mid] < pref) a = mid + 1; else b = mid;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+      const uint64_t k = dkey(v[u]);
+      if (i < n && k >= ka && k <= kb) atomicAdd(&lh[(uint32_t)((k - base) >> s)], 1u);
     }
-    if (a < ng && gs[a] == pref) atomicAdd(&H[(int64_t)a * MS_DIG + d], 1u);
   }
-  if (first) {
+  __syncthreads();
+  uint32_t *row = rows + (int64_t)blockIdx.x * MS0_DIG;
+  for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) row[i] = lh[i];
+}
+
+// column sums of the level-0 rows; blockIdx.y takes every gridDim.y-th row
+// (H is zero on entry)
+__global__ void __launch_bounds__(TPB)
+    msel_reduce0(const uint32_t *__restrict__ rows, int nrows, uint32_t *__restrict__ H) {
+  const int d = blockIdx.x * TPB + threadIdx.x;
+  uint32_t s = 0;
+  for (int r = blockIdx.y; r < nrows; r += gridDim.y) s += rows[(int64_t)r * MS0_DIG + d];
+  if (s) atomicAdd(&H[d], s);
+}
+
+// levels >= 1: keys (from x on level 1, from the previous compact list
+// after) whose prefix is an active group add to that group's digit row and
+// are appended to the next compact list (when there is a next level).  Each
+// block owns a contiguous chunk and stages its members in LDS, so the shared
+// list counter sees one atomic per flush, not one per wave.
+constexpr int MS_U = 8;                  // elements per thread per iteration
+constexpr int MS_STEP = TPB * MS_U;
+constexpr int MS_STAGE = 2 * MS_STEP;    // staged members before a flush
+
+template <bool FROM_X>
+__global__ void __launch_bounds__(TPB)
+    msel_filter(const double *__restrict__ x, int64_t n, uint64_t ka, uint64_t kb, uint64_t base,
+                const uint64_t *__restrict__ in, const uint32_t *__restrict__ in_cnt, int s, int w,
+                const uint64_t *__restrict__ groups, const int32_t *__restrict__ ng_ptr,
+                uint32_t *__restrict__ H, uint64_t *__restrict__ out,
+                uint32_t *__restrict__ out_cnt) {
+  __shared__ uint64_t gs[MS_MAXQ];
+  __shared__ uint32_t bm[MS0_DIG / 32];  // level 1: the chosen level-0 digits
+  __shared__ uint64_t stage[MS_STAGE];
+  __shared__ uint32_t scnt, sbase;
+  const int ng = *ng_ptr;
+  for (int i = threadIdx.x; i < ng; i += TPB) gs[i] = groups[i];
+  if (threadIdx.x == 0) scnt = 0;
+  if (FROM_X) {
+    for (int i = threadIdx.x; i < MS0_DIG / 32; i += TPB) bm[i] = 0;
     __syncthreads();
-    for (int i = threadIdx.x; i < MS_DIG; i += TPB)
-      if (lh[i]) atomicAdd(&H[i], lh[i]);
+    for (int i = threadIdx.x; i < ng; i += TPB)
+      atomicOr(&bm[(uint32_t)gs[i] >> 5], 1u << ((uint32_t)gs[i] & 31));
+  }
+  __syncthreads();
+  const int64_t cnt = FROM_X ? n : (int64_t)*in_cnt;
+  const int64_t chunk = (cnt + (int64_t)gridDim.x * MS_STEP - 1) / ((int64_t)gridDim.x * MS_STEP) * MS_STEP;
+  const int64_t beg = (int64_t)blockIdx.x * chunk, end = std::min<int64_t>(cnt, beg + chunk);
+  const uint64_t dmask = (1ull << w) - 1;
+  const uint32_t lane = lane_id();
+  for (int64_t it = beg; it < end; it += MS_STEP) {
+    uint64_t raw[MS_U];  // all loads of the step first, then the work
+    uint32_t hidx[MS_U];
+#pragma unroll
+    for (int u = 0; u < MS_U; ++u) {
+      const int64_t i = it + u * TPB + threadIdx.x;
+      raw[u] = i < end ? (FROM_X ? __builtin_bit_cast(uint64_t, x[i]) : in[i]) : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < MS_U; ++u) {
+      const int64_t i = it + u * TPB + threadIdx.x;
+      bool mem = false;
+      uint64_t off = 0;
+      int a = 0;
+      if (i < end) {
+        if (FROM_X) {
+          const uint64_t k = dkey(__builtin_bit_cast(double, raw[u]));
+          if (k >= ka && k <= kb) {
+            off = k - base;
+            const uint32_t p = (uint32_t)(off >> (s + w));
+            mem = (bm[p >> 5] >> (p & 31)) & 1u;
+          }
+        } else {
+          off = raw[u];
+          mem = true;
+        }
+        if (mem) {
+          const uint64_t pref = off >> (s + w);
+          int b = ng;
+          while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (gs[mid] < pref) a = mid + 1; else b = mid;
+          }
+          mem = a < ng && gs[a] == pref;
+        }
+      }
+      // histogram slot; the global atomics are issued after the step's LDS
+      // work (interleaved, each one would stall on the next VGPR reuse)
+      hidx[u] = mem ? (uint32_t)a * MS_DIG + (uint32_t)((off >> s) & dmask) : ~0u;
+      if (out) {  // wave-aggregated append into the LDS stage
+        const uint64_t bal = __ballot(mem);
+        if (bal) {
+          const uint32_t leader = (uint32_t)__builtin_ctzll(bal);
+          uint32_t wb = 0;
+          if (lane == leader) wb = atomicAdd(&scnt, (uint32_t)__builtin_popcountll(bal));
+          wb = __shfl(wb, (int)leader, 64);
+          if (mem) stage[wb + rank_below(bal)] = off;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < MS_U; ++u)
+      if (hidx[u] != ~0u) atomicAdd(&H[hidx[u]], 1u);
+    if (out) {
+      __syncthreads();
+      const uint32_t c = scnt;
+      if (c > (uint32_t)(MS_STAGE - MS_STEP) || it + MS_STEP >= end) {  // block-uniform
+        if (threadIdx.x == 0 && c) sbase = atomicAdd(out_cnt, c);
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < c; j += TPB) out[sbase + j] = stage[j];
+        __syncthreads();
+        if (threadIdx.x == 0) scnt = 0;
+      }
+      __syncthreads();  // every thread has read scnt before it changes again
+    }
   }
 }
 
-// one block per active group: prefix sums of its histogram (the row is
-// zeroed for the next level), then every rank of the group picks its digit
+// one block per active group: prefix sums of its DIG-bin histogram (the row
+// is zeroed for the next level), then every rank of the group picks its
+// digit
+template <int DIG>
 __global__ void __launch_bounds__(TPB)
     msel_resolve(uint32_t *__restrict__ H, const int32_t *__restrict__ ng_ptr,
                  MsRank *__restrict__ R, int nq, int first, int64_t nbins, int w,
                  int64_t *__restrict__ m_out) {
+  constexpr int PT = DIG / TPB;
   const int g = blockIdx.x;
   const int ng = first ? 1 : *ng_ptr;
   if (g >= ng) return;
-  __shared__ uint32_t incl[MS_DIG];
+  __shared__ uint32_t incl[DIG];
   __shared__ uint32_t wsum[NWAVE];
-  uint32_t *row = H + (int64_t)g * MS_DIG;
-  uint32_t v[MS_DIG / TPB];
+  uint32_t *row = H + (int64_t)g * DIG;
+  uint32_t v[PT];
   uint32_t tot = 0;
 #pragma unroll
-  for (int k = 0; k < MS_DIG / TPB; ++k) {
-    v[k] = row[threadIdx.x * (MS_DIG / TPB) + k];
+  for (int k = 0; k < PT; ++k) {
+    v[k] = row[threadIdx.x * PT + k];
     tot += v[k];
   }
   uint32_t run = block_excl_scan(tot, wsum, nullptr);
 #pragma unroll
-  for (int k = 0; k < MS_DIG / TPB; ++k) {
+  for (int k = 0; k < PT; ++k) {
     run += v[k];
-    incl[threadIdx.x * (MS_DIG / TPB) + k] = run;
-    row[threadIdx.x * (MS_DIG / TPB) + k] = 0;
+    incl[threadIdx.x * PT + k] = run;
+    row[threadIdx.x * PT + k] = 0;
   }
   __syncthreads();
   if (first) {  // the window size m and the reference's ranks (bins.py:738-744)
-    const int64_t m = (int64_t)incl[MS_DIG - 1];
+    const int64_t m = (int64_t)incl[DIG - 1];
     if (threadIdx.x == 0) *m_out = m;
     for (int q = threadIdx.x; q < nq; q += TPB) {
       int64_t r = 0;
@@ -315,10 +431,11 @@ __global__ void __launch_bounds__(TPB)
     }
     __syncthreads();
   }
+  const int top = (1 << w) - 1;
   for (int q = threadIdx.x; q < nq; q += TPB) {
     if (R[q].group != g) continue;
     const int64_t rr = R[q].rr;
-    int a = 0, b = MS_DIG - 1;  // first digit whose inclusive count exceeds rr
+    int a = 0, b = top;  // first digit whose inclusive count exceeds rr
     while (a < b) {
       const int mid = (a + b) >> 1;
       if ((int64_t)incl[mid] <= rr) a = mid + 1; else b = mid;
@@ -328,51 +445,48 @@ __global__ void __launch_bounds__(TPB)
   }
 }
 
-// the active groups of the next level: sorted unique prefixes (one block)
+// the active groups of the next level.  The ranks are non-decreasing in q,
+// so are the values they select and so are the chosen prefixes: the sorted
+// unique prefixes are the run starts, numbered by a scan (one block)
 __global__ void __launch_bounds__(1024)
     msel_groups(MsRank *__restrict__ R, int nq, uint64_t *__restrict__ groups,
                 int32_t *__restrict__ ng_out) {
-  __shared__ uint64_t key[2048];
-  __shared__ int32_t cnt[2048];
-  for (int i = threadIdx.x; i < 2048; i += 1024) key[i] = i < nq ? R[i].prefix : ~0ull;
-  __syncthreads();
-  for (int size = 2; size <= 2048; size <<= 1)  // bitonic sort
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < 2048; i += 1024) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool up = (i & size) == 0;
-          const uint64_t a = key[i], b = key[j];
-          if ((a > b) == up) {
-            key[i] = b;
-            key[j] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  for (int i = threadIdx.x; i < 2048; i += 1024)
-    cnt[i] = (i < nq && (i == 0 || key[i] != key[i - 1])) ? 1 : 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {  // compact the unique prefixes (nq <= 1025: serial is fine)
-    int u = 0;
-    for (int i = 0; i < nq; ++i)
-      if (cnt[i]) key[u++] = key[i];
-    *ng_out = u;
-    cnt[0] = u;
+  __shared__ uint32_t wtot[16];
+  const int q0 = 2 * threadIdx.x;  // two ranks per thread covers nq <= 2048
+  uint32_t f[2];
+  uint64_t p[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = q0 + k;
+    p[k] = q < nq ? R[q].prefix : 0;
+    f[k] = (q < nq && (q == 0 || R[q - 1].prefix != p[k])) ? 1u : 0u;
   }
-  __syncthreads();
-  const int ng = cnt[0];
-  for (int i = threadIdx.x; i < ng; i += 1024) groups[i] = key[i];
-  for (int q = threadIdx.x; q < nq; q += 1024) {
-    const uint64_t p = R[q].prefix;
-    int a = 0, b = ng;
-    while (a < b) {
-      const int mid = (a + b) >> 1;
-      if (key[mid] < p) a = mid + 1; else b = mid;
-    }
-    R[q].group = a;
+  const uint32_t v = f[0] + f[1], lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  uint32_t xs = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(xs, o, 64);
+    if (lane >= (uint32_t)o) xs += y;
   }
+  if (lane == 63) wtot[wv] = xs;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    off += (k < wv) ? wtot[k] : 0u;
+    tot += wtot[k];
+  }
+  uint32_t c = off + xs - v;  // groups started before q0
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = q0 + k;
+    if (q >= nq) break;
+    if (f[k]) groups[c] = p[k];
+    c += f[k];
+    R[q].group = (int32_t)c - 1;
+  }
+  if (threadIdx.x == 0) *ng_out = (int32_t)tot;
 }
 
 __global__ void msel_edges(const MsRank *__restrict__ R, int nq, uint64_t base,
@@ -397,9 +511,12 @@ __device__ __forceinline__ uint32_t bin_of(double v, const double *e, int nb) {
   return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
 }
 
+// per-tile bin counts double as the CSR's radix histogram ([digit][tile],
+// one 8-bit pass) when nb < RADIX: tile_hist is then written, else null
 __global__ void __launch_bounds__(TPB)
     assign_bins(const double *__restrict__ x, int64_t n, const double *__restrict__ edges, int nb,
-                uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts) {
+                uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts,
+                uint32_t *__restrict__ tile_hist, uint32_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double *e = (double *)smem;
   const bool lds_edges = (nb + 1) <= LDS_EDGES;
@@ -410,18 +527,29 @@ __global__ void __launch_bounds__(TPB)
   __syncthreads();
   const double *ee = lds_edges ? e : edges;
   const int64_t base = (int64_t)blockIdx.x * TILE;
-#pragma unroll 4
+  double v[IPT];  // every load of the tile in flight first
+#pragma unroll
   for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + k * TPB + threadIdx.x;
-    if (i < n) {
-      uint32_t b = bin_of(x[i], ee, nb);
-      bins[i] = b;
-      atomicAdd(&cnt[b], 1u);
-    }
+    const int64_t i = base + k * TPB + threadIdx.x;
+    v[k] = i < n ? x[i] : 0.0;
+  }
+  uint32_t b[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int64_t i = base + k * TPB + threadIdx.x;
+    b[k] = bin_of(v[k], ee, nb);
+    if (i < n) atomicAdd(&cnt[b[k]], 1u);
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int64_t i = base + k * TPB + threadIdx.x;
+    if (i < n) bins[i] = b[k];
   }
   __syncthreads();
   for (int k = threadIdx.x; k < nb; k += TPB)
     if (cnt[k]) atomicAdd(&counts[k], (unsigned long long)cnt[k]);
+  if (tile_hist)  // TPB == RADIX > nb
+    tile_hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = threadIdx.x <= nb ? cnt[threadIdx.x] : 0u;
 }
 
 // ----------------------------------------------------------------- moments
@@ -440,16 +568,21 @@ __global__ void __launch_bounds__(TPB)
   double *tgt = in_lds ? acc : global_acc;
   // grid-stride over tiles: at most gridDim.x slabs to reduce afterwards
   for (int64_t base = (int64_t)blockIdx.x * TILE; base < n; base += (int64_t)gridDim.x * TILE) {
-#pragma unroll 4
+    uint32_t bv[IPT];  // the tile's loads first, then the LDS accumulation
+    double fv[IPT], wv[IPT];
+#pragma unroll
     for (int k = 0; k < IPT; ++k) {
-      int64_t i = base + k * TPB + threadIdx.x;
-      if (i >= n) continue;
-      uint32_t b = bins[i];
-      if (b >= (uint32_t)nb) continue;
-      double v = f[i];
-      double a = __builtin_fabs(v);
-      double ww = WMODE ? wt[i] : 1.0;
-      double *t = tgt + (int64_t)b * NMOM;
+      const int64_t i = base + k * TPB + threadIdx.x;
+      const bool ok = i < n;
+      bv[k] = ok ? bins[i] : (uint32_t)nb;
+      fv[k] = ok ? f[i] : 0.0;
+      wv[k] = (WMODE && ok) ? wt[i] : 1.0;
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      if (bv[k] >= (uint32_t)nb) continue;
+      const double v = fv[k], a = __builtin_fabs(v), ww = wv[k];
+      double *t = tgt + (int64_t)bv[k] * NMOM;
       if (WMODE) {
         atomicAdd(&t[0], ww);
         atomicAdd(&t[1], v * ww);
@@ -468,25 +601,30 @@ __global__ void __launch_bounds__(TPB)
   }
 }
 
-// Sum slab[tile][len] over tiles in a fixed order: each block owns 64
-// outputs, its 4 waves take every 4th tile, then wave partials are added in
-// wave order (deterministic).
-__global__ void __launch_bounds__(TPB) reduce_slab(const double *__restrict__ slab, int64_t ntiles,
-                                                   int64_t len, double *__restrict__ out) {
-  __shared__ double part[NWAVE][64];
-  const int w = threadIdx.x >> 6;
-  const int64_t col = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+// Sum slab[row][len] over rows in a fixed order (deterministic): first
+// SLAB_G partials, partial g = rows g, g+SLAB_G, ... in turn; then the
+// partials in g order.
+constexpr int SLAB_G = 64;
+
+__global__ void __launch_bounds__(TPB) reduce_slab_part(const double *__restrict__ slab,
+                                                        int64_t rows, int64_t len,
+                                                        double *__restrict__ part) {
+  const int64_t col = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  const int g = blockIdx.y;
+  if (col >= len) return;
   double s = 0.0;
-  if (col < len)
-    for (int64_t b = w; b < ntiles; b += NWAVE) s += slab[b * len + col];
-  part[w][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (w == 0 && col < len) {
-    double t = part[0][threadIdx.x];
-#pragma unroll
-    for (int k = 1; k < NWAVE; ++k) t += part[k][threadIdx.x];
-    out[col] = t;
-  }
+  for (int64_t r = g; r < rows; r += SLAB_G) s += slab[r * len + col];
+  part[(int64_t)g * len + col] = s;
+}
+
+__global__ void __launch_bounds__(TPB) reduce_slab_final(const double *__restrict__ part,
+                                                         int64_t len, double *__restrict__ out) {
+  const int64_t col = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (col >= len) return;
+  double s = 0.0;
+#pragma unroll 8
+  for (int g = 0; g < SLAB_G; ++g) s += part[(int64_t)g * len + col];
+  out[col] = s;
 }
 
 __global__ void gather_by_idx(const double *__restrict__ src, const int32_t *__restrict__ idx,
@@ -509,9 +647,10 @@ struct Profile {
   bool has_w = false;
   bool has_idx = false;
   bool csr_ready = false;
+  bool csrh_ready = false;  // csrh = the CSR pass histogram, from assign_bins
   bool mm_valid = false;   // mm = min / max key of x, cached on the host
   uint64_t mm[2] = {0, 0};
-  Buf msH, msR, msG, msNg, msM;
+  Buf msH, msR, msG, msNg, msM, msRows, msL0, msL1, msCnt, csrh, slabp;
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
 };
@@ -592,24 +731,45 @@ static void equaln_select(Profile &P, hipStream_t st, int64_t nbins, int has_min
   if (empty || lo > hi) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
   const uint64_t span = hi - lo;
   const int B = span ? 64 - __builtin_clzll(span) : 1;
-  const int L = (B + MS_BITS - 1) / MS_BITS;
-  uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * (size_t)nq * MS_DIG);
+  int wd[MS_MAXL], L = 1;
+  wd[0] = std::min(B, MS0_BITS);
+  for (int rem = B - wd[0]; rem > 0; rem -= MS_BITS) wd[L++] = std::min(rem, MS_BITS);
+  const int64_t n = P.n;
+  const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
+  const unsigned grid = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (n + TPB - 1) / TPB));
+  uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * std::max<size_t>((size_t)nq * MS_DIG, MS0_DIG));
+  uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
   MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
   uint64_t *G = (uint64_t *)P.msG.get(sizeof(uint64_t) * (size_t)nq);
   int32_t *ng = (int32_t *)P.msNg.get(16);
   int64_t *m_dev = (int64_t *)P.msM.get(16);
+  uint32_t *cnt = (uint32_t *)P.msCnt.get(sizeof(uint32_t) * MS_MAXL);
+  uint64_t *list[2] = {nullptr, nullptr};
+  if (L > 1) list[0] = (uint64_t *)P.msL0.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
+  if (L > 2) list[1] = (uint64_t *)P.msL1.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
   double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
-  PBX_HIP(hipMemsetAsync(H, 0, sizeof(uint32_t) * (size_t)nq * MS_DIG, st));
-  const int64_t n = P.n;
-  const unsigned grid = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (n + TPB - 1) / TPB));
-  for (int l = 0; l < L; ++l) {
-    const int w = (l == 0) ? B - MS_BITS * (L - 1) : MS_BITS;
-    const int sh = MS_BITS * (L - 1 - l);
-    hipLaunchKernelGGL(msel_hist, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n, ka, kb,
-                       lo, sh, w, l == 0 ? 1 : 0, G, ng, H);
-    hipLaunchKernelGGL(msel_resolve, dim3(l == 0 ? 1 : nq), dim3(TPB), 0, st, H, ng, R, nq,
-                       l == 0 ? 1 : 0, nbins, w, m_dev);
-    if (l + 1 < L) hipLaunchKernelGGL(msel_groups, dim3(1), dim3(1024), 0, st, R, nq, G, ng);
+  PBX_HIP(hipMemsetAsync(H, 0, sizeof(uint32_t) * std::max<size_t>((size_t)nq * MS_DIG, MS0_DIG), st));
+  PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * MS_MAXL, st));
+  int s = B - wd[0];
+  hipLaunchKernelGGL(msel_hist0, dim3(g0), dim3(MS0_TPB), 0, st, (const double *)P.x.p, n, ka, kb,
+                     lo, s, rows);
+  hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st, rows, g0, H);
+  hipLaunchKernelGGL(msel_resolve<MS0_DIG>, dim3(1), dim3(TPB), 0, st, H, ng, R, nq, 1, nbins,
+                     wd[0], m_dev);
+  for (int l = 1; l < L; ++l) {
+    hipLaunchKernelGGL(msel_groups, dim3(1), dim3(1024), 0, st, R, nq, G, ng);
+    s -= wd[l];
+    uint64_t *out = (l + 1 < L) ? list[(l - 1) & 1] : nullptr;
+    if (l == 1)
+      hipLaunchKernelGGL(msel_filter<true>, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n,
+                         ka, kb, lo, (const uint64_t *)nullptr, (const uint32_t *)nullptr, s, wd[l],
+                         G, ng, H, out, cnt + l);
+    else
+      hipLaunchKernelGGL(msel_filter<false>, dim3(grid), dim3(TPB), 0, st, (const double *)nullptr,
+                         n, ka, kb, lo, (const uint64_t *)list[l & 1], cnt + l - 1, s, wd[l], G, ng,
+                         H, out, cnt + l);
+    hipLaunchKernelGGL(msel_resolve<MS_DIG>, dim3(nq), dim3(TPB), 0, st, H, ng, R, nq, 0, nbins,
+                       wd[l], m_dev);
   }
   hipLaunchKernelGGL(msel_edges, dim3(ceil_div(nq, TPB)), dim3(TPB), 0, st, R, nq, lo, de);
   PBX_HIP(hipGetLastError());
@@ -654,7 +814,7 @@ int pbx_profile_destroy(void *handle) {
     Buf *all[] = {&p->x, &p->w, &p->idx, &p->bins, &p->perm, &p->keys0, &p->keys1, &p->vtmp,
                   &p->hist, &p->tsum, &p->edges, &p->counts, &p->minmax, &p->slab, &p->acc,
                   &p->field, &p->weight, &p->ranks, &p->bounds, &p->msH, &p->msR, &p->msG,
-                  &p->msNg, &p->msM};
+                  &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp};
     for (Buf *b : all) b->release();
     delete p;
   });
@@ -672,6 +832,7 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
     P.has_w = false;
     P.has_idx = false;
     P.csr_ready = false;
+    P.csrh_ready = false;
     P.mm_valid = false;
     P.nb = -1;
   });
@@ -749,6 +910,7 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
     P.has_w = true;
     P.has_idx = true;
     P.csr_ready = false;
+    P.csrh_ready = false;
     P.nb = -1;
     *n_kept = kept;
   });
@@ -890,8 +1052,12 @@ int pbx_profile_assign(void *handle, const double *h_edges, int64_t n_edges, int
       size_t lds = ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
                    sizeof(uint32_t) * (nb + 1);
       if (lds > 150 * 1024) fail(PBX_ERR_VALUE, "too many bins for the device histogram (%lld)", (long long)nb);
-      hipLaunchKernelGGL(assign_bins, dim3(ntiles_of(n)), dim3(TPB), lds, st,
-                         (const double *)P.x.p, n, (const double *)de, (int)nb, bins, cnt);
+      const uint32_t nt = ntiles_of(n);
+      uint32_t *th = (nb < RADIX) ? (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX)
+                                  : nullptr;
+      hipLaunchKernelGGL(assign_bins, dim3(nt), dim3(TPB), lds, st, (const double *)P.x.p, n,
+                         (const double *)de, (int)nb, bins, cnt, th, nt);
+      P.csrh_ready = th != nullptr;
       PBX_HIP(hipGetLastError());
     }
     PBX_HIP(hipMemcpyAsync(h_counts, cnt, sizeof(int64_t) * nb, hipMemcpyDeviceToHost, st));
@@ -928,11 +1094,17 @@ int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets) {
       const uint32_t *kin = (const uint32_t *)P.bins.p;
       bool first = true;
       for (int shift = 0; shift < bits; shift += 8) {
-        if (first) {
-          radix_pass<uint32_t>(P, st, kin, nullptr, VAL_IOTA, n, shift, ka, va);
+        const bool last = shift + 8 >= bits;  // the sorted bin ids themselves are not needed
+        if (first && P.csrh_ready) {  // bins < 256: assign_bins counted the only pass
+          prim::radix_pass<uint32_t>(P.csrh, P.tsum, st, kin, nullptr, VAL_IOTA, n, shift,
+                                     last ? nullptr : ka, va, true);
+          P.csrh_ready = false;  // scanned in place: now offsets
+          first = false;
+        } else if (first) {
+          radix_pass<uint32_t>(P, st, kin, nullptr, VAL_IOTA, n, shift, last ? nullptr : ka, va);
           first = false;
         } else {
-          radix_pass<uint32_t>(P, st, ka, va, VAL_ARRAY, n, shift, kb, vb);
+          radix_pass<uint32_t>(P, st, ka, va, VAL_ARRAY, n, shift, last ? nullptr : kb, vb);
           std::swap(ka, kb);
           std::swap(va, vb);
         }
@@ -1002,8 +1174,8 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, c
     double *acc = (double *)P.acc.get(sizeof(double) * (size_t)len);
     PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * len, st));
     if (n && nb > 0) {
-      // <= 512 resident blocks (2 per CU) stride over the tiles
-      uint32_t nt = std::min<uint32_t>(ntiles_of(n), 512u);
+      // <= 1024 blocks (4 per CU) stride over the tiles
+      uint32_t nt = std::min<uint32_t>(ntiles_of(n), 1024u);
       const bool in_lds = nb <= LDS_MOM_BINS;
       double *slab = in_lds ? (double *)P.slab.get(sizeof(double) * (size_t)nt * len) : nullptr;
       size_t lds = in_lds ? sizeof(double) * (size_t)len : 0;
@@ -1015,8 +1187,11 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, c
                            (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab, acc);
       PBX_HIP(hipGetLastError());
       if (in_lds) {
-        hipLaunchKernelGGL(reduce_slab, dim3(ceil_div(len, 64)), dim3(TPB), 0, st, slab,
-                           (int64_t)nt, len, acc);
+        double *part = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * len);
+        hipLaunchKernelGGL(reduce_slab_part, dim3(ceil_div(len, TPB), SLAB_G), dim3(TPB), 0, st,
+                           slab, (int64_t)nt, len, part);
+        hipLaunchKernelGGL(reduce_slab_final, dim3(ceil_div(len, TPB)), dim3(TPB), 0, st, part,
+                           len, acc);
         PBX_HIP(hipGetLastError());
       }
     }

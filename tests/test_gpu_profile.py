@@ -262,3 +262,35 @@ def test_large_n_properties(gpu):
     s = np.sort(x)
     ref = [s[0]] + [s[int(i * n / 256)] for i in range(1, 256)] + [s[-1]]
     assert np.array_equal(edges, np.array(ref))
+
+
+@pytest.mark.parametrize("case", ["mixed_sign", "few_distinct", "one_hot_digit", "tiny_span",
+                                  "max_bins", "sort_path", "clipped_wide"])
+def test_equaln_radix_select_adversarial(gpu, case):
+    """The radix select (level-0 14-bit LDS histogram, compacted deeper levels)
+    against the oracle's sort-based equaln (bins.py:734-744) on inputs that
+    stress it: keys spanning all 64 bits, heavy duplicates (everything lands in
+    one compact list), one crowded level-0 digit, spans under one digit, the
+    largest nbins on the select path and the first one past it."""
+    rng = np.random.default_rng(11)
+    n, nb, lo, hi = 1_500_000, 128, None, None
+    if case == "mixed_sign":
+        x = rng.normal(size=n) * 10.0 ** rng.integers(-200, 200, n)
+    elif case == "few_distinct":
+        x = rng.choice(np.array([-1.0, 0.0, 2.5, 2.5000000000000004, 7.0]), n)
+    elif case == "one_hot_digit":
+        x = 1.0 + rng.uniform(0, 1e-9, n)
+        x[:1000] = rng.uniform(1e-6, 1e6, 1000)
+    elif case == "tiny_span":
+        x = np.nextafter(1.0, 2.0, dtype=np.float64) * np.ones(n)
+        x[::3] = 1.0
+    elif case == "max_bins":
+        x, nb = rng.exponential(size=n), 1024
+    elif case == "sort_path":
+        x, nb = rng.exponential(size=n), 1025
+    else:
+        x, lo, hi = rng.lognormal(0, 3, n), 1e-3, 50.0
+    d = DeviceBins.from_x(x)
+    got = d.edges_equaln(nb, lo, hi)
+    want = pr.edges_equaln(x, nb, lo, hi)
+    assert np.array_equal(got, want, equal_nan=True), case
