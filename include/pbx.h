@@ -54,6 +54,15 @@ int pbx_version(void);                   /* returns e.g. 100 for 0.1.0 */
 int pbx_device_count(int *count);
 int pbx_set_device(int device);          /* per calling thread */
 int pbx_get_device(int *device);
+/* Direct-sum precision (process-wide).  precise=1: every 1/sqrt is
+ * v_rsq_f64 + one Newton step (~1e-16 relative, the reference's IEEE
+ * 1.0/sqrt to rounding).  precise=0 (default; env PBX_PRECISE=1 flips it):
+ * the all-particles Newtonian symmetric kernel (n >= 8192) uses v_rsq_f64
+ * unrefined, ~5e-8 relative per pair, results within ~1e-7 of the reference
+ * (contract 1e-5; direct.rs:165-180 / :296-308 replaced).  No equivalent in
+ * the PyO3 module (gravity.rs:448-709). */
+int pbx_set_precise(int on);
+int pbx_get_precise(int *on);
 int pbx_device_synchronize(void);
 int pbx_device_name(char *buf, int buflen);
 

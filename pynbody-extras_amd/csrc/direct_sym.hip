@@ -7,7 +7,10 @@
 // arithmetic is the scaled form of direct.hip (w = 2/r refined from
 // v_rsq_f64; potential and force accumulate m w and m w^3 d; the epilogue
 // multiplies by -1/2 and 1/8) and is shared by both particles of a pair:
-// 22 FP64 instructions + 1 rsq per unordered pair instead of 2 x (16 + 1).
+// 21 FP64 instructions + 1 rsq per unordered pair instead of 2 x (16 + 1).
+// Fast mode (the default, pbx_set_precise(0)) skips the Newton step: w is
+// v_rsq_f64 itself (1/r to ~5e-8 relative, measured), 18 FP64 instructions
+// per pair, results within ~1e-7 of the reference (contract: 1e-5).
 //
 // Decomposition: particles padded to a multiple of 1024 (pads: zero mass,
 // far away, distinct).  I-block = 256 targets of one wave (4 per lane),
@@ -24,6 +27,7 @@
 // is added once per work unit.  Atomic bytes ~ 16 N^2 / 1024 (3 % of the
 // runtime at 1M).  Float atomics make the last bits depend on arrival order.
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "pbx_common.h"
@@ -55,7 +59,7 @@ __device__ __forceinline__ double rot(double v, int addr) {
 
 // One J-chunk for one wave.  SYMM: both sides; else the diagonal chunk
 // (target side only, self pair masked at rotation 0).
-template <int WANT, bool SYMM>
+template <int WANT, bool SYMM, bool RAW>
 __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t jbase, int lane,
                                       const double (&tx)[kT], const double (&ty)[kT],
                                       const double (&tz)[kT], const double (&tm)[kT],
@@ -88,8 +92,10 @@ __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t j
         const double s2 =
             __builtin_fma(dx, dx, __builtin_fma(dy, dy, __builtin_fma(dz, dz, kR2Tiny)));
         const double y0 = __builtin_amdgcn_rsq(s2);
-        const double w = y0 * __builtin_fma(-s2, y0 * y0, 3.0);  // 2/r
-        const double q = w * (w * w);                              // 8/r^3
+        // precise: one Newton step, w = 2/r (~1e-16); fast: w = v_rsq_f64 =
+        // 1/r to ~5e-8 relative (3 FP64 instructions fewer per pair)
+        const double w = RAW ? y0 : y0 * __builtin_fma(-s2, y0 * y0, 3.0);
+        const double q = w * (w * w);  // w^3
         if (WANT & PBX_WANT_POT) tp[kt] = __builtin_fma(ms, w, tp[kt]);
         if (WANT & PBX_WANT_ACC) {
           const double g = ms * q;
@@ -125,7 +131,7 @@ __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t j
   }
 }
 
-template <int WANT>
+template <int WANT, bool RAW>
 __global__ void __launch_bounds__(kWaves * 64)
     sym_kernel(const double4 *__restrict__ rec, const Unit *__restrict__ units,
                double *__restrict__ acc4) {
@@ -148,10 +154,10 @@ __global__ void __launch_bounds__(kWaves * 64)
 #pragma unroll
     for (int k = 0; k < kS; ++k) sp[k] = sa[k] = sb[k] = sc[k] = 0.0;
     if (j > iblk)
-      chunk<WANT, true>(rec, (int64_t)j * kBlk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa, sb,
+      chunk<WANT, true, RAW>(rec, (int64_t)j * kBlk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa, sb,
                         sc);
     else if (j == iblk)
-      chunk<WANT, false>(rec, (int64_t)j * kBlk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa,
+      chunk<WANT, false, RAW>(rec, (int64_t)j * kBlk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa,
                          sb, sc);
 #pragma unroll
     for (int k = 0; k < kS; ++k) {
@@ -196,15 +202,16 @@ __global__ void pad_records(double4 *__restrict__ rec, int64_t n, int64_t npad) 
 
 // undo the scaled accumulation: particles [lo, hi) -> outputs
 __global__ void finish_kernel(const double *__restrict__ acc4, int64_t lo, int64_t hi, int want,
-                              double *__restrict__ pot, double *__restrict__ acc) {
+                              int raw, double *__restrict__ pot, double *__restrict__ acc) {
   int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (lo + t >= hi) return;
   const double *a = acc4 + (lo + t) * 4;
-  if (want & PBX_WANT_POT) pot[t] = -0.5 * a[0];
+  const double kp = raw ? -1.0 : -0.5, ka = raw ? 1.0 : 0.125;  // undo the w scale
+  if (want & PBX_WANT_POT) pot[t] = kp * a[0];
   if (want & PBX_WANT_ACC) {
-    acc[3 * t + 0] = 0.125 * a[1];
-    acc[3 * t + 1] = 0.125 * a[2];
-    acc[3 * t + 2] = 0.125 * a[3];
+    acc[3 * t + 0] = ka * a[1];
+    acc[3 * t + 1] = ka * a[2];
+    acc[3 * t + 2] = ka * a[3];
   }
 }
 
@@ -254,13 +261,20 @@ void sym_accumulate(Device &d, double4 *rec, int64_t n, int64_t u0, int64_t u1, 
   PBX_HIP(hipMemcpyAsync(du, mine.data(), sizeof(sym::Unit) * mine.size(), hipMemcpyHostToDevice,
                          st));
   const dim3 grid((unsigned)mine.size()), block(sym::kWaves * 64);
-  if (want == PBX_WANT_POT)
-    hipLaunchKernelGGL(sym::sym_kernel<PBX_WANT_POT>, grid, block, 0, st, rec, du, acc4);
-  else if (want == PBX_WANT_ACC)
-    hipLaunchKernelGGL(sym::sym_kernel<PBX_WANT_ACC>, grid, block, 0, st, rec, du, acc4);
+  auto launch = [&](auto raw) {
+    constexpr bool R = decltype(raw)::value;
+    if (want == PBX_WANT_POT)
+      hipLaunchKernelGGL((sym::sym_kernel<PBX_WANT_POT, R>), grid, block, 0, st, rec, du, acc4);
+    else if (want == PBX_WANT_ACC)
+      hipLaunchKernelGGL((sym::sym_kernel<PBX_WANT_ACC, R>), grid, block, 0, st, rec, du, acc4);
+    else
+      hipLaunchKernelGGL((sym::sym_kernel<PBX_WANT_POT | PBX_WANT_ACC, R>), grid, block, 0, st,
+                         rec, du, acc4);
+  };
+  if (precise_mode())
+    launch(std::false_type{});
   else
-    hipLaunchKernelGGL(sym::sym_kernel<PBX_WANT_POT | PBX_WANT_ACC>, grid, block, 0, st, rec, du,
-                       acc4);
+    launch(std::true_type{});
   PBX_HIP(hipGetLastError());
   // the unit table must outlive the launch before the host buffer goes away
   PBX_HIP(hipStreamSynchronize(st));
@@ -270,7 +284,7 @@ void sym_finish(Device &d, const double *acc4, int64_t lo, int64_t hi, int want,
                 double *acc) {
   if (hi <= lo) return;
   hipLaunchKernelGGL(sym::finish_kernel, dim3(ceil_div(hi - lo, 256)), dim3(256), 0, d.stream,
-                     acc4, lo, hi, want, pot, acc);
+                     acc4, lo, hi, want, precise_mode() ? 0 : 1, pot, acc);
   PBX_HIP(hipGetLastError());
 }
 

@@ -123,8 +123,34 @@ struct ScopedTimer {
   }
 };
 
+// Direct-sum precision mode (pbx_set_precise): true -> Newton-refined
+// 1/sqrt everywhere (~1e-16); false (default, or PBX_PRECISE=0) -> the
+// all-particles symmetric kernel uses v_rsq_f64 unrefined (~5e-8).
+bool precise_mode();
+void set_precise_mode(bool on);
+
 inline unsigned int ceil_div(int64_t a, int64_t b) {
   return (unsigned int)((a + b - 1) / b);
+}
+
+// XCD-aware block order (a speed hint only: correctness never depends on
+// placement).  The dispatcher is observed to deal workgroups round-robin
+// over the 8 XCDs, each with its own L2; this bijection hands every XCD one
+// contiguous run of logical blocks, so neighbouring blocks (spatially
+// adjacent targets) share an L2 instead of being spread over all eight.
+constexpr unsigned kNumXcd = 8;
+__device__ __forceinline__ unsigned xcd_swizzle(unsigned b, unsigned nblocks) {
+  const unsigned q = nblocks / kNumXcd, r = nblocks % kNumXcd;
+  const unsigned x = b % kNumXcd, k = b / kNumXcd;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+// The same with the grid cut into rounds of kNumXcd chunks of `chunk`
+// logical blocks: every XCD works through contiguous chunks, and the XCDs
+// still advance over the grid together (uneven per-block cost stays
+// balanced).  nblocks must be a multiple of kNumXcd * chunk.
+__device__ __forceinline__ unsigned xcd_chunk_swizzle(unsigned b, unsigned chunk) {
+  const unsigned x = b % kNumXcd, k = b / kNumXcd;
+  return ((k / chunk) * kNumXcd + x) * chunk + k % chunk;
 }
 
 }  // namespace pbx

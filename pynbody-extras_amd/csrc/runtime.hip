@@ -1,5 +1,6 @@
 // runtime.hip — device selection, HBM allocation, the library stream and
 // HIP events, thread-local error text.  No kernels live here.
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <strings.h>
@@ -109,6 +110,22 @@ bool timing_enabled() {
   return cached == 1;
 }
 
+static std::atomic<int> g_precise{-1};
+
+bool precise_mode() {
+  int v = g_precise.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = std::getenv("PBX_PRECISE");
+    v = (e && e[0] && std::strcmp(e, "0") != 0) ? 1 : 0;
+    int expect = -1;
+    g_precise.compare_exchange_strong(expect, v);
+    v = g_precise.load(std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+
+void set_precise_mode(bool on) { g_precise.store(on ? 1 : 0, std::memory_order_relaxed); }
+
 void set_thread_device(int d) { g_thread_device = d; }
 int thread_device() { return g_thread_device < 0 ? 0 : g_thread_device; }
 
@@ -138,6 +155,14 @@ int pbx_set_device(int device) {
 
 int pbx_get_device(int *device) {
   return guard([&] { *device = thread_device(); });
+}
+
+int pbx_set_precise(int on) {
+  return guard([&] { set_precise_mode(on != 0); });
+}
+
+int pbx_get_precise(int *on) {
+  return guard([&] { *on = precise_mode() ? 1 : 0; });
 }
 
 int pbx_device_synchronize(void) {

@@ -770,6 +770,7 @@ struct WalkParams {
   unsigned long long *counters;  // [accepted nodes, leaf pairs, fault, wave steps, active lanes]
   int64_t max_steps;             // > number of nodes
   unsigned int *fault;           // set when a wave exceeds max_steps
+  unsigned xcd_chunk;            // blocks per XCD chunk (0: launch order)
 };
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -845,7 +846,8 @@ template <int P, int WANT, bool SOFT>
 __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
   constexpr int RS = rec_stride<P>();
   constexpr int NCH = (P == 2 || P == 3) ? RS / 8 : 1;  // chunks loaded eagerly
-  const int64_t t = (int64_t)blockIdx.x * WALK_TPB + threadIdx.x;
+  const unsigned lb = wp.xcd_chunk ? xcd_chunk_swizzle(blockIdx.x, wp.xcd_chunk) : blockIdx.x;
+  const int64_t t = (int64_t)lb * WALK_TPB + threadIdx.x;
   const bool valid = t < wp.m;
   const bool self_mode = wp.tgt == nullptr;
   double tx = 0.0, ty = 0.0, tz = 0.0, th = 0.0;
@@ -1380,9 +1382,23 @@ static void build_payload(Octree &T, hipStream_t st) {
   T.has_bh = true;
 }
 
+// blocks per XCD chunk of the walk grid (PBX_WALK_XCD_CHUNK, 0 = launch order)
+static unsigned walk_xcd_chunk() {
+  static const unsigned c = [] {
+    const char *v = std::getenv("PBX_WALK_XCD_CHUNK");
+    return v ? (unsigned)std::strtoul(v, nullptr, 10) : 64u;
+  }();
+  return c;
+}
+
 template <int P, int WANT>
-static void launch_walk_pw(const WalkParams &wp, bool soft, hipStream_t st) {
-  const unsigned grid = (unsigned)((wp.m + WALK_TPB - 1) / WALK_TPB);
+static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
+  unsigned grid = (unsigned)((wp.m + WALK_TPB - 1) / WALK_TPB);
+  wp.xcd_chunk = walk_xcd_chunk();
+  if (wp.xcd_chunk) {  // whole rounds of kNumXcd chunks; the extra blocks find no targets
+    const unsigned round = kNumXcd * wp.xcd_chunk;
+    grid = (grid + round - 1) / round * round;
+  }
   if (soft)
     hipLaunchKernelGGL((walk_kernel<P, WANT, true>), dim3(grid), dim3(WALK_TPB), 0, st, wp);
   else

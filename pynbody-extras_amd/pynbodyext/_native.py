@@ -55,6 +55,8 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_device_count": (c_int, [POINTER(c_int)]),
     "pbx_set_device": (c_int, [c_int]),
     "pbx_get_device": (c_int, [POINTER(c_int)]),
+    "pbx_set_precise": (c_int, [c_int]),
+    "pbx_get_precise": (c_int, [POINTER(c_int)]),
     "pbx_device_synchronize": (c_int, []),
     "pbx_device_name": (c_int, [c_char_p, c_int]),
     "pbx_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
@@ -188,6 +190,36 @@ def device_name() -> str:
     buf = ctypes.create_string_buffer(256)
     call("pbx_device_name", buf, 256)
     return buf.value.decode()
+
+
+def set_precise(on: bool) -> None:
+    """Direct-sum precision (include/pbx.h pbx_set_precise): True refines
+    every 1/sqrt with a Newton step (~1e-16); False (default) lets the
+    all-particles symmetric kernel use v_rsq_f64 as is (~1e-7 of the
+    reference, inside the 1e-5 contract)."""
+    call("pbx_set_precise", 1 if on else 0)
+
+
+def get_precise() -> bool:
+    v = ctypes.c_int()
+    call("pbx_get_precise", ctypes.byref(v))
+    return bool(v.value)
+
+
+class precise_mode:
+    """``with precise_mode(True): ...`` — set the precision, restore after."""
+
+    def __init__(self, on: bool = True):
+        self.on = on
+
+    def __enter__(self):
+        self.prev = get_precise()
+        set_precise(self.on)
+        return self
+
+    def __exit__(self, *exc):
+        set_precise(self.prev)
+        return False
 
 
 def synchronize() -> None:

@@ -106,9 +106,10 @@ def test_symmetric_units_split_across_ranks(gpu):
         nat.call("pbx_direct_sym_finish", d_acc4.ptr, lo, hi, 3, d_pot.ptr, d_acc.ptr)
         pot = d_pot.download(np.empty(hi - lo))
         acc = d_acc.download(np.empty((hi - lo, 3)))
-        assert np.max(np.abs(pot - pr[lo:hi]) / np.abs(pr[lo:hi])) < 1e-10
+        lim = 1e-10 if nat.get_precise() else 1e-6  # fast mode: raw v_rsq_f64
+        assert np.max(np.abs(pot - pr[lo:hi]) / np.abs(pr[lo:hi])) < lim
         assert np.max(np.linalg.norm(acc - ar[lo:hi], axis=1) /
-                      np.linalg.norm(ar[lo:hi], axis=1)) < 1e-10
+                      np.linalg.norm(ar[lo:hi], axis=1)) < lim
 
 
 def test_sharded_direct_symmetric_world1(gpu):
@@ -123,4 +124,4 @@ def test_sharded_direct_symmetric_world1(gpu):
     finally:
         comm.destroy()
     pr = og.direct_potentials(pos, mass)
-    assert np.max(np.abs(pot - pr) / np.abs(pr)) < 1e-10
+    assert np.max(np.abs(pot - pr) / np.abs(pr)) < (1e-10 if nat.get_precise() else 1e-6)
