@@ -135,32 +135,42 @@ PROFILE_BYTES_PER_PARTICLE = 49  # equaln profile, algorithmic H
 HBM_PEAK_GBS = 8000.0
 
 
-def bench_profile(sizes, steps: int, warmup: int, cpu: bool):
+def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
     """Config 3: RadialProfileBuilder(ndim=3, weight='mass', equaln, 128 bins)
     behind Sphere(R=10) & FamilyFilter('dm'), positions / masses resident in
     HBM.  One step = fused select (mask + r + compaction) -> equaln edges ->
     bin assignment + counts -> CSR (binind) built in HBM -> per-bin Σ mass and
-    mass-weighted <r>.  particles/s counts every INPUT particle."""
+    mass-weighted <r>.  particles/s counts every INPUT particle.
+
+    With several ranks (weak scaling): every rank holds n particles of its own
+    (seed + rank), the edges are the global equaln (distributed radix select,
+    RCCL all-reduce of the digit histograms), counts and sums are
+    all-reduced; particles/s = world * n / (max-over-ranks step time)."""
+    from pynbodyext.parallel import ShardedProfile
     from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X, DeviceBins
     from pynbodyext.synthetic import family_slices
 
+    comm = dist.comm if dist is not None else None
+    world = dist.world if dist is not None else 1
+    rank = dist.rank if dist is not None else 0
     out = []
     for n in sizes:
-        pos, mass = plummer(n, seed=SEEDS.get(n, 1002))
+        pos, mass = plummer(n, seed=SEEDS.get(n, 1002) + 7919 * rank)
         dm = family_slices(n)["dm"]
         d_pos = nat.DeviceArray.from_host(pos)
         d_mass = nat.DeviceArray.from_host(mass)
         dev = DeviceBins()
+        sp = ShardedProfile(comm, dev, offset=rank * n)
         e0, e1 = nat.Event(), nat.Event()
 
         def step():
             DeviceBins.select(d_pos.ptr, d_mass.ptr, sphere=((0.0, 0.0, 0.0), 10.0),
                               families=[(dm.start, dm.stop)], ndim=3, on_device=True, n=n, into=dev)
-            edges = dev.edges_equaln(128)
-            dev.assign(edges)
+            edges = sp.edges_equaln(128)
+            sp.assign(edges)
             dev.build_csr_on_device()
-            msum = dev.moments(SRC_W, SRC_NONE)[:, 3]
-            rmean = dev.moments(SRC_X, SRC_W)
+            msum = sp.moments(SRC_W, SRC_NONE)[:, 3]
+            rmean = sp.moments(SRC_X, SRC_W)
             return edges, msum, rmean
 
         for _ in range(warmup):
@@ -168,20 +178,28 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool):
         nat.synchronize()
         times, dev_ms = [], []
         for _ in range(steps):
+            if dist is not None:
+                dist.barrier()
             t0 = time.perf_counter()
             e0.record()
             res = step()
             e1.record()
             nat.synchronize()
-            times.append(time.perf_counter() - t0)
+            dt = time.perf_counter() - t0
+            times.append(dist.max(dt) if dist is not None else dt)
             dev_ms.append(e0.elapsed_ms(e1))
         t = float(np.median(times))
         td = float(np.median(dev_ms)) * 1e-3
-        row = {"n": n, "n_kept": dev.n, "ms": t * 1e3, "particles_per_s": n / t,
-               "hbm_gbs_algorithmic": n * PROFILE_BYTES_PER_PARTICLE / td / 1e9,
+        if dist is not None:
+            td = dist.max(td)
+        n_all = n * world
+        row = {"n": n_all, "n_per_gpu": n, "n_kept_rank0": dev.n, "ms": t * 1e3,
+               "particles_per_s": n_all / t,
+               "hbm_gbs_algorithmic": n_all * PROFILE_BYTES_PER_PARTICLE / td / 1e9,
+               "hbm_gbs_algorithmic_per_gpu": n * PROFILE_BYTES_PER_PARTICLE / td / 1e9,
                "stream_ms": td * 1e3}
         out.append(row)
-        if cpu and n == sizes[0]:
+        if cpu and n == sizes[0] and world == 1:
             from oracle import profile_ref as pr
 
             mask = pr.sphere_mask(pos, 10.0)
@@ -470,25 +488,30 @@ def main():
         },
         "cpu_baseline": cpu,
     }
-    if not args.no_profile and world == 1:
+    if not args.no_profile:
         sizes = [int(s) for s in args.profile_sizes.split(",") if s]
         sweep = bench_profile(sizes, steps=max(3, args.steps), warmup=1,
-                              cpu=not args.no_cpu_baseline)
+                              cpu=not args.no_cpu_baseline and rank == 0,
+                              dist=dist if dist.comm is not None else None)
         head = sweep[0]
-        big = max(sweep, key=lambda r: r["hbm_gbs_algorithmic"])
+        big = max(sweep, key=lambda r: r["hbm_gbs_algorithmic_per_gpu"])
         out["profile"] = {
             "metric": "particles/sec (RadialProfileBuilder equaln 128, Sphere&FamilyFilter, "
                       "weight=mass)",
             "value": head["particles_per_s"],
             "unit": "particles/s",
-            "config": {"workload": f"{head['n']}-particle Plummer sphere, Sphere(R=10) & "
-                                   "FamilyFilter('dm'), equaln 128 bins, mass sum + mean r",
-                       "kept": head["n_kept"]},
-            "roofline": {"bound": "hbm", "achieved": big["hbm_gbs_algorithmic"],
+            "config": {"workload": f"{head['n_per_gpu']}-particle Plummer sphere per GPU "
+                                   f"(x{world}), Sphere(R=10) & FamilyFilter('dm'), equaln 128 "
+                                   "bins, mass sum + mean r"
+                                   + (", global edges by distributed radix select"
+                                      if world > 1 else ""),
+                       "kept_rank0": head["n_kept_rank0"]},
+            "scaling": "weak",
+            "roofline": {"bound": "hbm", "achieved": big["hbm_gbs_algorithmic_per_gpu"],
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": big["hbm_gbs_algorithmic"] / HBM_PEAK_GBS,
-                         "at_n": big["n"], "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE,
-                         "traffic": None},
+                         "frac": big["hbm_gbs_algorithmic_per_gpu"] / HBM_PEAK_GBS,
+                         "at_n_per_gpu": big["n_per_gpu"],
+                         "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE, "traffic": None},
             "sweep": sweep,
             "cpu_baseline": head.get("cpu_baseline"),
         }

@@ -203,10 +203,11 @@ int pbx_octree_compute_range(pbx_octree *tree, double theta, int want, int64_t f
  * particles [first, first + count), into device buffers (any may be NULL) */
 int pbx_octree_leaf_particles(pbx_octree *tree, int64_t first, int64_t count, double *d_pos,
                               double *d_mass, int64_t *d_idx);
-/* out[10] = {n, nodes, levels, has_mass_payload, has_hmax,
+/* out[13] = {n, nodes, levels, has_mass_payload, has_hmax,
  *            accepted node interactions and leaf pairs of the last walk,
  *            path words, wave steps and active-lane steps of the last walk
- *            (SIMD efficiency = active / (64 * steps))} */
+ *            (SIMD efficiency = active / (64 * steps)), leaf wave steps,
+ *            their active lanes, wave steps that descended} */
 int pbx_octree_info(pbx_octree *tree, int64_t *out);
 /* Node arrays for parity tests (any pointer may be NULL), node ids in the
  * device's breadth-first numbering:
@@ -250,6 +251,22 @@ int pbx_profile_minmax(void *handle, double *mn, double *mx);
 int pbx_profile_edges_equaln(void *handle, int64_t nbins, int has_min, double bin_min,
                              int has_max, double bin_max, double *h_edges,
                              int64_t *n_edges);
+/* Distributed equaln (no reference counterpart — the
+ * reference is single-process): the radix select of
+ * pbx_profile_edges_equaln in stages.  Every rank: key_range (local
+ * order-preserving u64 keys of x; (~0, 0) when empty) -> min/max over ranks
+ * -> msel_begin(global range, same bounds on every rank; returns the level
+ * count L) -> for level 0..L-1: msel_hist (this rank's digit histogram,
+ * *count u32 at *d_hist on the device) -> sum *d_hist over ranks in place
+ * (pbx_comm_allreduce, dtype u32) -> msel_resolve -> msel_edges (identical
+ * on every rank; same results and errors as pbx_profile_edges_equaln on the
+ * concatenated x).  nbins <= 1024. */
+int pbx_profile_key_range(void *profile, uint64_t *kmin, uint64_t *kmax);
+int pbx_profile_msel_begin(void *profile, int64_t nbins, int has_min, double bin_min, int has_max,
+                           double bin_max, uint64_t kmin, uint64_t kmax, int *levels);
+int pbx_profile_msel_hist(void *profile, int level, uint32_t **d_hist, int64_t *count);
+int pbx_profile_msel_resolve(void *profile, int level);
+int pbx_profile_msel_edges(void *profile, double *h_edges, int64_t *n_edges);
 /* bin ids + counts (nb = n_edges - 1 int64) for ascending edges */
 int pbx_profile_assign(void *handle, const double *h_edges, int64_t n_edges,
                        int64_t *h_counts, int64_t *n_valid);
@@ -281,6 +298,9 @@ int pbx_comm_allgatherv(void *comm, void *d_buf, const int64_t *counts,
                         const int64_t *displs);
 int pbx_comm_allreduce_f64(void *comm, const double *d_send, double *d_recv,
                            int64_t count);
+/* generic: dtype 0 f64, 1 i64, 2 u64, 3 u32; op 0 sum, 1 min, 2 max */
+int pbx_comm_allreduce(void *comm, const void *d_send, void *d_recv, int64_t count, int dtype,
+                       int op);
 int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv,
                            int64_t count);
 /* Control plane on the same communicator: device barrier (returns after

@@ -140,4 +140,22 @@ int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv, i
   });
 }
 
+// Generic all-reduce on the library stream.  dtype: 0 f64, 1 i64, 2 u64,
+// 3 u32; op: 0 sum, 1 min, 2 max (e.g. the u32 digit histograms and the u64
+// key range of the distributed equaln).
+int pbx_comm_allreduce(void *comm, const void *d_send, void *d_recv, int64_t count, int dtype,
+                       int op) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) fail(PBX_ERR_VALUE, "null communicator");
+    static const ncclDataType_t types[] = {ncclFloat64, ncclInt64, ncclUint64, ncclUint32};
+    static const ncclRedOp_t ops[] = {ncclSum, ncclMin, ncclMax};
+    if (dtype < 0 || dtype > 3) fail(PBX_ERR_VALUE, "bad dtype %d", dtype);
+    if (op < 0 || op > 2) fail(PBX_ERR_VALUE, "bad reduction op %d", op);
+    Device &d = current_device();
+    PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, types[dtype], ops[op], c->nccl,
+                           d.stream));
+  });
+}
+
 }  // extern "C"

@@ -639,6 +639,14 @@ __global__ void widen_perm(const int32_t *__restrict__ p, int64_t n, int64_t *__
 }
 
 // ----------------------------------------------------------------- handle
+struct MselState {  // radix select in progress (equaln)
+  bool active = false;
+  int nq = 0, B = 0, L = 0, next = 0;
+  int wd[MS_MAXL] = {};
+  int64_t nbins = 0;
+  uint64_t ka = 0, kb = 0, lo = 0;
+};
+
 struct Profile {
   int device = -1;
   int64_t n = 0;          // elements in the binned space
@@ -650,6 +658,7 @@ struct Profile {
   bool csrh_ready = false;  // csrh = the CSR pass histogram, from assign_bins
   bool mm_valid = false;   // mm = min / max key of x, cached on the host
   uint64_t mm[2] = {0, 0};
+  MselState ms;
   Buf msH, msR, msG, msNg, msM, msRows, msL0, msL1, msCnt, csrh, slabp;
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
@@ -708,11 +717,18 @@ static bool select_enabled() {
 // then [sorted_x <= bin_max] (bins.py:734-737; NaN fails both and a NaN
 // bound keeps nothing; without bounds NaN sorts last and stays), then
 // edges = s[0], s[int(i*m/nb)], s[m-1] (bins.py:738-744).
-static void equaln_select(Profile &P, hipStream_t st, int64_t nbins, int has_min, double bin_min,
-                          int has_max, double bin_max, double *h_edges, int64_t *n_edges) {
-  const int nq = (int)nbins + 1;
-  uint64_t mm[2];
-  minmax_of(P, st, mm);
+//
+// Staged so the per-level digit histograms can be summed over ranks
+// (distributed equaln): begin (global key range) -> per
+// level: hist (this rank's keys) [+ all-reduce of the histogram] -> resolve
+// (identical on every rank) -> edges.  Single GPU: the same stages back to
+// back (equaln_select).
+static void msel_begin(Profile &P, int64_t nbins, int has_min, double bin_min, int has_max,
+                       double bin_max, uint64_t kmin, uint64_t kmax) {
+  MselState &S = P.ms;
+  S = MselState();
+  S.nbins = nbins;
+  S.nq = (int)nbins + 1;
   bool empty = false;
   uint64_t ka = 0ull, kb = ~0ull;
   if (has_min || has_max) {
@@ -726,59 +742,117 @@ static void equaln_select(Profile &P, hipStream_t st, int64_t nbins, int has_min
       else kb = std::min<uint64_t>(kb, dkey(bin_max));
     }
   }
-  const uint64_t lo = std::max<uint64_t>(ka, mm[0]);
-  const uint64_t hi = std::min<uint64_t>(kb, mm[1]);
+  const uint64_t lo = std::max<uint64_t>(ka, kmin);
+  const uint64_t hi = std::min<uint64_t>(kb, kmax);
   if (empty || lo > hi) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
   const uint64_t span = hi - lo;
-  const int B = span ? 64 - __builtin_clzll(span) : 1;
-  int wd[MS_MAXL], L = 1;
-  wd[0] = std::min(B, MS0_BITS);
-  for (int rem = B - wd[0]; rem > 0; rem -= MS_BITS) wd[L++] = std::min(rem, MS_BITS);
+  S.B = span ? 64 - __builtin_clzll(span) : 1;
+  S.L = 1;
+  S.wd[0] = std::min(S.B, MS0_BITS);
+  for (int rem = S.B - S.wd[0]; rem > 0; rem -= MS_BITS) S.wd[S.L++] = std::min(rem, MS_BITS);
+  S.ka = ka;
+  S.kb = kb;
+  S.lo = lo;
+  S.next = 0;
+  S.active = true;
+}
+
+static size_t msel_hbytes(const MselState &S) {
+  return sizeof(uint32_t) * std::max<size_t>((size_t)S.nq * MS_DIG, MS0_DIG);
+}
+
+// this rank's digit histogram of `level` into H; returns the u32 count that
+// a distributed caller sums over ranks
+static int64_t msel_hist(Profile &P, hipStream_t st, int level) {
+  MselState &S = P.ms;
+  if (!S.active || level != S.next || level >= S.L)
+    fail(PBX_ERR_VALUE, "radix select: level %d out of order", level);
   const int64_t n = P.n;
-  const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
+  const int nq = S.nq;
   const unsigned grid = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (n + TPB - 1) / TPB));
-  uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * std::max<size_t>((size_t)nq * MS_DIG, MS0_DIG));
-  uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
+  uint32_t *H = (uint32_t *)P.msH.get(msel_hbytes(S));
+  uint64_t *G = (uint64_t *)P.msG.get(sizeof(uint64_t) * (size_t)nq);
+  int32_t *ng = (int32_t *)P.msNg.get(16);
+  uint32_t *cnt = (uint32_t *)P.msCnt.get(sizeof(uint32_t) * MS_MAXL);
+  int s = S.B;
+  for (int l = 0; l <= level; ++l) s -= S.wd[l];
+  if (level == 0) {
+    PBX_HIP(hipMemsetAsync(H, 0, msel_hbytes(S), st));
+    PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * MS_MAXL, st));
+    const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
+    uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
+    if (n) {
+      hipLaunchKernelGGL(msel_hist0, dim3(g0), dim3(MS0_TPB), 0, st, (const double *)P.x.p, n,
+                         S.ka, S.kb, S.lo, s, rows);
+      hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st, rows, g0, H);
+    }
+    PBX_HIP(hipGetLastError());
+    return MS0_DIG;
+  }
+  uint64_t *list[2] = {nullptr, nullptr};
+  if (S.L > 1) list[0] = (uint64_t *)P.msL0.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
+  if (S.L > 2) list[1] = (uint64_t *)P.msL1.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
+  uint64_t *out = (level + 1 < S.L) ? list[(level - 1) & 1] : nullptr;
+  if (level == 1)
+    hipLaunchKernelGGL(msel_filter<true>, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n,
+                       S.ka, S.kb, S.lo, (const uint64_t *)nullptr, (const uint32_t *)nullptr, s,
+                       S.wd[level], G, ng, H, out, cnt + level);
+  else
+    hipLaunchKernelGGL(msel_filter<false>, dim3(grid), dim3(TPB), 0, st, (const double *)nullptr,
+                       n, S.ka, S.kb, S.lo, (const uint64_t *)list[level & 1], cnt + level - 1, s,
+                       S.wd[level], G, ng, H, out, cnt + level);
+  PBX_HIP(hipGetLastError());
+  return (int64_t)nq * MS_DIG;
+}
+
+// digits of `level` from the (summed) histogram; then the next level's groups
+static void msel_resolve_level(Profile &P, hipStream_t st, int level) {
+  MselState &S = P.ms;
+  if (!S.active || level != S.next) fail(PBX_ERR_VALUE, "radix select: level %d out of order", level);
+  const int nq = S.nq;
+  uint32_t *H = (uint32_t *)P.msH.p;
   MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
   uint64_t *G = (uint64_t *)P.msG.get(sizeof(uint64_t) * (size_t)nq);
   int32_t *ng = (int32_t *)P.msNg.get(16);
   int64_t *m_dev = (int64_t *)P.msM.get(16);
-  uint32_t *cnt = (uint32_t *)P.msCnt.get(sizeof(uint32_t) * MS_MAXL);
-  uint64_t *list[2] = {nullptr, nullptr};
-  if (L > 1) list[0] = (uint64_t *)P.msL0.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
-  if (L > 2) list[1] = (uint64_t *)P.msL1.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
+  if (level == 0)
+    hipLaunchKernelGGL(msel_resolve<MS0_DIG>, dim3(1), dim3(TPB), 0, st, H, ng, R, nq, 1,
+                       S.nbins, S.wd[0], m_dev);
+  else
+    hipLaunchKernelGGL(msel_resolve<MS_DIG>, dim3(nq), dim3(TPB), 0, st, H, ng, R, nq, 0,
+                       S.nbins, S.wd[level], m_dev);
+  if (level + 1 < S.L) hipLaunchKernelGGL(msel_groups, dim3(1), dim3(1024), 0, st, R, nq, G, ng);
+  PBX_HIP(hipGetLastError());
+  S.next = level + 1;
+}
+
+static void msel_edges_out(Profile &P, hipStream_t st, double *h_edges, int64_t *n_edges) {
+  MselState &S = P.ms;
+  if (!S.active || S.next != S.L) fail(PBX_ERR_VALUE, "radix select: %d of %d levels resolved", S.next, S.L);
+  const int nq = S.nq;
   double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
-  PBX_HIP(hipMemsetAsync(H, 0, sizeof(uint32_t) * std::max<size_t>((size_t)nq * MS_DIG, MS0_DIG), st));
-  PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * MS_MAXL, st));
-  int s = B - wd[0];
-  hipLaunchKernelGGL(msel_hist0, dim3(g0), dim3(MS0_TPB), 0, st, (const double *)P.x.p, n, ka, kb,
-                     lo, s, rows);
-  hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st, rows, g0, H);
-  hipLaunchKernelGGL(msel_resolve<MS0_DIG>, dim3(1), dim3(TPB), 0, st, H, ng, R, nq, 1, nbins,
-                     wd[0], m_dev);
-  for (int l = 1; l < L; ++l) {
-    hipLaunchKernelGGL(msel_groups, dim3(1), dim3(1024), 0, st, R, nq, G, ng);
-    s -= wd[l];
-    uint64_t *out = (l + 1 < L) ? list[(l - 1) & 1] : nullptr;
-    if (l == 1)
-      hipLaunchKernelGGL(msel_filter<true>, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n,
-                         ka, kb, lo, (const uint64_t *)nullptr, (const uint32_t *)nullptr, s, wd[l],
-                         G, ng, H, out, cnt + l);
-    else
-      hipLaunchKernelGGL(msel_filter<false>, dim3(grid), dim3(TPB), 0, st, (const double *)nullptr,
-                         n, ka, kb, lo, (const uint64_t *)list[l & 1], cnt + l - 1, s, wd[l], G, ng,
-                         H, out, cnt + l);
-    hipLaunchKernelGGL(msel_resolve<MS_DIG>, dim3(nq), dim3(TPB), 0, st, H, ng, R, nq, 0, nbins,
-                       wd[l], m_dev);
-  }
-  hipLaunchKernelGGL(msel_edges, dim3(ceil_div(nq, TPB)), dim3(TPB), 0, st, R, nq, lo, de);
+  hipLaunchKernelGGL(msel_edges, dim3(ceil_div(nq, TPB)), dim3(TPB), 0, st,
+                     (const MsRank *)P.msR.p, nq, S.lo, de);
   PBX_HIP(hipGetLastError());
   int64_t m = 0;
-  PBX_HIP(hipMemcpyAsync(&m, m_dev, 8, hipMemcpyDeviceToHost, st));
+  PBX_HIP(hipMemcpyAsync(&m, P.msM.p, 8, hipMemcpyDeviceToHost, st));
   PBX_HIP(hipMemcpyAsync(h_edges, de, sizeof(double) * nq, hipMemcpyDeviceToHost, st));
   PBX_HIP(hipStreamSynchronize(st));
+  S.active = false;
   if (m == 0) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
   *n_edges = (m < 2) ? 2 : nq;
+}
+
+static void equaln_select(Profile &P, hipStream_t st, int64_t nbins, int has_min, double bin_min,
+                          int has_max, double bin_max, double *h_edges, int64_t *n_edges) {
+  uint64_t mm[2];
+  minmax_of(P, st, mm);
+  msel_begin(P, nbins, has_min, bin_min, has_max, bin_max, mm[0], mm[1]);
+  for (int l = 0; l < P.ms.L; ++l) {
+    msel_hist(P, st, l);
+    msel_resolve_level(P, st, l);
+  }
+  msel_edges_out(P, st, h_edges, n_edges);
 }
 
 static Profile &as_profile(void *h) {
@@ -833,6 +907,7 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
     P.has_idx = false;
     P.csr_ready = false;
     P.csrh_ready = false;
+    P.ms.active = false;
     P.mm_valid = false;
     P.nb = -1;
   });
@@ -911,6 +986,7 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
     P.has_idx = true;
     P.csr_ready = false;
     P.csrh_ready = false;
+    P.ms.active = false;
     P.nb = -1;
     *n_kept = kept;
   });
@@ -952,6 +1028,58 @@ int pbx_profile_minmax(void *handle, double *mn, double *mx) {
     if (hi != hi) lo = hi;  // any NaN -> both NaN
     *mn = lo;
     *mx = hi;
+  });
+}
+
+// ---- distributed equaln: the radix select in stages ----
+int pbx_profile_key_range(void *handle, uint64_t *kmin, uint64_t *kmax) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    uint64_t h[2] = {~0ull, 0ull};
+    if (P.n) minmax_of(P, d.stream, h);
+    *kmin = h[0];
+    *kmax = h[1];
+  });
+}
+
+int pbx_profile_msel_begin(void *handle, int64_t nbins, int has_min, double bin_min, int has_max,
+                           double bin_max, uint64_t kmin, uint64_t kmax, int *levels) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (nbins < 1) fail(PBX_ERR_VALUE, "nbins must be >= 1");
+    if (nbins + 1 > MS_MAXQ) fail(PBX_ERR_VALUE, "distributed equaln supports nbins <= %d", MS_MAXQ - 1);
+    msel_begin(P, nbins, has_min, bin_min, has_max, bin_max, kmin, kmax);
+    *levels = P.ms.L;
+  });
+}
+
+int pbx_profile_msel_hist(void *handle, int level, uint32_t **d_hist, int64_t *count) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    *count = msel_hist(P, d.stream, level);
+    *d_hist = (uint32_t *)P.msH.p;
+  });
+}
+
+int pbx_profile_msel_resolve(void *handle, int level) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    msel_resolve_level(P, d.stream, level);
+  });
+}
+
+int pbx_profile_msel_edges(void *handle, double *h_edges, int64_t *n_edges) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    msel_edges_out(P, d.stream, h_edges, n_edges);
   });
 }
 

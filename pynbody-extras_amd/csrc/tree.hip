@@ -58,7 +58,7 @@ using namespace prim;
 static constexpr double kR2Tiny = 2.2250738585072014e-308;  // tree.rs:36
 constexpr int LPW = 21;                                      // octree levels per key word
 constexpr int MAX_WORDS = 53;  // 1113 levels: half underflows to 0 before that
-constexpr int WALK_TPB = 64;   // one wave per block
+constexpr int WALK_TPB = 256;  // max threads per walk block (waves are independent)
 
 // --------------------------------------------------------------- moments
 // Cartesian slots in graded order (the field order of MultipoleMoment,
@@ -771,6 +771,7 @@ struct WalkParams {
   int64_t max_steps;             // > number of nodes
   unsigned int *fault;           // set when a wave exceeds max_steps
   unsigned xcd_chunk;            // blocks per XCD chunk (0: launch order)
+  unsigned long long *trace;     // diagnostic (PBX_WALK_TRACE): per block start, end, steps
 };
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -841,13 +842,20 @@ __device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, doubl
   }
 }
 
-// SOFT: h_max guard and/or softened leaf sums are live
+// SOFT: h_max guard and/or softened leaf sums are live.  The walk hides
+// its scalar-load latency with other waves: orders <= 3 without softening
+// are held to 8 waves per SIMD (the compiler then parks a few SGPRs in VGPR
+// lanes instead of taking ~100 SGPRs, which leaves room for only 6 waves).
 template <int P, int WANT, bool SOFT>
-__global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
+__global__ void __launch_bounds__(WALK_TPB)
+    __attribute__((amdgpu_waves_per_eu((P <= 3 && !SOFT) ? 8 : 1, 8)))
+    walk_kernel(WalkParams wp) {
   constexpr int RS = rec_stride<P>();
   constexpr int NCH = (P == 2 || P == 3) ? RS / 8 : 1;  // chunks loaded eagerly
+  const unsigned long long t_start = wp.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const unsigned lb = wp.xcd_chunk ? xcd_chunk_swizzle(blockIdx.x, wp.xcd_chunk) : blockIdx.x;
-  const int64_t t = (int64_t)lb * WALK_TPB + threadIdx.x;
+  const int64_t t = (int64_t)lb * blockDim.x + threadIdx.x;
+  const bool lane0 = (threadIdx.x & 63) == 0;
   const bool valid = t < wp.m;
   const bool self_mode = wp.tgt == nullptr;
   double tx = 0.0, ty = 0.0, tz = 0.0, th = 0.0;
@@ -870,12 +878,13 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
   const bool has_th = SOFT && self_mode && wp.soft != nullptr;
   double ph = 0.0, ax = 0.0, ay = 0.0, az = 0.0;
   unsigned long long n_node = 0, n_pp = 0, n_active = 0;
+  unsigned long long leaf_steps = 0, leaf_active = 0, open_steps = 0;  // wave-uniform
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
   int64_t steps = 0;           // the wave moves strictly forward in DFS order
   while (w >= 0) {
     if (++steps > wp.max_steps) {  // corrupted links: stop instead of hanging
-      if (threadIdx.x == 0) atomicOr(wp.fault, 1u);
+      if (lane0) atomicOr(wp.fault, 1u);
       break;
     }
     u32x16 c[NCH];
@@ -890,9 +899,12 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
       continue;
     }
     if (first < 0) {  // leaf: direct sum in ascending index order
+      ++leaf_steps;
+      leaf_active += (unsigned long long)__popcll(__ballot(act));
       if (act) {
         const int32_t s = chunk_i(c[0], 14), e = s + chunk_i(c[0], 15);
         n_pp += (unsigned long long)(e - s);
+#ifndef PBX_DIAG_SKIP_LEAF  // timing diagnostic: leaves visited, pairs not evaluated
         for (int32_t j = s; j < e; j += 4) {  // 4 records (128 B) per round trip
           u32x16 r[2];
           load_chunks<2>((const double *)(wp.rec + j), r);
@@ -909,6 +921,7 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
                                     ty, tz, th, ph, ax, ay, az);
           }
         }
+#endif
         p = next;
       }
       w = next;
@@ -1000,7 +1013,15 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
         p = first;
       }
     }
-    w = (__ballot(open) != 0ull) ? first : next;
+    const bool descend = __ballot(open) != 0ull;
+    open_steps += descend ? 1ull : 0ull;
+    w = descend ? first : next;
+  }
+  if (wp.trace && lane0) {
+    const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    wp.trace[3 * wv] = t_start;
+    wp.trace[3 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+    wp.trace[3 * wv + 2] = (unsigned long long)steps;
   }
   if (!valid) return;
   const int64_t o = (self_mode && !wp.compact) ? (int64_t)wp.perm[wp.first + t] : t;
@@ -1017,11 +1038,14 @@ __global__ void __launch_bounds__(WALK_TPB) walk_kernel(WalkParams wp) {
       n_node += __shfl_xor(n_node, sh, 64);
       n_pp += __shfl_xor(n_pp, sh, 64);
     }
-    if (threadIdx.x == 0) {
+    if (lane0) {
       atomicAdd(&wp.counters[0], n_node);
       atomicAdd(&wp.counters[1], n_pp);
       atomicAdd(&wp.counters[3], (unsigned long long)steps);
       atomicAdd(&wp.counters[4], n_active);
+      atomicAdd(&wp.counters[5], leaf_steps);
+      atomicAdd(&wp.counters[6], leaf_active);
+      atomicAdd(&wp.counters[7], open_steps);
     }
   }
 }
@@ -1058,6 +1082,7 @@ struct Octree {
   std::vector<int32_t> lvl;  // first node id of every level (+ end)
   Buf pos, mass, soft;       // original order (device copies)
   Buf perm, rec, soft_s;     // leaf order
+  Buf trace;                 // PBX_WALK_TRACE diagnostic
   Buf nstart, ncount, nfirst, nnext, nchild, ncen, pre, size;
   Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
@@ -1065,11 +1090,12 @@ struct Octree {
     Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
                    &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &keys, &ktmp0,
                    &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
-                   &counters};
+                   &counters, &trace};
     for (Buf *b : bufs) b->release();
   }
   // accepted nodes, leaf pairs, fault flag, wave steps, active-lane steps
-  unsigned long long last_counts[5] = {0, 0, 0, 0, 0};
+  // + leaf wave steps, their active lanes, descending wave steps
+  unsigned long long last_counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int moment_order() const { return order < 5 ? order : 5; }
 };
 
@@ -1391,18 +1417,29 @@ static unsigned walk_xcd_chunk() {
   return c;
 }
 
+// threads per walk block (PBX_WALK_TPB: 64, 128 or 256)
+static unsigned walk_tpb() {
+  static const unsigned c = [] {
+    const char *v = std::getenv("PBX_WALK_TPB");
+    const unsigned t = v ? (unsigned)std::strtoul(v, nullptr, 10) : 64u;
+    return (t == 128 || t == 256) ? t : 64u;
+  }();
+  return c;
+}
+
 template <int P, int WANT>
 static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
-  unsigned grid = (unsigned)((wp.m + WALK_TPB - 1) / WALK_TPB);
+  const unsigned tpb = walk_tpb();
+  unsigned grid = (unsigned)((wp.m + tpb - 1) / tpb);
   wp.xcd_chunk = walk_xcd_chunk();
   if (wp.xcd_chunk) {  // whole rounds of kNumXcd chunks; the extra blocks find no targets
     const unsigned round = kNumXcd * wp.xcd_chunk;
     grid = (grid + round - 1) / round * round;
   }
   if (soft)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, true>), dim3(grid), dim3(WALK_TPB), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, true>), dim3(grid), dim3(tpb), 0, st, wp);
   else
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false>), dim3(grid), dim3(WALK_TPB), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false>), dim3(grid), dim3(tpb), 0, st, wp);
 }
 
 template <int P>
@@ -1441,6 +1478,16 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   wp.pot = d_pot;
   wp.acc = d_acc;
   wp.counters = ctr;
+  wp.trace = nullptr;
+  const char *trace_path = std::getenv("PBX_WALK_TRACE");  // diagnostic only
+  unsigned tgrid = 0;
+  if (trace_path) {
+    tgrid = (unsigned)((m + walk_tpb() - 1) / walk_tpb());
+    const unsigned c = walk_xcd_chunk();
+    if (c) tgrid = (tgrid + kNumXcd * c - 1) / (kNumXcd * c) * (kNumXcd * c);
+    tgrid *= walk_tpb() / 64;  // one trace record per wave
+    wp.trace = (unsigned long long *)T.trace.get(24 * (size_t)tgrid);
+  }
   wp.max_steps = T.nn + 16;
   wp.fault = (unsigned int *)(ctr + 2);
   // softened leaves need softenings; the guard needs h_max; at query points
@@ -1460,6 +1507,15 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
     default: launch_walk_p<5>(wp, want, soft, st); break;
   }
   PBX_HIP(hipGetLastError());
+  if (trace_path) {  // append (start, end, steps) per block, launch order
+    std::vector<unsigned long long> h(3 * (size_t)tgrid);
+    PBX_HIP(hipMemcpyAsync(h.data(), wp.trace, 24 * (size_t)tgrid, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    if (FILE *f = std::fopen(trace_path, "ab")) {
+      std::fwrite(h.data(), 8, h.size(), f);
+      std::fclose(f);
+    }
+  }
 }
 
 static Octree &as_tree(pbx_octree *h) {
@@ -1615,7 +1671,7 @@ int pbx_octree_compute(pbx_octree *t, double theta, int want, double *pot, doubl
       if (want & PBX_WANT_ACC) da = (double *)dev.slot(kSlotAcc).ensure(24 * (size_t)std::max<int64_t>(n, 1));
     }
     walk(T, theta, want, nullptr, n, dp, da, st);
-    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 40, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 64, hipMemcpyDeviceToHost, st));
     if (!on_device) {
       if (dp && n) PBX_HIP(hipMemcpyAsync(pot, dp, 8 * (size_t)n, hipMemcpyDeviceToHost, st));
       if (da && n) PBX_HIP(hipMemcpyAsync(acc, da, 24 * (size_t)n, hipMemcpyDeviceToHost, st));
@@ -1653,7 +1709,7 @@ int pbx_octree_at_points(pbx_octree *t, const double *points, int64_t m, double 
     }
     // at points there is no target softening and no self skip
     walk(T, theta, want, dt, m, dp, da, st);
-    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 40, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 64, hipMemcpyDeviceToHost, st));
     if (!on_device) {
       if (dp && m) PBX_HIP(hipMemcpyAsync(pot, dp, 8 * (size_t)m, hipMemcpyDeviceToHost, st));
       if (da && m) PBX_HIP(hipMemcpyAsync(acc, da, 24 * (size_t)m, hipMemcpyDeviceToHost, st));
@@ -1680,7 +1736,7 @@ int pbx_octree_compute_range(pbx_octree *t, double theta, int want, int64_t firs
     ScopedTimer tm("octree.compute_range");
     walk(T, theta, want, nullptr, count, (want & PBX_WANT_POT) ? d_pot : nullptr,
          (want & PBX_WANT_ACC) ? d_acc : nullptr, st, first, compact, d_cost);
-    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 40, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipMemcpyAsync(T.last_counts, T.counters.p, 64, hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
     if (T.last_counts[2] & 0xffffffffull) fail(PBX_ERR_RUNTIME, "octree walk exceeded its step bound");
   });
@@ -1717,6 +1773,9 @@ int pbx_octree_info(pbx_octree *t, int64_t *out) {
     out[7] = T.nwords;
     out[8] = (int64_t)T.last_counts[3];
     out[9] = (int64_t)T.last_counts[4];
+    out[10] = (int64_t)T.last_counts[5];
+    out[11] = (int64_t)T.last_counts[6];
+    out[12] = (int64_t)T.last_counts[7];
   });
 }
 

@@ -295,10 +295,11 @@ class Octree:
 
     # -- introspection -----------------------------------------------------
     def info(self) -> dict:
-        out = np.zeros(10, dtype=np.int64)
+        out = np.zeros(13, dtype=np.int64)
         nat.call("pbx_octree_info", self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
         keys = ("n", "nodes", "levels", "has_mass_payload", "has_hmax", "node_interactions",
-                "leaf_pairs", "path_words", "wave_steps", "active_lane_steps")
+                "leaf_pairs", "path_words", "wave_steps", "active_lane_steps", "leaf_wave_steps",
+                "leaf_active_lanes", "descend_wave_steps")
         return {k: int(v) for k, v in zip(keys, out)}
 
     def export(self) -> dict:

@@ -13,7 +13,8 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_void_p
+from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint64,
+                    c_void_p)
 from pathlib import Path
 
 import numpy as np
@@ -116,6 +117,13 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_comm_allgatherv": (c_int, [c_void_p, c_void_p, _i64p, _i64p]),
     "pbx_comm_allreduce_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
     "pbx_comm_allreduce_i64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64]),
+    "pbx_comm_allreduce": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int]),
+    "pbx_profile_key_range": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
+    "pbx_profile_msel_begin": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double,
+                                       c_uint64, c_uint64, POINTER(c_int)]),
+    "pbx_profile_msel_hist": (c_int, [c_void_p, c_int, POINTER(c_void_p), POINTER(c_int64)]),
+    "pbx_profile_msel_resolve": (c_int, [c_void_p, c_int]),
+    "pbx_profile_msel_edges": (c_int, [c_void_p, _dp, POINTER(c_int64)]),
     "pbx_comm_barrier": (c_int, [c_void_p]),
     "pbx_comm_max_f64": (c_int, [c_void_p, c_double, POINTER(c_double)]),
 }

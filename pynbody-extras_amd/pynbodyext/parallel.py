@@ -10,6 +10,11 @@ this module is the MI355X scale-out of the same solve:
   for its own targets with self-skip offset lo_r.  Outputs stay sharded.
 * profile partials (int64 counts, f64 per-bin sums) are summed with one
   all-reduce.
+* profiles over particles sharded across ranks (ShardedProfile): equaln
+  edges are the global order statistics, found by the device radix select
+  with its per-level digit histograms summed over ranks (u32 all-reduce:
+  64 KB at level 0, nbins+1 rows of 16 KB after); counts, per-bin sums and
+  the global CSR offsets are all-reduced.
 
 The control plane (unique-id exchange, barriers) is the caller's, e.g.
 torch.distributed with the gloo backend; the data path is RCCL only.
@@ -25,6 +30,10 @@ from . import _native as nat
 
 
 SYM_MIN_N = 8192  # all-particles solves of at least this size use direct_sym.hip
+
+# pbx_comm_allreduce dtypes / ops
+DT_F64, DT_I64, DT_U64, DT_U32 = 0, 1, 2, 3
+OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
 
 
 def shard_bounds(n_total: int, world: int, rank: int) -> tuple[int, int]:
@@ -72,6 +81,25 @@ class Communicator:
 
     def allreduce_sum_i64(self, d_send, d_recv, count: int) -> None:
         nat.call("pbx_comm_allreduce_i64", self.handle, d_send, d_recv, int(count))
+
+    def allreduce(self, d_send, d_recv, count: int, dtype: int, op: int = OP_SUM) -> None:
+        """Device all-reduce (dtype DT_*, op OP_*), e.g. in place."""
+        nat.call("pbx_comm_allreduce", self.handle, d_send, d_recv, int(count), int(dtype),
+                 int(op))
+
+    def allreduce_host(self, a: np.ndarray, op: int = OP_SUM) -> np.ndarray:
+        """All-reduce of a small host array (f64 / i64 / u64 / u32) through HBM."""
+        a = np.ascontiguousarray(a)
+        dt = {np.dtype(np.float64): DT_F64, np.dtype(np.int64): DT_I64,
+              np.dtype(np.uint64): DT_U64, np.dtype(np.uint32): DT_U32}[a.dtype]
+        buf = nat.DeviceArray.from_host(a)
+        try:
+            self.allreduce(buf.ptr, buf.ptr, a.size, dt, op)
+            out = np.empty_like(a)
+            buf.download(out)
+        finally:
+            buf.free()
+        return out
 
     def barrier(self) -> None:
         nat.call("pbx_comm_barrier", self.handle)
@@ -311,3 +339,64 @@ class ShardedTree:
             self.tree = None
         for a in (self.d_pot, self.d_acc, self.d_spos, self.d_smass, self.d_cost):
             a.free()
+
+
+def distributed_equaln(dev, comm, nbins: int, bin_min=None, bin_max=None) -> np.ndarray:
+    """Global equaln edges of the x values held by all ranks (bins.py:720-746
+    on the concatenation), every rank the same.  ``dev`` offers the staged
+    radix select (DeviceBins.key_range / msel_*); ``comm`` the all-reduces
+    (Communicator: allreduce_host for the key range, allreduce in place on
+    the device histogram).  The histograms are summed before every resolve,
+    so each rank picks the same digits and no particle moves."""
+    kmin, kmax = dev.key_range()
+    kmin = int(comm.allreduce_host(np.array([kmin], dtype=np.uint64), OP_MIN)[0])
+    kmax = int(comm.allreduce_host(np.array([kmax], dtype=np.uint64), OP_MAX)[0])
+    levels = dev.msel_begin(nbins, bin_min, bin_max, kmin, kmax)
+    for level in range(levels):
+        ptr, count = dev.msel_hist(level)
+        comm.allreduce(ptr, ptr, count, DT_U32, OP_SUM)
+        dev.msel_resolve(level)
+    return dev.msel_edges()
+
+
+class ShardedProfile:
+    """RadialProfile over particles sharded across ranks:
+    each rank selects and bins its own particles; edges (equaln: distributed
+    radix select), counts and per-bin sums are global.  ``offset`` is this
+    rank's first global particle index (for the global binind)."""
+
+    def __init__(self, comm, dev, offset: int = 0):
+        self.comm, self.dev, self.offset = comm, dev, int(offset)
+        self.world = comm.nranks if comm is not None else 1
+        self.rank = comm.rank if comm is not None else 0
+
+    def edges_equaln(self, nbins: int, bin_min=None, bin_max=None) -> np.ndarray:
+        if self.comm is None:
+            return self.dev.edges_equaln(nbins, bin_min, bin_max)
+        return distributed_equaln(self.dev, self.comm, nbins, bin_min, bin_max)
+
+    def assign(self, edges) -> np.ndarray:
+        """Global per-bin counts (this rank's stay in dev.counts)."""
+        local = self.dev.assign(edges)
+        return local.copy() if self.comm is None else self.comm.allreduce_host(local)
+
+    def moments(self, field, weights) -> np.ndarray:
+        local = self.dev.moments(field, weights)
+        return local if self.comm is None else self.comm.allreduce_host(local)
+
+    def csr(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(global particle indices of this rank's members, global offsets
+        (nbins + 1), start of this rank's run inside every bin).  Bin b of
+        the global binind = the ranks' runs in rank order."""
+        perm, _ = self.dev.csr()
+        local = self.dev.counts
+        nb = local.shape[0]
+        table = np.zeros((self.world, nb), dtype=np.int64)
+        table[self.rank] = local
+        if self.comm is not None:
+            table = self.comm.allreduce_host(table)
+        glob = table.sum(0)
+        offs = np.zeros(nb + 1, dtype=np.int64)
+        np.cumsum(glob, out=offs[1:])
+        start = offs[:-1] + table[:self.rank].sum(0)
+        return perm + self.offset, offs, start

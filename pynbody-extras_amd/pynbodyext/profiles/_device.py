@@ -8,7 +8,7 @@ computed by the HIP kernels of csrc/profile.hip.
 from __future__ import annotations
 
 import ctypes
-from ctypes import byref, c_double, c_int64, c_void_p
+from ctypes import byref, c_double, c_int, c_int64, c_uint64, c_void_p
 
 import numpy as np
 
@@ -121,6 +121,47 @@ class DeviceBins:
             nat.call("pbx_profile_edges_equaln", self._h, int(nbins), int(bin_min is not None),
                      float(bin_min) if bin_min is not None else 0.0, int(bin_max is not None),
                      float(bin_max) if bin_max is not None else 0.0, nat.dptr(out), byref(ne))
+        except ValueError as e:
+            if str(e).startswith("index 0 is out of bounds"):
+                raise IndexError(str(e)) from None
+            raise
+        return out[: ne.value].copy()
+
+    # -- staged equaln (distributed radix select, parallel.distributed_equaln)
+    def key_range(self) -> tuple[int, int]:
+        """Local (min, max) order-preserving u64 keys of x ((2^64-1, 0) if empty)."""
+        lo, hi = c_uint64(), c_uint64()
+        nat.call("pbx_profile_key_range", self._h, byref(lo), byref(hi))
+        return lo.value, hi.value
+
+    def msel_begin(self, nbins: int, bin_min, bin_max, kmin: int, kmax: int) -> int:
+        lv = c_int(0)
+        try:
+            nat.call("pbx_profile_msel_begin", self._h, int(nbins), int(bin_min is not None),
+                     float(bin_min) if bin_min is not None else 0.0, int(bin_max is not None),
+                     float(bin_max) if bin_max is not None else 0.0, int(kmin), int(kmax),
+                     byref(lv))
+        except ValueError as e:
+            if str(e).startswith("index 0 is out of bounds"):
+                raise IndexError(str(e)) from None
+            raise
+        self._msel_nq = int(nbins) + 1
+        return lv.value
+
+    def msel_hist(self, level: int) -> tuple[int, int]:
+        """(device pointer, u32 count) of this rank's digit histogram."""
+        ptr, cnt = c_void_p(), c_int64()
+        nat.call("pbx_profile_msel_hist", self._h, int(level), byref(ptr), byref(cnt))
+        return ptr.value, cnt.value
+
+    def msel_resolve(self, level: int) -> None:
+        nat.call("pbx_profile_msel_resolve", self._h, int(level))
+
+    def msel_edges(self) -> np.ndarray:
+        out = np.empty(self._msel_nq)
+        ne = c_int64(0)
+        try:
+            nat.call("pbx_profile_msel_edges", self._h, nat.dptr(out), byref(ne))
         except ValueError as e:
             if str(e).startswith("index 0 is out of bounds"):
                 raise IndexError(str(e)) from None

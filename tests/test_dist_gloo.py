@@ -206,3 +206,56 @@ def test_sharded_tree_world2_profile_matches_unsharded():
     np.add.at(full[:, 1], b[ok], mass[ok] * pot[ok])
     for _, _, _, part in res:
         np.testing.assert_allclose(part, full, rtol=1e-12, atol=1e-15)
+
+
+def _equaln_worker(rank, world, port, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd"), str(ROOT / "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from _msel_mock import GlooComm, NumpyMsel
+    from pynbodyext.parallel import distributed_equaln
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(5)
+        x = rng.lognormal(0.0, 2.0, 20_000)
+        x[::101] = np.nan
+        parts = np.split(x, [3000, 3000, 11_000])  # rank 1 holds nothing
+        comm = GlooComm(dist, torch)
+        out = {}
+        for key, nb, lo, hi in (("plain", 64, None, None), ("clip", 100, 0.1, 30.0)):
+            out[key] = distributed_equaln(NumpyMsel(parts[rank]), comm, nb, lo, hi)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_equaln_world4_protocol():
+    """The distributed equaln protocol (parallel.distributed_equaln) over 4
+    gloo ranks with uneven shards and an empty rank: every rank's edges equal
+    the single-process equaln of the concatenation (bins.py:720-746).  The
+    per-rank radix select is the numpy restatement of the device stages."""
+    import multiprocessing as mp
+
+    from oracle import profile_ref as pr
+
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_equaln_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(5)
+    x = rng.lognormal(0.0, 2.0, 20_000)
+    x[::101] = np.nan
+    want = {"plain": pr.edges_equaln(x, 64), "clip": pr.edges_equaln(x, 100, 0.1, 30.0)}
+    for _, out in res:
+        for key in want:
+            assert np.array_equal(out[key], want[key], equal_nan=True), key

@@ -125,3 +125,90 @@ def test_sharded_direct_symmetric_world1(gpu):
         comm.destroy()
     pr = og.direct_potentials(pos, mass)
     assert np.max(np.abs(pot - pr) / np.abs(pr)) < (1e-10 if nat.get_precise() else 1e-6)
+
+
+def _emulated_ranks_equaln(devs, nbins, lo=None, hi=None):
+    """The distributed equaln protocol with R ranks emulated on one GPU: the
+    'all-reduce' of every level's histogram is a host sum over the handles."""
+    import ctypes
+
+    kr = [d.key_range() for d in devs]
+    kmin, kmax = min(k[0] for k in kr), max(k[1] for k in kr)
+    levels = [d.msel_begin(nbins, lo, hi, kmin, kmax) for d in devs]
+    assert len(set(levels)) == 1
+    for level in range(levels[0]):
+        hs = [d.msel_hist(level) for d in devs]
+        tot = None
+        for ptr, cnt in hs:
+            h = np.empty(cnt, dtype=np.uint32)
+            nat.call("pbx_memcpy_dtoh", h.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr),
+                     ctypes.c_size_t(h.nbytes))
+            tot = h.astype(np.uint64) if tot is None else tot + h
+        tot = tot.astype(np.uint32)
+        for ptr, _ in hs:
+            nat.call("pbx_memcpy_htod", ctypes.c_void_p(ptr), tot.ctypes.data_as(ctypes.c_void_p),
+                     ctypes.c_size_t(tot.nbytes))
+        for d in devs:
+            d.msel_resolve(level)
+    return [d.msel_edges() for d in devs]
+
+
+@pytest.mark.parametrize("case", ["halves", "uneven", "empty_rank", "bounds", "nan", "dups"])
+def test_distributed_equaln_emulated_ranks(gpu, case):
+    """Edges from rank-local radix-select histograms summed over ranks equal
+    the single-process equaln of the concatenated x (bins.py:720-746)."""
+    from oracle import profile_ref as pr
+    from pynbodyext.profiles._device import DeviceBins
+
+    rng = np.random.default_rng(21)
+    x = rng.lognormal(0.0, 1.5, 300_000)
+    nb, lo, hi, cuts = 128, None, None, [150_000]
+    if case == "uneven":
+        cuts = [1000, 250_000]
+    elif case == "empty_rank":
+        cuts = [0, 100_000]
+    elif case == "bounds":
+        lo, hi, cuts = 0.05, 20.0, [50_000, 120_000, 290_000]
+    elif case == "nan":
+        x[::97] = np.nan
+    elif case == "dups":
+        x = rng.choice(np.array([0.5, 1.0, 1.0000000000000002, 3.0]), 300_000)
+        nb = 256
+    parts = np.split(x, cuts)
+    devs = [DeviceBins.from_x(p) if p.size else DeviceBins.from_x(np.zeros(0)) for p in parts]
+    try:
+        got = _emulated_ranks_equaln(devs, nb, lo, hi)
+    finally:
+        for d in devs:
+            d.close()
+    want = pr.edges_equaln(x, nb, lo, hi)
+    for g in got:
+        assert np.array_equal(g, want, equal_nan=True), case
+
+
+def test_sharded_profile_world1_matches_single(gpu):
+    """ShardedProfile through a 1-rank RCCL communicator (the all-reduce
+    plumbing of the multi-GPU profile) = the single-device profile."""
+    from pynbodyext.parallel import ShardedProfile
+    from pynbodyext.profiles._device import SRC_W, SRC_X, DeviceBins
+
+    pos, mass = plummer(200_000, seed=31)
+    comm = Communicator(1, 0, Communicator.unique_id())
+    a = DeviceBins.select(pos, mass, sphere=((0.0, 0.0, 0.0), 10.0), ndim=3)
+    b = DeviceBins.select(pos, mass, sphere=((0.0, 0.0, 0.0), 10.0), ndim=3)
+    try:
+        sp = ShardedProfile(comm, a, offset=0)
+        e = sp.edges_equaln(128)
+        assert np.array_equal(e, b.edges_equaln(128))
+        c = sp.assign(e)
+        assert np.array_equal(c, b.assign(e))
+        m = sp.moments(SRC_X, SRC_W)
+        np.testing.assert_allclose(m, b.moments(SRC_X, SRC_W), rtol=1e-12)
+        perm, offs, start = sp.csr()
+        p2, o2 = b.csr()
+        assert np.array_equal(offs, o2) and np.array_equal(start, o2[:-1])
+        assert np.array_equal(perm, p2)
+    finally:
+        a.close()
+        b.close()
+        comm.destroy()

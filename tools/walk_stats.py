@@ -29,3 +29,6 @@ print(inf)
 print(f"lane eff {al / ws / 64:.3f}  wave steps/target-wave {ws / (n / 64):.0f}  "
       f"lane steps/target {al / n:.0f}  nodes/target {inf['node_interactions'] / n:.0f}  "
       f"pairs/target {inf['leaf_pairs'] / n:.0f}")
+lws, lal, dws = inf["leaf_wave_steps"], inf["leaf_active_lanes"], inf["descend_wave_steps"]
+print(f"leaf wave steps {lws / ws:.3f} of steps, leaf lane eff {lal / max(lws, 1) / 64:.3f}; "
+      f"node steps lane eff {(al - lal) / max(ws - lws, 1) / 64:.3f}; descending steps {dws / ws:.3f}")
