@@ -48,14 +48,15 @@ def main():
 
     root = Path(__file__).resolve().parent.parent / "profiles"
     src = str((out / "pmc_summary.csv").relative_to(root.parent))
-    d = pick("direct_kernel")
+    d = pick("sym_kernel") or pick("direct_kernel")  # the bench's all-particles kernel
     if d:
         r = d[0]
         (root / "pmc_direct_latest.json").write_text(json.dumps({
             "kernel": r["kernel"], "hbm_bytes_per_launch": r["read_bytes_corrected_avg"] + (r["write_bytes_avg"] or 0),
             "read_bytes_per_launch": r["read_bytes_corrected_avg"], "write_bytes_per_launch": r["write_bytes_avg"],
-            "note": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); sources are scalar loads, "
-                    "memory-side requests incl. Infinity-Cache hits", "source": src}, indent=1))
+            "note": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); memory-side requests "
+                    "incl. Infinity-Cache hits and the f64 accumulator atomics", "source": src},
+            indent=1))
     t = pick("walk_kernel<3, 3")
     if t:
         r = t[0]
