@@ -161,15 +161,25 @@ __global__ void __launch_bounds__(TPB)
   const int64_t tbase = (int64_t)blockIdx.x * TILE;
   const int64_t wbase = tbase + (int64_t)w * (TILE / NWAVE);
   K key[IPT];
-  // phase 1: per-wave digit counts
+  uint32_t lp[IPT];  // rank among this wave's earlier elements of the same digit
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {  // every load of the tile in flight first
+    const int64_t i = wbase + k * 64 + lane;
+    key[k] = i < n ? kin[i] : (K)0;
+  }
+  // phase 1: per-wave digit counts; each element keeps its wave-local rank
+  // (items in (k, lane) order = index order), so phase 2 needs no ballots
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
-    int64_t i = wbase + k * 64 + lane;
-    bool ok = i < n;
-    key[k] = ok ? kin[i] : (K)0;
-    uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
-    uint64_t m = peers8(d, __ballot(ok));
-    if (ok && rank_below(m) == 0) run[w][d] += (uint32_t)__popcll(m);
+    const int64_t i = wbase + k * 64 + lane;
+    const bool ok = i < n;
+    const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    const uint64_t m = peers8(d, __ballot(ok));
+    const uint32_t before = ok ? run[w][d] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    if (ok && rank_below(m) == 0) run[w][d] = before + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    lp[k] = before + rank_below(m);
   }
   __syncthreads();
   // tile-local digit starts, per-wave starts inside them, global run starts
@@ -193,17 +203,10 @@ __global__ void __launch_bounds__(TPB)
   // phase 2: tile-local positions -> LDS
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
-    int64_t i = wbase + k * 64 + lane;
-    bool ok = i < n;
-    uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
-    uint64_t m = peers8(d, __ballot(ok));
-    uint32_t r = rank_below(m);
-    uint32_t base = ok ? run[w][d] : 0u;
-    __builtin_amdgcn_wave_barrier();
-    if (ok && r == 0) run[w][d] = base + (uint32_t)__popcll(m);
-    __builtin_amdgcn_wave_barrier();
-    if (ok) {
-      const uint32_t pos = base + r;
+    const int64_t i = wbase + k * 64 + lane;
+    if (i < n) {
+      const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+      const uint32_t pos = run[w][d] + lp[k];
       sk[pos] = key[k];
       if (VM == VAL_IOTA) sv[pos] = (int32_t)i;
       if (VM == VAL_ARRAY) sv[pos] = vin[i];

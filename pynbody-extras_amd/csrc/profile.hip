@@ -24,6 +24,7 @@
 //     fixed-order reduction over tiles.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "prims.h"
@@ -72,37 +73,34 @@ __device__ __forceinline__ bool select_one(const double *__restrict__ pos, int64
   return keep;
 }
 
-__global__ void __launch_bounds__(TPB) select_count(const double *__restrict__ pos, int64_t n,
-                                                    SelectParams p, uint32_t *__restrict__ tile_cnt) {
-  __shared__ uint32_t wsum[NWAVE];
-  const int w = threadIdx.x >> 6;
-  const uint32_t lane = lane_id();
-  const int64_t wbase = (int64_t)blockIdx.x * TILE + (int64_t)w * (TILE / NWAVE);
-  uint32_t c = 0;
-#pragma unroll 4
-  for (int k = 0; k < IPT; ++k) {
-    int64_t i = wbase + k * 64 + lane;
-    double x;
-    bool keep = (i < n) && select_one(pos, i, p, x);
-    c += keep;
-  }
-  uint32_t tot;
-  block_excl_scan(c, wsum, &tot);
-  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
-}
+// One pass: mask + x of a tile, then the tile's output offset by a
+// decoupled look-back over its predecessors' published counts, then the
+// order-preserving write of x, weight and original index; also the key
+// min / max of the kept x (NaN-aware: NaN keys are the maximum key).
+// Tiles are numbered in the order blocks start (atomic ticket), so every
+// predecessor a block waits for is already running and publishes its
+// count before it looks back itself: the chain always drains.  The status
+// words are relaxed device-scope atomics: the counts they carry are the
+// only thing another block reads (a release would write back the XCD's
+// whole L2 — the tile outputs — per tile).  status[t]
+// = flag (bits 62-63: 1 count of tile t, 2 inclusive prefix through t) |
+// value; ctrl[0] = ticket, ctrl[1] = watchdog flag (bounded spin).
+constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 62) - 1;
 
-// writes the kept x, weight, original index in index order; also the key
-// min / max of the kept x (NaN-aware: NaN keys are the maximum key)
 __global__ void __launch_bounds__(TPB)
-    select_write(const double *__restrict__ pos, const double *__restrict__ mass, int64_t n,
-                 SelectParams p, const uint32_t *__restrict__ tile_off, double *__restrict__ xo,
-                 double *__restrict__ wo, int32_t *__restrict__ io,
-                 unsigned long long *__restrict__ minmax) {
+    select_onepass(const double *__restrict__ pos, const double *__restrict__ mass, int64_t n,
+                   SelectParams p, uint64_t *__restrict__ status, uint32_t *__restrict__ ctrl,
+                   double *__restrict__ xo, double *__restrict__ wo, int32_t *__restrict__ io,
+                   unsigned long long *__restrict__ minmax) {
   __shared__ uint32_t wcnt[NWAVE];
   __shared__ unsigned long long wmin[NWAVE], wmax[NWAVE];
+  __shared__ uint32_t s_tile, s_excl;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&ctrl[0], 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
-  const int64_t wbase = (int64_t)blockIdx.x * TILE + (int64_t)w * (TILE / NWAVE);
+  const int64_t wbase = (int64_t)tile * TILE + (int64_t)w * (TILE / NWAVE);
   double xv[IPT];
   uint32_t keepbits = 0, c = 0;
   unsigned long long kmin = ~0ull, kmax = 0ull;
@@ -111,15 +109,13 @@ __global__ void __launch_bounds__(TPB)
     int64_t i = wbase + k * 64 + lane;
     bool keep = (i < n) && select_one(pos, i, p, xv[k]);
     keepbits |= (uint32_t)keep << k;
-    uint64_t b = __ballot(keep);
-    c += (uint32_t)__popcll(b);
+    c += (uint32_t)__popcll(__ballot(keep));
     if (keep) {
       unsigned long long kk = dkey(xv[k]);
       kmin = kk < kmin ? kk : kmin;
       kmax = kk > kmax ? kk : kmax;
     }
   }
-  // wave min / max
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     unsigned long long a = __shfl_xor(kmin, o, 64);
@@ -133,17 +129,57 @@ __global__ void __launch_bounds__(TPB)
     wmax[w] = kmax;
   }
   __syncthreads();
-  uint32_t run = tile_off[blockIdx.x];
-  for (int ww = 0; ww < w; ++ww) run += wcnt[ww];
-  if (threadIdx.x == 0) {
+  if (w == 0) {  // wave 0: publish this tile's count, then look back 64 tiles at a time
+    uint32_t tot = 0;
     unsigned long long a = wmin[0], b = wmax[0];
-    for (int ww = 1; ww < NWAVE; ++ww) {
+    for (int ww = 0; ww < NWAVE; ++ww) {
+      tot += wcnt[ww];
       a = wmin[ww] < a ? wmin[ww] : a;
       b = wmax[ww] > b ? wmax[ww] : b;
     }
-    if (a != ~0ull) atomicMin(&minmax[0], a);
-    if (b != 0ull) atomicMax(&minmax[1], b);
+    if (lane == 0) {
+      if (a != ~0ull) atomicMin(&minmax[0], a);
+      if (b != 0ull) atomicMax(&minmax[1], b);
+      __hip_atomic_store(&status[tile], (tile == 0 ? kStPre : kStAgg) | (uint64_t)tot,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint64_t excl = 0;
+    uint32_t spins = 0;
+    // lane l inspects tile (hi - l): lane 0 is the nearest predecessor;
+    // tiles before 0 read as an inclusive prefix of 0
+    for (int64_t hi = (int64_t)tile - 1; tile != 0 && hi >= -1;) {
+      const int64_t q = hi - (int64_t)lane;
+      const uint64_t s = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                : kStPre;
+      const uint64_t pre = __ballot((s >> 62) == 2);
+      const uint64_t notready = __ballot((s >> 62) == 0);
+      const uint64_t need = pre ? (((pre & -pre) << 1) - 1) : ~0ull;  // lanes up to the nearest prefix
+      if (notready & need) {  // a predecessor is still counting
+        if (++spins > (1u << 24)) {
+          if (lane == 0) atomicOr(&ctrl[1], 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      uint64_t v = ((need >> lane) & 1ull) ? (s & kStVal) : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      excl += v;
+      if (pre) break;
+      hi -= 64;
+    }
+    if (lane == 0) {
+      if (tile != 0)
+        __hip_atomic_store(&status[tile], kStPre | (excl + tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_excl = (uint32_t)excl;
+    }
   }
+  __syncthreads();
+  uint32_t run = s_excl;
+  for (int ww = 0; ww < w; ++ww) run += wcnt[ww];
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     bool keep = (keepbits >> k) & 1u;
@@ -289,11 +325,12 @@ __global__ void __launch_bounds__(TPB)
 // levels >= 1: keys (from x on level 1, from the previous compact list
 // after) whose prefix is an active group add to that group's digit row and
 // are appended to the next compact list (when there is a next level).  Each
-// block owns a contiguous chunk and stages its members in LDS, so the shared
-// list counter sees one atomic per flush, not one per wave.
-constexpr int MS_U = 8;                  // elements per thread per iteration
+// block owns a contiguous chunk; every wave stages its own members in LDS
+// (positions from ballots, no LDS atomics, no block barriers) and flushes
+// them with one global atomic per ~512 members.
+constexpr int MS_U = 8;                        // elements per thread per iteration
 constexpr int MS_STEP = TPB * MS_U;
-constexpr int MS_STAGE = 2 * MS_STEP;    // staged members before a flush
+constexpr int MS_WSTAGE = 64 * MS_U + 128;     // staged members per wave (flush above 128)
 
 template <bool FROM_X>
 __global__ void __launch_bounds__(TPB)
@@ -302,91 +339,101 @@ __global__ void __launch_bounds__(TPB)
                 const uint64_t *__restrict__ groups, const int32_t *__restrict__ ng_ptr,
                 uint32_t *__restrict__ H, uint64_t *__restrict__ out,
                 uint32_t *__restrict__ out_cnt) {
-  __shared__ uint64_t gs[MS_MAXQ];
-  __shared__ uint32_t bm[MS0_DIG / 32];  // level 1: the chosen level-0 digits
-  __shared__ uint64_t stage[MS_STAGE];
-  __shared__ uint32_t scnt, sbase;
+  __shared__ uint64_t gs[FROM_X ? 1 : MS_MAXQ];
+  // level 1: group index of every level-0 digit (0xffff: no rank chose it)
+  __shared__ uint16_t gidx[FROM_X ? MS0_DIG : 1];
+  __shared__ uint64_t stage[NWAVE][MS_WSTAGE];
   const int ng = *ng_ptr;
-  for (int i = threadIdx.x; i < ng; i += TPB) gs[i] = groups[i];
-  if (threadIdx.x == 0) scnt = 0;
   if (FROM_X) {
-    for (int i = threadIdx.x; i < MS0_DIG / 32; i += TPB) bm[i] = 0;
+    for (int i = threadIdx.x; i < MS0_DIG / 2; i += TPB) ((uint32_t *)gidx)[i] = ~0u;
     __syncthreads();
-    for (int i = threadIdx.x; i < ng; i += TPB)
-      atomicOr(&bm[(uint32_t)gs[i] >> 5], 1u << ((uint32_t)gs[i] & 31));
+    for (int i = threadIdx.x; i < ng; i += TPB) gidx[(uint32_t)groups[i]] = (uint16_t)i;
+  } else {
+    for (int i = threadIdx.x; i < ng; i += TPB) gs[i] = groups[i];
   }
   __syncthreads();
   const int64_t cnt = FROM_X ? n : (int64_t)*in_cnt;
-  const int64_t chunk = (cnt + (int64_t)gridDim.x * MS_STEP - 1) / ((int64_t)gridDim.x * MS_STEP) * MS_STEP;
-  const int64_t beg = (int64_t)blockIdx.x * chunk, end = std::min<int64_t>(cnt, beg + chunk);
+  // grid-stride steps: at any time the resident blocks sweep one contiguous
+  // window of the input (a chunk per block left ~700 concurrent streams and
+  // ran at a quarter of the read bandwidth)
+  const int64_t beg = (int64_t)blockIdx.x * MS_STEP, end = cnt;
+  const int64_t stride = (int64_t)gridDim.x * MS_STEP;
   const uint64_t dmask = (1ull << w) - 1;
   const uint32_t lane = lane_id();
-  for (int64_t it = beg; it < end; it += MS_STEP) {
-    uint64_t raw[MS_U];  // all loads of the step first, then the work
+  uint64_t *wst = stage[threadIdx.x >> 6];
+  uint32_t wcount = 0;  // wave-uniform
+  auto flush = [&]() {
+    uint32_t wb = 0;
+    if (lane == 0) wb = atomicAdd(out_cnt, wcount);
+    wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wb);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t j = lane; j < wcount; j += 64) out[wb + j] = wst[j];
+    __builtin_amdgcn_wave_barrier();
+    wcount = 0;
+  };
+  // software-pipelined: the next step's loads are in flight while this
+  // step's keys are processed (memory parallelism at 3 waves / SIMD)
+  auto load_step = [&](int64_t it, uint64_t (&r)[MS_U]) {
+#pragma unroll
+    for (int u = 0; u < MS_U; ++u) {
+      const int64_t i = it + u * TPB + threadIdx.x;
+      r[u] = i < end ? (FROM_X ? __builtin_bit_cast(uint64_t, x[i]) : in[i]) : 0ull;
+    }
+  };
+  uint64_t nxt[MS_U];
+  load_step(beg, nxt);
+  for (int64_t it = beg; it < end; it += stride) {
+    uint64_t raw[MS_U];
     uint32_t hidx[MS_U];
 #pragma unroll
-    for (int u = 0; u < MS_U; ++u) {
-      const int64_t i = it + u * TPB + threadIdx.x;
-      raw[u] = i < end ? (FROM_X ? __builtin_bit_cast(uint64_t, x[i]) : in[i]) : 0ull;
-    }
+    for (int u = 0; u < MS_U; ++u) raw[u] = nxt[u];
+    load_step(it + stride, nxt);
+    // phase 1: every key's group (all LDS lookups of the step in flight
+    // together); phase 2: ballots, staging, histogram slots
+    int ga[MS_U];
+    uint64_t offs[MS_U];
 #pragma unroll
     for (int u = 0; u < MS_U; ++u) {
       const int64_t i = it + u * TPB + threadIdx.x;
-      bool mem = false;
+      int a = 0xffff;
       uint64_t off = 0;
-      int a = 0;
       if (i < end) {
-        if (FROM_X) {
+        if (FROM_X) {  // one LDS lookup: no per-key search on the full pass
           const uint64_t k = dkey(__builtin_bit_cast(double, raw[u]));
-          if (k >= ka && k <= kb) {
-            off = k - base;
-            const uint32_t p = (uint32_t)(off >> (s + w));
-            mem = (bm[p >> 5] >> (p & 31)) & 1u;
-          }
-        } else {
+          off = k - base;
+          if (k >= ka && k <= kb) a = gidx[(uint32_t)(off >> (s + w))];
+        } else {  // compact list (few keys): search the sorted active groups
           off = raw[u];
-          mem = true;
-        }
-        if (mem) {
           const uint64_t pref = off >> (s + w);
-          int b = ng;
-          while (a < b) {
-            const int mid = (a + b) >> 1;
-            if (gs[mid] < pref) a = mid + 1; else b = mid;
+          int lo = 0, b = ng;
+          while (lo < b) {
+            const int mid = (lo + b) >> 1;
+            if (gs[mid] < pref) lo = mid + 1; else b = mid;
           }
-          mem = a < ng && gs[a] == pref;
+          if (lo < ng && gs[lo] == pref) a = lo;
         }
       }
-      // histogram slot; the global atomics are issued after the step's LDS
-      // work (interleaved, each one would stall on the next VGPR reuse)
-      hidx[u] = mem ? (uint32_t)a * MS_DIG + (uint32_t)((off >> s) & dmask) : ~0u;
-      if (out) {  // wave-aggregated append into the LDS stage
+      ga[u] = a;
+      offs[u] = off;
+    }
+#pragma unroll
+    for (int u = 0; u < MS_U; ++u) {
+      const bool mem = ga[u] != 0xffff;
+      hidx[u] = mem ? (uint32_t)ga[u] * MS_DIG + (uint32_t)((offs[u] >> s) & dmask) : ~0u;
+      if (out) {
         const uint64_t bal = __ballot(mem);
-        if (bal) {
-          const uint32_t leader = (uint32_t)__builtin_ctzll(bal);
-          uint32_t wb = 0;
-          if (lane == leader) wb = atomicAdd(&scnt, (uint32_t)__builtin_popcountll(bal));
-          wb = __shfl(wb, (int)leader, 64);
-          if (mem) stage[wb + rank_below(bal)] = off;
-        }
+        if (mem) wst[wcount + rank_below(bal)] = offs[u];
+        wcount += (uint32_t)__popcll(bal);
       }
     }
+#ifndef PBX_DIAG_NO_HATOMIC
 #pragma unroll
     for (int u = 0; u < MS_U; ++u)
       if (hidx[u] != ~0u) atomicAdd(&H[hidx[u]], 1u);
-    if (out) {
-      __syncthreads();
-      const uint32_t c = scnt;
-      if (c > (uint32_t)(MS_STAGE - MS_STEP) || it + MS_STEP >= end) {  // block-uniform
-        if (threadIdx.x == 0 && c) sbase = atomicAdd(out_cnt, c);
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < c; j += TPB) out[sbase + j] = stage[j];
-        __syncthreads();
-        if (threadIdx.x == 0) scnt = 0;
-      }
-      __syncthreads();  // every thread has read scnt before it changes again
-    }
+#endif
+    if (out && wcount > (uint32_t)(MS_WSTAGE - 64 * MS_U)) flush();
   }
+  if (out && wcount) flush();
 }
 
 // one block per active group: prefix sums of its DIG-bin histogram (the row
@@ -498,7 +545,8 @@ __global__ void msel_edges(const MsRank *__restrict__ R, int nq, uint64_t base,
 // ----------------------------------------------------------------- assign
 // bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
 // x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379)
-__device__ __forceinline__ uint32_t bin_of(double v, const double *e, int nb) {
+template <typename E>
+__device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
   int lo = 0, hi = nb + 1;  // first k with e[k] >= v  (NaN: never -> nb+1)
   while (lo < hi) {
     int mid = (lo + hi) >> 1;
@@ -511,61 +559,96 @@ __device__ __forceinline__ uint32_t bin_of(double v, const double *e, int nb) {
   return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
 }
 
-// per-tile bin counts double as the CSR's radix histogram ([digit][tile],
-// one 8-bit pass) when nb < RADIX: tile_hist is then written, else null
+// One block takes AS_TILES consecutive 4096-element tiles.  Per-tile bin
+// counts double as the CSR pass's radix histogram ([digit][tile], one
+// 8-bit pass) when nb < RADIX: tile_hist is then written, 8 consecutive
+// tiles per digit row at once (one 32-B segment instead of 8 scattered
+// words); else tile_hist is null.  Block totals go to `counts` with one
+// contiguous atomic per bin.
+constexpr int AS_TILES = 8;
+
 __global__ void __launch_bounds__(TPB)
     assign_bins(const double *__restrict__ x, int64_t n, const double *__restrict__ edges, int nb,
                 uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts,
                 uint32_t *__restrict__ tile_hist, uint32_t ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t th[AS_TILES][RADIX];
   double *e = (double *)smem;
   const bool lds_edges = (nb + 1) <= LDS_EDGES;
   uint32_t *cnt = (uint32_t *)(smem + (lds_edges ? sizeof(double) * (nb + 1) : 0));
   if (lds_edges)
     for (int k = threadIdx.x; k <= nb; k += TPB) e[k] = edges[k];
   for (int k = threadIdx.x; k <= nb; k += TPB) cnt[k] = 0;
+  for (int k = threadIdx.x; k < AS_TILES * RADIX; k += TPB) (&th[0][0])[k] = 0;
   __syncthreads();
-  const double *ee = lds_edges ? e : edges;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
-  double v[IPT];  // every load of the tile in flight first
+  const uint32_t t0 = blockIdx.x * AS_TILES;
+  const uint32_t t1 = min(ntiles, t0 + AS_TILES);
+  // software-pipelined: the next tile's loads fly while this one is binned
+  double nv[IPT];
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
-    const int64_t i = base + k * TPB + threadIdx.x;
-    v[k] = i < n ? x[i] : 0.0;
+    const int64_t i = (int64_t)t0 * TILE + k * TPB + threadIdx.x;
+    nv[k] = (t0 < t1 && i < n) ? x[i] : 0.0;
   }
-  uint32_t b[IPT];
+  for (uint32_t t = t0; t < t1; ++t) {
+    const int64_t base = (int64_t)t * TILE;
+    double v[IPT];
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int64_t i = base + k * TPB + threadIdx.x;
-    b[k] = bin_of(v[k], ee, nb);
-    if (i < n) atomicAdd(&cnt[b[k]], 1u);
-  }
+    for (int k = 0; k < IPT; ++k) {
+      v[k] = nv[k];
+      const int64_t i = base + TILE + k * TPB + threadIdx.x;
+      nv[k] = (t + 1 < t1 && i < n) ? x[i] : 0.0;
+    }
+    uint32_t b[IPT];  // the searches of all 16 keys interleave; LDS atomics after
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int64_t i = base + k * TPB + threadIdx.x;
-    if (i < n) bins[i] = b[k];
+    for (int k = 0; k < IPT; ++k)  // (two uniform paths: a pointer that may be
+      b[k] = lds_edges ? bin_of(v[k], e, nb) : bin_of(v[k], edges, nb);  // either is flat)
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int64_t i = base + k * TPB + threadIdx.x;
+      if (i < n) atomicAdd(tile_hist ? &th[t - t0][b[k]] : &cnt[b[k]], 1u);
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int64_t i = base + k * TPB + threadIdx.x;
+      if (i < n) bins[i] = b[k];
+    }
   }
   __syncthreads();
+  if (tile_hist) {  // TPB == RADIX > nb: thread d owns digit d
+    const int d = threadIdx.x;
+    uint32_t tot = 0;
+    for (uint32_t t = t0; t < t1; ++t) {
+      const uint32_t c = th[t - t0][d];
+      tile_hist[(int64_t)d * ntiles + t] = c;
+      tot += c;
+    }
+    if (d <= nb) cnt[d] = tot;
+    __syncthreads();
+  }
   for (int k = threadIdx.x; k < nb; k += TPB)
     if (cnt[k]) atomicAdd(&counts[k], (unsigned long long)cnt[k]);
-  if (tile_hist)  // TPB == RADIX > nb
-    tile_hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = threadIdx.x <= nb ? cnt[threadIdx.x] : 0u;
 }
 
 // ----------------------------------------------------------------- moments
-template <int WMODE>  // 0: no weights, 1: weights
+// LDS: accumulators in LDS (nb <= LDS_MOM_BINS), one slab row per block;
+// else straight to global_acc.  Templated so the LDS path indexes the
+// __shared__ array itself (ds_add_f64): through a pointer that may be either,
+// every atomic would be a flat atomic.
+template <int WMODE, bool LDS>  // WMODE 0: no weights, 1: weights
 __global__ void __launch_bounds__(TPB)
     moments_kernel(const uint32_t *__restrict__ bins, const double *__restrict__ f,
                    const double *__restrict__ wt, int64_t n, int nb, double *__restrict__ slab,
                    double *__restrict__ global_acc) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double *acc = (double *)smem;
-  const bool in_lds = nb <= LDS_MOM_BINS;
-  if (in_lds) {
-    for (int k = threadIdx.x; k < nb * NMOM; k += TPB) acc[k] = 0.0;
+  extern __shared__ double acc_lds[];
+  if (LDS) {
+    for (int k = threadIdx.x; k < nb * NMOM; k += TPB) acc_lds[k] = 0.0;
     __syncthreads();
   }
-  double *tgt = in_lds ? acc : global_acc;
+  auto add = [&](int64_t idx, double v) {
+    if (LDS) atomicAdd(&acc_lds[idx], v);
+    else atomicAdd(&global_acc[idx], v);
+  };
   // grid-stride over tiles: at most gridDim.x slabs to reduce afterwards
   for (int64_t base = (int64_t)blockIdx.x * TILE; base < n; base += (int64_t)gridDim.x * TILE) {
     uint32_t bv[IPT];  // the tile's loads first, then the LDS accumulation
@@ -582,22 +665,22 @@ __global__ void __launch_bounds__(TPB)
     for (int k = 0; k < IPT; ++k) {
       if (bv[k] >= (uint32_t)nb) continue;
       const double v = fv[k], a = __builtin_fabs(v), ww = wv[k];
-      double *t = tgt + (int64_t)bv[k] * NMOM;
+      const int64_t t = (int64_t)bv[k] * NMOM;
       if (WMODE) {
-        atomicAdd(&t[0], ww);
-        atomicAdd(&t[1], v * ww);
-        atomicAdd(&t[2], (v * v) * ww);
-        atomicAdd(&t[5], a * ww);
+        add(t + 0, ww);
+        add(t + 1, v * ww);
+        add(t + 2, (v * v) * ww);
+        add(t + 5, a * ww);
       }
-      atomicAdd(&t[3], v);
-      atomicAdd(&t[4], v * v);
-      atomicAdd(&t[6], a);
+      add(t + 3, v);
+      add(t + 4, v * v);
+      add(t + 6, a);
     }
   }
-  if (in_lds) {
+  if (LDS) {
     __syncthreads();
     double *dst = slab + (int64_t)blockIdx.x * nb * NMOM;
-    for (int k = threadIdx.x; k < nb * NMOM; k += TPB) dst[k] = acc[k];
+    for (int k = threadIdx.x; k < nb * NMOM; k += TPB) dst[k] = acc_lds[k];
   }
 }
 
@@ -659,7 +742,7 @@ struct Profile {
   bool mm_valid = false;   // mm = min / max key of x, cached on the host
   uint64_t mm[2] = {0, 0};
   MselState ms;
-  Buf msH, msR, msG, msNg, msM, msRows, msL0, msL1, msCnt, csrh, slabp;
+  Buf msH, msR, msG, msNg, msM, msRows, msL0, msL1, msCnt, csrh, slabp, selst;
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
 };
@@ -888,7 +971,7 @@ int pbx_profile_destroy(void *handle) {
     Buf *all[] = {&p->x, &p->w, &p->idx, &p->bins, &p->perm, &p->keys0, &p->keys1, &p->vtmp,
                   &p->hist, &p->tsum, &p->edges, &p->counts, &p->minmax, &p->slab, &p->acc,
                   &p->field, &p->weight, &p->ranks, &p->bounds, &p->msH, &p->msR, &p->msG,
-                  &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp};
+                  &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst};
     for (Buf *b : all) b->release();
     delete p;
   });
@@ -951,9 +1034,9 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
       }
     }
     uint32_t nt = ntiles_of(n);
-    // tile counts live in the (idle) radix histogram buffer; scan_u32 uses
-    // P.tsum as its own scratch
-    uint32_t *tc = (uint32_t *)P.hist.get(sizeof(uint32_t) * (size_t)(nt + 1));
+    // per-tile look-back status words + ticket / watchdog (selection scratch)
+    uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * ((size_t)nt + 2));
+    uint32_t *ctrl = (uint32_t *)(stat + nt);
     double *xo = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
     double *wo = (double *)P.w.get(sizeof(double) * (size_t)(n ? n : 1));
     int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(n ? n : 1));
@@ -962,21 +1045,19 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
     PBX_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, st));
     int64_t kept = 0;
     if (n) {
-      // tile counts -> exclusive scan (tile offsets) -> order-preserving write
-      hipLaunchKernelGGL(select_count, dim3(nt), dim3(TPB), 0, st, d_pos, n, sp, tc);
+      PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * ((size_t)nt + 2), st));
+      hipLaunchKernelGGL(select_onepass, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, stat,
+                         ctrl, xo, wo, io, mm);
       PBX_HIP(hipGetLastError());
-      uint32_t last = 0;
-      PBX_HIP(hipMemcpyAsync(&last, tc + nt - 1, 4, hipMemcpyDeviceToHost, st));
-      scan_u32(P, st, tc, nt);
-      uint32_t off_last = 0;
-      PBX_HIP(hipMemcpyAsync(&off_last, tc + nt - 1, 4, hipMemcpyDeviceToHost, st));
-      hipLaunchKernelGGL(select_write, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, tc, xo,
-                         wo, io, mm);
-      PBX_HIP(hipGetLastError());
+      uint64_t last = 0;
+      uint32_t hctrl[2] = {0, 0};
       unsigned long long hm[2];
+      PBX_HIP(hipMemcpyAsync(&last, stat + nt - 1, 8, hipMemcpyDeviceToHost, st));
+      PBX_HIP(hipMemcpyAsync(hctrl, ctrl, 8, hipMemcpyDeviceToHost, st));
       PBX_HIP(hipMemcpyAsync(hm, mm, 16, hipMemcpyDeviceToHost, st));
       PBX_HIP(hipStreamSynchronize(st));
-      kept = (int64_t)off_last + last;
+      if (hctrl[1] || (last >> 62) != 2) fail(PBX_ERR_RUNTIME, "selection look-back did not complete");
+      kept = (int64_t)(last & kStVal);
       P.mm[0] = hm[0];
       P.mm[1] = hm[1];
     }
@@ -1183,7 +1264,8 @@ int pbx_profile_assign(void *handle, const double *h_edges, int64_t n_edges, int
       const uint32_t nt = ntiles_of(n);
       uint32_t *th = (nb < RADIX) ? (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX)
                                   : nullptr;
-      hipLaunchKernelGGL(assign_bins, dim3(nt), dim3(TPB), lds, st, (const double *)P.x.p, n,
+      hipLaunchKernelGGL(assign_bins, dim3(ceil_div(nt, AS_TILES)), dim3(TPB), lds, st,
+                         (const double *)P.x.p, n,
                          (const double *)de, (int)nb, bins, cnt, th, nt);
       P.csrh_ready = th != nullptr;
       PBX_HIP(hipGetLastError());
@@ -1307,12 +1389,17 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, c
       const bool in_lds = nb <= LDS_MOM_BINS;
       double *slab = in_lds ? (double *)P.slab.get(sizeof(double) * (size_t)nt * len) : nullptr;
       size_t lds = in_lds ? sizeof(double) * (size_t)len : 0;
-      if (w)
-        hipLaunchKernelGGL(moments_kernel<1>, dim3(nt), dim3(TPB), lds, st,
-                           (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab, acc);
-      else
-        hipLaunchKernelGGL(moments_kernel<0>, dim3(nt), dim3(TPB), lds, st,
-                           (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab, acc);
+      auto launch = [&](auto wm, auto lds_t) {
+        hipLaunchKernelGGL((moments_kernel<decltype(wm)::value, decltype(lds_t)::value>), dim3(nt),
+                           dim3(TPB), lds, st, (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab,
+                           acc);
+      };
+      using W1 = std::integral_constant<int, 1>;
+      using W0 = std::integral_constant<int, 0>;
+      if (w && in_lds) launch(W1{}, std::true_type{});
+      else if (w) launch(W1{}, std::false_type{});
+      else if (in_lds) launch(W0{}, std::true_type{});
+      else launch(W0{}, std::false_type{});
       PBX_HIP(hipGetLastError());
       if (in_lds) {
         double *part = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * len);

@@ -887,6 +887,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       if (lane0) atomicOr(wp.fault, 1u);
       break;
     }
+    w = __builtin_amdgcn_readfirstlane(w);  // uniform: keep it (and the address math) scalar
     u32x16 c[NCH];
     load_chunks<NCH>(wp.walk + (int64_t)w * RS, c);
     const double mass = chunk_d(c[0], 3);
