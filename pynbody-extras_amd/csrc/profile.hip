@@ -322,27 +322,25 @@ __global__ void __launch_bounds__(TPB)
   if (s) atomicAdd(&H[d], s);
 }
 
-// levels >= 1: keys (from x on level 1, from the previous compact list
-// after) whose prefix is an active group add to that group's digit row and
-// are appended to the next compact list (when there is a next level).  Each
-// block owns a contiguous chunk; every wave stages its own members in LDS
-// (positions from ballots, no LDS atomics, no block barriers) and flushes
-// them with one global atomic per ~512 members.
-constexpr int MS_U = 8;                        // elements per thread per iteration
+// levels >= 1: keys whose prefix is an active group add to that group's
+// digit row and are kept for the next level (when there is one).  Every
+// wave owns a fixed region of the key list (cap keys) and keeps its members
+// there, compacted in place from level to level, with its count in
+// wcnt[wave]: no shared counter at all (one global counter took ~20k
+// same-address atomics and serialised the pass).  Level 1 reads x
+// grid-stride; later levels read each wave's own region.
+constexpr int MS_U = 8;  // keys per lane per step
 constexpr int MS_STEP = TPB * MS_U;
-constexpr int MS_WSTAGE = 64 * MS_U + 128;     // staged members per wave (flush above 128)
 
 template <bool FROM_X>
 __global__ void __launch_bounds__(TPB)
     msel_filter(const double *__restrict__ x, int64_t n, uint64_t ka, uint64_t kb, uint64_t base,
-                const uint64_t *__restrict__ in, const uint32_t *__restrict__ in_cnt, int s, int w,
+                uint64_t *list, const uint32_t *__restrict__ wcnt_in, int64_t cap, int s, int w,
                 const uint64_t *__restrict__ groups, const int32_t *__restrict__ ng_ptr,
-                uint32_t *__restrict__ H, uint64_t *__restrict__ out,
-                uint32_t *__restrict__ out_cnt) {
+                uint32_t *__restrict__ H, int keep, uint32_t *__restrict__ wcnt_out) {
   __shared__ uint64_t gs[FROM_X ? 1 : MS_MAXQ];
   // level 1: group index of every level-0 digit (0xffff: no rank chose it)
   __shared__ uint16_t gidx[FROM_X ? MS0_DIG : 1];
-  __shared__ uint64_t stage[NWAVE][MS_WSTAGE];
   const int ng = *ng_ptr;
   if (FROM_X) {
     for (int i = threadIdx.x; i < MS0_DIG / 2; i += TPB) ((uint32_t *)gidx)[i] = ~0u;
@@ -352,32 +350,26 @@ __global__ void __launch_bounds__(TPB)
     for (int i = threadIdx.x; i < ng; i += TPB) gs[i] = groups[i];
   }
   __syncthreads();
-  const int64_t cnt = FROM_X ? n : (int64_t)*in_cnt;
-  // grid-stride steps: at any time the resident blocks sweep one contiguous
-  // window of the input (a chunk per block left ~700 concurrent streams and
-  // ran at a quarter of the read bandwidth)
-  const int64_t beg = (int64_t)blockIdx.x * MS_STEP, end = cnt;
-  const int64_t stride = (int64_t)gridDim.x * MS_STEP;
-  const uint64_t dmask = (1ull << w) - 1;
   const uint32_t lane = lane_id();
-  uint64_t *wst = stage[threadIdx.x >> 6];
+  const int64_t wave = (int64_t)blockIdx.x * NWAVE + (threadIdx.x >> 6);
+  uint64_t *region = list + wave * cap;
+  // level 1: x[it + u*TPB + threadIdx.x] for it = blockIdx*MS_STEP + k*stride;
+  // later: region[it + u*64 + lane] for it = 0, 512, ... < wcnt_in[wave]
+  const int64_t beg = FROM_X ? (int64_t)blockIdx.x * MS_STEP : 0;
+  const int64_t end = FROM_X ? n : (int64_t)wcnt_in[wave];
+  const int64_t stride = FROM_X ? (int64_t)gridDim.x * MS_STEP : 64 * MS_U;
+  const uint64_t dmask = (1ull << w) - 1;
   uint32_t wcount = 0;  // wave-uniform
-  auto flush = [&]() {
-    uint32_t wb = 0;
-    if (lane == 0) wb = atomicAdd(out_cnt, wcount);
-    wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wb);
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t j = lane; j < wcount; j += 64) out[wb + j] = wst[j];
-    __builtin_amdgcn_wave_barrier();
-    wcount = 0;
+  auto idx_of = [&](int64_t it, int u) -> int64_t {
+    return FROM_X ? it + u * TPB + threadIdx.x : it + u * 64 + lane;
   };
   // software-pipelined: the next step's loads are in flight while this
-  // step's keys are processed (memory parallelism at 3 waves / SIMD)
+  // step's keys are processed
   auto load_step = [&](int64_t it, uint64_t (&r)[MS_U]) {
 #pragma unroll
     for (int u = 0; u < MS_U; ++u) {
-      const int64_t i = it + u * TPB + threadIdx.x;
-      r[u] = i < end ? (FROM_X ? __builtin_bit_cast(uint64_t, x[i]) : in[i]) : 0ull;
+      const int64_t i = idx_of(it, u);
+      r[u] = i < end ? (FROM_X ? __builtin_bit_cast(uint64_t, x[i]) : region[i]) : 0ull;
     }
   };
   uint64_t nxt[MS_U];
@@ -389,12 +381,12 @@ __global__ void __launch_bounds__(TPB)
     for (int u = 0; u < MS_U; ++u) raw[u] = nxt[u];
     load_step(it + stride, nxt);
     // phase 1: every key's group (all LDS lookups of the step in flight
-    // together); phase 2: ballots, staging, histogram slots
+    // together); phase 2: ballots, the kept keys, histogram slots
     int ga[MS_U];
     uint64_t offs[MS_U];
 #pragma unroll
     for (int u = 0; u < MS_U; ++u) {
-      const int64_t i = it + u * TPB + threadIdx.x;
+      const int64_t i = idx_of(it, u);
       int a = 0xffff;
       uint64_t off = 0;
       if (i < end) {
@@ -402,7 +394,7 @@ __global__ void __launch_bounds__(TPB)
           const uint64_t k = dkey(__builtin_bit_cast(double, raw[u]));
           off = k - base;
           if (k >= ka && k <= kb) a = gidx[(uint32_t)(off >> (s + w))];
-        } else {  // compact list (few keys): search the sorted active groups
+        } else {  // few keys: search the sorted active groups
           off = raw[u];
           const uint64_t pref = off >> (s + w);
           int lo = 0, b = ng;
@@ -416,24 +408,22 @@ __global__ void __launch_bounds__(TPB)
       ga[u] = a;
       offs[u] = off;
     }
+    // (in place is safe: keys kept so far sit below every key already read)
 #pragma unroll
     for (int u = 0; u < MS_U; ++u) {
       const bool mem = ga[u] != 0xffff;
       hidx[u] = mem ? (uint32_t)ga[u] * MS_DIG + (uint32_t)((offs[u] >> s) & dmask) : ~0u;
-      if (out) {
+      if (keep) {
         const uint64_t bal = __ballot(mem);
-        if (mem) wst[wcount + rank_below(bal)] = offs[u];
+        if (mem) region[wcount + rank_below(bal)] = offs[u];
         wcount += (uint32_t)__popcll(bal);
       }
     }
-#ifndef PBX_DIAG_NO_HATOMIC
 #pragma unroll
     for (int u = 0; u < MS_U; ++u)
       if (hidx[u] != ~0u) atomicAdd(&H[hidx[u]], 1u);
-#endif
-    if (out && wcount > (uint32_t)(MS_WSTAGE - 64 * MS_U)) flush();
   }
-  if (out && wcount) flush();
+  if (keep && lane == 0) wcnt_out[wave] = wcount;
 }
 
 // one block per active group: prefix sums of its DIG-bin histogram (the row
@@ -856,12 +846,10 @@ static int64_t msel_hist(Profile &P, hipStream_t st, int level) {
   uint32_t *H = (uint32_t *)P.msH.get(msel_hbytes(S));
   uint64_t *G = (uint64_t *)P.msG.get(sizeof(uint64_t) * (size_t)nq);
   int32_t *ng = (int32_t *)P.msNg.get(16);
-  uint32_t *cnt = (uint32_t *)P.msCnt.get(sizeof(uint32_t) * MS_MAXL);
   int s = S.B;
   for (int l = 0; l <= level; ++l) s -= S.wd[l];
   if (level == 0) {
     PBX_HIP(hipMemsetAsync(H, 0, msel_hbytes(S), st));
-    PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * MS_MAXL, st));
     const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
     uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
     if (n) {
@@ -872,18 +860,22 @@ static int64_t msel_hist(Profile &P, hipStream_t st, int level) {
     PBX_HIP(hipGetLastError());
     return MS0_DIG;
   }
-  uint64_t *list[2] = {nullptr, nullptr};
-  if (S.L > 1) list[0] = (uint64_t *)P.msL0.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
-  if (S.L > 2) list[1] = (uint64_t *)P.msL1.get(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
-  uint64_t *out = (level + 1 < S.L) ? list[(level - 1) & 1] : nullptr;
+  // per-wave key regions (msel_filter): the level-1 grid-stride pass gives
+  // each wave at most steps * 64 * MS_U keys
+  const int64_t steps = (n + (int64_t)grid * MS_STEP - 1) / ((int64_t)grid * MS_STEP);
+  const int64_t cap = std::max<int64_t>(1, steps) * 64 * MS_U;
+  const int64_t nw = (int64_t)grid * NWAVE;
+  uint64_t *list = (uint64_t *)P.msL0.get(sizeof(uint64_t) * (size_t)(nw * cap));
+  uint32_t *wc = (uint32_t *)P.msL1.get(sizeof(uint32_t) * (size_t)(nw * MS_MAXL));
+  const int keep = level + 1 < S.L ? 1 : 0;
   if (level == 1)
     hipLaunchKernelGGL(msel_filter<true>, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n,
-                       S.ka, S.kb, S.lo, (const uint64_t *)nullptr, (const uint32_t *)nullptr, s,
-                       S.wd[level], G, ng, H, out, cnt + level);
+                       S.ka, S.kb, S.lo, list, (const uint32_t *)nullptr, cap, s, S.wd[level], G,
+                       ng, H, keep, wc + nw * level);
   else
     hipLaunchKernelGGL(msel_filter<false>, dim3(grid), dim3(TPB), 0, st, (const double *)nullptr,
-                       n, S.ka, S.kb, S.lo, (const uint64_t *)list[level & 1], cnt + level - 1, s,
-                       S.wd[level], G, ng, H, out, cnt + level);
+                       n, S.ka, S.kb, S.lo, list, (const uint32_t *)(wc + nw * (level - 1)), cap,
+                       s, S.wd[level], G, ng, H, keep, wc + nw * level);
   PBX_HIP(hipGetLastError());
   return (int64_t)nq * MS_DIG;
 }
