@@ -176,8 +176,10 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
             edges = sp.edges_equaln(128)
             sp.assign(edges)
             dev.build_csr_on_device()
-            msum = sp.moments(SRC_W, SRC_NONE)[:, 3]
-            rmean = sp.moments(SRC_X, SRC_W)
+            # the columns these two statistics read (proarray Sum: Σf; weighted
+            # Mean: Σw, Σf·w) — what pynbodyext.profiles requests for them
+            msum = sp.moments(SRC_W, SRC_NONE, cols=1 << 3)[:, 3]
+            rmean = sp.moments(SRC_X, SRC_W, cols=(1 << 0) | (1 << 1))
             return edges, msum, rmean
 
         for _ in range(warmup):

@@ -279,6 +279,11 @@ int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets);
  * HBM by pbx_octree_compute); w_src = -1: unweighted */
 int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src,
                         const double *h_w, double *h_out);
+/* the same for the columns whose bit is set in cols (bit k = column k of
+ * h_out; the others are 0): each statistic reads only some of the sums
+ * (proarray.py:632-860 — Sum: Σf; weighted Mean: Σw, Σf·w; ...) */
+int pbx_profile_moments_cols(void *handle, int f_src, const double *h_f, int w_src,
+                             const double *h_w, uint32_t cols, double *h_out);
 
 /* ------------------------------------------------------------------ */
 /* multi-GPU: RCCL communicator (one process per GPU, over xGMI)       */

@@ -95,7 +95,11 @@ __global__ void __launch_bounds__(TPB)
   __shared__ uint32_t wcnt[NWAVE];
   __shared__ unsigned long long wmin[NWAVE], wmax[NWAVE];
   __shared__ uint32_t s_tile, s_excl;
+#ifdef PBX_DIAG_NO_TICKET
+  if (threadIdx.x == 0) s_tile = blockIdx.x;
+#else
   if (threadIdx.x == 0) s_tile = atomicAdd(&ctrl[0], 1u);
+#endif
   __syncthreads();
   const uint32_t tile = s_tile;
   const int w = threadIdx.x >> 6;
@@ -628,8 +632,8 @@ __global__ void __launch_bounds__(TPB)
 template <int WMODE, bool LDS>  // WMODE 0: no weights, 1: weights
 __global__ void __launch_bounds__(TPB)
     moments_kernel(const uint32_t *__restrict__ bins, const double *__restrict__ f,
-                   const double *__restrict__ wt, int64_t n, int nb, double *__restrict__ slab,
-                   double *__restrict__ global_acc) {
+                   const double *__restrict__ wt, int64_t n, int nb, uint32_t cols,
+                   double *__restrict__ slab, double *__restrict__ global_acc) {
   extern __shared__ double acc_lds[];
   if (LDS) {
     for (int k = threadIdx.x; k < nb * NMOM; k += TPB) acc_lds[k] = 0.0;
@@ -656,15 +660,16 @@ __global__ void __launch_bounds__(TPB)
       if (bv[k] >= (uint32_t)nb) continue;
       const double v = fv[k], a = __builtin_fabs(v), ww = wv[k];
       const int64_t t = (int64_t)bv[k] * NMOM;
+      // only the requested columns (cols is uniform: scalar branches)
       if (WMODE) {
-        add(t + 0, ww);
-        add(t + 1, v * ww);
-        add(t + 2, (v * v) * ww);
-        add(t + 5, a * ww);
+        if (cols & 1u) add(t + 0, ww);
+        if (cols & 2u) add(t + 1, v * ww);
+        if (cols & 4u) add(t + 2, (v * v) * ww);
+        if (cols & 32u) add(t + 5, a * ww);
       }
-      add(t + 3, v);
-      add(t + 4, v * v);
-      add(t + 6, a);
+      if (cols & 8u) add(t + 3, v);
+      if (cols & 16u) add(t + 4, v * v);
+      if (cols & 64u) add(t + 6, a);
     }
   }
   if (LDS) {
@@ -1339,6 +1344,14 @@ int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets) {
 // weighted columns are then left 0).
 int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, const double *h_w,
                         double *h_out) {
+  return pbx_profile_moments_cols(handle, f_src, h_f, w_src, h_w, 0x7fu, h_out);
+}
+
+// the same, accumulating only the columns in `cols` (bit k = column k; the
+// others are returned as 0): e.g. Sum needs Σf only, a weighted Mean Σw
+// and Σf·w (pynbodyext.profiles.proarray derives the set per statistic)
+int pbx_profile_moments_cols(void *handle, int f_src, const double *h_f, int w_src,
+                             const double *h_w, uint32_t cols, double *h_out) {
   return guard([&] {
     Profile &P = as_profile(handle);
     if (P.nb < 0) fail(PBX_ERR_VALUE, "call pbx_profile_assign first");
@@ -1383,8 +1396,8 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src, c
       size_t lds = in_lds ? sizeof(double) * (size_t)len : 0;
       auto launch = [&](auto wm, auto lds_t) {
         hipLaunchKernelGGL((moments_kernel<decltype(wm)::value, decltype(lds_t)::value>), dim3(nt),
-                           dim3(TPB), lds, st, (const uint32_t *)P.bins.p, f, w, n, (int)nb, slab,
-                           acc);
+                           dim3(TPB), lds, st, (const uint32_t *)P.bins.p, f, w, n, (int)nb, cols,
+                           slab, acc);
       };
       using W1 = std::integral_constant<int, 1>;
       using W0 = std::integral_constant<int, 0>;

@@ -13,8 +13,8 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint64,
-                    c_void_p)
+from ctypes import (POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint32,
+                    c_uint64, c_void_p)
 from pathlib import Path
 
 import numpy as np
@@ -110,6 +110,8 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_profile_assign": (c_int, [c_void_p, _dp, c_int64, _i64p, _i64p]),
     "pbx_profile_csr": (c_int, [c_void_p, _i64p, _i64p]),
     "pbx_profile_moments": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, _dp]),
+    "pbx_profile_moments_cols": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_uint32,
+                                         _dp]),
     "pbx_comm_unique_id_size": (c_int, []),
     "pbx_comm_unique_id": (c_int, [c_char_p, c_int]),
     "pbx_comm_init": (c_int, [POINTER(c_void_p), c_int, c_int, c_char_p]),

@@ -380,8 +380,8 @@ class ShardedProfile:
         local = self.dev.assign(edges)
         return local.copy() if self.comm is None else self.comm.allreduce_host(local)
 
-    def moments(self, field, weights) -> np.ndarray:
-        local = self.dev.moments(field, weights)
+    def moments(self, field, weights, cols: int = (1 << 7) - 1) -> np.ndarray:
+        local = self.dev.moments(field, weights, cols)
         return local if self.comm is None else self.comm.allreduce_host(local)
 
     def csr(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:

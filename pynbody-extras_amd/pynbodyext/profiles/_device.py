@@ -15,6 +15,7 @@ import numpy as np
 from .. import _native as nat
 
 NMOM = 7  # Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|
+ALL_COLS = (1 << NMOM) - 1
 SRC_X, SRC_W, SRC_HOST, SRC_DEVICE, SRC_NONE = 0, 1, 2, 3, -1
 
 _i64p = ctypes.POINTER(c_int64)
@@ -195,11 +196,12 @@ class DeviceBins:
         nat.call("pbx_profile_csr", self._h, None, None)
 
     # -- reductions ---------------------------------------------------------
-    def moments(self, field=SRC_X, weights=SRC_NONE) -> np.ndarray:
+    def moments(self, field=SRC_X, weights=SRC_NONE, cols: int = ALL_COLS) -> np.ndarray:
         """Per-bin sums (nbins, 7): Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|.
 
         field / weights: SRC_X, SRC_W (selection mass), a host array of
-        length n, or (weights only) SRC_NONE.
+        length n, or (weights only) SRC_NONE.  cols: bit mask of the columns
+        to accumulate (the others come back 0).
         """
         if self.nbins is None:
             raise ValueError("assign() first")
@@ -220,7 +222,8 @@ class DeviceBins:
         def ptr(a):
             return a if isinstance(a, ctypes.c_void_p) else nat.vptr(a)
 
-        nat.call("pbx_profile_moments", self._h, fs, ptr(fa), ws, ptr(wa), nat.dptr(out))
+        nat.call("pbx_profile_moments_cols", self._h, fs, ptr(fa), ws, ptr(wa), int(cols) & ALL_COLS,
+                 nat.dptr(out))
         return out
 
     def close(self) -> None:

@@ -117,7 +117,8 @@ class ProfileArray(SimArray):
         fast = calc.from_moments if hasattr(calc, "from_moments") else None
         dev = getattr(profile.bins, "_device", None) if fast is not None else None
         if dev is not None and dev.nbins == profile.nbins:
-            vals = fast(_moments_for(profile, dev, name, arr_pp, weights),
+            cols = _columns_of(fast, profile.nbins, weights is not None)
+            vals = fast(_moments_for(profile, dev, name, arr_pp, weights, cols),
                         np.asarray(profile.npart_bins), weights is not None)
         else:
             vals = np.zeros(profile.nbins)
@@ -180,8 +181,28 @@ class ProfileArray(SimArray):
         return x[:-1] + flag + "')"
 
 
-def _moments_for(profile, dev, name, arr_pp, weights) -> np.ndarray:
-    """(nbins, 7) device sums of a field, reusing device-resident arrays."""
+class _ColumnProbe:
+    """Stands in for the (nbins, 7) moments in one dry run of a statistic's
+    ``from_moments`` to learn which columns it reads."""
+
+    def __init__(self, nb):
+        self.nb, self.cols = nb, 0
+
+    def __getitem__(self, key):
+        self.cols |= 1 << int(key[1])
+        return np.ones(self.nb)
+
+
+def _columns_of(fast, nb, weighted) -> int:
+    probe = _ColumnProbe(nb)
+    with np.errstate(all="ignore"):
+        fast(probe, np.ones(nb), weighted)
+    return probe.cols
+
+
+def _moments_for(profile, dev, name, arr_pp, weights, cols=(1 << 7) - 1) -> np.ndarray:
+    """(nbins, 7) device sums of a field, reusing device-resident arrays;
+    only the columns in ``cols`` are accumulated."""
     bins = profile.bins
     if name is not None and isinstance(bins.bins_by, str) and name == bins.bins_by:
         fsrc = SRC_X
@@ -195,7 +216,7 @@ def _moments_for(profile, dev, name, arr_pp, weights) -> np.ndarray:
         wsrc = SRC_W
     else:
         wsrc = np.asarray(weights, dtype=np.float64)
-    return dev.moments(fsrc, wsrc)
+    return dev.moments(fsrc, wsrc, cols)
 
 
 # ---------------------------------------------------------------- plug-ins

@@ -294,3 +294,37 @@ def test_equaln_radix_select_adversarial(gpu, case):
     got = d.edges_equaln(nb, lo, hi)
     want = pr.edges_equaln(x, nb, lo, hi)
     assert np.array_equal(got, want, equal_nan=True), case
+
+
+def test_moment_column_masks(gpu):
+    """pbx_profile_moments_cols: requested columns equal the full moments
+    (same kernel, same order), the others are 0; the per-statistic column
+    sets found by the dry-run probe cover what each statistic reads."""
+    from pynbodyext.profiles import proarray as pa
+    from pynbodyext.profiles._device import SRC_W, SRC_X
+
+    rng = np.random.default_rng(8)
+    x = rng.lognormal(0.0, 1.0, 200_000)
+    w = rng.uniform(0.5, 2.0, x.size)
+    d = DeviceBins.from_x(x)
+    try:
+        d.assign(d.edges_equaln(64))
+        full = d.moments(SRC_X, w)
+        for cols in (1, 2 | 1, 8, 16 | 4, 64 | 32, 0x7f):
+            got = d.moments(SRC_X, w, cols)
+            for c in range(7):
+                if cols >> c & 1:
+                    np.testing.assert_allclose(got[:, c], full[:, c], rtol=1e-12)
+                else:
+                    assert np.all(got[:, c] == 0.0)
+    finally:
+        d.close()
+    W, FW, F2W, F, F2, AW, A = range(7)
+    want = {("mean", True): {W, FW}, ("mean", False): {F}, ("sum", True): {F},
+            ("sum_w", True): {FW}, ("rms", True): {W, F2W}, ("rms", False): {F2},
+            ("disp", True): {W, FW, F2W}, ("disp", False): {F, F2}, ("abs", True): {W, AW},
+            ("abs_sum", False): {A}}
+    for (key, weighted), cols in want.items():
+        calc = pa.ProfileArray.get_statistic(key)
+        got = pa._columns_of(calc.from_moments, 8, weighted)
+        assert got == sum(1 << c for c in cols), (key, weighted, bin(got))
