@@ -95,6 +95,12 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
   return __builtin_fma(0.5 * y, e, y);
 }
 
+// 1/sqrt(x) of the walk: RAW (fast mode, pbx_set_precise(0)) is v_rsq_f64
+// as is (~5e-8 relative), else one Newton step (~1e-16)
+template <bool RAW> __device__ __forceinline__ double rsq_walk(double x) {
+  return RAW ? __builtin_amdgcn_rsq(x) : rsqrt_nr(x);
+}
+
 // Derivative tensor D[s] = d^(l+m+n)/dx^l dy^m dz^n of 1/|R| at R = (x, y, z)
 // up to order P, from the recurrence obtained by differentiating
 // r^2 dphi/dx + x phi = 0 (Leibniz):
@@ -810,7 +816,7 @@ __device__ __forceinline__ void load_chunks(const double *ptr, u32x16 (&c)[NCH])
 }
 
 // one source pair of a leaf (tree.rs:98-417), self pair neutralised
-template <int WANT, bool SOFT>
+template <int WANT, bool SOFT, bool RAW>
 __device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, double sy, double sz,
                                           double sm, double sh, bool me, double tx, double ty,
                                           double tz, double th, double &ph, double &ax,
@@ -822,7 +828,7 @@ __device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, doubl
   double h = 0.0;
   if (SOFT) h = wp.soft ? __builtin_fmax(__builtin_fmax(sh, 0.0), th) : th;
   if (!SOFT || h <= 0.0 || (wp.kernel == 1 && r2 >= h * h)) {
-    const double y = rsqrt_nr(r2 + kR2Tiny);
+    const double y = rsq_walk<RAW>(r2 + kR2Tiny);
     if (WANT & PBX_WANT_POT) ph = __builtin_fma(-m, y, ph);
     if (WANT & PBX_WANT_ACC) {
       const double g = m * (y * y * y);
@@ -846,7 +852,7 @@ __device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, doubl
 // its scalar-load latency with other waves: orders <= 3 without softening
 // are held to 8 waves per SIMD (the compiler then parks a few SGPRs in VGPR
 // lanes instead of taking ~100 SGPRs, which leaves room for only 6 waves).
-template <int P, int WANT, bool SOFT>
+template <int P, int WANT, bool SOFT, bool RAW>
 __global__ void __launch_bounds__(WALK_TPB)
     __attribute__((amdgpu_waves_per_eu((P <= 3 && !SOFT) ? 8 : 1, 8)))
     walk_kernel(WalkParams wp) {
@@ -915,7 +921,7 @@ __global__ void __launch_bounds__(WALK_TPB)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (j + q < e)
-              leaf_pair<WANT, SOFT>(wp, chunk_d(r[q / 2], 4 * (q & 1)),
+              leaf_pair<WANT, SOFT, RAW>(wp, chunk_d(r[q / 2], 4 * (q & 1)),
                                     chunk_d(r[q / 2], 4 * (q & 1) + 1),
                                     chunk_d(r[q / 2], 4 * (q & 1) + 2),
                                     chunk_d(r[q / 2], 4 * (q & 1) + 3), hv[q], j + q == self, tx,
@@ -945,7 +951,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       if (soft_ok && chunk_d(c[0], 4) < wp.theta2 * dist2) {
         ++n_node;
         if constexpr (P == 0) {  // monopole without multipoles (tree.rs:1126-1129, 1284-1291)
-          const double y = rsqrt_nr(dist2 + kR2Tiny);
+          const double y = rsq_walk<RAW>(dist2 + kR2Tiny);
           if (WANT & PBX_WANT_POT) ph = __builtin_fma(-mass, y, ph);
           if (WANT & PBX_WANT_ACC) {
             const double g = mass * (y * y * y);
@@ -956,7 +962,7 @@ __global__ void __launch_bounds__(WALK_TPB)
         } else {
           // derivative builders add eps2 = R2_TINY and R2_TINY again
           // (multipole.rs:594, tree.rs:1429)
-          const double inv_r = rsqrt_nr(dist2 + kR2Tiny);
+          const double inv_r = rsq_walk<RAW>(dist2 + kR2Tiny);
           if constexpr (P == 1) {  // stored as O0: monopole with the D1 tensor (multipole.rs:272)
             double D[4];
             derivs<1>(dx, dy, dz, inv_r, D);
@@ -1437,10 +1443,15 @@ static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
     const unsigned round = kNumXcd * wp.xcd_chunk;
     grid = (grid + round - 1) / round * round;
   }
-  if (soft)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, true>), dim3(grid), dim3(tpb), 0, st, wp);
+  const bool raw = !precise_mode();
+  if (soft && raw)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, true, true>), dim3(grid), dim3(tpb), 0, st, wp);
+  else if (soft)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
+  else if (raw)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true>), dim3(grid), dim3(tpb), 0, st, wp);
   else
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false>), dim3(grid), dim3(tpb), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false>), dim3(grid), dim3(tpb), 0, st, wp);
 }
 
 template <int P>

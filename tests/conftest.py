@@ -12,6 +12,7 @@ for p in (ROOT, ROOT / "pynbody-extras_amd"):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; runs the HIP path")
+    config.addinivalue_line("markers", "fast: runs the default fast-precision mode (tree tests default to precise)")
 
 
 @pytest.fixture(scope="session")

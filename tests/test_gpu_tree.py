@@ -25,8 +25,19 @@ from pynbodyext.synthetic import plummer
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
-TIGHT = 1e-9
+TIGHT = 1e-9     # precise mode (Newton-refined 1/sqrt): the oracle to rounding
+FAST = 2e-6      # default fast mode (raw v_rsq_f64, ~5e-8 per interaction)
 NCOEF = {2: 10, 3: 20, 4: 35, 5: 56}
+
+
+@pytest.fixture(autouse=True)
+def _precise(request):
+    """Decision/value parity tests run the precise walk; the tests marked
+    ``fast`` run the default fast mode against the same oracle."""
+    from pynbodyext import _native as nat
+
+    with nat.precise_mode("fast" not in request.keywords):
+        yield
 
 
 def rel_pot(a, b):
@@ -324,3 +335,33 @@ def test_rebuild_reuses_handle(gpu):
     ref = ot.RefOctree(pos2, m2, 8, 3)
     check_structure(t, ref, 3)
     check_walk(t, ref, 0.5, len(pos2))
+
+
+@pytest.mark.fast
+@pytest.mark.parametrize("order", [0, 1, 3, 5])
+def test_fast_mode_walk(gpu, order):
+    """Default (fast) mode: v_rsq_f64 unrefined in node and leaf interactions;
+    same decisions and interaction counts, values within 2e-6 of the oracle
+    (contract 1e-5)."""
+    pos, mass = plummer(20_000, seed=401 + order)
+    dev = _engine.Octree(pos, mass, leaf_capacity=8, multipole_order=order)
+    ref = ot.RefOctree(pos, mass, 8, order)
+    pot_d = dev.compute_potentials(0.5)
+    cnt_d = dev.info()
+    acc_d = dev.compute_accelerations(0.5)
+    pot_r, acc_r, nn_r, np_r = ref.compute_subset(np.arange(len(pos)), 0.5)
+    assert cnt_d["node_interactions"] == int(nn_r.sum())
+    assert cnt_d["leaf_pairs"] == int(np_r.sum())
+    rp, ra = rel_pot(pot_d, pot_r), rel_acc(acc_d, acc_r)
+    assert rp < FAST and ra < FAST, (rp, ra)
+
+
+@pytest.mark.fast
+def test_fast_mode_softened_at_points(gpu):
+    pos, mass = plummer(6000, seed=77)
+    h = np.full(len(pos), 0.02)
+    dev = _engine.Octree(pos, mass, leaf_capacity=8, multipole_order=3, softenings=h, kernel=0)
+    ref = ot.RefOctree(pos, mass, 8, 3, softenings=h, kernel=0)
+    assert rel_pot(dev.compute_potentials(0.5), ref.compute_potentials(0.5)) < FAST
+    pts = np.random.default_rng(3).normal(size=(500, 3))
+    assert rel_acc(dev.accelerations_at_points(pts, 0.5), ref.accelerations_at_points(pts, 0.5)) < FAST
