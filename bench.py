@@ -386,6 +386,17 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
     return out
 
 
+def pmc_profile_step_bytes(n: int):
+    """HBM bytes of one 64M profile step from the committed PMC summary."""
+    f = ROOT / "profiles" / "pmc_profile_latest.json"
+    if n != 64_000_000 or not f.exists():
+        return None
+    try:
+        return json.loads(f.read_text()).get("hbm_bytes_per_step")
+    except Exception:
+        return None
+
+
 def pmc_traffic(which: str = "direct"):
     """HBM bytes per launch of a bench kernel from the committed rocprofv3
     PMC summary (profiles/pmc_<which>_latest.json, tools/pmc_summary.py), or None."""
@@ -524,7 +535,10 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": big["hbm_gbs_algorithmic_per_gpu"] / HBM_PEAK_GBS,
                          "at_n_per_gpu": big["n_per_gpu"],
-                         "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE, "traffic": None},
+                         "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE,
+                         "traffic": pmc_profile_step_bytes(big["n_per_gpu"]),
+                         "traffic_note": "HBM bytes per 64M step (all profile kernels, PMC "
+                                         "run committed in profiles/pmc_profile_latest.json)"},
             "sweep": sweep,
             "cpu_baseline": head.get("cpu_baseline"),
         }

@@ -7,7 +7,7 @@ coalesced streaming reads, so the corrected read traffic is 2 x FETCH_SIZE;
 WRITE_SIZE is exact for 16-B-per-lane stores.  Both are memory-side (L2
 fabric) requests, Infinity-Cache hits included.
 
-usage: tools/pmc_summary.py FETCH_CSV WRITE_CSV OUT_DIR
+usage: tools/pmc_summary.py FETCH_CSV WRITE_CSV OUT_DIR [--skip-profile | --only-profile]
 writes OUT_DIR/pmc_summary.csv (per kernel) and the per-launch traffic of the
 bench's dominant kernels as profiles/pmc_{direct,tree,profile}_latest.json.
 """
@@ -27,7 +27,10 @@ def load(path):
 
 
 def main():
-    fetch, write, out = load(sys.argv[1]), load(sys.argv[2]), Path(sys.argv[3]).resolve()
+    skip_profile = "--skip-profile" in sys.argv  # (a run whose profile kernels are the tree's)
+    only_profile = "--only-profile" in sys.argv  # (a profile-only run: its direct solve is a stub)
+    argv = [a for a in sys.argv if a not in ("--skip-profile", "--only-profile")]
+    fetch, write, out = load(argv[1]), load(argv[2]), Path(argv[3]).resolve()
     out.mkdir(parents=True, exist_ok=True)
     rows = []
     for name in sorted(set(fetch) | set(write), key=lambda k: -sum(fetch.get(k, [0]))):
@@ -48,7 +51,7 @@ def main():
 
     root = Path(__file__).resolve().parent.parent / "profiles"
     src = str((out / "pmc_summary.csv").relative_to(root.parent))
-    d = pick("sym_kernel") or pick("direct_kernel")  # the bench's all-particles kernel
+    d = [] if only_profile else (pick("sym_kernel") or pick("direct_kernel"))  # all-particles kernel
     if d:
         r = d[0]
         (root / "pmc_direct_latest.json").write_text(json.dumps({
@@ -57,7 +60,7 @@ def main():
             "note": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); memory-side requests "
                     "incl. Infinity-Cache hits and the f64 accumulator atomics", "source": src},
             indent=1))
-    t = pick("walk_kernel<3, 3")
+    t = [] if only_profile else pick("walk_kernel<3, 3")
     if t:
         r = t[0]
         (root / "pmc_tree_latest.json").write_text(json.dumps({
@@ -66,11 +69,23 @@ def main():
             "note": "2 x FETCH_SIZE + WRITE_SIZE; node records / leaf particles are scalar loads",
             "source": src}, indent=1))
     prof = [r for r in rows if "pbx::prof::" in r["kernel"] or "radix_" in r["kernel"] or "scan_t" in r["kernel"]]
-    if prof:
+    if prof and not skip_profile:
+        # one profile step of the PMC run = the dispatches of its selection
+        # kernel (one per step); shared radix/scan kernels of the tree build
+        # are excluded from the per-step sum
+        sel = [r for r in prof if "select_onepass" in r["kernel"]]
+        steps = sel[0]["dispatches"] if sel else None
+        own = [r for r in prof if "pbx::prof::" in r["kernel"] or "unsigned int, 1>" in r["kernel"]]
+        per_step = None
+        if steps:
+            per_step = sum(((r["read_bytes_corrected_avg"] or 0) + (r["write_bytes_avg"] or 0))
+                           * r["dispatches"] for r in own) / steps
         (root / "pmc_profile_latest.json").write_text(json.dumps({
             "kernels": [r["kernel"] for r in prof],
+            "hbm_bytes_per_step": per_step, "steps": steps,
             "note": "per-dispatch averages of every profile-path kernel in the 64M run "
-                    "(radix/scan kernels are shared with the octree build)",
+                    "(radix/scan kernels are shared with the octree build); hbm_bytes_per_step = "
+                    "sum over the profile's own kernels of 2 x FETCH_SIZE + WRITE_SIZE per step",
             "per_kernel": prof, "source": src}, indent=1))
     for r in rows[:25]:
         print(f"{r['dispatches']:5d}  read {r['read_bytes_corrected_avg'] or 0:14.0f}  "
