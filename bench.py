@@ -170,16 +170,21 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
         sp = ShardedProfile(comm, dev, offset=rank * n)
         e0, e1 = nat.Event(), nat.Event()
 
+        # the columns these two statistics read (proarray Sum: Σf; weighted
+        # Mean: Σw, Σf·w) — what pynbodyext.profiles requests for them
+        stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, (1 << 0) | (1 << 1))]
+
         def step():
             DeviceBins.select(d_pos.ptr, d_mass.ptr, sphere=((0.0, 0.0, 0.0), 10.0),
                               families=[(dm.start, dm.stop)], ndim=3, on_device=True, n=n, into=dev)
+            if comm is None:  # edges, counts, CSR and sums with one host round trip
+                edges, _, (msum, rmean) = dev.binned_equaln(128, stats=stats, csr=True)
+                return edges, msum[:, 3], rmean
             edges = sp.edges_equaln(128)
             sp.assign(edges)
             dev.build_csr_on_device()
-            # the columns these two statistics read (proarray Sum: Σf; weighted
-            # Mean: Σw, Σf·w) — what pynbodyext.profiles requests for them
-            msum = sp.moments(SRC_W, SRC_NONE, cols=1 << 3)[:, 3]
-            rmean = sp.moments(SRC_X, SRC_W, cols=(1 << 0) | (1 << 1))
+            msum = sp.moments(*stats[0])[:, 3]
+            rmean = sp.moments(*stats[1])
             return edges, msum, rmean
 
         for _ in range(warmup):

@@ -284,6 +284,18 @@ int pbx_profile_moments(void *handle, int f_src, const double *h_f, int w_src,
  * (proarray.py:632-860 — Sum: Σf; weighted Mean: Σw, Σf·w; ...) */
 int pbx_profile_moments_cols(void *handle, int f_src, const double *h_f, int w_src,
                              const double *h_w, uint32_t cols, double *h_out);
+/* One equaln radial-profile pass after pbx_profile_select with a single host
+ * round trip (bins.py:720-746 edges, :346-395 assignment, the CSR when
+ * build_csr, and per-bin sums of n_stats <= 16 requests (f_src / w_src in
+ * {0 x, 1 weights} / -1, column mask cols[k]) as h_moments[k][nb][7]).
+ * Same results and errors as pbx_profile_edges_equaln + pbx_profile_assign
+ * (+ pbx_profile_csr) + pbx_profile_moments_cols; *n_edges = nbins + 1 or 2
+ * (the reference's degenerate case, then nb = 1).  nbins <= 1024. */
+int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double bin_min,
+                              int has_max, double bin_max, int build_csr, int n_stats,
+                              const int *f_src, const int *w_src, const uint32_t *cols,
+                              double *h_edges, int64_t *n_edges, int64_t *h_counts,
+                              int64_t *n_valid, double *h_moments);
 
 /* ------------------------------------------------------------------ */
 /* multi-GPU: RCCL communicator (one process per GPU, over xGMI)       */

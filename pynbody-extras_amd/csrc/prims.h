@@ -247,6 +247,28 @@ struct Buf {
   }
 };
 
+// Pinned host staging (hipHostMalloc), grown on demand: D2H copies into it
+// stay asynchronous, so a batch of readbacks costs one stream sync.
+struct HostBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  void *get(size_t need) {
+    if (need <= bytes) return p;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    size_t want = need < 4096 ? 4096 : need;
+    PBX_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+    bytes = want;
+    return p;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
 static inline uint32_t ntiles_of(int64_t n) { return (uint32_t)((n + TILE - 1) / TILE); }
 
 // Exclusive scan of len u32 in place, any length (recursive over tile sums).

@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(TPB)
       b = wmax[ww] > b ? wmax[ww] : b;
     }
     if (lane == 0) {
-      if (a != ~0ull) atomicMin(&minmax[0], a);
+      if (a != ~0ull) atomicMax(&minmax[0], ~a);  // complemented min: zero-filled start
       if (b != 0ull) atomicMax(&minmax[1], b);
       __hip_atomic_store(&status[tile], (tile == 0 ? kStPre : kStAgg) | (uint64_t)tot,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -553,7 +553,9 @@ __device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
   return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
 }
 
-// One block takes AS_TILES consecutive 4096-element tiles.  Per-tile bin
+// One block takes `tpbk` (<= AS_TILES) consecutive 4096-element tiles:
+// AS_TILES on big inputs (LDS init and the tile_hist rows amortised), fewer
+// when that would leave the chip with too few blocks.  Per-tile bin
 // counts double as the CSR pass's radix histogram ([digit][tile], one
 // 8-bit pass) when nb < RADIX: tile_hist is then written, 8 consecutive
 // tiles per digit row at once (one 32-B segment instead of 8 scattered
@@ -564,7 +566,7 @@ constexpr int AS_TILES = 8;
 __global__ void __launch_bounds__(TPB)
     assign_bins(const double *__restrict__ x, int64_t n, const double *__restrict__ edges, int nb,
                 uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts,
-                uint32_t *__restrict__ tile_hist, uint32_t ntiles) {
+                uint32_t *__restrict__ tile_hist, uint32_t ntiles, uint32_t tpbk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t th[AS_TILES][RADIX];
   double *e = (double *)smem;
@@ -575,8 +577,8 @@ __global__ void __launch_bounds__(TPB)
   for (int k = threadIdx.x; k <= nb; k += TPB) cnt[k] = 0;
   for (int k = threadIdx.x; k < AS_TILES * RADIX; k += TPB) (&th[0][0])[k] = 0;
   __syncthreads();
-  const uint32_t t0 = blockIdx.x * AS_TILES;
-  const uint32_t t1 = min(ntiles, t0 + AS_TILES);
+  const uint32_t t0 = blockIdx.x * tpbk;
+  const uint32_t t1 = min(ntiles, t0 + tpbk);
   // software-pipelined: the next tile's loads fly while this one is binned
   double nv[IPT];
 #pragma unroll
@@ -737,7 +739,8 @@ struct Profile {
   bool mm_valid = false;   // mm = min / max key of x, cached on the host
   uint64_t mm[2] = {0, 0};
   MselState ms;
-  Buf msH, msR, msG, msNg, msM, msRows, msL0, msL1, msCnt, csrh, slabp, selst;
+  Buf msH, msR, msG, msNg, msM, msRows, msL0, msL1, msCnt, csrh, slabp, selst, accs;
+  prim::HostBuf pin;  // pinned readback staging (async D2H, one sync)
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
 };
@@ -935,6 +938,127 @@ static void equaln_select(Profile &P, hipStream_t st, int64_t nbins, int has_min
   msel_edges_out(P, st, h_edges, n_edges);
 }
 
+// ---- device-side stages shared by the entry points ----------------------
+// bin ids + per-bin counts (P.counts, device) for nb bins of device edges
+static void assign_device(Profile &P, hipStream_t st, const double *de, int64_t nb) {
+  if (nb >= (int64_t)1 << 24) fail(PBX_ERR_VALUE, "too many bins");
+  const int64_t n = P.n;
+  unsigned long long *cnt = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
+  PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint64_t) * (nb + 1), st));
+  uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n ? n : 1));
+  P.csrh_ready = false;
+  if (n) {
+    size_t lds = ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
+                 sizeof(uint32_t) * (nb + 1);
+    if (lds > 150 * 1024) fail(PBX_ERR_VALUE, "too many bins for the device histogram (%lld)", (long long)nb);
+    const uint32_t nt = ntiles_of(n);
+    uint32_t *th = (nb < RADIX) ? (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX)
+                                : nullptr;
+    // >= ~1024 blocks where the input allows it
+    const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
+    hipLaunchKernelGGL(assign_bins, dim3(ceil_div(nt, tpbk)), dim3(TPB), lds, st,
+                       (const double *)P.x.p, n, de, (int)nb, bins, cnt, th, nt, tpbk);
+    P.csrh_ready = th != nullptr;
+    PBX_HIP(hipGetLastError());
+  }
+  P.nb = nb;
+  P.csr_ready = false;
+}
+
+// stable counting sort of the bin ids (nb = dropped) carrying indices -> P.perm
+static void csr_device(Profile &P, hipStream_t st) {
+  const int64_t n = P.n, nb = P.nb;
+  if (P.csr_ready || !n) return;
+  int bits = 0;
+  while (((int64_t)1 << bits) <= nb) ++bits;
+  uint32_t *ka = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n);
+  uint32_t *kb = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n);
+  int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n);
+  int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n);
+  const uint32_t *kin = (const uint32_t *)P.bins.p;
+  bool first = true;
+  for (int shift = 0; shift < bits; shift += 8) {
+    const bool last = shift + 8 >= bits;  // the sorted bin ids themselves are not needed
+    if (first && P.csrh_ready) {  // bins < 256: assign_bins counted the only pass
+      prim::radix_pass<uint32_t>(P.csrh, P.tsum, st, kin, nullptr, VAL_IOTA, n, shift,
+                                 last ? nullptr : ka, va, true);
+      P.csrh_ready = false;  // scanned in place: now offsets
+      first = false;
+    } else if (first) {
+      radix_pass<uint32_t>(P, st, kin, nullptr, VAL_IOTA, n, shift, last ? nullptr : ka, va);
+      first = false;
+    } else {
+      radix_pass<uint32_t>(P, st, ka, va, VAL_ARRAY, n, shift, last ? nullptr : kb, vb);
+      std::swap(ka, kb);
+      std::swap(va, vb);
+    }
+  }
+  if ((void *)va != P.perm.p)
+    PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+  P.csr_ready = true;
+}
+
+// per-bin sums of the requested columns into acc (nb x NMOM doubles, device)
+static void moments_device(Profile &P, hipStream_t st, int f_src, const double *h_f, Buf &fstage,
+                           int w_src, const double *h_w, Buf &wstage, uint32_t cols,
+                           double *acc) {
+  const int64_t n = P.n, nb = P.nb;
+  auto src = [&](int which, const double *hp, Buf &stage) -> const double * {
+    if (which == 0) return (const double *)P.x.p;
+    if (which == 1) {
+      if (!P.has_w) fail(PBX_ERR_VALUE, "profile has no selection weights");
+      return (const double *)P.w.p;
+    }
+    if (which == 2) {
+      if (!hp && n) fail(PBX_ERR_VALUE, "host array is NULL");
+      double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
+      if (n) PBX_HIP(hipMemcpyAsync(dp, hp, sizeof(double) * n, hipMemcpyHostToDevice, st));
+      return dp;
+    }
+    if (which == 3) {  // device array per ORIGINAL particle (e.g. a tree potential)
+      if (!hp && n) fail(PBX_ERR_VALUE, "device array is NULL");
+      if (!P.has_idx) return hp;
+      double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
+      if (n)
+        hipLaunchKernelGGL(gather_by_idx, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st, hp,
+                           (const int32_t *)P.idx.p, n, dp);
+      return dp;
+    }
+    fail(PBX_ERR_VALUE, "bad source selector %d", which);
+  };
+  const double *f = src(f_src, h_f, fstage);
+  const double *w = (w_src < 0) ? nullptr : src(w_src, h_w, wstage);
+  const int64_t len = nb * NMOM;
+  PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * len, st));
+  if (n && nb > 0) {
+    // <= 1024 blocks (4 per CU) stride over the tiles
+    uint32_t nt = std::min<uint32_t>(ntiles_of(n), 1024u);
+    const bool in_lds = nb <= LDS_MOM_BINS;
+    double *slab = in_lds ? (double *)P.slab.get(sizeof(double) * (size_t)nt * len) : nullptr;
+    size_t lds = in_lds ? sizeof(double) * (size_t)len : 0;
+    auto launch = [&](auto wm, auto lds_t) {
+      hipLaunchKernelGGL((moments_kernel<decltype(wm)::value, decltype(lds_t)::value>), dim3(nt),
+                         dim3(TPB), lds, st, (const uint32_t *)P.bins.p, f, w, n, (int)nb, cols,
+                         slab, acc);
+    };
+    using W1 = std::integral_constant<int, 1>;
+    using W0 = std::integral_constant<int, 0>;
+    if (w && in_lds) launch(W1{}, std::true_type{});
+    else if (w) launch(W1{}, std::false_type{});
+    else if (in_lds) launch(W0{}, std::true_type{});
+    else launch(W0{}, std::false_type{});
+    PBX_HIP(hipGetLastError());
+    if (in_lds) {
+      double *part = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * len);
+      hipLaunchKernelGGL(reduce_slab_part, dim3(ceil_div(len, TPB), SLAB_G), dim3(TPB), 0, st,
+                         slab, (int64_t)nt, len, part);
+      hipLaunchKernelGGL(reduce_slab_final, dim3(ceil_div(len, TPB)), dim3(TPB), 0, st, part,
+                         len, acc);
+      PBX_HIP(hipGetLastError());
+    }
+  }
+}
+
 static Profile &as_profile(void *h) {
   if (!h) fail(PBX_ERR_VALUE, "null profile handle");
   Profile *p = (Profile *)h;
@@ -968,8 +1092,9 @@ int pbx_profile_destroy(void *handle) {
     Buf *all[] = {&p->x, &p->w, &p->idx, &p->bins, &p->perm, &p->keys0, &p->keys1, &p->vtmp,
                   &p->hist, &p->tsum, &p->edges, &p->counts, &p->minmax, &p->slab, &p->acc,
                   &p->field, &p->weight, &p->ranks, &p->bounds, &p->msH, &p->msR, &p->msG,
-                  &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst};
+                  &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst, &p->accs};
     for (Buf *b : all) b->release();
+    p->pin.release();
     delete p;
   });
 }
@@ -1032,31 +1157,28 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
     }
     uint32_t nt = ntiles_of(n);
     // per-tile look-back status words + ticket / watchdog (selection scratch)
-    uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * ((size_t)nt + 2));
+    // [stat nt][ctrl: ticket, watchdog][~min key][max key]: one zero fill,
+    // one 32-byte readback from stat + nt - 1
+    uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * ((size_t)nt + 3));
     uint32_t *ctrl = (uint32_t *)(stat + nt);
     double *xo = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
     double *wo = (double *)P.w.get(sizeof(double) * (size_t)(n ? n : 1));
     int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(n ? n : 1));
-    unsigned long long *mm = (unsigned long long *)P.minmax.get(16);
-    unsigned long long init[2] = {~0ull, 0ull};
-    PBX_HIP(hipMemcpyAsync(mm, init, 16, hipMemcpyHostToDevice, st));
+    unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
     int64_t kept = 0;
     if (n) {
-      PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * ((size_t)nt + 2), st));
+      PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * ((size_t)nt + 3), st));
       hipLaunchKernelGGL(select_onepass, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, stat,
                          ctrl, xo, wo, io, mm);
       PBX_HIP(hipGetLastError());
-      uint64_t last = 0;
-      uint32_t hctrl[2] = {0, 0};
-      unsigned long long hm[2];
-      PBX_HIP(hipMemcpyAsync(&last, stat + nt - 1, 8, hipMemcpyDeviceToHost, st));
-      PBX_HIP(hipMemcpyAsync(hctrl, ctrl, 8, hipMemcpyDeviceToHost, st));
-      PBX_HIP(hipMemcpyAsync(hm, mm, 16, hipMemcpyDeviceToHost, st));
+      uint64_t *h = (uint64_t *)P.pin.get(32);
+      PBX_HIP(hipMemcpyAsync(h, stat + nt - 1, 32, hipMemcpyDeviceToHost, st));
       PBX_HIP(hipStreamSynchronize(st));
-      if (hctrl[1] || (last >> 62) != 2) fail(PBX_ERR_RUNTIME, "selection look-back did not complete");
+      const uint64_t last = h[0];
+      if ((h[1] >> 32) || (last >> 62) != 2) fail(PBX_ERR_RUNTIME, "selection look-back did not complete");
       kept = (int64_t)(last & kStVal);
-      P.mm[0] = hm[0];
-      P.mm[1] = hm[1];
+      P.mm[0] = ~h[2];
+      P.mm[1] = h[3];
     }
     P.mm_valid = true;
     P.n = kept;
@@ -1242,38 +1364,19 @@ int pbx_profile_assign(void *handle, const double *h_edges, int64_t n_edges, int
   return guard([&] {
     Profile &P = as_profile(handle);
     if (n_edges < 2) fail(PBX_ERR_VALUE, "Explicit bin_edges must be a 1D array of length >= 2");
-    const int64_t nb = n_edges - 1;
-    if (nb >= (int64_t)1 << 24) fail(PBX_ERR_VALUE, "too many bins");
     Device &d = current_device();
     std::lock_guard<std::mutex> lk(d.mu);
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.assign");
-    const int64_t n = P.n;
     double *de = (double *)P.edges.get(sizeof(double) * (size_t)n_edges);
     PBX_HIP(hipMemcpyAsync(de, h_edges, sizeof(double) * n_edges, hipMemcpyHostToDevice, st));
-    unsigned long long *cnt = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
-    PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint64_t) * (nb + 1), st));
-    uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n ? n : 1));
-    if (n) {
-      size_t lds = ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
-                   sizeof(uint32_t) * (nb + 1);
-      if (lds > 150 * 1024) fail(PBX_ERR_VALUE, "too many bins for the device histogram (%lld)", (long long)nb);
-      const uint32_t nt = ntiles_of(n);
-      uint32_t *th = (nb < RADIX) ? (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX)
-                                  : nullptr;
-      hipLaunchKernelGGL(assign_bins, dim3(ceil_div(nt, AS_TILES)), dim3(TPB), lds, st,
-                         (const double *)P.x.p, n,
-                         (const double *)de, (int)nb, bins, cnt, th, nt);
-      P.csrh_ready = th != nullptr;
-      PBX_HIP(hipGetLastError());
-    }
-    PBX_HIP(hipMemcpyAsync(h_counts, cnt, sizeof(int64_t) * nb, hipMemcpyDeviceToHost, st));
+    assign_device(P, st, de, n_edges - 1);
+    PBX_HIP(hipMemcpyAsync(h_counts, P.counts.p, sizeof(int64_t) * (n_edges - 1),
+                           hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
     int64_t s = 0;
-    for (int64_t k = 0; k < nb; ++k) s += h_counts[k];
-    P.nb = nb;
+    for (int64_t k = 0; k < n_edges - 1; ++k) s += h_counts[k];
     P.n_valid = s;
-    P.csr_ready = false;
     *n_valid = s;
   });
 }
@@ -1289,37 +1392,8 @@ int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets) {
     std::lock_guard<std::mutex> lk(d.mu);
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.csr");
-    const int64_t n = P.n, nb = P.nb;
-    if (!P.csr_ready && n) {
-      // stable counting sort of the bin ids (nb = dropped) carrying indices
-      int bits = 0;
-      while (((int64_t)1 << bits) <= nb) ++bits;
-      uint32_t *ka = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n);
-      uint32_t *kb = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n);
-      int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n);
-      int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n);
-      const uint32_t *kin = (const uint32_t *)P.bins.p;
-      bool first = true;
-      for (int shift = 0; shift < bits; shift += 8) {
-        const bool last = shift + 8 >= bits;  // the sorted bin ids themselves are not needed
-        if (first && P.csrh_ready) {  // bins < 256: assign_bins counted the only pass
-          prim::radix_pass<uint32_t>(P.csrh, P.tsum, st, kin, nullptr, VAL_IOTA, n, shift,
-                                     last ? nullptr : ka, va, true);
-          P.csrh_ready = false;  // scanned in place: now offsets
-          first = false;
-        } else if (first) {
-          radix_pass<uint32_t>(P, st, kin, nullptr, VAL_IOTA, n, shift, last ? nullptr : ka, va);
-          first = false;
-        } else {
-          radix_pass<uint32_t>(P, st, ka, va, VAL_ARRAY, n, shift, last ? nullptr : kb, vb);
-          std::swap(ka, kb);
-          std::swap(va, vb);
-        }
-      }
-      if ((void *)va != P.perm.p)
-        PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
-      P.csr_ready = true;
-    }
+    const int64_t nb = P.nb;
+    csr_device(P, st);
     if (h_offsets) {
       std::vector<int64_t> c((size_t)nb);
       PBX_HIP(hipMemcpyAsync(c.data(), P.counts.p, sizeof(int64_t) * nb, hipMemcpyDeviceToHost, st));
@@ -1359,64 +1433,96 @@ int pbx_profile_moments_cols(void *handle, int f_src, const double *h_f, int w_s
     std::lock_guard<std::mutex> lk(d.mu);
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.moments");
-    const int64_t n = P.n, nb = P.nb;
-    auto src = [&](int which, const double *hp, Buf &stage) -> const double * {
-      if (which == 0) return (const double *)P.x.p;
-      if (which == 1) {
-        if (!P.has_w) fail(PBX_ERR_VALUE, "profile has no selection weights");
-        return (const double *)P.w.p;
-      }
-      if (which == 2) {
-        if (!hp && n) fail(PBX_ERR_VALUE, "host array is NULL");
-        double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
-        if (n) PBX_HIP(hipMemcpyAsync(dp, hp, sizeof(double) * n, hipMemcpyHostToDevice, st));
-        return dp;
-      }
-      if (which == 3) {  // device array per ORIGINAL particle (e.g. a tree potential)
-        if (!hp && n) fail(PBX_ERR_VALUE, "device array is NULL");
-        if (!P.has_idx) return hp;
-        double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
-        if (n)
-          hipLaunchKernelGGL(gather_by_idx, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st, hp,
-                             (const int32_t *)P.idx.p, n, dp);
-        return dp;
-      }
-      fail(PBX_ERR_VALUE, "bad source selector %d", which);
-    };
-    const double *f = src(f_src, h_f, P.field);
-    const double *w = (w_src < 0) ? nullptr : src(w_src, h_w, P.weight);
-    const int64_t len = nb * NMOM;
-    double *acc = (double *)P.acc.get(sizeof(double) * (size_t)len);
-    PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * len, st));
-    if (n && nb > 0) {
-      // <= 1024 blocks (4 per CU) stride over the tiles
-      uint32_t nt = std::min<uint32_t>(ntiles_of(n), 1024u);
-      const bool in_lds = nb <= LDS_MOM_BINS;
-      double *slab = in_lds ? (double *)P.slab.get(sizeof(double) * (size_t)nt * len) : nullptr;
-      size_t lds = in_lds ? sizeof(double) * (size_t)len : 0;
-      auto launch = [&](auto wm, auto lds_t) {
-        hipLaunchKernelGGL((moments_kernel<decltype(wm)::value, decltype(lds_t)::value>), dim3(nt),
-                           dim3(TPB), lds, st, (const uint32_t *)P.bins.p, f, w, n, (int)nb, cols,
-                           slab, acc);
-      };
-      using W1 = std::integral_constant<int, 1>;
-      using W0 = std::integral_constant<int, 0>;
-      if (w && in_lds) launch(W1{}, std::true_type{});
-      else if (w) launch(W1{}, std::false_type{});
-      else if (in_lds) launch(W0{}, std::true_type{});
-      else launch(W0{}, std::false_type{});
-      PBX_HIP(hipGetLastError());
-      if (in_lds) {
-        double *part = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * len);
-        hipLaunchKernelGGL(reduce_slab_part, dim3(ceil_div(len, TPB), SLAB_G), dim3(TPB), 0, st,
-                           slab, (int64_t)nt, len, part);
-        hipLaunchKernelGGL(reduce_slab_final, dim3(ceil_div(len, TPB)), dim3(TPB), 0, st, part,
-                           len, acc);
-        PBX_HIP(hipGetLastError());
-      }
-    }
+    const int64_t len = P.nb * NMOM;
+    double *acc = (double *)P.acc.get(sizeof(double) * (size_t)std::max<int64_t>(len, 1));
+    moments_device(P, st, f_src, h_f, P.field, w_src, h_w, P.weight, cols, acc);
     PBX_HIP(hipMemcpyAsync(h_out, acc, sizeof(double) * len, hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
+  });
+}
+
+// One radial-profile pass after pbx_profile_select, with a single host
+// round trip: equaln edges (radix select, kept on the device), assignment
+// with those edges, the CSR (optional) and the per-bin sums of n_stats
+// (field, weight, columns) requests, then one batch of copies back.
+int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double bin_min,
+                              int has_max, double bin_max, int build_csr, int n_stats,
+                              const int *f_src, const int *w_src, const uint32_t *cols,
+                              double *h_edges, int64_t *n_edges, int64_t *h_counts,
+                              int64_t *n_valid, double *h_moments) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (nbins < 1) fail(PBX_ERR_VALUE, "nbins must be >= 1");
+    if (nbins + 1 > MS_MAXQ) fail(PBX_ERR_VALUE, "the fused path supports nbins <= %d", MS_MAXQ - 1);
+    if (n_stats < 0 || n_stats > 16) fail(PBX_ERR_VALUE, "at most 16 statistics");
+    for (int k = 0; k < n_stats; ++k)
+      if (f_src[k] < 0 || f_src[k] > 1 || w_src[k] < -1 || w_src[k] > 1)
+        fail(PBX_ERR_VALUE, "the fused path takes the profile's x / weights only");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.binned_equaln");
+    if (P.n == 0) fail(PBX_ERR_VALUE, "Cannot create bins: input array is empty");
+    uint64_t mm[2];
+    minmax_of(P, st, mm);
+    msel_begin(P, nbins, has_min, bin_min, has_max, bin_max, mm[0], mm[1]);
+    for (int l = 0; l < P.ms.L; ++l) {
+      msel_hist(P, st, l);
+      msel_resolve_level(P, st, l);
+    }
+    const int nq = P.ms.nq;
+    double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
+    hipLaunchKernelGGL(msel_edges, dim3(ceil_div(nq, TPB)), dim3(TPB), 0, st,
+                       (const MsRank *)P.msR.p, nq, P.ms.lo, de);
+    PBX_HIP(hipGetLastError());
+    P.ms.active = false;
+    // speculate m >= 2 (nbins bins): everything stays on the device
+    assign_device(P, st, de, nbins);
+    if (build_csr) csr_device(P, st);
+    const int64_t len = nbins * NMOM;
+    double *accs = (double *)P.accs.get(sizeof(double) * (size_t)std::max<int64_t>(1, n_stats * len));
+    for (int k = 0; k < n_stats; ++k)
+      moments_device(P, st, f_src[k], nullptr, P.field, w_src[k], nullptr, P.weight, cols[k],
+                     accs + k * len);
+    // async readbacks into pinned staging, one sync
+    char *hp = (char *)P.pin.get(8 * (1 + nq + nbins + n_stats * len));
+    int64_t *hm = (int64_t *)hp;
+    double *he = (double *)(hm + 1);
+    int64_t *hc = (int64_t *)(he + nq);
+    double *hmo = (double *)(hc + nbins);
+    PBX_HIP(hipMemcpyAsync(hm, P.msM.p, 8, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipMemcpyAsync(he, de, sizeof(double) * nq, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipMemcpyAsync(hc, P.counts.p, sizeof(int64_t) * nbins, hipMemcpyDeviceToHost, st));
+    if (n_stats)
+      PBX_HIP(hipMemcpyAsync(hmo, accs, sizeof(double) * n_stats * len, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    const int64_t m = *hm;
+    std::memcpy(h_edges, he, sizeof(double) * nq);
+    std::memcpy(h_counts, hc, sizeof(int64_t) * nbins);
+    if (n_stats) std::memcpy(h_moments, hmo, sizeof(double) * n_stats * len);
+    if (m == 0) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
+    if (m < 2) {  // the reference's degenerate [s0, s0]: one bin, redo with 2 edges
+      h_edges[1] = h_edges[0];
+      PBX_HIP(hipMemcpyAsync(de, h_edges, sizeof(double) * 2, hipMemcpyHostToDevice, st));
+      assign_device(P, st, de, 1);
+      if (build_csr) csr_device(P, st);
+      for (int k = 0; k < n_stats; ++k)
+        moments_device(P, st, f_src[k], nullptr, P.field, w_src[k], nullptr, P.weight, cols[k],
+                       accs + k * NMOM);
+      PBX_HIP(hipMemcpyAsync(h_counts, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      if (n_stats)
+        PBX_HIP(hipMemcpyAsync(h_moments, accs, sizeof(double) * n_stats * NMOM,
+                               hipMemcpyDeviceToHost, st));
+      PBX_HIP(hipStreamSynchronize(st));
+      *n_edges = 2;
+    } else {
+      *n_edges = nq;
+    }
+    const int64_t nb = *n_edges - 1;
+    int64_t s = 0;
+    for (int64_t k = 0; k < nb; ++k) s += h_counts[k];
+    P.n_valid = s;
+    *n_valid = s;
   });
 }
 

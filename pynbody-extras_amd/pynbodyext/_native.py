@@ -112,6 +112,10 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_profile_moments": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, _dp]),
     "pbx_profile_moments_cols": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_uint32,
                                          _dp]),
+    "pbx_profile_binned_equaln": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double,
+                                          c_int, c_int, POINTER(c_int), POINTER(c_int),
+                                          POINTER(c_uint32), _dp, POINTER(c_int64), _i64p,
+                                          POINTER(c_int64), _dp]),
     "pbx_comm_unique_id_size": (c_int, []),
     "pbx_comm_unique_id": (c_int, [c_char_p, c_int]),
     "pbx_comm_init": (c_int, [POINTER(c_void_p), c_int, c_int, c_char_p]),

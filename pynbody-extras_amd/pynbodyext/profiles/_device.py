@@ -8,7 +8,7 @@ computed by the HIP kernels of csrc/profile.hip.
 from __future__ import annotations
 
 import ctypes
-from ctypes import byref, c_double, c_int, c_int64, c_uint64, c_void_p
+from ctypes import byref, c_double, c_int, c_int64, c_uint32, c_uint64, c_void_p
 
 import numpy as np
 
@@ -168,6 +168,41 @@ class DeviceBins:
                 raise IndexError(str(e)) from None
             raise
         return out[: ne.value].copy()
+
+    def binned_equaln(self, nbins: int, bin_min=None, bin_max=None, stats=(), csr=True):
+        """equaln edges + assignment (+ CSR) + per-bin sums in one pass with a
+        single host round trip.  stats: (field, weights, cols) with field in
+        {SRC_X, SRC_W} and weights in {SRC_X, SRC_W, SRC_NONE}.  Returns
+        (edges, counts, [moments (nbins, 7) per stat]) exactly as
+        edges_equaln / assign / moments would."""
+        nq = int(nbins) + 1
+        k = len(stats)
+        fs = (c_int * max(k, 1))(*[int(s[0]) for s in stats])
+        ws = (c_int * max(k, 1))(*[int(s[1]) for s in stats])
+        cs = (c_uint32 * max(k, 1))(*[int(s[2]) & ALL_COLS for s in stats])
+        edges = np.empty(nq)
+        counts = np.zeros(nbins, dtype=np.int64)
+        mom = np.zeros((max(k, 1), nbins, NMOM))
+        ne, nv = c_int64(0), c_int64(0)
+        try:
+            nat.call("pbx_profile_binned_equaln", self._h, int(nbins), int(bin_min is not None),
+                     float(bin_min) if bin_min is not None else 0.0, int(bin_max is not None),
+                     float(bin_max) if bin_max is not None else 0.0, int(bool(csr)), k, fs, ws,
+                     cs, nat.dptr(edges), byref(ne), _i64(counts), byref(nv), nat.dptr(mom))
+        except ValueError as e:
+            if str(e).startswith("index 0 is out of bounds"):
+                raise IndexError(str(e)) from None
+            raise
+        nb = ne.value - 1
+        self.nbins = nb
+        self.n_valid = nv.value
+        self._csr = None
+        if nb != nbins:  # degenerate: one bin, compact layout [k][1][7]
+            flat = mom.reshape(-1)[: max(k, 1) * NMOM].reshape(max(k, 1), 1, NMOM)
+            mom = flat
+            counts = counts[:1].copy()
+        self.counts = counts
+        return edges[: ne.value].copy(), counts, [mom[i] for i in range(k)]
 
     # -- assignment ---------------------------------------------------------
     def assign(self, edges) -> np.ndarray:

@@ -328,3 +328,50 @@ def test_moment_column_masks(gpu):
         calc = pa.ProfileArray.get_statistic(key)
         got = pa._columns_of(calc.from_moments, 8, weighted)
         assert got == sum(1 << c for c in cols), (key, weighted, bin(got))
+
+
+@pytest.mark.parametrize("case", ["plummer", "clip", "nan", "single", "dups"])
+def test_binned_equaln_matches_stepwise(gpu, case):
+    """pbx_profile_binned_equaln (one host round trip) = edges_equaln +
+    assign + csr + moments_cols called one by one (edges, counts, CSR
+    bit-identical; sums to rounding), including the reference's degenerate
+    one-value window and the empty-window error."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(12)
+    pos = rng.normal(scale=3.0, size=(300_000, 3))
+    mass = rng.uniform(0.5, 1.5, len(pos))
+    lo = hi = None
+    if case == "clip":
+        lo, hi = 0.5, 6.0
+    elif case == "nan":
+        pos[::50] = np.nan
+    elif case == "single":
+        lo, hi = 1.0, 1.0
+        pos[7] = [1.0, 0.0, 0.0]
+    elif case == "dups":
+        pos = np.round(pos)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11), (SRC_X, SRC_NONE, 0x7f)]
+    a = DeviceBins.select(pos, mass, ndim=3)
+    b = DeviceBins.select(pos, mass, ndim=3)
+    try:
+        e1, c1, m1 = a.binned_equaln(128, lo, hi, stats)
+        e2 = b.edges_equaln(128, lo, hi)
+        c2 = b.assign(e2)
+        assert np.array_equal(e1, e2, equal_nan=True) and np.array_equal(c1, c2)
+        for (f, w, cols), got in zip(stats, m1):  # LDS float atomics: order varies
+            np.testing.assert_allclose(got, b.moments(f, w, cols), rtol=1e-12, atol=0)
+        p1, o1 = a.csr()
+        p2, o2 = b.csr()
+        assert np.array_equal(p1, p2) and np.array_equal(o1, o2)
+    finally:
+        a.close()
+        b.close()
+    if case == "single":
+        assert len(e1) == 2
+    d = DeviceBins.select(pos, mass, ndim=3)
+    try:
+        with pytest.raises(IndexError):
+            d.binned_equaln(16, 1e9, 2e9, stats)
+    finally:
+        d.close()
