@@ -296,6 +296,16 @@ int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double b
                               const int *f_src, const int *w_src, const uint32_t *cols,
                               double *h_edges, int64_t *n_edges, int64_t *h_counts,
                               int64_t *n_valid, double *h_moments);
+/* Per-bin percentiles of the last assignment — replaces the per-bin loop of
+ * ProfileArray._compute for Percentile / Median / Abs_pXX
+ * (proarray.py:272-334 + :689-722): h_out[bin*nq + k] = np.interp(q[k],
+ * cdf, sorted field) with cdf = (cumsum(w[order]) - c0) / (c_last - c0)
+ * (np.cumsum order and rounding) or np.linspace(0, 1, m) when w_src = -1;
+ * empty bins NaN.  f_src / w_src as above; absval: statistic of |f|;
+ * q[k] = p/100, 1 <= nq <= 4096. */
+int pbx_profile_percentiles(void *handle, int f_src, const double *h_f, int w_src,
+                            const double *h_w, int absval, int nq, const double *q,
+                            double *h_out);
 
 /* ------------------------------------------------------------------ */
 /* multi-GPU: RCCL communicator (one process per GPU, over xGMI)       */

@@ -718,6 +718,205 @@ __global__ void widen_perm(const int32_t *__restrict__ p, int64_t n, int64_t *__
   if (t < n) out[t] = p[t];
 }
 
+// ---------------------------------------------- per-bin order statistics
+// Percentile / Median / Abs_pXX (proarray.py:689-722): per bin, argsort the
+// field, cumsum the weights in that order (or linspace(0, 1, m) without
+// weights), normalise, np.interp(p/100, cdf, sorted field).
+//
+// Segmented sort: every element of the binned space is sorted by (bin id,
+// value key) with stable LSD radix passes (value key first, then bin id);
+// ties keep index order (numpy's argsort is not stable: tied values are
+// equal, only the summation order of tied weights can differ).  Dropped
+// elements (bin id nb) land behind the last bin.
+
+// value keys of f (|f| for abs_*), NaN last like np.argsort
+__global__ void pct_keys(const double *__restrict__ f, int64_t n, int absval,
+                         uint64_t *__restrict__ keys) {
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t >= n) return;
+  double v = f[t];
+  if (absval) v = fabs(v);
+  keys[t] = dkey(v);
+}
+
+__global__ void gather_bin_ids(const uint32_t *__restrict__ bins, const int32_t *__restrict__ e,
+                               int64_t n, uint32_t *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t < n) out[t] = bins[e[t]];
+}
+
+// offsets[b] = Σ counts[< b] (nb + 1 entries), one block
+__global__ void __launch_bounds__(1024) counts_to_offsets(const uint64_t *__restrict__ counts,
+                                                          int64_t nb, int64_t *__restrict__ off) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t a = std::min<int64_t>(nb, t * per), b = std::min<int64_t>(nb, a + per);
+  int64_t s = 0;
+  for (int64_t k = a; k < b; ++k) s += (int64_t)counts[k];
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    int64_t run = 0;
+    for (int k = 0; k < 1024; ++k) {
+      const int64_t v = part[k];
+      part[k] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  s = part[t];
+  for (int64_t k = a; k < b; ++k) {
+    off[k] = s;
+    s += (int64_t)counts[k];
+  }
+  if (t == 1023) off[nb] = s;
+}
+
+// numpy's binary_search_with_guess (numpy/_core/src/multiarray/
+// compiled_base.c), literally: the index it returns for NaN-containing or
+// non-monotone xp (negative weights) depends on the probe sequence.
+template <typename XP>
+__device__ int64_t np_bsearch_guess(double key, const XP &xp, int64_t len, int64_t guess) {
+  constexpr int64_t LIKELY_IN_CACHE_SIZE = 8;
+  int64_t imin = 0, imax = len;
+  if (key > xp(len - 1)) return len;
+  if (key < xp(0)) return -1;
+  if (len <= 4) {
+    int64_t i = 1;
+    for (; i < len && key >= xp(i); ++i) {
+    }
+    return i - 1;
+  }
+  if (guess > len - 3) guess = len - 3;
+  if (guess < 1) guess = 1;
+  if (key < xp(guess)) {
+    if (key < xp(guess - 1)) {
+      imax = guess - 1;
+      if (guess > LIKELY_IN_CACHE_SIZE && key >= xp(guess - LIKELY_IN_CACHE_SIZE))
+        imin = guess - LIKELY_IN_CACHE_SIZE;
+    } else {
+      return guess - 1;
+    }
+  } else {
+    if (key < xp(guess + 1)) return guess;
+    if (key < xp(guess + 2)) return guess + 1;
+    imin = guess + 2;
+    if (guess < len - LIKELY_IN_CACHE_SIZE - 1 && key < xp(guess + LIKELY_IN_CACHE_SIZE))
+      imax = guess + LIKELY_IN_CACHE_SIZE;
+  }
+  while (imin < imax) {
+    const int64_t imid = imin + ((imax - imin) >> 1);
+    if (key >= xp(imid)) imin = imid + 1;
+    else imax = imid;
+  }
+  return imin - 1;
+}
+
+// np.interp(x, xp, fp) for one scalar x (arr_interp, default left/right)
+template <typename XP, typename FP>
+__device__ double np_interp1(double x, const XP &xp, const FP &fp, int64_t len) {
+#pragma clang fp contract(off)
+  const double lval = fp(0), rval = fp(len - 1);
+  if (len == 1) {
+    const double xv = xp(0);
+    return (x < xv) ? lval : ((x > xv) ? rval : fp(0));
+  }
+  if (x != x) return x;
+  const int64_t j = np_bsearch_guess(x, xp, len, 0);
+  if (j == -1) return lval;
+  if (j == len) return rval;
+  if (j == len - 1) return fp(j);
+  const double xj = xp(j);
+  if (xj == x) return fp(j);
+  const double xj1 = xp(j + 1), fj = fp(j), fj1 = fp(j + 1);
+  const double slope = (fj1 - fj) / (xj1 - xj);
+  double r = slope * (x - xj) + fj;
+  if (r != r) {
+    r = slope * (x - xj1) + fj1;
+    if (r != r && fj == fj1) r = fj;
+  }
+  return r;
+}
+
+constexpr int PCT_CH = 2048;  // weights per LDS chunk of the sequential cumsum
+
+// One block per bin.  e: element ids sorted by (bin, value); off: bin
+// offsets into e; q: the nq fractions p/100.  Weighted: the cumulative sum
+// runs on ONE lane in the reference's order (np.cumsum is sequential, so
+// this reproduces its rounding), staged through LDS; cdf scratch holds it.
+__global__ void __launch_bounds__(TPB)
+pct_bins(const int32_t *__restrict__ e, const int64_t *__restrict__ off,
+         const double *__restrict__ f, const double *__restrict__ w, int absval,
+         const double *__restrict__ q, int nq, double *__restrict__ cdf,
+         double *__restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ double ws[PCT_CH];
+  __shared__ double cs[PCT_CH];
+  const int b = blockIdx.x;
+  const int64_t o = off[b], m = off[b + 1] - o;
+  const int tid = threadIdx.x;
+  if (m == 0) {
+    for (int k = tid; k < nq; k += TPB) out[(int64_t)b * nq + k] = __builtin_nan("");
+    return;
+  }
+  if (w && m >= 2) {
+    double c = 0.0;
+    for (int64_t base = 0; base < m; base += PCT_CH) {
+      const int len = (int)std::min<int64_t>(PCT_CH, m - base);
+      for (int i = tid; i < len; i += TPB) ws[i] = w[e[o + base + i]];
+      __syncthreads();
+      if (tid == 0) {
+        int i = 0;
+        if (base == 0) {
+          c = ws[0];
+          cs[0] = c;
+          i = 1;
+        }
+        for (; i + 8 <= len; i += 8) {
+          double v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = ws[i + j];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            c = c + v[j];
+            cs[i + j] = c;
+          }
+        }
+        for (; i < len; ++i) {
+          c = c + ws[i];
+          cs[i] = c;
+        }
+      }
+      __syncthreads();
+      for (int i = tid; i < len; i += TPB) cdf[o + base + i] = cs[i];
+      __syncthreads();
+    }
+  }
+  auto fp = [&](int64_t k) -> double {
+    const double v = f[e[o + k]];
+    return absval ? fabs(v) : v;
+  };
+  for (int k = tid; k < nq; k += TPB) {
+    const double x = q[k];
+    double r;
+    if (w && m >= 2) {
+      const double c0 = cdf[o];
+      const double d = cdf[o + m - 1] - c0;
+      auto xp = [&](int64_t i) -> double { return (cdf[o + i] - c0) / d; };
+      r = np_interp1(x, xp, fp, m);
+    } else if (m >= 2) {
+      // np.linspace(0, 1, m): k * (1 / (m - 1)), last element exactly 1
+      const double step = 1.0 / (double)(m - 1);
+      auto xp = [&](int64_t i) -> double { return i == m - 1 ? 1.0 : (double)i * step; };
+      r = np_interp1(x, xp, fp, m);
+    } else {
+      r = fp(0);  // one element: the single-point np.interp
+    }
+    out[(int64_t)b * nq + k] = r;
+  }
+}
+
 // ----------------------------------------------------------------- handle
 struct MselState {  // radix select in progress (equaln)
   bool active = false;
@@ -743,6 +942,7 @@ struct Profile {
   prim::HostBuf pin;  // pinned readback staging (async D2H, one sync)
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
+  Buf pk0, pk1, pv0, pv1, pbk, pcdf, poff, pq, pout;  // order statistics
 };
 
 // exclusive scan of len u32 in place
@@ -998,33 +1198,41 @@ static void csr_device(Profile &P, hipStream_t st) {
   P.csr_ready = true;
 }
 
+// device pointer of a per-element source: 0 = x, 1 = selection weights,
+// 2 = host array of n doubles (staged), 3 = device array per ORIGINAL particle
+static const double *resolve_src(Profile &P, hipStream_t st, int which, const double *hp,
+                                 Buf &stage) {
+  const int64_t n = P.n;
+  if (which == 0) return (const double *)P.x.p;
+  if (which == 1) {
+    if (!P.has_w) fail(PBX_ERR_VALUE, "profile has no selection weights");
+    return (const double *)P.w.p;
+  }
+  if (which == 2) {
+    if (!hp && n) fail(PBX_ERR_VALUE, "host array is NULL");
+    double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
+    if (n) PBX_HIP(hipMemcpyAsync(dp, hp, sizeof(double) * n, hipMemcpyHostToDevice, st));
+    return dp;
+  }
+  if (which == 3) {  // device array per ORIGINAL particle (e.g. a tree potential)
+    if (!hp && n) fail(PBX_ERR_VALUE, "device array is NULL");
+    if (!P.has_idx) return hp;
+    double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
+    if (n)
+      hipLaunchKernelGGL(gather_by_idx, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st, hp,
+                         (const int32_t *)P.idx.p, n, dp);
+    return dp;
+  }
+  fail(PBX_ERR_VALUE, "bad source selector %d", which);
+}
+
 // per-bin sums of the requested columns into acc (nb x NMOM doubles, device)
 static void moments_device(Profile &P, hipStream_t st, int f_src, const double *h_f, Buf &fstage,
                            int w_src, const double *h_w, Buf &wstage, uint32_t cols,
                            double *acc) {
   const int64_t n = P.n, nb = P.nb;
   auto src = [&](int which, const double *hp, Buf &stage) -> const double * {
-    if (which == 0) return (const double *)P.x.p;
-    if (which == 1) {
-      if (!P.has_w) fail(PBX_ERR_VALUE, "profile has no selection weights");
-      return (const double *)P.w.p;
-    }
-    if (which == 2) {
-      if (!hp && n) fail(PBX_ERR_VALUE, "host array is NULL");
-      double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
-      if (n) PBX_HIP(hipMemcpyAsync(dp, hp, sizeof(double) * n, hipMemcpyHostToDevice, st));
-      return dp;
-    }
-    if (which == 3) {  // device array per ORIGINAL particle (e.g. a tree potential)
-      if (!hp && n) fail(PBX_ERR_VALUE, "device array is NULL");
-      if (!P.has_idx) return hp;
-      double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
-      if (n)
-        hipLaunchKernelGGL(gather_by_idx, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st, hp,
-                           (const int32_t *)P.idx.p, n, dp);
-      return dp;
-    }
-    fail(PBX_ERR_VALUE, "bad source selector %d", which);
+    return resolve_src(P, st, which, hp, stage);
   };
   const double *f = src(f_src, h_f, fstage);
   const double *w = (w_src < 0) ? nullptr : src(w_src, h_w, wstage);
@@ -1056,6 +1264,57 @@ static void moments_device(Profile &P, hipStream_t st, int f_src, const double *
                          len, acc);
       PBX_HIP(hipGetLastError());
     }
+  }
+}
+
+// per-bin percentiles of a field (Percentile.__call__ per bin,
+// proarray.py:700-722) into out (nb x nq doubles, device)
+static void percentiles_device(Profile &P, hipStream_t st, int f_src, const double *h_f,
+                               int w_src, const double *h_w, int absval, int nq,
+                               const double *h_q, double *out) {
+  const int64_t n = P.n, nb = P.nb;
+  const double *f = resolve_src(P, st, f_src, h_f, P.field);
+  const double *w = (w_src < 0) ? nullptr : resolve_src(P, st, w_src, h_w, P.weight);
+  double *dq = (double *)P.pq.get(sizeof(double) * (size_t)nq);
+  PBX_HIP(hipMemcpyAsync(dq, h_q, sizeof(double) * nq, hipMemcpyHostToDevice, st));
+  int64_t *off = (int64_t *)P.poff.get(sizeof(int64_t) * (size_t)(nb + 1));
+  hipLaunchKernelGGL(counts_to_offsets, dim3(1), dim3(1024), 0, st, (const uint64_t *)P.counts.p,
+                     nb, off);
+  int32_t *e = nullptr;
+  if (n) {
+    uint64_t *ka = (uint64_t *)P.pk0.get(sizeof(uint64_t) * (size_t)n);
+    uint64_t *kb = (uint64_t *)P.pk1.get(sizeof(uint64_t) * (size_t)n);
+    int32_t *va = (int32_t *)P.pv0.get(sizeof(int32_t) * (size_t)n);
+    int32_t *vb = (int32_t *)P.pv1.get(sizeof(int32_t) * (size_t)n);
+    hipLaunchKernelGGL(pct_keys, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st, f, n, absval, ka);
+    // value key, 8 bits at a time (stable; first pass seeds the element ids)
+    for (int shift = 0; shift < 64; shift += 8) {
+      const bool last = shift + 8 >= 64;
+      radix_pass<uint64_t>(P, st, ka, shift == 0 ? nullptr : va, shift == 0 ? VAL_IOTA : VAL_ARRAY,
+                           n, shift, last ? nullptr : kb, vb);
+      std::swap(ka, kb);
+      std::swap(va, vb);
+    }
+    // then the bin id (stable: value order kept inside each bin)
+    uint32_t *ba = (uint32_t *)P.pbk.get(sizeof(uint32_t) * 2 * (size_t)n);
+    uint32_t *bb = ba + n;
+    hipLaunchKernelGGL(gather_bin_ids, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st,
+                       (const uint32_t *)P.bins.p, va, n, ba);
+    int bits = 0;
+    while (((int64_t)1 << bits) <= nb) ++bits;
+    for (int shift = 0; shift < bits; shift += 8) {
+      const bool last = shift + 8 >= bits;
+      radix_pass<uint32_t>(P, st, ba, va, VAL_ARRAY, n, shift, last ? nullptr : bb, vb);
+      std::swap(ba, bb);
+      std::swap(va, vb);
+    }
+    e = va;
+  }
+  if (nb > 0) {
+    double *cdf = (double *)P.pcdf.get(sizeof(double) * (size_t)(n ? n : 1));
+    hipLaunchKernelGGL(pct_bins, dim3((unsigned)nb), dim3(TPB), 0, st, (const int32_t *)e, off, f,
+                       w, absval, (const double *)dq, nq, cdf, out);
+    PBX_HIP(hipGetLastError());
   }
 }
 
@@ -1092,7 +1351,8 @@ int pbx_profile_destroy(void *handle) {
     Buf *all[] = {&p->x, &p->w, &p->idx, &p->bins, &p->perm, &p->keys0, &p->keys1, &p->vtmp,
                   &p->hist, &p->tsum, &p->edges, &p->counts, &p->minmax, &p->slab, &p->acc,
                   &p->field, &p->weight, &p->ranks, &p->bounds, &p->msH, &p->msR, &p->msG,
-                  &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst, &p->accs};
+                  &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst, &p->accs,
+                  &p->pk0, &p->pk1, &p->pv0, &p->pv1, &p->pbk, &p->pcdf, &p->poff, &p->pq, &p->pout};
     for (Buf *b : all) b->release();
     p->pin.release();
     delete p;
@@ -1523,6 +1783,33 @@ int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double b
     for (int64_t k = 0; k < nb; ++k) s += h_counts[k];
     P.n_valid = s;
     *n_valid = s;
+  });
+}
+
+// Per-bin percentiles (Percentile / Median / Abs_pXX, proarray.py:689-722)
+// of the last assignment: h_out[bin*nq + k] = np.interp(q[k], cdf_bin,
+// sorted field_bin), cdf = normalised cumsum of the weights in value order
+// (w_src -1: np.linspace(0, 1, m)); empty bins NaN.  f_src / w_src as in
+// pbx_profile_moments (3 = device array per original particle); absval:
+// statistic of |f|.  q[k] = p/100.
+int pbx_profile_percentiles(void *handle, int f_src, const double *h_f, int w_src,
+                            const double *h_w, int absval, int nq, const double *q,
+                            double *h_out) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (P.nb < 0) fail(PBX_ERR_VALUE, "call pbx_profile_assign first");
+    if (nq < 1 || nq > 4096) fail(PBX_ERR_VALUE, "1 to 4096 percentiles per call");
+    if (f_src < 0 || f_src > 3 || w_src < -1 || w_src > 3) fail(PBX_ERR_VALUE, "bad source selector");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.percentiles");
+    const int64_t nb = P.nb;
+    double *out = (double *)P.pout.get(sizeof(double) * (size_t)std::max<int64_t>(1, nb * nq));
+    percentiles_device(P, st, f_src, h_f, w_src, h_w, absval, nq, q, out);
+    if (nb > 0)
+      PBX_HIP(hipMemcpyAsync(h_out, out, sizeof(double) * nb * nq, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
   });
 }
 

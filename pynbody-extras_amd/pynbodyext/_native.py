@@ -112,6 +112,8 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_profile_moments": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, _dp]),
     "pbx_profile_moments_cols": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_uint32,
                                          _dp]),
+    "pbx_profile_percentiles": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
+                                        c_void_p, c_void_p]),
     "pbx_profile_binned_equaln": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double,
                                           c_int, c_int, POINTER(c_int), POINTER(c_int),
                                           POINTER(c_uint32), _dp, POINTER(c_int64), _i64p,

@@ -231,6 +231,34 @@ class DeviceBins:
         nat.call("pbx_profile_csr", self._h, None, None)
 
     # -- reductions ---------------------------------------------------------
+    def _src(self, v):
+        if isinstance(v, (int, np.integer)) and not isinstance(v, bool):
+            return int(v), None
+        if isinstance(v, nat.DeviceArray):  # per original particle, in HBM
+            return SRC_DEVICE, v.ptr
+        a = np.ascontiguousarray(np.asarray(v), dtype=np.float64).reshape(-1)
+        if a.shape[0] != self.n:
+            raise ValueError(f"array length {a.shape[0]} != {self.n}")
+        return SRC_HOST, a
+
+    @staticmethod
+    def _ptr(a):
+        return a if isinstance(a, ctypes.c_void_p) else nat.vptr(a)
+
+    def percentiles(self, q, field=SRC_X, weights=SRC_NONE, absval: bool = False) -> np.ndarray:
+        """Per-bin percentiles (nbins, len(q)), q = p/100 fractions: the
+        reference's Percentile per bin (np.argsort, np.cumsum of the weights
+        or np.linspace, np.interp); empty bins NaN."""
+        if self.nbins is None:
+            raise ValueError("assign() first")
+        qa = np.ascontiguousarray(np.atleast_1d(np.asarray(q, dtype=np.float64)))
+        fs, fa = self._src(field)
+        ws, wa = self._src(weights) if weights is not None else (SRC_NONE, None)
+        out = np.zeros((self.nbins, qa.shape[0]))
+        nat.call("pbx_profile_percentiles", self._h, fs, self._ptr(fa), ws, self._ptr(wa),
+                 int(bool(absval)), qa.shape[0], nat.dptr(qa), nat.dptr(out))
+        return out
+
     def moments(self, field=SRC_X, weights=SRC_NONE, cols: int = ALL_COLS) -> np.ndarray:
         """Per-bin sums (nbins, 7): Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|.
 

@@ -10,9 +10,11 @@ Evaluation: statistics that are functions of per-bin sums — ``mean``,
 ``sum``, ``sum_w``, ``rms``, ``disp`` and their ``abs_`` forms — are
 computed from one device reduction (Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w,
 Σ|f| per bin, csrc/profile.hip moments) using the reference's formulas.
-Order statistics (``pXX``, ``median``, ``abs_pXX``) and user-registered
-statistics run the reference's per-bin loop over the device-built bin
-index lists.
+Order statistics (``pXX``, ``median``, ``abs_pXX``) are computed on the
+device too (segmented radix sort by bin and value, the reference's
+sequential weight cumsum and np.interp per bin, pbx_profile_percentiles);
+user-registered statistics run the reference's per-bin loop over the
+device-built bin index lists.
 """
 from __future__ import annotations
 
@@ -116,10 +118,15 @@ class ProfileArray(SimArray):
         weights = profile._weight
         fast = calc.from_moments if hasattr(calc, "from_moments") else None
         dev = getattr(profile.bins, "_device", None) if fast is not None else None
+        pct = _percentile_of(calc)
+        pdev = getattr(profile.bins, "_device", None) if pct is not None else None
         if dev is not None and dev.nbins == profile.nbins:
             cols = _columns_of(fast, profile.nbins, weights is not None)
             vals = fast(_moments_for(profile, dev, name, arr_pp, weights, cols),
                         np.asarray(profile.npart_bins), weights is not None)
+        elif pdev is not None and pdev.nbins == profile.nbins:
+            fsrc, wsrc = _sources_for(profile, pdev, name, arr_pp, weights)
+            vals = pdev.percentiles([pct[0] / 100], fsrc, wsrc, absval=pct[1])[:, 0]
         else:
             vals = np.zeros(profile.nbins)
             for i, ind in enumerate(profile.binind):
@@ -200,9 +207,21 @@ def _columns_of(fast, nb, weighted) -> int:
     return probe.cols
 
 
-def _moments_for(profile, dev, name, arr_pp, weights, cols=(1 << 7) - 1) -> np.ndarray:
-    """(nbins, 7) device sums of a field, reusing device-resident arrays;
-    only the columns in ``cols`` are accumulated."""
+def _percentile_of(calc):
+    """(percent, absval) when ``calc`` is an order statistic the device
+    computes (pXX, median, abs_pXX, abs_median), else None."""
+    absval = False
+    if isinstance(calc, Abs):
+        calc, absval = calc._substat, True
+    if isinstance(calc, Percentile):
+        return calc.percentile, absval
+    if isinstance(calc, Median):
+        return 50, absval
+    return None
+
+
+def _sources_for(profile, dev, name, arr_pp, weights):
+    """Device source selectors (or host arrays) of a field and the weights."""
     bins = profile.bins
     if name is not None and isinstance(bins.bins_by, str) and name == bins.bins_by:
         fsrc = SRC_X
@@ -216,6 +235,13 @@ def _moments_for(profile, dev, name, arr_pp, weights, cols=(1 << 7) - 1) -> np.n
         wsrc = SRC_W
     else:
         wsrc = np.asarray(weights, dtype=np.float64)
+    return fsrc, wsrc
+
+
+def _moments_for(profile, dev, name, arr_pp, weights, cols=(1 << 7) - 1) -> np.ndarray:
+    """(nbins, 7) device sums of a field, reusing device-resident arrays;
+    only the columns in ``cols`` are accumulated."""
+    fsrc, wsrc = _sources_for(profile, dev, name, arr_pp, weights)
     return dev.moments(fsrc, wsrc, cols)
 
 

@@ -375,3 +375,98 @@ def test_binned_equaln_matches_stepwise(gpu, case):
             d.binned_equaln(16, 1e9, 2e9, stats)
     finally:
         d.close()
+
+
+def _pct_case(name, rng):
+    """(x, f, w) for a percentile edge case; x in [0, 1) binned on 16 lin bins."""
+    n = 20000
+    x = rng.random(n)
+    f = rng.normal(size=n)
+    w = rng.uniform(0.5, 1.5, n)
+    if name == "ties_equal_weights":  # tied values: tie order cannot change the cumsum
+        f = np.round(f, 1)
+        w = np.full(n, 0.75)
+    elif name == "zero_weights":
+        w[rng.random(n) < 0.3] = 0.0
+    elif name == "negative_weights":  # non-monotone cdf: numpy's probe sequence decides
+        w = rng.normal(size=n)
+    elif name == "nan_field":
+        f[rng.random(n) < 0.01] = np.nan
+    elif name == "signed_zero":
+        f = np.where(rng.random(n) < 0.5, 0.0, -0.0) * 1.0
+        f[::7] = rng.normal(size=len(f[::7]))
+    elif name == "tiny_bins":  # bins of 0, 1, 2, 3 ... elements
+        x = np.concatenate([np.full(k, (k + 0.5) / 16) for k in range(16)])
+        f = rng.normal(size=len(x))
+        w = rng.uniform(0.5, 1.5, len(x))
+    elif name == "all_zero_weight_bin":
+        w[x < 1 / 16] = 0.0
+    return x, f, w
+
+
+@pytest.mark.parametrize("case", ["plain", "ties_equal_weights", "zero_weights", "negative_weights",
+                                  "nan_field", "signed_zero", "tiny_bins", "all_zero_weight_bin"])
+def test_device_percentiles_match_oracle(gpu, case):
+    """pbx_profile_percentiles vs the reference Percentile (proarray.py:700-722)
+    per bin: bit-exact, weighted and unweighted, plain and abs_."""
+    rng = np.random.default_rng(77)
+    x, f, w = _pct_case(case, rng)
+    edges = np.linspace(0.0, 1.0, 17)
+    d = DeviceBins.from_x(x)
+    d.assign(edges)
+    perm, offsets, _ = pr.assign(x, edges)
+    qs = [0, 1, 16, 50, 84, 99, 100]
+    for weights in (w, None):
+        for absval in (False, True):
+            got = d.percentiles([q / 100 for q in qs], f, w if weights is not None else None,
+                                absval=absval)
+            for k, q in enumerate(qs):
+                key = ("abs_" if absval else "") + f"p{q}"
+                with warnings.catch_warnings():
+                    warnings.simplefilter("ignore", RuntimeWarning)
+                    ref, _ = pr.compute(f, weights, perm, offsets, key)
+                assert np.array_equal(got[:, k], ref, equal_nan=True), (case, key, weights is None,
+                                                                      got[:, k], ref)
+    d.close()
+
+
+def test_device_percentiles_large_bins(gpu):
+    """Bins larger than one LDS chunk of the sequential cumsum (2048) and a
+    field living on the device after a fused selection (SRC_W = mass)."""
+    rng = np.random.default_rng(5)
+    n = 300_000
+    x = rng.random(n)
+    f = rng.normal(size=n)
+    w = rng.uniform(0.5, 1.5, n)
+    edges = np.linspace(0.0, 1.0, 9)
+    d = DeviceBins.from_x(x)
+    d.assign(edges)
+    perm, offsets, _ = pr.assign(x, edges)
+    got = d.percentiles([0.16, 0.5, 0.84], f, w)
+    for k, q in enumerate((16, 50, 84)):
+        ref, _ = pr.compute(f, w, perm, offsets, f"p{q}")
+        assert np.array_equal(got[:, k], ref), q
+    d.close()
+
+
+def test_profile_median_uses_device(gpu, monkeypatch):
+    """ProfileArray['median'] / ['p84'] / ['abs_p16'] go through the device
+    kernel (the per-bin host loop is not taken) and equal the oracle."""
+    s = plummer_snapshot(50_000, seed=11)
+    prof = RadialProfile(s, ndim=3, weight="mass", bins_type="equaln", nbins=32)
+    calls = []
+    orig = DeviceBins.percentiles
+
+    def spy(self, *a, **k):
+        calls.append(1)
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(DeviceBins, "percentiles", spy)
+    perm, offsets = prof.bins.binind.csr
+    r = np.asarray(prof.sim["r"], dtype=np.float64)
+    m = np.asarray(prof.sim["mass"], dtype=np.float64)
+    for key in ("median", "p84", "abs_p16"):
+        got = np.asarray(prof["r"][key])
+        ref, _ = pr.compute(r, m, perm, offsets, key)
+        assert np.array_equal(got, ref), key
+    assert len(calls) == 3
