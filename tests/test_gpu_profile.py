@@ -392,9 +392,10 @@ def _pct_case(name, rng):
         w = rng.normal(size=n)
     elif name == "nan_field":
         f[rng.random(n) < 0.01] = np.nan
-    elif name == "signed_zero":
+    elif name == "signed_zero":  # -0.0 / +0.0 ties (equal weights: tie order is immaterial)
         f = np.where(rng.random(n) < 0.5, 0.0, -0.0) * 1.0
         f[::7] = rng.normal(size=len(f[::7]))
+        w = np.full(n, 1.25)
     elif name == "tiny_bins":  # bins of 0, 1, 2, 3 ... elements
         x = np.concatenate([np.full(k, (k + 0.5) / 16) for k in range(16)])
         f = rng.normal(size=len(x))
