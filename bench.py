@@ -175,11 +175,14 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
         stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, (1 << 0) | (1 << 1))]
 
         def step():
+            if comm is None:  # selection, edges, counts, CSR and sums: one host round trip
+                _, edges, _, (msum, rmean) = DeviceBins.radial_equaln(
+                    d_pos.ptr, d_mass.ptr, nbins=128, sphere=((0.0, 0.0, 0.0), 10.0),
+                    families=[(dm.start, dm.stop)], ndim=3, stats=stats, csr=True,
+                    on_device=True, n=n, into=dev)
+                return edges, msum[:, 3], rmean
             DeviceBins.select(d_pos.ptr, d_mass.ptr, sphere=((0.0, 0.0, 0.0), 10.0),
                               families=[(dm.start, dm.stop)], ndim=3, on_device=True, n=n, into=dev)
-            if comm is None:  # edges, counts, CSR and sums with one host round trip
-                edges, _, (msum, rmean) = dev.binned_equaln(128, stats=stats, csr=True)
-                return edges, msum[:, 3], rmean
             edges = sp.edges_equaln(128)
             sp.assign(edges)
             dev.build_csr_on_device()

@@ -296,6 +296,19 @@ int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double b
                               const int *f_src, const int *w_src, const uint32_t *cols,
                               double *h_edges, int64_t *n_edges, int64_t *h_counts,
                               int64_t *n_valid, double *h_moments);
+/* pbx_profile_select + pbx_profile_binned_equaln with ONE host round trip
+ * (the RadialProfileBuilder equaln path end to end: filters/filt.py:42-86,
+ * bins.py:720-746 / :346-395, proarray.py:272-334 sums).  Same arguments,
+ * results and errors as the two calls in sequence; *n_kept as
+ * pbx_profile_select (also set when the binning then fails). */
+int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mass, int64_t n,
+                              int on_device, int use_sphere, const double *sphere,
+                              const int64_t *fam, int nfam, int ndim, int64_t nbins, int has_min,
+                              double bin_min, int has_max, double bin_max, int build_csr,
+                              int n_stats, const int *f_src, const int *w_src,
+                              const uint32_t *cols, int64_t *n_kept, double *h_edges,
+                              int64_t *n_edges, int64_t *h_counts, int64_t *n_valid,
+                              double *h_moments);
 /* Per-bin percentiles of the last assignment — replaces the per-bin loop of
  * ProfileArray._compute for Percentile / Median / Abs_pXX
  * (proarray.py:272-334 + :689-722): h_out[bin*nq + k] = np.interp(q[k],

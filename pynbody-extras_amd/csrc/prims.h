@@ -121,8 +121,10 @@ __global__ void __launch_bounds__(TPB) scan_tiles(const uint32_t *in, int64_t le
 
 template <typename K>
 __global__ void __launch_bounds__(TPB) radix_hist(const K *__restrict__ keys, int64_t n, int shift,
-                                                  uint32_t *__restrict__ hist, uint32_t ntiles) {
+                                                  uint32_t *__restrict__ hist, uint32_t ntiles,
+                                                  const int64_t *__restrict__ n_dev) {
   __shared__ uint32_t cnt[RADIX];
+  if (n_dev) n = *n_dev;  // device-resident length (<= the n the grid was sized for)
   cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * TILE;
@@ -147,8 +149,9 @@ template <typename K, int VM>
 __global__ void __launch_bounds__(TPB)
     radix_scatter(const K *__restrict__ kin, const int32_t *__restrict__ vin, int64_t n, int shift,
                   const uint32_t *__restrict__ offs, uint32_t ntiles, K *__restrict__ kout,
-                  int32_t *__restrict__ vout) {
+                  int32_t *__restrict__ vout, const int64_t *__restrict__ n_dev) {
   __shared__ uint32_t run[NWAVE][RADIX];
+  if (n_dev) n = *n_dev;  // device-resident length (<= the n the grid was sized for)
   __shared__ uint32_t dstart[RADIX];  // tile-local start of each digit
   __shared__ uint32_t gofs[RADIX];    // global start of each digit's run of this tile
   __shared__ uint32_t wsum[NWAVE];
@@ -299,21 +302,22 @@ static inline void scan_u32(Buf &tsum, hipStream_t st, uint32_t *a, int64_t len,
 template <typename K>
 // (prehist: hist_buf already holds this pass's [digit][tile] counts)
 static void radix_pass(Buf &hist_buf, Buf &tsum, hipStream_t st, const K *kin, const int32_t *vin,
-                       int vm, int64_t n, int shift, K *kout, int32_t *vout, bool prehist = false) {
+                       int vm, int64_t n, int shift, K *kout, int32_t *vout, bool prehist = false,
+                       const int64_t *n_dev = nullptr) {
   uint32_t nt = ntiles_of(n);
   uint32_t *hist = (uint32_t *)hist_buf.get(sizeof(uint32_t) * (size_t)nt * RADIX);
   if (!prehist)
-    hipLaunchKernelGGL(radix_hist<K>, dim3(nt), dim3(TPB), 0, st, kin, n, shift, hist, nt);
+    hipLaunchKernelGGL(radix_hist<K>, dim3(nt), dim3(TPB), 0, st, kin, n, shift, hist, nt, n_dev);
   scan_u32(tsum, st, hist, (int64_t)nt * RADIX);
   if (vm == VAL_NONE)
     hipLaunchKernelGGL((radix_scatter<K, VAL_NONE>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
-                       shift, hist, nt, kout, vout);
+                       shift, hist, nt, kout, vout, n_dev);
   else if (vm == VAL_IOTA)
     hipLaunchKernelGGL((radix_scatter<K, VAL_IOTA>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
-                       shift, hist, nt, kout, vout);
+                       shift, hist, nt, kout, vout, n_dev);
   else
     hipLaunchKernelGGL((radix_scatter<K, VAL_ARRAY>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
-                       shift, hist, nt, kout, vout);
+                       shift, hist, nt, kout, vout, n_dev);
   PBX_HIP(hipGetLastError());
 }
 

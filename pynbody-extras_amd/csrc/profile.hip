@@ -57,13 +57,13 @@ struct SelectParams {
 __device__ __forceinline__ bool select_one(const double *__restrict__ pos, int64_t i,
                                           const SelectParams &p, double &x) {
 #pragma clang fp contract(off)
-  const double px = pos[3 * i + 0], py = pos[3 * i + 1], pz = pos[3 * i + 2];
   bool keep = true;
-  if (p.nfam > 0) {
+  if (p.nfam > 0) {  // family slices first: particles outside them are never read
     bool in = false;
     for (int f = 0; f < p.nfam; ++f) in |= (i >= p.fam_lo[f]) & (i < p.fam_hi[f]);
-    keep = in;
+    if (!in) return false;
   }
+  const double px = pos[3 * i + 0], py = pos[3 * i + 1], pz = pos[3 * i + 2];
   if (p.use_sphere) {
     double dx = px - p.cx, dy = py - p.cy, dz = pz - p.cz;
     keep = keep && (((dx * dx + dy * dy) + dz * dz) < p.r2max);
@@ -536,6 +536,385 @@ __global__ void msel_edges(const MsRank *__restrict__ R, int nq, uint64_t base,
   if (q < nq) out[q] = dkey_inv(base + R[q].prefix);
 }
 
+// ------------------------------------- one-sync equaln (select -> sums)
+// pbx_profile_radial_equaln: selection, equaln edges, assignment, CSR and
+// per-bin sums back to back on the stream with ONE host round trip at the
+// end.  Everything the host used to read between the stages (kept count,
+// key range, level digits) stays in a device control block, and the kernels
+// after the selection take their length from it (their grids are sized for
+// the input length).  equaln = level-0 radix select (top <= 14 bits of
+// key - base, as msel) + gather of the chosen level-0 buckets' keys into
+// per-group segments + one block per group that radix-selects the
+// remaining bits of each of its ranks (segment staged in LDS when small).  Same ranks and keys as the
+// multi-level msel path, so the same edges.
+struct FusedCtl {
+  int64_t n;       // kept particles
+  int64_t m;       // equaln window size
+  uint64_t lo;     // key base of the window
+  int32_t s0;      // bits below the level-0 digit
+  int32_t w0;      // level-0 digit width
+  int32_t err;     // 1: look-back incomplete, 2: empty window / no keys
+  int32_t ng;      // chosen level-0 buckets (groups)
+  int64_t total;   // keys gathered into the group segments
+  uint64_t kmin, kmax;
+};
+
+
+__global__ void fused_setup(const uint64_t *__restrict__ stat, uint32_t nt,
+                            const uint32_t *__restrict__ ctrl,
+                            const unsigned long long *__restrict__ mm, int64_t n_in, uint64_t ka,
+                            uint64_t kb, int empty_bounds, FusedCtl *__restrict__ ctl,
+                            unsigned long long *__restrict__ counts, int nb,
+                            uint32_t *__restrict__ H) {
+  for (int k = threadIdx.x; k <= nb; k += blockDim.x) counts[k] = 0;  // for assign_bins
+  for (int k = threadIdx.x; k < MS0_DIG; k += blockDim.x) H[k] = 0;   // level-0 histogram
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  FusedCtl c{};
+  if (n_in > 0) {
+    const uint64_t last = stat[nt - 1];
+    if (ctrl[1] || (last >> 62) != 2) c.err |= 1;
+    c.n = (int64_t)(last & kStVal);
+  }
+  c.kmin = ~mm[0];
+  c.kmax = mm[1];
+  const uint64_t lo = ka > c.kmin ? ka : c.kmin;
+  const uint64_t hi = kb < c.kmax ? kb : c.kmax;
+  if (c.n == 0 || empty_bounds || lo > hi) {
+    c.err |= 2;
+    c.w0 = 1;
+  } else {
+    const uint64_t span = hi - lo;
+    const int B = span ? 64 - __builtin_clzll(span) : 1;
+    c.w0 = B < MS0_BITS ? B : MS0_BITS;
+    c.s0 = B - c.w0;
+    c.lo = lo;
+  }
+  *ctl = c;
+}
+
+// level-0 histogram rows (msel_hist0 with the base / shift / length from ctl)
+__global__ void __launch_bounds__(MS0_TPB)
+    fused_hist0(const double *__restrict__ x, uint64_t ka, uint64_t kb,
+                const FusedCtl *__restrict__ ctl, uint32_t *__restrict__ rows) {
+  __shared__ uint32_t lh[MS0_DIG];
+  for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
+  __syncthreads();
+  const int64_t n = (ctl->err & 2) ? 0 : ctl->n;
+  const uint64_t base = ctl->lo;
+  const int s = ctl->s0;
+  constexpr int U = 8;
+  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * U; i0 < n; i0 += (int64_t)gridDim.x * MS0_TPB * U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+      v[u] = i < n ? x[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+      const uint64_t k = dkey(v[u]);
+      if (i < n && k >= ka && k <= kb) atomicAdd(&lh[(uint32_t)((k - base) >> s)], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t *row = rows + (int64_t)blockIdx.x * MS0_DIG;
+  for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) row[i] = lh[i];
+}
+
+// Level-0 resolve + groups, one block of 1024: the window size m, each
+// rank's level-0 digit and residual rank (bins.py:738-744 ranks), the
+// distinct chosen digits in rank order (= ascending), their key counts and
+// segment offsets.  H is left zeroed.
+constexpr int FR_TPB = 1024;
+__global__ void __launch_bounds__(FR_TPB)
+    fused_resolve0(uint32_t *__restrict__ H, FusedCtl *__restrict__ ctl, int64_t nbins, int nq,
+                   MsRank *__restrict__ R, uint32_t *__restrict__ gdig, uint32_t *__restrict__ goff,
+                   uint32_t *__restrict__ gq) {
+  constexpr int PT = MS0_DIG / FR_TPB;
+  __shared__ uint32_t incl[MS0_DIG];
+  __shared__ uint32_t wsum[FR_TPB / 64];
+  __shared__ uint32_t qdig[MS_MAXQ];
+  __shared__ uint32_t gstart[MS_MAXQ + 1];
+  __shared__ int sng;
+  const int tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const int wv = tid >> 6;
+  for (int k = tid; k < MS0_DIG; k += FR_TPB) {  // coalesced, via LDS
+    incl[k] = H[k];
+    H[k] = 0;
+  }
+  __syncthreads();
+  uint32_t v[PT], tot = 0;
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    v[k] = incl[tid * PT + k];
+    tot += v[k];
+  }
+  __syncthreads();
+  // block exclusive scan of the per-thread totals (16 waves)
+  uint32_t xs = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(xs, o, 64);
+    if (lane >= (uint32_t)o) xs += y;
+  }
+  if (lane == 63) wsum[wv] = xs;
+  __syncthreads();
+  uint32_t run = xs - tot;
+  for (int k = 0; k < wv; ++k) run += wsum[k];
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    run += v[k];
+    incl[tid * PT + k] = run;
+  }
+  __syncthreads();
+  const int64_t m = (ctl->err & 2) ? 0 : (int64_t)incl[MS0_DIG - 1];
+  const int top = (1 << ctl->w0) - 1;
+  for (int q = tid; q < nq; q += FR_TPB) {
+    int64_t r = 0;
+    if (m >= 2) r = (q == nq - 1) ? m - 1 : (int64_t)((double)(q * m) / (double)nbins);
+    int a = 0, b = top;  // first digit whose inclusive count exceeds r
+    while (a < b) {
+      const int mid = (a + b) >> 1;
+      if ((int64_t)incl[mid] <= r) a = mid + 1; else b = mid;
+    }
+    R[q].prefix = (uint64_t)a;
+    R[q].rr = r - (a ? (int64_t)incl[a - 1] : 0);
+    qdig[q] = (uint32_t)a;
+  }
+  __syncthreads();
+  // groups: run starts of the (non-decreasing) digits; one wave numbers them
+  if (wv == 0) {
+    uint32_t ng = 0;
+    for (int q0 = 0; q0 < nq; q0 += 64) {
+      const int q = q0 + (int)lane;
+      const bool st = q < nq && (q == 0 || qdig[q - 1] != qdig[q]);
+      const uint64_t bal = __ballot(st);
+      if (st) gstart[ng + rank_below(bal)] = (uint32_t)q;
+      ng += (uint32_t)__popcll(bal);
+    }
+    if (lane == 0) {
+      gstart[ng] = (uint32_t)nq;
+      sng = (int)ng;
+      ctl->ng = (int32_t)ng;
+      ctl->m = m;
+    }
+  }
+  __syncthreads();
+  const int ng = sng;
+  // group g: digit, count, segment offset (prefix over groups: one wave)
+  if (wv == 0) {
+    uint32_t base = 0;
+    for (int g0 = 0; g0 < ng; g0 += 64) {
+      const int g = g0 + (int)lane;
+      uint32_t c = 0, d = 0;
+      if (g < ng) {
+        d = qdig[gstart[g]];
+        c = incl[d] - (d ? incl[d - 1] : 0u);
+        gdig[g] = d;
+      }
+      uint32_t ys = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(ys, o, 64);
+        if (lane >= (uint32_t)o) ys += y;
+      }
+      if (g < ng) goff[g] = base + ys - c;
+      base += __shfl(ys, 63, 64);
+    }
+    if (lane == 0) {
+      goff[ng] = base;
+      ctl->total = base;
+    }
+  }
+  for (int g = tid; g <= ng; g += FR_TPB) gq[g] = gstart[g];  // each group's ranks
+  for (int q = tid; q < nq; q += FR_TPB) {  // every rank's group: last start <= q
+    int a = 0, b = ng - 1;
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if ((int)gstart[mid] <= q) a = mid; else b = mid - 1;
+    }
+    R[q].group = a;
+  }
+}
+
+// Per-block segment offsets of every group: block b of fused_hist0 counted
+// rows[b][digit of g] keys of group g, so its keys go to goff[g] + the
+// exclusive sum over earlier blocks (one block per group, one thread per
+// level-0 block).
+__global__ void __launch_bounds__(TPB)
+    fused_boff(const uint32_t *__restrict__ rows, int g0, const FusedCtl *__restrict__ ctl,
+               const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ goff,
+               uint32_t *__restrict__ boff) {
+  __shared__ uint32_t wsum[NWAVE];
+  const int g = blockIdx.x;
+  if ((ctl->err & 2) || g >= ctl->ng) return;
+  const int b = threadIdx.x;  // g0 <= TPB
+  const uint32_t c = b < g0 ? rows[(int64_t)b * MS0_DIG + gdig[g]] : 0u;
+  const uint32_t ex = block_excl_scan(c, wsum, nullptr);
+  if (b < g0) boff[(int64_t)b * MS_MAXQ + g] = goff[g] + ex;
+}
+
+// keys of the chosen level-0 buckets -> their group's segment (key - base).
+// Same grid and element order as fused_hist0, so block b owns exactly the
+// slots fused_boff gave it; inside the block an LDS counter per group hands
+// them out (no global atomics: the keys of one group are few and were
+// contended on a handful of addresses).
+__global__ void __launch_bounds__(MS0_TPB)
+    fused_gather(const double *__restrict__ x, uint64_t ka, uint64_t kb,
+                 const FusedCtl *__restrict__ ctl, const uint32_t *__restrict__ gdig,
+                 const uint32_t *__restrict__ boff, uint64_t *__restrict__ seg) {
+  __shared__ uint16_t gidx[MS0_DIG];
+  __shared__ uint32_t slot[MS_MAXQ];
+  if (ctl->err & 2) return;
+  const int64_t n = ctl->n;
+  const int ng = ctl->ng;
+  const uint64_t base = ctl->lo;
+  const int s = ctl->s0;
+  for (int i = threadIdx.x; i < MS0_DIG / 2; i += MS0_TPB) ((uint32_t *)gidx)[i] = ~0u;
+  __syncthreads();
+  for (int i = threadIdx.x; i < ng; i += MS0_TPB) {
+    gidx[gdig[i]] = (uint16_t)i;
+    slot[i] = boff[(int64_t)blockIdx.x * MS_MAXQ + i];
+  }
+  __syncthreads();
+  constexpr int U = 8;
+  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * U; i0 < n; i0 += (int64_t)gridDim.x * MS0_TPB * U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+      v[u] = i < n ? x[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+      const uint64_t key = dkey(v[u]);
+      if (i < n && key >= ka && key <= kb) {
+        const uint64_t off = key - base;
+        const uint32_t g = gidx[(uint32_t)(off >> s)];
+        if (g != 0xffffu) seg[atomicAdd(&slot[g], 1u)] = off;
+      }
+    }
+  }
+}
+
+// One block (FR_TPB threads) per group: for each of its ranks, an MSD radix
+// select (FS_BITS-bit digits, LDS histogram, parallel scan) over the group's
+// keys below the level-0 digit; the segment is staged in LDS when it fits
+// (<= FS_LDS keys), else every pass re-reads it from global memory.
+constexpr int FS_BITS = 11;
+constexpr int FS_DIG = 1 << FS_BITS;
+constexpr int FS_LDS = 8192;
+
+template <bool IN_LDS>
+__device__ void finish_group(const uint64_t *__restrict__ keys, int64_t S, uint64_t pref0, int s,
+                             int64_t rr, uint32_t *hist, uint32_t *wsum, uint64_t *pick,
+                             uint64_t &out) {
+  const int tid = threadIdx.x;
+  const uint32_t lane = lane_id();
+  const int wv = tid >> 6;
+  uint64_t pref = pref0;
+  int sh = s;
+  while (sh > 0) {
+    const int wd = sh >= FS_BITS ? FS_BITS : sh;
+    sh -= wd;
+    const uint64_t hmask = ~((1ull << (sh + wd)) - 1);  // bits above this digit
+    const uint32_t dm = (1u << wd) - 1;
+    for (int d = tid; d < FS_DIG; d += FR_TPB) hist[d] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < S; i += FR_TPB) {
+      const uint64_t k = keys[i];
+      if ((k & hmask) == pref) atomicAdd(&hist[(uint32_t)(k >> sh) & dm], 1u);
+    }
+    __syncthreads();
+    // inclusive scan of 2 digits per thread; the thread whose digits hold rank rr picks
+    const uint32_t c0 = hist[2 * tid], c1 = hist[2 * tid + 1];
+    uint32_t xs = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(xs, o, 64);
+      if (lane >= (uint32_t)o) xs += y;
+    }
+    if (lane == 63) wsum[wv] = xs;
+    __syncthreads();
+    uint32_t ex = xs - (c0 + c1);
+    for (int k = 0; k < wv; ++k) ex += wsum[k];
+    if ((int64_t)ex <= rr && rr < (int64_t)(ex + c0)) {
+      pick[0] = (uint64_t)(2 * tid);
+      pick[1] = ex;
+    } else if ((int64_t)(ex + c0) <= rr && rr < (int64_t)(ex + c0 + c1)) {
+      pick[0] = (uint64_t)(2 * tid + 1);
+      pick[1] = ex + c0;
+    }
+    __syncthreads();
+    pref |= pick[0] << sh;
+    rr -= (int64_t)pick[1];
+    __syncthreads();
+  }
+  out = pref;
+}
+
+__global__ void __launch_bounds__(FR_TPB)
+    fused_finish(const FusedCtl *__restrict__ ctl, const MsRank *__restrict__ R,
+                 const uint32_t *__restrict__ gq, const uint32_t *__restrict__ goff,
+                 const uint64_t *__restrict__ seg, double *__restrict__ edges) {
+  __shared__ uint64_t sk[FS_LDS];
+  __shared__ uint32_t hist[FS_DIG];
+  __shared__ uint32_t wsum[FR_TPB / 64];
+  __shared__ uint64_t pick[2];
+  static_assert(FS_DIG == 2 * FR_TPB, "two digits per thread");
+  const int g = blockIdx.x;
+  if ((ctl->err & 2) || g >= ctl->ng) return;
+  const uint64_t base = ctl->lo;
+  const int s = ctl->s0;
+  const int64_t o = goff[g], S = (int64_t)goff[g + 1] - o;
+  const bool in_lds = S <= FS_LDS;
+  const int tid = threadIdx.x;
+  if (in_lds) {
+    for (int64_t i = tid; i < S; i += FR_TPB) sk[i] = seg[o + i];
+    __syncthreads();
+  }
+  if (S <= FR_TPB) {  // small group: each key's rank by counting (one key per thread)
+    const uint64_t k = tid < S ? sk[tid] : ~0ull;
+    uint32_t less = 0, eq = 0;
+    for (int j = 0; j < (int)S; ++j) {
+      const uint64_t kj = sk[j];
+      less += kj < k ? 1u : 0u;
+      eq += kj == k ? 1u : 0u;
+    }
+    for (int q = (int)gq[g]; q < (int)gq[g + 1]; ++q) {
+      const int64_t rr = R[q].rr;
+      if (tid < S && (int64_t)less <= rr && rr < (int64_t)(less + eq))
+        edges[q] = dkey_inv(base + k);  // tied threads write the same value
+    }
+    return;
+  }
+  for (int q = (int)gq[g]; q < (int)gq[g + 1]; ++q) {  // this group's ranks
+    uint64_t key;
+    if (in_lds)
+      finish_group<true>(sk, S, (uint64_t)R[q].prefix << s, s, R[q].rr, hist, wsum, pick, key);
+    else
+      finish_group<false>(seg + o, S, (uint64_t)R[q].prefix << s, s, R[q].rr, hist, wsum, pick,
+                          key);
+    if (tid == 0) edges[q] = dkey_inv(base + key);
+  }
+}
+
+// the step's results in one contiguous staging block (one D2H copy):
+// [ctl][edges nq][counts nb][monomial sums nm x nb]
+__global__ void fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges,
+                           int nq, const unsigned long long *__restrict__ counts, int nb,
+                           const double *__restrict__ sums, int nsum, double *__restrict__ out) {
+  const int t = blockIdx.x * TPB + threadIdx.x;
+  constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+  if (t < NC) out[t] = ((const double *)ctl)[t];
+  else if (t < NC + nq) out[t] = edges[t - NC];
+  else if (t < NC + nq + nb) out[t] = __builtin_bit_cast(double, counts[t - NC - nq]);
+  else if (t < NC + nq + nb + nsum) out[t] = sums[t - NC - nq - nb];
+}
+
 // ----------------------------------------------------------------- assign
 // bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
 // x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379)
@@ -563,15 +942,38 @@ __device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
 // contiguous atomic per bin.
 constexpr int AS_TILES = 8;
 
+// Per-bin sums fused into the assignment pass (the one-sync equaln path):
+// the distinct per-element values ("monomials") the requested statistics'
+// columns sum — e.g. Sum of the mass and the weights column of a
+// mass-weighted Mean are the same Σw, accumulated once.  Monomial q is
+// column col[q] of pbx_profile_moments_cols for field f[q] (0 = x, 1 =
+// weights) and weights w[q] (0 = x, 1 = weights, -1 = none); block sums in
+// LDS, one slab row (nm x nb) per block.
+constexpr int AS_MAXM = 8;
+struct FusedStats {
+  int nm;
+  int f[AS_MAXM];
+  int w[AS_MAXM];
+  int col[AS_MAXM];
+};
+
+template <bool MOM>
 __global__ void __launch_bounds__(TPB)
     assign_bins(const double *__restrict__ x, int64_t n, const double *__restrict__ edges, int nb,
                 uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts,
-                uint32_t *__restrict__ tile_hist, uint32_t ntiles, uint32_t tpbk) {
+                uint32_t *__restrict__ tile_hist, uint32_t ntiles, uint32_t tpbk,
+                const int64_t *__restrict__ n_dev, const double *__restrict__ wsel, FusedStats fs,
+                double *__restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t th[AS_TILES][RADIX];
-  double *e = (double *)smem;
+  if (n_dev) n = *n_dev;  // device-resident length (<= the n the grid was sized for)
+  const int macc = MOM ? fs.nm * nb : 0;
+  double *acc = (double *)smem;  // MOM: the block's sums
+  double *e = acc + macc;
   const bool lds_edges = (nb + 1) <= LDS_EDGES;
-  uint32_t *cnt = (uint32_t *)(smem + (lds_edges ? sizeof(double) * (nb + 1) : 0));
+  uint32_t *cnt = (uint32_t *)(e + (lds_edges ? nb + 1 : 0));
+  if (MOM)
+    for (int k = threadIdx.x; k < macc; k += TPB) acc[k] = 0.0;
   if (lds_edges)
     for (int k = threadIdx.x; k <= nb; k += TPB) e[k] = edges[k];
   for (int k = threadIdx.x; k <= nb; k += TPB) cnt[k] = 0;
@@ -609,8 +1011,40 @@ __global__ void __launch_bounds__(TPB)
       const int64_t i = base + k * TPB + threadIdx.x;
       if (i < n) bins[i] = b[k];
     }
+    if (MOM) {
+      double wv[IPT];
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const int64_t i = base + k * TPB + threadIdx.x;
+        wv[k] = (wsel && i < n) ? wsel[i] : 1.0;
+      }
+#pragma unroll
+      for (int k = 0; k < IPT; ++k) {
+        const int64_t i = base + k * TPB + threadIdx.x;
+        if (i >= n || b[k] >= (uint32_t)nb) continue;
+        for (int q = 0; q < fs.nm; ++q) {  // uniform: scalar branches
+          const double f = fs.f[q] == 0 ? v[k] : wv[k];
+          const double ww = fs.w[q] == 0 ? v[k] : wv[k];
+          double val;  // the expression moments_kernel sums for this column
+          switch (fs.col[q]) {
+            case 0: val = ww; break;
+            case 1: val = f * ww; break;
+            case 2: val = (f * f) * ww; break;
+            case 3: val = f; break;
+            case 4: val = f * f; break;
+            case 5: val = __builtin_fabs(f) * ww; break;
+            default: val = __builtin_fabs(f); break;
+          }
+          atomicAdd(&acc[(int64_t)q * nb + b[k]], val);
+        }
+      }
+    }
   }
   __syncthreads();
+  if (MOM) {
+    double *dst = slab + (int64_t)blockIdx.x * macc;
+    for (int k = threadIdx.x; k < macc; k += TPB) dst[k] = acc[k];
+  }
   if (tile_hist) {  // TPB == RADIX > nb: thread d owns digit d
     const int d = threadIdx.x;
     uint32_t tot = 0;
@@ -943,6 +1377,7 @@ struct Profile {
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
   Buf pk0, pk1, pv0, pv1, pbk, pcdf, poff, pq, pout;  // order statistics
+  Buf fctl, fseg, fgrp, fslab, fpack;                // one-sync equaln path
 };
 
 // exclusive scan of len u32 in place
@@ -1156,8 +1591,10 @@ static void assign_device(Profile &P, hipStream_t st, const double *de, int64_t 
                                 : nullptr;
     // >= ~1024 blocks where the input allows it
     const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
-    hipLaunchKernelGGL(assign_bins, dim3(ceil_div(nt, tpbk)), dim3(TPB), lds, st,
-                       (const double *)P.x.p, n, de, (int)nb, bins, cnt, th, nt, tpbk);
+    hipLaunchKernelGGL(assign_bins<false>, dim3(ceil_div(nt, tpbk)), dim3(TPB), lds, st,
+                       (const double *)P.x.p, n, de, (int)nb, bins, cnt, th, nt, tpbk,
+                       (const int64_t *)nullptr, (const double *)nullptr, FusedStats{},
+                       (double *)nullptr);
     P.csrh_ready = th != nullptr;
     PBX_HIP(hipGetLastError());
   }
@@ -1196,6 +1633,70 @@ static void csr_device(Profile &P, hipStream_t st) {
   if ((void *)va != P.perm.p)
     PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
   P.csr_ready = true;
+}
+
+// Launch the fused selection (mask + x + compaction + key range) of n
+// particles into P.x / P.w / P.idx; the kept count and key range stay on
+// the device (status words / selst).  Returns the tile count.
+static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, const double *mass,
+                              int64_t n, int on_device, int use_sphere, const double *sphere,
+                              const int64_t *fam, int nfam, int ndim) {
+  check_n(n);
+  if (ndim != 2 && ndim != 3) fail(PBX_ERR_VALUE, "ndim must be either 2 or 3");
+  if (nfam < 0 || nfam > MAX_FAM) fail(PBX_ERR_VALUE, "at most %d family ranges", MAX_FAM);
+  SelectParams sp{};
+  sp.use_sphere = use_sphere;
+  sp.ndim = ndim;
+  sp.nfam = nfam;
+  if (use_sphere) {
+    sp.cx = sphere[0];
+    sp.cy = sphere[1];
+    sp.cz = sphere[2];
+    sp.r2max = sphere[3];
+  }
+  for (int f = 0; f < nfam; ++f) {
+    sp.fam_lo[f] = fam[2 * f];
+    sp.fam_hi[f] = fam[2 * f + 1];
+  }
+  const double *d_pos = pos, *d_mass = mass;
+  if (!on_device && n) {
+    double *tp = (double *)P.keys0.get(sizeof(double) * 3 * (size_t)n);
+    PBX_HIP(hipMemcpyAsync(tp, pos, sizeof(double) * 3 * n, hipMemcpyHostToDevice, st));
+    d_pos = tp;
+    if (mass) {
+      double *tm2 = (double *)P.keys1.get(sizeof(double) * (size_t)n);
+      PBX_HIP(hipMemcpyAsync(tm2, mass, sizeof(double) * n, hipMemcpyHostToDevice, st));
+      d_mass = tm2;
+    }
+  }
+  const uint32_t nt = ntiles_of(n);
+  // per-tile look-back status words + ticket / watchdog (selection scratch)
+  // [stat nt][ctrl: ticket, watchdog][~min key][max key]: one zero fill
+  uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * ((size_t)nt + 3));
+  uint32_t *ctrl = (uint32_t *)(stat + nt);
+  double *xo = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
+  double *wo = (double *)P.w.get(sizeof(double) * (size_t)(n ? n : 1));
+  int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(n ? n : 1));
+  unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
+  PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * ((size_t)nt + 3), st));
+  if (n) {
+    hipLaunchKernelGGL(select_onepass, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, stat,
+                       ctrl, xo, wo, io, mm);
+    PBX_HIP(hipGetLastError());
+  }
+  return nt;
+}
+
+// the handle's state after a selection of `kept` particles (key range in P.mm)
+static void select_commit(Profile &P, int64_t kept) {
+  P.mm_valid = true;
+  P.n = kept;
+  P.has_w = true;
+  P.has_idx = true;
+  P.csr_ready = false;
+  P.csrh_ready = false;
+  P.ms.active = false;
+  P.nb = -1;
 }
 
 // device pointer of a per-element source: 0 = x, 1 = selection weights,
@@ -1352,7 +1853,8 @@ int pbx_profile_destroy(void *handle) {
                   &p->hist, &p->tsum, &p->edges, &p->counts, &p->minmax, &p->slab, &p->acc,
                   &p->field, &p->weight, &p->ranks, &p->bounds, &p->msH, &p->msR, &p->msG,
                   &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst, &p->accs,
-                  &p->pk0, &p->pk1, &p->pv0, &p->pv1, &p->pbk, &p->pcdf, &p->poff, &p->pq, &p->pout};
+                  &p->pk0, &p->pk1, &p->pv0, &p->pv1, &p->pbk, &p->pcdf, &p->poff, &p->pq, &p->pout,
+                  &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack};
     for (Buf *b : all) b->release();
     p->pin.release();
     delete p;
@@ -1383,54 +1885,15 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
                        int nfam, int ndim, int64_t *n_kept) {
   return guard([&] {
     Profile &P = as_profile(handle);
-    check_n(n);
-    if (ndim != 2 && ndim != 3) fail(PBX_ERR_VALUE, "ndim must be either 2 or 3");
-    if (nfam < 0 || nfam > MAX_FAM) fail(PBX_ERR_VALUE, "at most %d family ranges", MAX_FAM);
     Device &d = current_device();
     std::lock_guard<std::mutex> lk(d.mu);
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.select");
-    SelectParams sp{};
-    sp.use_sphere = use_sphere;
-    sp.ndim = ndim;
-    sp.nfam = nfam;
-    if (use_sphere) {
-      sp.cx = sphere[0];
-      sp.cy = sphere[1];
-      sp.cz = sphere[2];
-      sp.r2max = sphere[3];
-    }
-    for (int f = 0; f < nfam; ++f) {
-      sp.fam_lo[f] = fam[2 * f];
-      sp.fam_hi[f] = fam[2 * f + 1];
-    }
-    const double *d_pos = pos, *d_mass = mass;
-    if (!on_device && n) {
-      double *tp = (double *)P.keys0.get(sizeof(double) * 3 * (size_t)n);
-      PBX_HIP(hipMemcpyAsync(tp, pos, sizeof(double) * 3 * n, hipMemcpyHostToDevice, st));
-      d_pos = tp;
-      if (mass) {
-        double *tm2 = (double *)P.keys1.get(sizeof(double) * (size_t)n);
-        PBX_HIP(hipMemcpyAsync(tm2, mass, sizeof(double) * n, hipMemcpyHostToDevice, st));
-        d_mass = tm2;
-      }
-    }
-    uint32_t nt = ntiles_of(n);
-    // per-tile look-back status words + ticket / watchdog (selection scratch)
-    // [stat nt][ctrl: ticket, watchdog][~min key][max key]: one zero fill,
-    // one 32-byte readback from stat + nt - 1
-    uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * ((size_t)nt + 3));
-    uint32_t *ctrl = (uint32_t *)(stat + nt);
-    double *xo = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
-    double *wo = (double *)P.w.get(sizeof(double) * (size_t)(n ? n : 1));
-    int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(n ? n : 1));
-    unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
+    const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
+                                      nfam, ndim);
     int64_t kept = 0;
     if (n) {
-      PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * ((size_t)nt + 3), st));
-      hipLaunchKernelGGL(select_onepass, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, stat,
-                         ctrl, xo, wo, io, mm);
-      PBX_HIP(hipGetLastError());
+      uint64_t *stat = (uint64_t *)P.selst.p;
       uint64_t *h = (uint64_t *)P.pin.get(32);
       PBX_HIP(hipMemcpyAsync(h, stat + nt - 1, 32, hipMemcpyDeviceToHost, st));
       PBX_HIP(hipStreamSynchronize(st));
@@ -1440,14 +1903,7 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
       P.mm[0] = ~h[2];
       P.mm[1] = h[3];
     }
-    P.mm_valid = true;
-    P.n = kept;
-    P.has_w = true;
-    P.has_idx = true;
-    P.csr_ready = false;
-    P.csrh_ready = false;
-    P.ms.active = false;
-    P.nb = -1;
+    select_commit(P, kept);
     *n_kept = kept;
   });
 }
@@ -1810,6 +2266,252 @@ int pbx_profile_percentiles(void *handle, int f_src, const double *h_f, int w_sr
     if (nb > 0)
       PBX_HIP(hipMemcpyAsync(h_out, out, sizeof(double) * nb * nq, hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
+  });
+}
+
+// Selection + equaln radial profile with ONE host round trip
+// (RadialProfileBuilder equaln path: filters/filt.py:42-86 mask and r,
+// bins.py:720-746 edges, :346-395 assignment, proarray sums).  Same results
+// and errors as pbx_profile_select followed by pbx_profile_binned_equaln;
+// the distinct sums of the requested statistics (<= AS_MAXM) are
+// accumulated inside the assignment pass (more: separate moment passes).
+int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mass, int64_t n,
+                              int on_device, int use_sphere, const double *sphere,
+                              const int64_t *fam, int nfam, int ndim, int64_t nbins, int has_min,
+                              double bin_min, int has_max, double bin_max, int build_csr,
+                              int n_stats, const int *f_src, const int *w_src,
+                              const uint32_t *cols, int64_t *n_kept, double *h_edges,
+                              int64_t *n_edges, int64_t *h_counts, int64_t *n_valid,
+                              double *h_moments) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (nbins < 1) fail(PBX_ERR_VALUE, "nbins must be >= 1");
+    if (nbins + 1 > MS_MAXQ) fail(PBX_ERR_VALUE, "the fused path supports nbins <= %d", MS_MAXQ - 1);
+    if (n_stats < 0 || n_stats > 16) fail(PBX_ERR_VALUE, "at most 16 statistics");
+    for (int k = 0; k < n_stats; ++k)
+      if (f_src[k] < 0 || f_src[k] > 1 || w_src[k] < -1 || w_src[k] > 1)
+        fail(PBX_ERR_VALUE, "the fused path takes the profile's x / weights only");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    hipStream_t st = d.stream;
+    ScopedTimer tm("pbx.profile.radial_equaln");
+    const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
+                                      nfam, ndim);
+    const int nq = (int)nbins + 1;
+    // the window of bins.py:734-737 as key bounds (msel_begin)
+    bool empty_bounds = false;
+    uint64_t ka = 0ull, kb = ~0ull;
+    if (has_min || has_max) {
+      kb = ~0ull - 1;
+      if (has_min) {
+        if (bin_min != bin_min) empty_bounds = true;
+        else ka = dkey(bin_min);
+      }
+      if (has_max) {
+        if (bin_max != bin_max) empty_bounds = true;
+        else kb = std::min<uint64_t>(kb, dkey(bin_max));
+      }
+    }
+    uint64_t *stat = (uint64_t *)P.selst.p;
+    FusedCtl *ctl = (FusedCtl *)P.fctl.get(sizeof(FusedCtl));
+    const int64_t nb = nbins;
+    unsigned long long *cnt = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
+    uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG);
+    hipLaunchKernelGGL(fused_setup, dim3(1), dim3(1024), 0, st, (const uint64_t *)stat, nt,
+                       (const uint32_t *)(stat + nt), (const unsigned long long *)(stat + nt + 1), n,
+                       ka, kb, (int)empty_bounds, ctl, cnt, (int)nb, H);
+    const int64_t *n_dev = &ctl->n;
+    const double *x = (const double *)P.x.p;
+    // level 0 (rows -> H), resolve + groups, per-block offsets, gather,
+    // per-group finish -> edges
+    const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
+    uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
+    hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
+                       (const FusedCtl *)ctl, rows);
+    hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
+                       (const uint32_t *)rows, g0, H);
+    MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
+    uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)g0) * (MS_MAXQ + 1));
+    uint32_t *goff = gdig + (MS_MAXQ + 1), *gq = goff + (MS_MAXQ + 1);
+    uint32_t *boff = gq + (MS_MAXQ + 1);
+    hipLaunchKernelGGL(fused_resolve0, dim3(1), dim3(FR_TPB), 0, st, H, ctl, nbins, nq, R, gdig,
+                       goff, gq);
+    hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
+                       (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff);
+    uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n ? n : 1));
+    hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
+                       (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff, seg);
+    double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
+    hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
+                       (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
+                       (const uint64_t *)seg, de);
+    PBX_HIP(hipGetLastError());
+    // assignment (+ the statistics' distinct sums) with the device edges
+    uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n ? n : 1));
+    // distinct monomials of the requested columns (x^a w^b |x|^c |w|^d);
+    // mono[k][c] = its slot, -1 = column not accumulated (0)
+    FusedStats fs{};
+    fs.nm = 0;
+    const int64_t len = nb * NMOM;
+    double *accs = (double *)P.accs.get(sizeof(double) * (size_t)std::max<int64_t>(1, n_stats * len));
+    std::vector<int> mono((size_t)n_stats * NMOM, -1);
+    std::vector<uint32_t> mkey;
+    bool fuse = n_stats > 0;
+    for (int k = 0; k < n_stats && fuse; ++k)
+      for (int c = 0; c < NMOM; ++c) {
+        if (!((cols[k] >> c) & 1u)) continue;
+        const bool wc = (c == 0 || c == 1 || c == 2 || c == 5);
+        if (wc && w_src[k] < 0) continue;  // unweighted: the weighted columns stay 0
+        uint32_t e[4] = {0, 0, 0, 0};       // powers of x, w, |x|, |w|
+        const int fp = (c == 2 || c == 4) ? 2 : (c == 0 ? 0 : 1);
+        const bool fa = (c == 5 || c == 6);
+        e[(fa ? 2 : 0) + f_src[k]] += fp;
+        if (wc) e[w_src[k]] += 1;
+        const uint32_t key = e[0] | e[1] << 4 | e[2] << 8 | e[3] << 12;
+        int slot = -1;
+        for (size_t j = 0; j < mkey.size(); ++j)
+          if (mkey[j] == key) slot = (int)j;
+        if (slot < 0) {
+          if (fs.nm == AS_MAXM || (int64_t)(fs.nm + 1) * nb > 2 * LDS_MOM_BINS * NMOM) {
+            fuse = false;
+            break;
+          }
+          slot = fs.nm++;
+          mkey.push_back(key);
+          fs.f[slot] = f_src[k];
+          fs.w[slot] = w_src[k];
+          fs.col[slot] = c;
+        }
+        mono[(size_t)k * NMOM + c] = slot;
+      }
+    if (!fuse) fs.nm = 0;
+    double *maccs = nullptr;
+    P.csrh_ready = false;
+    uint32_t ablocks = 0;
+    if (n) {
+      const int64_t macc = (int64_t)fs.nm * nb;
+      size_t lds = sizeof(double) * (size_t)macc +
+                   ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
+                   sizeof(uint32_t) * (nb + 1);
+      if (lds > 150 * 1024) fail(PBX_ERR_VALUE, "too many bins for the device histogram (%lld)", (long long)nb);
+      uint32_t *th = (nb < RADIX) ? (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX)
+                                  : nullptr;
+      const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
+      ablocks = ceil_div(nt, tpbk);
+      double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
+      if (fs.nm)
+        hipLaunchKernelGGL(assign_bins<true>, dim3(ablocks), dim3(TPB), lds, st, x, n,
+                           (const double *)de, (int)nb, bins, cnt, th, nt, tpbk, n_dev,
+                           (const double *)P.w.p, fs, slab);
+      else
+        hipLaunchKernelGGL(assign_bins<false>, dim3(ablocks), dim3(TPB), lds, st, x, n,
+                           (const double *)de, (int)nb, bins, cnt, th, nt, tpbk, n_dev,
+                           (const double *)nullptr, fs, (double *)nullptr);
+      PBX_HIP(hipGetLastError());
+      P.csrh_ready = th != nullptr;
+      if (fs.nm) {
+        maccs = (double *)P.acc.get(sizeof(double) * (size_t)macc);
+        double *part = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * macc);
+        hipLaunchKernelGGL(reduce_slab_part, dim3(ceil_div(macc, TPB), SLAB_G), dim3(TPB), 0, st,
+                           (const double *)slab, (int64_t)ablocks, macc, part);
+        hipLaunchKernelGGL(reduce_slab_final, dim3(ceil_div(macc, TPB)), dim3(TPB), 0, st,
+                           (const double *)part, macc, maccs);
+        PBX_HIP(hipGetLastError());
+      }
+      if (build_csr) {  // stable counting sort of the bin ids, device length
+        int bits = 0;
+        while (((int64_t)1 << bits) <= nb) ++bits;
+        uint32_t *ka2 = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n);
+        uint32_t *kb2 = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n);
+        int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n);
+        int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n);
+        const uint32_t *kin = bins;
+        bool first = true;
+        for (int shift = 0; shift < bits; shift += 8) {
+          const bool last = shift + 8 >= bits;
+          if (first) {
+            prim::radix_pass<uint32_t>(P.csrh_ready ? P.csrh : P.hist, P.tsum, st, kin, nullptr,
+                                       VAL_IOTA, n, shift, last ? nullptr : ka2, va, P.csrh_ready,
+                                       n_dev);
+            first = false;
+          } else {
+            prim::radix_pass<uint32_t>(P.hist, P.tsum, st, ka2, va, VAL_ARRAY, n, shift,
+                                       last ? nullptr : kb2, vb, false, n_dev);
+            std::swap(ka2, kb2);
+            std::swap(va, vb);
+          }
+        }
+        P.csrh_ready = false;
+        if ((void *)va != P.perm.p)
+          PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+      }
+    }
+    // the results packed on the device, one copy, one sync
+    constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+    static_assert(sizeof(FusedCtl) % sizeof(double) == 0, "FusedCtl packs as doubles");
+    const int nsum = maccs ? fs.nm * (int)nb : 0;
+    const int ntot = NC + nq + (int)nb + nsum;
+    double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)ntot);
+    hipLaunchKernelGGL(fused_pack, dim3(ceil_div(ntot, TPB)), dim3(TPB), 0, st,
+                       (const FusedCtl *)ctl, (const double *)de, nq,
+                       (const unsigned long long *)cnt, (int)nb, (const double *)maccs, nsum, dpk);
+    double *hp = (double *)P.pin.get(sizeof(double) * (size_t)ntot);
+    PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * ntot, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    const FusedCtl *hc = (const FusedCtl *)hp;
+    const double *he = hp + NC;
+    const int64_t *hcn = (const int64_t *)(he + nq);
+    const double *hmo = (const double *)(hcn + nb);
+    const FusedCtl c = *hc;
+    if (c.err & 1) fail(PBX_ERR_RUNTIME, "selection look-back did not complete");
+    P.mm[0] = c.kmin;
+    P.mm[1] = c.kmax;
+    select_commit(P, c.n);
+    *n_kept = c.n;
+    if (c.n == 0) fail(PBX_ERR_VALUE, "Cannot create bins: input array is empty");
+    const int64_t m = c.m;
+    if ((c.err & 2) || m == 0) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
+    std::memcpy(h_edges, he, sizeof(double) * nq);
+    if (m < 2) {  // the reference's degenerate [s0, s0]: one bin, stepwise
+      h_edges[1] = h_edges[0];
+      PBX_HIP(hipMemcpyAsync(de, h_edges, sizeof(double) * 2, hipMemcpyHostToDevice, st));
+      assign_device(P, st, de, 1);
+      if (build_csr) csr_device(P, st);
+      for (int k = 0; k < n_stats; ++k)
+        moments_device(P, st, f_src[k], nullptr, P.field, w_src[k], nullptr, P.weight, cols[k],
+                       accs + k * NMOM);
+      PBX_HIP(hipMemcpyAsync(h_counts, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      if (n_stats)
+        PBX_HIP(hipMemcpyAsync(h_moments, accs, sizeof(double) * n_stats * NMOM,
+                               hipMemcpyDeviceToHost, st));
+      PBX_HIP(hipStreamSynchronize(st));
+      *n_edges = 2;
+    } else {
+      P.nb = nb;
+      P.csr_ready = build_csr != 0;
+      std::memcpy(h_counts, hcn, sizeof(int64_t) * nb);
+      if (fs.nm) {  // expand the monomial sums into [stat][bin][column]
+        for (int k = 0; k < n_stats; ++k)
+          for (int64_t b2 = 0; b2 < nb; ++b2)
+            for (int c = 0; c < NMOM; ++c) {
+              const int slot = mono[(size_t)k * NMOM + c];
+              h_moments[(k * nb + b2) * NMOM + c] = slot < 0 ? 0.0 : hmo[slot * nb + b2];
+            }
+      } else if (n_stats) {  // too many distinct sums to fuse: separate passes
+        for (int k = 0; k < n_stats; ++k)
+          moments_device(P, st, f_src[k], nullptr, P.field, w_src[k], nullptr, P.weight, cols[k],
+                         accs + k * len);
+        PBX_HIP(hipMemcpyAsync(h_moments, accs, sizeof(double) * n_stats * len,
+                               hipMemcpyDeviceToHost, st));
+        PBX_HIP(hipStreamSynchronize(st));
+      }
+      *n_edges = nq;
+    }
+    const int64_t nbo = *n_edges - 1;
+    int64_t sv = 0;
+    for (int64_t k = 0; k < nbo; ++k) sv += h_counts[k];
+    P.n_valid = sv;
+    *n_valid = sv;
   });
 }
 

@@ -114,6 +114,11 @@ _SIGNATURES: dict[str, tuple] = {
                                          _dp]),
     "pbx_profile_percentiles": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
                                         c_void_p, c_void_p]),
+    "pbx_profile_radial_equaln": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int,
+                                          c_void_p, c_void_p, c_int, c_int, c_int64, c_int,
+                                          c_double, c_int, c_double, c_int, c_int, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_void_p]),
     "pbx_profile_binned_equaln": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double,
                                           c_int, c_int, POINTER(c_int), POINTER(c_int),
                                           POINTER(c_uint32), _dp, POINTER(c_int64), _i64p,

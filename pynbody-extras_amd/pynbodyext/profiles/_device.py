@@ -66,6 +66,18 @@ class DeviceBins:
         """
         d = into if into is not None else cls()
         d.nbins, d._csr = None, None
+        args, keep = cls._select_args(pos, mass, sphere, families, ndim, on_device, n)
+        kept = c_int64(0)
+        nat.call("pbx_profile_select", d._h, *args, byref(kept))
+        del keep
+        d.n = kept.value
+        d.has_selection = True
+        return d
+
+    @staticmethod
+    def _select_args(pos, mass, sphere, families, ndim, on_device, n):
+        """ctypes arguments of a selection (pbx_profile_select order) and the
+        host arrays to keep alive during the call."""
         if on_device:
             p_pos, p_mass, n_part = pos, mass, int(n)
             keep = ()
@@ -77,7 +89,7 @@ class DeviceBins:
             mass = None if mass is None else np.ascontiguousarray(mass, dtype=np.float64)
             p_pos = pos.ctypes.data_as(c_void_p)
             p_mass = None if mass is None else mass.ctypes.data_as(c_void_p)
-            keep = (pos, mass)  # noqa: F841 - keep alive during the call
+            keep = (pos, mass)
         sph = np.zeros(4)
         if sphere is not None:
             cen, radius = sphere
@@ -92,13 +104,53 @@ class DeviceBins:
             if nfam == 0:  # an empty family set keeps nothing
                 fam = np.array([[0, 0]], dtype=np.int64)
                 nfam = 1
-        kept = c_int64(0)
-        nat.call("pbx_profile_select", d._h, p_pos, p_mass, n_part, int(on_device),
-                 int(sphere is not None), nat.dptr(sph), _i64(fam), nfam, int(ndim), byref(kept))
-        del keep
-        d.n = kept.value
-        d.has_selection = True
-        return d
+        keep = keep + (sph, fam)
+        args = (p_pos, p_mass, n_part, int(on_device), int(sphere is not None), nat.dptr(sph),
+                _i64(fam), nfam, int(ndim))
+        return args, keep
+
+    @classmethod
+    def radial_equaln(cls, pos, mass=None, *, nbins: int, sphere=None, families=None,
+                      ndim: int = 3, bin_min=None, bin_max=None, stats=(), csr=True,
+                      on_device: bool = False, n: int | None = None,
+                      into: "DeviceBins | None" = None):
+        """select() followed by binned_equaln() with ONE host round trip
+        (pbx_profile_radial_equaln).  Returns (handle, edges, counts, moments)
+        with the same values and errors as the two calls."""
+        d = into if into is not None else cls()
+        d.nbins, d._csr = None, None
+        args, keep = cls._select_args(pos, mass, sphere, families, ndim, on_device, n)
+        nq = int(nbins) + 1
+        k = len(stats)
+        fs = (c_int * max(k, 1))(*[int(s[0]) for s in stats])
+        ws = (c_int * max(k, 1))(*[int(s[1]) for s in stats])
+        cs = (c_uint32 * max(k, 1))(*[int(s[2]) & ALL_COLS for s in stats])
+        edges = np.empty(nq)
+        counts = np.zeros(nbins, dtype=np.int64)
+        mom = np.zeros((max(k, 1), nbins, NMOM))
+        kept, ne, nv = c_int64(0), c_int64(0), c_int64(0)
+        try:
+            nat.call("pbx_profile_radial_equaln", d._h, *args, int(nbins), int(bin_min is not None),
+                     float(bin_min) if bin_min is not None else 0.0, int(bin_max is not None),
+                     float(bin_max) if bin_max is not None else 0.0, int(bool(csr)), k, fs, ws,
+                     cs, byref(kept), nat.dptr(edges), byref(ne), _i64(counts), byref(nv),
+                     nat.dptr(mom))
+        except ValueError as e:
+            if str(e).startswith("index 0 is out of bounds"):
+                raise IndexError(str(e)) from None
+            raise
+        finally:
+            del keep
+            d.n = kept.value
+            d.has_selection = True
+        nb = ne.value - 1
+        d.nbins = nb
+        d.n_valid = nv.value
+        if nb != nbins:  # degenerate: one bin, compact layout [k][1][7]
+            mom = mom.reshape(-1)[: max(k, 1) * NMOM].reshape(max(k, 1), 1, NMOM)
+            counts = counts[:1].copy()
+        d.counts = counts
+        return d, edges[: ne.value].copy(), counts, [mom[i] for i in range(k)]
 
     def selection(self, idx=True, x=True, w=True):
         """(original indices int64, x, weights) of the fused selection."""

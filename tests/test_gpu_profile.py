@@ -471,3 +471,76 @@ def test_profile_median_uses_device(gpu, monkeypatch):
         ref, _ = pr.compute(r, m, perm, offsets, key)
         assert np.array_equal(got, ref), key
     assert len(calls) == 3
+
+
+@pytest.mark.parametrize("case", ["plummer", "sphere_family", "clip", "nan", "single", "dups",
+                                  "skewed", "empty_window", "nothing_kept", "many_stats"])
+def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
+    """pbx_profile_radial_equaln (select + equaln + assign + CSR + sums with
+    one host round trip, level-0 select + per-group LDS sort / radix finish)
+    = pbx_profile_select + pbx_profile_binned_equaln: edges, counts, CSR
+    bit-identical, sums to float-atomic rounding, same errors."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(21)
+    n = 400_000
+    pos = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    lo = hi = None
+    sphere, fams = None, None
+    nb = 128
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    if case == "sphere_family":
+        sphere, fams = ((0.5, -0.25, 0.0), 6.0), [(0, 150_000), (200_000, 390_000)]
+    elif case == "clip":
+        lo, hi = 0.5, 6.0
+    elif case == "nan":
+        pos[::50] = np.nan
+    elif case == "single":
+        lo, hi = 1.0, 1.0
+        pos[7] = [1.0, 0.0, 0.0]
+    elif case == "dups":  # heavy level-0 buckets of identical keys (radix finish)
+        pos = np.round(pos)
+    elif case == "skewed":  # one level-0 bucket of > 4096 distinct keys
+        pos = np.zeros((n, 3))
+        pos[:, 0] = 1.0 + rng.random(n) * 1e-9
+        pos[:100, 0] = rng.uniform(1e3, 2e3, 100)
+    elif case == "empty_window":
+        lo, hi = 1e9, 2e9
+    elif case == "nothing_kept":
+        sphere = ((1e6, 0.0, 0.0), 1.0)
+    elif case == "many_stats":  # more statistics than the assignment pass fuses
+        nb = 64
+        stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11), (SRC_X, SRC_NONE, 0x7f),
+                 (SRC_W, SRC_W, 0x7f), (SRC_X, SRC_W, 0x7f), (SRC_W, SRC_NONE, 0x18)]
+    b = DeviceBins.select(pos, mass, sphere=sphere, families=fams, ndim=3)
+    try:
+        if case in ("empty_window", "nothing_kept"):
+            exc = IndexError if case == "empty_window" else ValueError
+            with pytest.raises(exc) as e_ref:
+                b.binned_equaln(nb, lo, hi, stats)
+            with pytest.raises(exc) as e_got:
+                DeviceBins.radial_equaln(pos, mass, nbins=nb, sphere=sphere, families=fams,
+                                         bin_min=lo, bin_max=hi, stats=stats)
+            assert str(e_got.value) == str(e_ref.value)
+            return
+        e2, c2, m2 = b.binned_equaln(nb, lo, hi, stats)
+        a, e1, c1, m1 = DeviceBins.radial_equaln(pos, mass, nbins=nb, sphere=sphere,
+                                                 families=fams, bin_min=lo, bin_max=hi,
+                                                 stats=stats)
+        try:
+            assert a.n == b.n
+            assert np.array_equal(e1, e2, equal_nan=True), (e1, e2)
+            assert np.array_equal(c1, c2)
+            for got, ref in zip(m1, m2):
+                np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-300)
+            p1, o1 = a.csr()
+            p2, o2 = b.csr()
+            assert np.array_equal(p1, p2) and np.array_equal(o1, o2)
+            # the handle is usable afterwards like a stepwise one
+            np.testing.assert_allclose(a.moments(SRC_X, SRC_W, 0x7f), b.moments(SRC_X, SRC_W, 0x7f),
+                                       rtol=1e-12, atol=1e-300)
+        finally:
+            a.close()
+    finally:
+        b.close()
