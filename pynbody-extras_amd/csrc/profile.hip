@@ -52,21 +52,24 @@ struct SelectParams {
   int64_t fam_hi[MAX_FAM];
 };
 
-// mask and x of particle i (no FMA contraction: numpy evaluates these as
-// separate multiplies and adds; sqrt is correctly rounded)
-__device__ __forceinline__ bool select_one(const double *__restrict__ pos, int64_t i,
-                                          const SelectParams &p, double &x) {
+// family membership of particle i (contiguous slices; no slices = all)
+__device__ __forceinline__ bool in_family(int64_t i, const SelectParams &p) {
+  if (p.nfam == 0) return true;
+  bool in = false;
+  for (int f = 0; f < p.nfam; ++f) in |= (i >= p.fam_lo[f]) & (i < p.fam_hi[f]);
+  return in;
+}
+
+// mask and x of one particle from its loaded position (no FMA contraction:
+// numpy evaluates these as separate multiplies and adds; sqrt is correctly
+// rounded)
+__device__ __forceinline__ bool select_xyz(double px, double py, double pz, const SelectParams &p,
+                                          double &x) {
 #pragma clang fp contract(off)
   bool keep = true;
-  if (p.nfam > 0) {  // family slices first: particles outside them are never read
-    bool in = false;
-    for (int f = 0; f < p.nfam; ++f) in |= (i >= p.fam_lo[f]) & (i < p.fam_hi[f]);
-    if (!in) return false;
-  }
-  const double px = pos[3 * i + 0], py = pos[3 * i + 1], pz = pos[3 * i + 2];
   if (p.use_sphere) {
     double dx = px - p.cx, dy = py - p.cy, dz = pz - p.cz;
-    keep = keep && (((dx * dx + dy * dy) + dz * dz) < p.r2max);
+    keep = ((dx * dx + dy * dy) + dz * dz) < p.r2max;
   }
   x = (p.ndim == 2) ? __builtin_sqrt(px * px + py * py)
                     : __builtin_sqrt((px * px + py * py) + pz * pz);
@@ -85,6 +88,7 @@ __device__ __forceinline__ bool select_one(const double *__restrict__ pos, int64
 // whole L2 — the tile outputs — per tile).  status[t]
 // = flag (bits 62-63: 1 count of tile t, 2 inclusive prefix through t) |
 // value; ctrl[0] = ticket, ctrl[1] = watchdog flag (bounded spin).
+constexpr int MM_SLOTS = 8;  // key min / max slot pairs of the selection
 constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 62) - 1;
 
 __global__ void __launch_bounds__(TPB)
@@ -108,16 +112,38 @@ __global__ void __launch_bounds__(TPB)
   double xv[IPT];
   uint32_t keepbits = 0, c = 0;
   unsigned long long kmin = ~0ull, kmax = 0ull;
+  // all IPT positions in flight at once (particles outside the range or the
+  // family slices read particle 0: no branch around the loads, no extra lines)
+  double px[IPT], py[IPT], pz[IPT];
+  uint32_t inbits = 0;
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
-    int64_t i = wbase + k * 64 + lane;
-    bool keep = (i < n) && select_one(pos, i, p, xv[k]);
+    const int64_t i = wbase + k * 64 + lane;
+    const bool in = (i < n) && in_family(i, p);
+    inbits |= (uint32_t)in << k;
+    const double *q = pos + 3 * (in ? i : 0);
+    px[k] = q[0];
+    py[k] = q[1];
+    pz[k] = q[2];
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    bool keep = ((inbits >> k) & 1u) && select_xyz(px[k], py[k], pz[k], p, xv[k]);
     keepbits |= (uint32_t)keep << k;
     c += (uint32_t)__popcll(__ballot(keep));
     if (keep) {
       unsigned long long kk = dkey(xv[k]);
       kmin = kk < kmin ? kk : kmin;
       kmax = kk > kmax ? kk : kmax;
+    }
+  }
+  // the kept particles' weights: loads issued now, consumed after the look-back
+  double mv[IPT];
+  if (wo) {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int64_t i = wbase + k * 64 + lane;
+      mv[k] = mass ? mass[((keepbits >> k) & 1u) ? i : 0] : 1.0;
     }
   }
 #pragma unroll
@@ -142,8 +168,11 @@ __global__ void __launch_bounds__(TPB)
       b = wmax[ww] > b ? wmax[ww] : b;
     }
     if (lane == 0) {
-      if (a != ~0ull) atomicMax(&minmax[0], ~a);  // complemented min: zero-filled start
-      if (b != 0ull) atomicMax(&minmax[1], b);
+      // complemented min: zero-filled start; MM_SLOTS slot pairs (by tile)
+      // so that no single L2 address takes every block's atomics
+      unsigned long long *mmq = minmax + 2 * (tile % MM_SLOTS);
+      if (a != ~0ull) atomicMax(&mmq[0], ~a);
+      if (b != 0ull) atomicMax(&mmq[1], b);
       __hip_atomic_store(&status[tile], (tile == 0 ? kStPre : kStAgg) | (uint64_t)tot,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -192,7 +221,7 @@ __global__ void __launch_bounds__(TPB)
       int64_t i = wbase + k * 64 + lane;
       uint32_t pos_out = run + rank_below(b);
       xo[pos_out] = xv[k];
-      if (wo) wo[pos_out] = mass ? mass[i] : 1.0;
+      if (wo) wo[pos_out] = mv[k];
       io[pos_out] = (int32_t)i;
     }
     run += (uint32_t)__popcll(b);
@@ -575,8 +604,12 @@ __global__ void fused_setup(const uint64_t *__restrict__ stat, uint32_t nt,
     if (ctrl[1] || (last >> 62) != 2) c.err |= 1;
     c.n = (int64_t)(last & kStVal);
   }
-  c.kmin = ~mm[0];
-  c.kmax = mm[1];
+  c.kmin = ~0ull;
+  c.kmax = 0ull;
+  for (int q = 0; q < MM_SLOTS; ++q) {
+    c.kmin = ~mm[2 * q] < c.kmin ? ~mm[2 * q] : c.kmin;
+    c.kmax = mm[2 * q + 1] > c.kmax ? mm[2 * q + 1] : c.kmax;
+  }
   const uint64_t lo = ka > c.kmin ? ka : c.kmin;
   const uint64_t hi = kb < c.kmax ? kb : c.kmax;
   if (c.n == 0 || empty_bounds || lo > hi) {
@@ -917,14 +950,21 @@ __global__ void fused_pack(const FusedCtl *__restrict__ ctl, const double *__res
 
 // ----------------------------------------------------------------- assign
 // bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
-// x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379)
-template <typename E>
+// x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379).
+// Branchless lower bound over the nb+1 edges: the trip count depends on nb
+// only (uniform), so a wave's searches never diverge.  "e[k] < v" is
+// monotone in k for sorted edges (a NaN edge, sorted last by numpy, compares
+// false like +inf), so this is the first k with !(e[k] < v) exactly as the
+// classic bisection finds it.
+template <class E>
 __device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
-  int lo = 0, hi = nb + 1;  // first k with e[k] >= v  (NaN: never -> nb+1)
-  while (lo < hi) {
-    int mid = (lo + hi) >> 1;
-    if (e[mid] < v) lo = mid + 1; else hi = mid;
+  int base = 0, len = nb + 1;
+  while (len > 1) {
+    const int half = len >> 1;
+    base = (e[base + half] < v) ? base + half : base;
+    len -= half;
   }
+  const int lo = base + (e[base] < v ? 1 : 0);  // first k with e[k] >= v  (NaN: 0)
   int b = lo - 1;
   if (v == e[0]) b = 0;
   if (v == e[nb]) b = nb - 1;
@@ -957,7 +997,20 @@ struct FusedStats {
   int col[AS_MAXM];
 };
 
-template <bool MOM>
+// monomial value of column `col` (the expression moments_kernel sums):
+// a(f) in {1, f, f*f, |f|} times b in {1, ww}; x*1.0 is exact, so this is
+// bit-identical to the per-column expressions
+__device__ __forceinline__ double monomial(int col, double f, double ww) {
+  const int am = (col == 0) ? 0 : (col == 1 || col == 3) ? 1 : (col == 2 || col == 4) ? 2 : 3;
+  const bool wb = (col == 0 || col == 1 || col == 2 || col == 5);
+  const double a = am == 0 ? 1.0 : am == 1 ? f : am == 2 ? f * f : __builtin_fabs(f);
+  return wb ? a * ww : a;
+}
+
+// LDSE: the edges sit in LDS (nb + 1 <= LDS_EDGES); else they are read from
+// global memory (L2-resident).  Loads of tile t+1 (x and weights) are in
+// flight while tile t is binned.
+template <bool MOM, bool LDSE, bool WL>
 __global__ void __launch_bounds__(TPB)
     assign_bins(const double *__restrict__ x, int64_t n, const double *__restrict__ edges, int nb,
                 uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts,
@@ -970,72 +1023,67 @@ __global__ void __launch_bounds__(TPB)
   const int macc = MOM ? fs.nm * nb : 0;
   double *acc = (double *)smem;  // MOM: the block's sums
   double *e = acc + macc;
-  const bool lds_edges = (nb + 1) <= LDS_EDGES;
-  uint32_t *cnt = (uint32_t *)(e + (lds_edges ? nb + 1 : 0));
+  uint32_t *cnt = (uint32_t *)(e + (LDSE ? nb + 1 : 0));
   if (MOM)
     for (int k = threadIdx.x; k < macc; k += TPB) acc[k] = 0.0;
-  if (lds_edges)
+  if (LDSE)
     for (int k = threadIdx.x; k <= nb; k += TPB) e[k] = edges[k];
   for (int k = threadIdx.x; k <= nb; k += TPB) cnt[k] = 0;
   for (int k = threadIdx.x; k < AS_TILES * RADIX; k += TPB) (&th[0][0])[k] = 0;
   __syncthreads();
   const uint32_t t0 = blockIdx.x * tpbk;
   const uint32_t t1 = min(ntiles, t0 + tpbk);
-  // software-pipelined: the next tile's loads fly while this one is binned
-  double nv[IPT];
+  constexpr bool wload = MOM && WL;  // weights loaded (else 1.0)
+  // half tiles of AS_IPT x TPB elements; software-pipelined: the next half
+  // tile's loads (x and weights) fly while this one is binned (indices past
+  // n read element 0: unconditional loads, no branches)
+  constexpr int AS_IPT = IPT / 2, HALF = AS_IPT * TPB;
+  const uint32_t s0 = 2 * t0, s1 = 2 * t1;
+  double nv[AS_IPT], nw[AS_IPT];
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int64_t i = (int64_t)t0 * TILE + k * TPB + threadIdx.x;
-    nv[k] = (t0 < t1 && i < n) ? x[i] : 0.0;
+  for (int k = 0; k < AS_IPT; ++k) {
+    const int64_t i = (int64_t)s0 * HALF + k * TPB + threadIdx.x;
+    const int64_t j = (s0 < s1 && i < n) ? i : 0;
+    nv[k] = x[j];
+    if (wload) nw[k] = wsel[j];
   }
-  for (uint32_t t = t0; t < t1; ++t) {
-    const int64_t base = (int64_t)t * TILE;
-    double v[IPT];
+  for (uint32_t sh = s0; sh < s1; ++sh) {
+    const int64_t base = (int64_t)sh * HALF;
+    uint32_t *hrow = tile_hist ? th[(sh >> 1) - t0] : cnt;
+    double v[AS_IPT], wv[AS_IPT];
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
+    for (int k = 0; k < AS_IPT; ++k) {
       v[k] = nv[k];
-      const int64_t i = base + TILE + k * TPB + threadIdx.x;
-      nv[k] = (t + 1 < t1 && i < n) ? x[i] : 0.0;
+      wv[k] = wload ? nw[k] : 1.0;
+      const int64_t i = base + HALF + k * TPB + threadIdx.x;
+      const int64_t j = (sh + 1 < s1 && i < n) ? i : 0;
+      nv[k] = x[j];
+      if (wload) nw[k] = wsel[j];
     }
-    uint32_t b[IPT];  // the searches of all 16 keys interleave; LDS atomics after
+    uint32_t b[AS_IPT];  // the searches interleave; LDS atomics after
 #pragma unroll
-    for (int k = 0; k < IPT; ++k)  // (two uniform paths: a pointer that may be
-      b[k] = lds_edges ? bin_of(v[k], e, nb) : bin_of(v[k], edges, nb);  // either is flat)
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) {
+    for (int k = 0; k < AS_IPT; ++k) {
       const int64_t i = base + k * TPB + threadIdx.x;
-      if (i < n) atomicAdd(tile_hist ? &th[t - t0][b[k]] : &cnt[b[k]], 1u);
+      b[k] = (i < n) ? (LDSE ? bin_of(v[k], e, nb) : bin_of(v[k], edges, nb)) : (uint32_t)nb + 1;
     }
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
+    for (int k = 0; k < AS_IPT; ++k)
+      if (b[k] <= (uint32_t)nb) atomicAdd(&hrow[b[k]], 1u);
+#pragma unroll
+    for (int k = 0; k < AS_IPT; ++k) {
       const int64_t i = base + k * TPB + threadIdx.x;
       if (i < n) bins[i] = b[k];
     }
     if (MOM) {
-      double wv[IPT];
+      for (int q = 0; q < fs.nm; ++q) {  // uniform
+        const int col = fs.col[q], fq = fs.f[q], wq = fs.w[q];
+        double *aq = acc + (int64_t)q * nb;
 #pragma unroll
-      for (int k = 0; k < IPT; ++k) {
-        const int64_t i = base + k * TPB + threadIdx.x;
-        wv[k] = (wsel && i < n) ? wsel[i] : 1.0;
-      }
-#pragma unroll
-      for (int k = 0; k < IPT; ++k) {
-        const int64_t i = base + k * TPB + threadIdx.x;
-        if (i >= n || b[k] >= (uint32_t)nb) continue;
-        for (int q = 0; q < fs.nm; ++q) {  // uniform: scalar branches
-          const double f = fs.f[q] == 0 ? v[k] : wv[k];
-          const double ww = fs.w[q] == 0 ? v[k] : wv[k];
-          double val;  // the expression moments_kernel sums for this column
-          switch (fs.col[q]) {
-            case 0: val = ww; break;
-            case 1: val = f * ww; break;
-            case 2: val = (f * f) * ww; break;
-            case 3: val = f; break;
-            case 4: val = f * f; break;
-            case 5: val = __builtin_fabs(f) * ww; break;
-            default: val = __builtin_fabs(f); break;
-          }
-          atomicAdd(&acc[(int64_t)q * nb + b[k]], val);
+        for (int k = 0; k < AS_IPT; ++k) {
+          if (b[k] >= (uint32_t)nb) continue;
+          const double f = fq == 0 ? v[k] : wv[k];
+          const double ww = wq == 0 ? v[k] : wv[k];
+          atomicAdd(&aq[b[k]], monomial(col, f, ww));
         }
       }
     }
@@ -1058,6 +1106,26 @@ __global__ void __launch_bounds__(TPB)
   }
   for (int k = threadIdx.x; k < nb; k += TPB)
     if (cnt[k]) atomicAdd(&counts[k], (unsigned long long)cnt[k]);
+}
+
+template <bool MOM>
+static void launch_assign(uint32_t blocks, size_t lds, hipStream_t st, const double *x, int64_t n,
+                          const double *edges, int nb, uint32_t *bins,
+                          unsigned long long *counts, uint32_t *tile_hist, uint32_t ntiles,
+                          uint32_t tpbk, const int64_t *n_dev, const double *wsel,
+                          const FusedStats &fs, double *slab) {
+  const bool wl = MOM && wsel;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(TPB), lds, st, x, n, edges, nb, bins, counts,
+                       tile_hist, ntiles, tpbk, n_dev, wsel, fs, slab);
+  };
+  if ((nb + 1) <= LDS_EDGES) {
+    if (wl) go(assign_bins<MOM, true, true>);
+    else go(assign_bins<MOM, true, false>);
+  } else {
+    if (wl) go(assign_bins<MOM, false, true>);
+    else go(assign_bins<MOM, false, false>);
+  }
 }
 
 // ----------------------------------------------------------------- moments
@@ -1591,10 +1659,8 @@ static void assign_device(Profile &P, hipStream_t st, const double *de, int64_t 
                                 : nullptr;
     // >= ~1024 blocks where the input allows it
     const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
-    hipLaunchKernelGGL(assign_bins<false>, dim3(ceil_div(nt, tpbk)), dim3(TPB), lds, st,
-                       (const double *)P.x.p, n, de, (int)nb, bins, cnt, th, nt, tpbk,
-                       (const int64_t *)nullptr, (const double *)nullptr, FusedStats{},
-                       (double *)nullptr);
+    launch_assign<false>(ceil_div(nt, tpbk), lds, st, (const double *)P.x.p, n, de, (int)nb, bins,
+                         cnt, th, nt, tpbk, nullptr, nullptr, FusedStats{}, nullptr);
     P.csrh_ready = th != nullptr;
     PBX_HIP(hipGetLastError());
   }
@@ -1671,14 +1737,15 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, con
   }
   const uint32_t nt = ntiles_of(n);
   // per-tile look-back status words + ticket / watchdog (selection scratch)
-  // [stat nt][ctrl: ticket, watchdog][~min key][max key]: one zero fill
-  uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * ((size_t)nt + 3));
+  // [stat nt][ctrl: ticket, watchdog][MM_SLOTS x (~min key, max key)]: one zero fill
+  const size_t nst = (size_t)nt + 1 + 2 * MM_SLOTS;
+  uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * nst);
   uint32_t *ctrl = (uint32_t *)(stat + nt);
   double *xo = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
   double *wo = (double *)P.w.get(sizeof(double) * (size_t)(n ? n : 1));
   int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(n ? n : 1));
   unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
-  PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * ((size_t)nt + 3), st));
+  PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * nst, st));
   if (n) {
     hipLaunchKernelGGL(select_onepass, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, stat,
                        ctrl, xo, wo, io, mm);
@@ -1894,14 +1961,19 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
     int64_t kept = 0;
     if (n) {
       uint64_t *stat = (uint64_t *)P.selst.p;
-      uint64_t *h = (uint64_t *)P.pin.get(32);
-      PBX_HIP(hipMemcpyAsync(h, stat + nt - 1, 32, hipMemcpyDeviceToHost, st));
+      const size_t nh = 2 + 2 * MM_SLOTS;
+      uint64_t *h = (uint64_t *)P.pin.get(sizeof(uint64_t) * nh);
+      PBX_HIP(hipMemcpyAsync(h, stat + nt - 1, sizeof(uint64_t) * nh, hipMemcpyDeviceToHost, st));
       PBX_HIP(hipStreamSynchronize(st));
       const uint64_t last = h[0];
       if ((h[1] >> 32) || (last >> 62) != 2) fail(PBX_ERR_RUNTIME, "selection look-back did not complete");
       kept = (int64_t)(last & kStVal);
-      P.mm[0] = ~h[2];
-      P.mm[1] = h[3];
+      P.mm[0] = ~0ull;
+      P.mm[1] = 0ull;
+      for (int q = 0; q < MM_SLOTS; ++q) {
+        P.mm[0] = std::min<uint64_t>(P.mm[0], ~h[2 + 2 * q]);
+        P.mm[1] = std::max<uint64_t>(P.mm[1], h[3 + 2 * q]);
+      }
     }
     select_commit(P, kept);
     *n_kept = kept;
@@ -2400,13 +2472,11 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       ablocks = ceil_div(nt, tpbk);
       double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
       if (fs.nm)
-        hipLaunchKernelGGL(assign_bins<true>, dim3(ablocks), dim3(TPB), lds, st, x, n,
-                           (const double *)de, (int)nb, bins, cnt, th, nt, tpbk, n_dev,
-                           (const double *)P.w.p, fs, slab);
+        launch_assign<true>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, cnt, th,
+                            nt, tpbk, n_dev, (const double *)P.w.p, fs, slab);
       else
-        hipLaunchKernelGGL(assign_bins<false>, dim3(ablocks), dim3(TPB), lds, st, x, n,
-                           (const double *)de, (int)nb, bins, cnt, th, nt, tpbk, n_dev,
-                           (const double *)nullptr, fs, (double *)nullptr);
+        launch_assign<false>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, cnt, th,
+                             nt, tpbk, n_dev, nullptr, fs, nullptr);
       PBX_HIP(hipGetLastError());
       P.csrh_ready = th != nullptr;
       if (fs.nm) {
