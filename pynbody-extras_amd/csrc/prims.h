@@ -128,10 +128,16 @@ __global__ void __launch_bounds__(TPB) radix_hist(const K *__restrict__ keys, in
   cnt[threadIdx.x] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * TILE;
+  K kv[IPT];  // every load of the tile in flight first (index 0 past n)
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
-    int64_t i = base + k * TPB + threadIdx.x;
-    if (i < n) atomicAdd(&cnt[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    const int64_t i = base + k * TPB + threadIdx.x;
+    kv[k] = keys[i < n ? i : 0];
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int64_t i = base + k * TPB + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[(uint32_t)(kv[k] >> shift) & 255u], 1u);
   }
   __syncthreads();
   hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
@@ -164,11 +170,13 @@ __global__ void __launch_bounds__(TPB)
   const int64_t tbase = (int64_t)blockIdx.x * TILE;
   const int64_t wbase = tbase + (int64_t)w * (TILE / NWAVE);
   K key[IPT];
+  int32_t val[VM == VAL_ARRAY ? IPT : 1];
   uint32_t lp[IPT];  // rank among this wave's earlier elements of the same digit
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {  // every load of the tile in flight first
     const int64_t i = wbase + k * 64 + lane;
     key[k] = i < n ? kin[i] : (K)0;
+    if (VM == VAL_ARRAY) val[k] = vin[i < n ? i : 0];
   }
   // phase 1: per-wave digit counts; each element keeps its wave-local rank
   // (items in (k, lane) order = index order), so phase 2 needs no ballots
@@ -212,7 +220,7 @@ __global__ void __launch_bounds__(TPB)
       const uint32_t pos = run[w][d] + lp[k];
       sk[pos] = key[k];
       if (VM == VAL_IOTA) sv[pos] = (int32_t)i;
-      if (VM == VAL_ARRAY) sv[pos] = vin[i];
+      if (VM == VAL_ARRAY) sv[pos] = val[k];
     }
   }
   __syncthreads();
