@@ -117,6 +117,106 @@ __global__ void __launch_bounds__(TPB) scan_tiles(const uint32_t *in, int64_t le
   }
 }
 
+// Single-pass exclusive scan in place (decoupled look-back).  Tiles are
+// claimed in launch order by a ticket, so every predecessor a tile waits for
+// is already running (workgroup ids alone do not promise that: the XCDs
+// dispatch their shares independently); the block drawing the last ticket
+// re-arms the counter for the next launch.  Status word of a tile:
+// epoch (30 bits) | flag (2: 1 = tile sum, 2 = inclusive prefix) | value
+// (32); words of an earlier call carry another epoch and read as "not
+// ready", so the status array is zeroed only when it is (re)allocated.
+// The look-back is wave 0's: lane l inspects tile (hi - l).
+constexpr uint64_t kScAgg = 1ull << 32, kScPre = 2ull << 32;
+__global__ void __launch_bounds__(TPB)
+    scan_onepass(uint32_t *a, int64_t len, uint64_t *__restrict__ status,
+                 unsigned long long *__restrict__ ctr, uint32_t epoch) {
+  __shared__ uint32_t wsum[NWAVE];
+  __shared__ uint32_t s_tile, s_excl;
+  if (threadIdx.x == 0) {
+    const uint32_t t = (uint32_t)atomicAdd(&ctr[0], 1ull);
+    if (t == gridDim.x - 1) atomicExch(&ctr[0], 0ull);  // every ticket is out
+    s_tile = t;
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const int64_t base = (int64_t)tile * TILE + (int64_t)threadIdx.x * IPT;
+  uint32_t v[IPT];
+  uint32_t sum = 0;
+  const bool full = base + IPT <= len && (((uintptr_t)a & 15u) == 0);  // four 16-B loads
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < IPT / 4; ++k) {
+      const uint4 q = ((const uint4 *)(a + base))[k];
+      v[4 * k] = q.x;
+      v[4 * k + 1] = q.y;
+      v[4 * k + 2] = q.z;
+      v[4 * k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) v[k] = (base + k < len) ? a[base + k] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) sum += v[k];
+  uint32_t tot;
+  const uint32_t in_tile = block_excl_scan(sum, wsum, &tot);
+  const uint64_t tag = (uint64_t)epoch << 34;
+  if (threadIdx.x < 64) {
+    const uint32_t lane = threadIdx.x;
+    if (lane == 0)
+      __hip_atomic_store(&status[tile], tag | (tile == 0 ? kScPre : kScAgg) | tot, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t excl = 0, spins = 0;
+    for (int64_t hi = (int64_t)tile - 1; tile != 0 && hi >= 0;) {
+      const int64_t q = hi - (int64_t)lane;
+      uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : (tag | kScPre);  // before tile 0: an inclusive prefix of 0
+      const bool mine = (st >> 34) == epoch;
+      const uint32_t fl = mine ? (uint32_t)(st >> 32) & 3u : 0u;
+      const uint64_t pre = __ballot(fl == 2);
+      const uint64_t notready = __ballot(fl == 0);
+      const uint64_t need = pre ? (((pre & -pre) << 1) - 1) : ~0ull;  // lanes up to the nearest prefix
+      if (notready & need) {
+        if (++spins > (1u << 24)) {  // watchdog (the ticket order makes it unreachable)
+          if (lane == 0) atomicOr(&ctr[1], 1ull);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      uint32_t val = ((need >> lane) & 1ull) ? (uint32_t)st : 0u;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) val += __shfl_xor(val, o, 64);
+      excl += val;
+      if (pre) break;
+      hi -= 64;
+    }
+    if (lane == 0) {
+      if (tile != 0)
+        __hip_atomic_store(&status[tile], tag | kScPre | (uint32_t)(excl + tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_excl = excl;
+    }
+  }
+  __syncthreads();
+  uint32_t run = s_excl + in_tile;
+  uint32_t o[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    o[k] = run;
+    run += v[k];
+  }
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < IPT / 4; ++k)
+      ((uint4 *)(a + base))[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k)
+      if (base + k < len) a[base + k] = o[k];
+  }
+}
+
 }  // namespace
 
 template <typename K>
@@ -179,18 +279,27 @@ __global__ void __launch_bounds__(TPB)
     if (VM == VAL_ARRAY) val[k] = vin[i < n ? i : 0];
   }
   // phase 1: per-wave digit counts; each element keeps its wave-local rank
-  // (items in (k, lane) order = index order), so phase 2 needs no ballots
+  // (items in (k, lane) order = index order), so phase 2 needs no ballots.
+  // One leader per (k, digit) adds its peer count with a returning LDS
+  // atomic; a wave's LDS operations execute in issue order, so the 16
+  // atomics go out back to back and each returns the count of that digit
+  // in the wave's earlier items (no round trip per k).
+  uint32_t ret[IPT];
+  uint64_t pm[IPT];
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     const int64_t i = wbase + k * 64 + lane;
     const bool ok = i < n;
     const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
     const uint64_t m = peers8(d, __ballot(ok));
-    const uint32_t before = ok ? run[w][d] : 0u;
-    __builtin_amdgcn_wave_barrier();
-    if (ok && rank_below(m) == 0) run[w][d] = before + (uint32_t)__popcll(m);
-    __builtin_amdgcn_wave_barrier();
-    lp[k] = before + rank_below(m);
+    pm[k] = ok ? m : 0ull;
+    ret[k] = (ok && rank_below(m) == 0) ? atomicAdd(&run[w][d], (uint32_t)__popcll(m)) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
+    const uint32_t before = (uint32_t)__shfl((int)ret[k], leader, 64);
+    lp[k] = before + rank_below(pm[k]);
   }
   __syncthreads();
   // tile-local digit starts, per-wave starts inside them, global run starts
@@ -240,6 +349,7 @@ __global__ void __launch_bounds__(TPB)
 struct Buf {
   void *p = nullptr;
   size_t bytes = 0;
+  uint32_t epoch = 0;  // scan workspaces: the current call's status tag
   void *get(size_t need) {
     if (need <= bytes) return p;
     if (p) (void)hipFree(p);
@@ -282,27 +392,25 @@ struct HostBuf {
 
 static inline uint32_t ntiles_of(int64_t n) { return (uint32_t)((n + TILE - 1) / TILE); }
 
-// Exclusive scan of len u32 in place, any length (recursive over tile sums).
-// `tsum` holds the per-level tile sums (grown on demand, one region per
-// recursion level).
-static inline void scan_u32(Buf &tsum, hipStream_t st, uint32_t *a, int64_t len,
-                            size_t tsum_off = 0) {
+// Exclusive scan of len u32 in place, any length: one launch (scan_onepass).
+// `ws` holds [ticket counter, watchdog][status word per tile]; its host-side
+// epoch tags this call's status words.
+static inline void scan_u32(Buf &ws, hipStream_t st, uint32_t *a, int64_t len) {
   if (len <= 0) return;
-  int64_t nt = (len + TILE - 1) / TILE;
-  if (nt == 1) {
-    hipLaunchKernelGGL(scan_tiles, dim3(1), dim3(TPB), 0, st, a, len, nullptr, a);
-  } else {
-    // room for this level's sums plus every deeper level's
-    size_t need = tsum_off + sizeof(uint32_t) * (size_t)(nt + nt / TILE + 64);
-    if (tsum.bytes < need) {
-      if (tsum_off != 0) fail(PBX_ERR_RUNTIME, "scan workspace too small");
-      tsum.get(need);
+  const int64_t nt = (len + TILE - 1) / TILE;
+  if (nt >= ((int64_t)1 << 31)) fail(PBX_ERR_VALUE, "scan too long");
+  const size_t need = sizeof(uint64_t) * (size_t)(2 + nt);
+  if (ws.bytes < need || ++ws.epoch >= (1u << 30)) {
+    if (ws.bytes < need) {
+      ws.release();
+      ws.get(need + need / 2);
     }
-    uint32_t *sums = (uint32_t *)((char *)tsum.p + tsum_off);
-    hipLaunchKernelGGL(scan_tile_sums, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, sums);
-    scan_u32(tsum, st, sums, nt, tsum_off + sizeof(uint32_t) * (size_t)nt);
-    hipLaunchKernelGGL(scan_tiles, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, sums, a);
+    PBX_HIP(hipMemsetAsync(ws.p, 0, ws.bytes, st));
+    ws.epoch = 1;
   }
+  uint64_t *w = (uint64_t *)ws.p;
+  hipLaunchKernelGGL(scan_onepass, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, w + 2,
+                     (unsigned long long *)w, ws.epoch);
   PBX_HIP(hipGetLastError());
 }
 

@@ -589,18 +589,24 @@ struct FusedCtl {
 };
 
 
-__global__ void fused_setup(const uint64_t *__restrict__ stat, uint32_t nt,
-                            const uint32_t *__restrict__ ctrl,
-                            const unsigned long long *__restrict__ mm, int64_t n_in, uint64_t ka,
-                            uint64_t kb, int empty_bounds, FusedCtl *__restrict__ ctl,
-                            unsigned long long *__restrict__ counts, int nb,
-                            uint32_t *__restrict__ H) {
-  for (int k = threadIdx.x; k <= nb; k += blockDim.x) counts[k] = 0;  // for assign_bins
-  for (int k = threadIdx.x; k < MS0_DIG; k += blockDim.x) H[k] = 0;   // level-0 histogram
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// The step's control record from the selection's status words: kept count
+// (inclusive prefix of the last tile), key range (min over the slot pairs),
+// the equaln window's key base and level-0 digit geometry.  Every block of
+// fused_hist0 derives it (a few scalar loads); block 0 publishes it.
+struct FusedSetup {
+  const uint64_t *stat;
+  uint32_t nt;
+  int64_t n_in;
+  uint64_t ka, kb;
+  int empty_bounds;
+};
+
+__device__ FusedCtl fused_ctl(const FusedSetup &f) {
   FusedCtl c{};
-  if (n_in > 0) {
-    const uint64_t last = stat[nt - 1];
+  const uint32_t *ctrl = (const uint32_t *)(f.stat + f.nt);
+  const unsigned long long *mm = (const unsigned long long *)(f.stat + f.nt + 1);
+  if (f.n_in > 0) {
+    const uint64_t last = f.stat[f.nt - 1];
     if (ctrl[1] || (last >> 62) != 2) c.err |= 1;
     c.n = (int64_t)(last & kStVal);
   }
@@ -610,9 +616,9 @@ __global__ void fused_setup(const uint64_t *__restrict__ stat, uint32_t nt,
     c.kmin = ~mm[2 * q] < c.kmin ? ~mm[2 * q] : c.kmin;
     c.kmax = mm[2 * q + 1] > c.kmax ? mm[2 * q + 1] : c.kmax;
   }
-  const uint64_t lo = ka > c.kmin ? ka : c.kmin;
-  const uint64_t hi = kb < c.kmax ? kb : c.kmax;
-  if (c.n == 0 || empty_bounds || lo > hi) {
+  const uint64_t lo = f.ka > c.kmin ? f.ka : c.kmin;
+  const uint64_t hi = f.kb < c.kmax ? f.kb : c.kmax;
+  if (c.n == 0 || f.empty_bounds || lo > hi) {
     c.err |= 2;
     c.w0 = 1;
   } else {
@@ -622,19 +628,27 @@ __global__ void fused_setup(const uint64_t *__restrict__ stat, uint32_t nt,
     c.s0 = B - c.w0;
     c.lo = lo;
   }
-  *ctl = c;
+  return c;
 }
 
 // level-0 histogram rows (msel_hist0 with the base / shift / length from ctl)
 __global__ void __launch_bounds__(MS0_TPB)
-    fused_hist0(const double *__restrict__ x, uint64_t ka, uint64_t kb,
-                const FusedCtl *__restrict__ ctl, uint32_t *__restrict__ rows) {
+    fused_hist0(const double *__restrict__ x, FusedSetup fsu, FusedCtl *__restrict__ ctl_out,
+                unsigned long long *__restrict__ counts, int nb, uint32_t *__restrict__ H,
+                uint32_t *__restrict__ rows) {
   __shared__ uint32_t lh[MS0_DIG];
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
+  const FusedCtl ctl = fused_ctl(fsu);
+  if (blockIdx.x == 0) {  // the step's shared state: control record, zeroed counts / H
+    if (threadIdx.x == 0) *ctl_out = ctl;
+    for (int k = threadIdx.x; k <= nb; k += MS0_TPB) counts[k] = 0;  // for assign_bins
+    for (int k = threadIdx.x; k < MS0_DIG; k += MS0_TPB) H[k] = 0;   // for msel_reduce0
+  }
   __syncthreads();
-  const int64_t n = (ctl->err & 2) ? 0 : ctl->n;
-  const uint64_t base = ctl->lo;
-  const int s = ctl->s0;
+  const uint64_t ka = fsu.ka, kb = fsu.kb;
+  const int64_t n = (ctl.err & 2) ? 0 : ctl.n;
+  const uint64_t base = ctl.lo;
+  const int s = ctl.s0;
   constexpr int U = 8;
   for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * U; i0 < n; i0 += (int64_t)gridDim.x * MS0_TPB * U) {
     double v[U];
@@ -936,16 +950,25 @@ __global__ void __launch_bounds__(FR_TPB)
 }
 
 // the step's results in one contiguous staging block (one D2H copy):
-// [ctl][edges nq][counts nb][monomial sums nm x nb]
+// [ctl][edges nq][counts nb][monomial sums nm x nb]; the sums are the last
+// stage of the slab reduction (reduce_slab_final's fixed g order over the
+// SLAB_G partial rows `part`)
+constexpr int SLAB_G = 64;
 __global__ void fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges,
                            int nq, const unsigned long long *__restrict__ counts, int nb,
-                           const double *__restrict__ sums, int nsum, double *__restrict__ out) {
+                           const double *__restrict__ part, int nsum, double *__restrict__ out) {
   const int t = blockIdx.x * TPB + threadIdx.x;
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
   if (t < NC) out[t] = ((const double *)ctl)[t];
   else if (t < NC + nq) out[t] = edges[t - NC];
   else if (t < NC + nq + nb) out[t] = __builtin_bit_cast(double, counts[t - NC - nq]);
-  else if (t < NC + nq + nb + nsum) out[t] = sums[t - NC - nq - nb];
+  else if (t < NC + nq + nb + nsum) {
+    const int j = t - NC - nq - nb;
+    double s = 0.0;
+#pragma unroll 8
+    for (int g = 0; g < SLAB_G; ++g) s += part[(int64_t)g * nsum + j];
+    out[t] = s;
+  }
 }
 
 // ----------------------------------------------------------------- assign
@@ -1186,8 +1209,6 @@ __global__ void __launch_bounds__(TPB)
 // Sum slab[row][len] over rows in a fixed order (deterministic): first
 // SLAB_G partials, partial g = rows g, g+SLAB_G, ... in turn; then the
 // partials in g order.
-constexpr int SLAB_G = 64;
-
 __global__ void __launch_bounds__(TPB) reduce_slab_part(const double *__restrict__ slab,
                                                         int64_t rows, int64_t len,
                                                         double *__restrict__ part) {
@@ -2389,17 +2410,15 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     const int64_t nb = nbins;
     unsigned long long *cnt = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
     uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG);
-    hipLaunchKernelGGL(fused_setup, dim3(1), dim3(1024), 0, st, (const uint64_t *)stat, nt,
-                       (const uint32_t *)(stat + nt), (const unsigned long long *)(stat + nt + 1), n,
-                       ka, kb, (int)empty_bounds, ctl, cnt, (int)nb, H);
     const int64_t *n_dev = &ctl->n;
     const double *x = (const double *)P.x.p;
     // level 0 (rows -> H), resolve + groups, per-block offsets, gather,
     // per-group finish -> edges
     const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
     uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
-    hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
-                       (const FusedCtl *)ctl, rows);
+    const FusedSetup fsu{(const uint64_t *)stat, nt, n, ka, kb, (int)empty_bounds};
+    hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
+                       rows);
     hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
                        (const uint32_t *)rows, g0, H);
     MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
@@ -2480,12 +2499,10 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       PBX_HIP(hipGetLastError());
       P.csrh_ready = th != nullptr;
       if (fs.nm) {
-        maccs = (double *)P.acc.get(sizeof(double) * (size_t)macc);
-        double *part = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * macc);
+        // partial rows here, their fixed-order sum inside fused_pack
+        maccs = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * macc);
         hipLaunchKernelGGL(reduce_slab_part, dim3(ceil_div(macc, TPB), SLAB_G), dim3(TPB), 0, st,
-                           (const double *)slab, (int64_t)ablocks, macc, part);
-        hipLaunchKernelGGL(reduce_slab_final, dim3(ceil_div(macc, TPB)), dim3(TPB), 0, st,
-                           (const double *)part, macc, maccs);
+                           (const double *)slab, (int64_t)ablocks, macc, maccs);
         PBX_HIP(hipGetLastError());
       }
       if (build_csr) {  // stable counting sort of the bin ids, device length
