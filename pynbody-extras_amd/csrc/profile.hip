@@ -954,14 +954,28 @@ __global__ void __launch_bounds__(FR_TPB)
 // stage of the slab reduction (reduce_slab_final's fixed g order over the
 // SLAB_G partial rows `part`)
 constexpr int SLAB_G = 64;
+// offs (optional): the CSR pass's scanned [bin][tile] histogram (ntiles
+// columns); the bin counts are then its row-start differences, and are
+// also stored to `counts` (assign_bins skipped its global count atomics).
 __global__ void fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges,
-                           int nq, const unsigned long long *__restrict__ counts, int nb,
-                           const double *__restrict__ part, int nsum, double *__restrict__ out) {
+                           int nq, unsigned long long *__restrict__ counts, int nb,
+                           const double *__restrict__ part, int nsum, double *__restrict__ out,
+                           const uint32_t *__restrict__ offs, uint32_t ntiles) {
   const int t = blockIdx.x * TPB + threadIdx.x;
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
   if (t < NC) out[t] = ((const double *)ctl)[t];
   else if (t < NC + nq) out[t] = edges[t - NC];
-  else if (t < NC + nq + nb) out[t] = __builtin_bit_cast(double, counts[t - NC - nq]);
+  else if (t < NC + nq + nb) {
+    const int b = t - NC - nq;
+    unsigned long long c;
+    if (offs) {
+      c = (unsigned long long)(offs[(int64_t)(b + 1) * ntiles] - offs[(int64_t)b * ntiles]);
+      counts[b] = c;
+    } else {
+      c = counts[b];
+    }
+    out[t] = __builtin_bit_cast(double, c);
+  }
   else if (t < NC + nq + nb + nsum) {
     const int j = t - NC - nq - nb;
     double s = 0.0;
@@ -1106,7 +1120,11 @@ __global__ void __launch_bounds__(TPB)
           if (b[k] >= (uint32_t)nb) continue;
           const double f = fq == 0 ? v[k] : wv[k];
           const double ww = wq == 0 ? v[k] : wv[k];
+#ifdef PBX_DIAG_NO_MOM_ATOMICS  // timing diagnostic only: sums not accumulated
+          if (monomial(col, f, ww) == 1234.5) aq[0] = 0.0;
+#else
           atomicAdd(&aq[b[k]], monomial(col, f, ww));
+#endif
         }
       }
     }
@@ -1127,8 +1145,9 @@ __global__ void __launch_bounds__(TPB)
     if (d <= nb) cnt[d] = tot;
     __syncthreads();
   }
-  for (int k = threadIdx.x; k < nb; k += TPB)
-    if (cnt[k]) atomicAdd(&counts[k], (unsigned long long)cnt[k]);
+  if (counts)  // (null: the caller derives the counts from the scanned tile_hist)
+    for (int k = threadIdx.x; k < nb; k += TPB)
+      if (cnt[k]) atomicAdd(&counts[k], (unsigned long long)cnt[k]);
 }
 
 template <bool MOM>
@@ -2479,6 +2498,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     double *maccs = nullptr;
     P.csrh_ready = false;
     uint32_t ablocks = 0;
+    const uint32_t *cnt_offs = nullptr;  // scanned CSR histogram the counts come from
     if (n) {
       const int64_t macc = (int64_t)fs.nm * nb;
       size_t lds = sizeof(double) * (size_t)macc +
@@ -2490,11 +2510,15 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
       ablocks = ceil_div(nt, tpbk);
       double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
+      // with the CSR pass, the bin counts are differences of its scanned
+      // [bin][tile] histogram: no global count atomics in assign_bins
+      if (th && build_csr) cnt_offs = th;
+      unsigned long long *acnt = cnt_offs ? nullptr : cnt;
       if (fs.nm)
-        launch_assign<true>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, cnt, th,
+        launch_assign<true>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, acnt, th,
                             nt, tpbk, n_dev, (const double *)P.w.p, fs, slab);
       else
-        launch_assign<false>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, cnt, th,
+        launch_assign<false>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, acnt, th,
                              nt, tpbk, n_dev, nullptr, fs, nullptr);
       PBX_HIP(hipGetLastError());
       P.csrh_ready = th != nullptr;
@@ -2541,7 +2565,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)ntot);
     hipLaunchKernelGGL(fused_pack, dim3(ceil_div(ntot, TPB)), dim3(TPB), 0, st,
                        (const FusedCtl *)ctl, (const double *)de, nq,
-                       (const unsigned long long *)cnt, (int)nb, (const double *)maccs, nsum, dpk);
+                       cnt, (int)nb, (const double *)maccs, nsum, dpk, cnt_offs, nt);
     double *hp = (double *)P.pin.get(sizeof(double) * (size_t)ntot);
     PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * ntot, hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
