@@ -68,14 +68,16 @@ def main():
             "read_bytes_per_launch": r["read_bytes_corrected_avg"], "write_bytes_per_launch": r["write_bytes_avg"],
             "note": "2 x FETCH_SIZE + WRITE_SIZE; node records / leaf particles are scalar loads",
             "source": src}, indent=1))
-    prof = [r for r in rows if "pbx::prof::" in r["kernel"] or "radix_" in r["kernel"] or "scan_t" in r["kernel"]]
+    prof = [r for r in rows if "pbx::prof::" in r["kernel"] or "radix_" in r["kernel"] or "scan_t" in r["kernel"]
+            or "scan_onepass" in r["kernel"]]
     if prof and not skip_profile:
         # one profile step of the PMC run = the dispatches of its selection
         # kernel (one per step); shared radix/scan kernels of the tree build
         # are excluded from the per-step sum
         sel = [r for r in prof if "select_onepass" in r["kernel"]]
         steps = sel[0]["dispatches"] if sel else None
-        own = [r for r in prof if "pbx::prof::" in r["kernel"] or "unsigned int, 1>" in r["kernel"]]
+        own = [r for r in prof if "pbx::prof::" in r["kernel"] or "unsigned int, 1>" in r["kernel"]
+               or "scan_onepass" in r["kernel"]]
         per_step = None
         if steps:
             per_step = sum(((r["read_bytes_corrected_avg"] or 0) + (r["write_bytes_avg"] or 0))
