@@ -850,11 +850,13 @@ __device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, doubl
 
 // SOFT: h_max guard and/or softened leaf sums are live.  The walk hides
 // its scalar-load latency with other waves: orders <= 3 without softening
-// are held to 8 waves per SIMD (the compiler then parks a few SGPRs in VGPR
-// lanes instead of taking ~100 SGPRs, which leaves room for only 6 waves).
+// are held to 7 waves per SIMD (~100 SGPRs would leave room for only 6; at
+// 8 the 64-VGPR budget spilled to scratch inside the accept path and parked
+// ~30 SGPRs in VGPR lanes — 110 v_readlane; at 7: 88 SGPRs, 65 VGPRs, no
+// scratch, 20 v_readlane, walk 44.5 -> 44.2 ms same-box A/B).
 template <int P, int WANT, bool SOFT, bool RAW>
 __global__ void __launch_bounds__(WALK_TPB)
-    __attribute__((amdgpu_waves_per_eu((P <= 3 && !SOFT) ? 8 : 1, 8)))
+    __attribute__((amdgpu_waves_per_eu((P <= 3 && !SOFT) ? 7 : 1, 7)))
     walk_kernel(WalkParams wp) {
   constexpr int RS = rec_stride<P>();
   constexpr int NCH = (P == 2 || P == 3) ? RS / 8 : 1;  // chunks loaded eagerly
