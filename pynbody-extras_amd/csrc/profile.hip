@@ -91,13 +91,18 @@ __device__ __forceinline__ bool select_xyz(double px, double py, double pz, cons
 constexpr int MM_SLOTS = 8;  // key min / max slot pairs of the selection
 constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 62) - 1;
 
-__global__ void __launch_bounds__(TPB)
+// BT threads per block, one 4096-element tile each: 256 (16 items per
+// lane) on big inputs; 1024 (4 per lane) when there are few tiles, so a
+// small input still puts 16 waves on each CU.
+template <int BT>
+__global__ void __launch_bounds__(BT)
     select_onepass(const double *__restrict__ pos, const double *__restrict__ mass, int64_t n,
                    SelectParams p, uint64_t *__restrict__ status, uint32_t *__restrict__ ctrl,
                    double *__restrict__ xo, double *__restrict__ wo, int32_t *__restrict__ io,
                    unsigned long long *__restrict__ minmax) {
-  __shared__ uint32_t wcnt[NWAVE];
-  __shared__ unsigned long long wmin[NWAVE], wmax[NWAVE];
+  constexpr int NW = BT / 64, SI = TILE / BT;  // waves, items per lane
+  __shared__ uint32_t wcnt[NW];
+  __shared__ unsigned long long wmin[NW], wmax[NW];
   __shared__ uint32_t s_tile, s_excl;
 #ifdef PBX_DIAG_NO_TICKET
   if (threadIdx.x == 0) s_tile = blockIdx.x;
@@ -108,16 +113,16 @@ __global__ void __launch_bounds__(TPB)
   const uint32_t tile = s_tile;
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
-  const int64_t wbase = (int64_t)tile * TILE + (int64_t)w * (TILE / NWAVE);
-  double xv[IPT];
+  const int64_t wbase = (int64_t)tile * TILE + (int64_t)w * (TILE / NW);
+  double xv[SI];
   uint32_t keepbits = 0, c = 0;
   unsigned long long kmin = ~0ull, kmax = 0ull;
-  // all IPT positions in flight at once (particles outside the range or the
+  // all SI positions in flight at once (particles outside the range or the
   // family slices read particle 0: no branch around the loads, no extra lines)
-  double px[IPT], py[IPT], pz[IPT];
+  double px[SI], py[SI], pz[SI];
   uint32_t inbits = 0;
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
+  for (int k = 0; k < SI; ++k) {
     const int64_t i = wbase + k * 64 + lane;
     const bool in = (i < n) && in_family(i, p);
     inbits |= (uint32_t)in << k;
@@ -127,7 +132,7 @@ __global__ void __launch_bounds__(TPB)
     pz[k] = q[2];
   }
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
+  for (int k = 0; k < SI; ++k) {
     bool keep = ((inbits >> k) & 1u) && select_xyz(px[k], py[k], pz[k], p, xv[k]);
     keepbits |= (uint32_t)keep << k;
     c += (uint32_t)__popcll(__ballot(keep));
@@ -138,10 +143,10 @@ __global__ void __launch_bounds__(TPB)
     }
   }
   // the kept particles' weights: loads issued now, consumed after the look-back
-  double mv[IPT];
+  double mv[SI];
   if (wo) {
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
+    for (int k = 0; k < SI; ++k) {
       const int64_t i = wbase + k * 64 + lane;
       mv[k] = mass ? mass[((keepbits >> k) & 1u) ? i : 0] : 1.0;
     }
@@ -162,7 +167,7 @@ __global__ void __launch_bounds__(TPB)
   if (w == 0) {  // wave 0: publish this tile's count, then look back 64 tiles at a time
     uint32_t tot = 0;
     unsigned long long a = wmin[0], b = wmax[0];
-    for (int ww = 0; ww < NWAVE; ++ww) {
+    for (int ww = 0; ww < NW; ++ww) {
       tot += wcnt[ww];
       a = wmin[ww] < a ? wmin[ww] : a;
       b = wmax[ww] > b ? wmax[ww] : b;
@@ -214,7 +219,7 @@ __global__ void __launch_bounds__(TPB)
   uint32_t run = s_excl;
   for (int ww = 0; ww < w; ++ww) run += wcnt[ww];
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
+  for (int k = 0; k < SI; ++k) {
     bool keep = (keepbits >> k) & 1u;
     uint64_t b = __ballot(keep);
     if (keep) {
@@ -1047,8 +1052,10 @@ __device__ __forceinline__ double monomial(int col, double f, double ww) {
 // LDSE: the edges sit in LDS (nb + 1 <= LDS_EDGES); else they are read from
 // global memory (L2-resident).  Loads of tile t+1 (x and weights) are in
 // flight while tile t is binned.
-template <bool MOM, bool LDSE, bool WL>
-__global__ void __launch_bounds__(TPB)
+// BT threads per block: 256, or 1024 when every block takes one tile of a
+// small input (more waves per CU for the same tiles)
+template <bool MOM, bool LDSE, bool WL, int BT>
+__global__ void __launch_bounds__(BT)
     assign_bins(const double *__restrict__ x, int64_t n, const double *__restrict__ edges, int nb,
                 uint32_t *__restrict__ bins, unsigned long long *__restrict__ counts,
                 uint32_t *__restrict__ tile_hist, uint32_t ntiles, uint32_t tpbk,
@@ -1062,24 +1069,24 @@ __global__ void __launch_bounds__(TPB)
   double *e = acc + macc;
   uint32_t *cnt = (uint32_t *)(e + (LDSE ? nb + 1 : 0));
   if (MOM)
-    for (int k = threadIdx.x; k < macc; k += TPB) acc[k] = 0.0;
+    for (int k = threadIdx.x; k < macc; k += BT) acc[k] = 0.0;
   if (LDSE)
-    for (int k = threadIdx.x; k <= nb; k += TPB) e[k] = edges[k];
-  for (int k = threadIdx.x; k <= nb; k += TPB) cnt[k] = 0;
-  for (int k = threadIdx.x; k < AS_TILES * RADIX; k += TPB) (&th[0][0])[k] = 0;
+    for (int k = threadIdx.x; k <= nb; k += BT) e[k] = edges[k];
+  for (int k = threadIdx.x; k <= nb; k += BT) cnt[k] = 0;
+  for (int k = threadIdx.x; k < AS_TILES * RADIX; k += BT) (&th[0][0])[k] = 0;
   __syncthreads();
   const uint32_t t0 = blockIdx.x * tpbk;
   const uint32_t t1 = min(ntiles, t0 + tpbk);
   constexpr bool wload = MOM && WL;  // weights loaded (else 1.0)
-  // half tiles of AS_IPT x TPB elements; software-pipelined: the next half
+  // half tiles of AS_IPT x BT elements; software-pipelined: the next half
   // tile's loads (x and weights) fly while this one is binned (indices past
   // n read element 0: unconditional loads, no branches)
-  constexpr int AS_IPT = IPT / 2, HALF = AS_IPT * TPB;
+  constexpr int AS_IPT = TILE / BT / 2, HALF = AS_IPT * BT;
   const uint32_t s0 = 2 * t0, s1 = 2 * t1;
   double nv[AS_IPT], nw[AS_IPT];
 #pragma unroll
   for (int k = 0; k < AS_IPT; ++k) {
-    const int64_t i = (int64_t)s0 * HALF + k * TPB + threadIdx.x;
+    const int64_t i = (int64_t)s0 * HALF + k * BT + threadIdx.x;
     const int64_t j = (s0 < s1 && i < n) ? i : 0;
     nv[k] = x[j];
     if (wload) nw[k] = wsel[j];
@@ -1092,7 +1099,7 @@ __global__ void __launch_bounds__(TPB)
     for (int k = 0; k < AS_IPT; ++k) {
       v[k] = nv[k];
       wv[k] = wload ? nw[k] : 1.0;
-      const int64_t i = base + HALF + k * TPB + threadIdx.x;
+      const int64_t i = base + HALF + k * BT + threadIdx.x;
       const int64_t j = (sh + 1 < s1 && i < n) ? i : 0;
       nv[k] = x[j];
       if (wload) nw[k] = wsel[j];
@@ -1100,7 +1107,7 @@ __global__ void __launch_bounds__(TPB)
     uint32_t b[AS_IPT];  // the searches interleave; LDS atomics after
 #pragma unroll
     for (int k = 0; k < AS_IPT; ++k) {
-      const int64_t i = base + k * TPB + threadIdx.x;
+      const int64_t i = base + k * BT + threadIdx.x;
       b[k] = (i < n) ? (LDSE ? bin_of(v[k], e, nb) : bin_of(v[k], edges, nb)) : (uint32_t)nb + 1;
     }
 #pragma unroll
@@ -1108,7 +1115,7 @@ __global__ void __launch_bounds__(TPB)
       if (b[k] <= (uint32_t)nb) atomicAdd(&hrow[b[k]], 1u);
 #pragma unroll
     for (int k = 0; k < AS_IPT; ++k) {
-      const int64_t i = base + k * TPB + threadIdx.x;
+      const int64_t i = base + k * BT + threadIdx.x;
       if (i < n) bins[i] = b[k];
     }
     if (MOM) {
@@ -1132,21 +1139,23 @@ __global__ void __launch_bounds__(TPB)
   __syncthreads();
   if (MOM) {
     double *dst = slab + (int64_t)blockIdx.x * macc;
-    for (int k = threadIdx.x; k < macc; k += TPB) dst[k] = acc[k];
+    for (int k = threadIdx.x; k < macc; k += BT) dst[k] = acc[k];
   }
-  if (tile_hist) {  // TPB == RADIX > nb: thread d owns digit d
+  if (tile_hist) {  // RADIX > nb: thread d < RADIX owns digit d
     const int d = threadIdx.x;
-    uint32_t tot = 0;
-    for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t c = th[t - t0][d];
-      tile_hist[(int64_t)d * ntiles + t] = c;
-      tot += c;
+    if (d < RADIX) {
+      uint32_t tot = 0;
+      for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t c = th[t - t0][d];
+        tile_hist[(int64_t)d * ntiles + t] = c;
+        tot += c;
+      }
+      if (d <= nb) cnt[d] = tot;
     }
-    if (d <= nb) cnt[d] = tot;
     __syncthreads();
   }
   if (counts)  // (null: the caller derives the counts from the scanned tile_hist)
-    for (int k = threadIdx.x; k < nb; k += TPB)
+    for (int k = threadIdx.x; k < nb; k += BT)
       if (cnt[k]) atomicAdd(&counts[k], (unsigned long long)cnt[k]);
 }
 
@@ -1157,16 +1166,25 @@ static void launch_assign(uint32_t blocks, size_t lds, hipStream_t st, const dou
                           uint32_t tpbk, const int64_t *n_dev, const double *wsel,
                           const FusedStats &fs, double *slab) {
   const bool wl = MOM && wsel;
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(TPB), lds, st, x, n, edges, nb, bins, counts,
+  const bool wide = tpbk == 1 && ntiles < 1024;  // few tiles: 1024-thread blocks
+  auto go = [&](auto kern, int bt) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(bt), lds, st, x, n, edges, nb, bins, counts,
                        tile_hist, ntiles, tpbk, n_dev, wsel, fs, slab);
   };
-  if ((nb + 1) <= LDS_EDGES) {
-    if (wl) go(assign_bins<MOM, true, true>);
-    else go(assign_bins<MOM, true, false>);
+  if (wide) {
+    if ((nb + 1) <= LDS_EDGES) {
+      if (wl) go(assign_bins<MOM, true, true, 1024>, 1024);
+      else go(assign_bins<MOM, true, false, 1024>, 1024);
+    } else {
+      if (wl) go(assign_bins<MOM, false, true, 1024>, 1024);
+      else go(assign_bins<MOM, false, false, 1024>, 1024);
+    }
+  } else if ((nb + 1) <= LDS_EDGES) {
+    if (wl) go(assign_bins<MOM, true, true, TPB>, TPB);
+    else go(assign_bins<MOM, true, false, TPB>, TPB);
   } else {
-    if (wl) go(assign_bins<MOM, false, true>);
-    else go(assign_bins<MOM, false, false>);
+    if (wl) go(assign_bins<MOM, false, true, TPB>, TPB);
+    else go(assign_bins<MOM, false, false, TPB>, TPB);
   }
 }
 
@@ -1787,8 +1805,12 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, con
   unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
   PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * nst, st));
   if (n) {
-    hipLaunchKernelGGL(select_onepass, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp, stat,
-                       ctrl, xo, wo, io, mm);
+    if (nt < 1024)
+      hipLaunchKernelGGL(select_onepass<1024>, dim3(nt), dim3(1024), 0, st, d_pos, d_mass, n, sp,
+                         stat, ctrl, xo, wo, io, mm);
+    else
+      hipLaunchKernelGGL(select_onepass<TPB>, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp,
+                         stat, ctrl, xo, wo, io, mm);
     PBX_HIP(hipGetLastError());
   }
   return nt;

@@ -5,7 +5,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-idx = [i for i, r in enumerate(rows) if r['Kernel_Name'].startswith('pbx::prof::select_onepass')]
+idx = [i for i, r in enumerate(rows) if 'select_onepass' in r['Kernel_Name']]
 print("selects (grid):", [rows[i]['Grid_Size_X'] for i in idx])
 which = [int(a) for a in sys.argv[2:]] or [1]
 for w in which:
