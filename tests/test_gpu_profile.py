@@ -204,6 +204,27 @@ def test_fused_builder_matches_oracle_config3(gpu):
                                rtol=1e-12)
 
 
+def test_fused_config3_large_input_path(gpu):
+    """Config 3 at 8M particles (> 1024 tiles): the 256-thread selection, the
+    8-tiles-per-block assignment and the bin counts taken from the scanned
+    CSR histogram, bit-exact against the oracle (the 1M case above runs the
+    small-input 1024-thread kernels)."""
+    n = 8_000_000
+    sim = plummer_snapshot(n, seed=1004)
+    prof = RadialProfileBuilder(ndim=3, weight="mass", bins_type="equaln", nbins=128).filter(
+        Sphere(10.0) & FamilyFilter("dm"))(sim)
+    pos, mass = plummer(n, seed=1004)
+    mask = pr.sphere_mask(pos, 10.0)
+    mask[family_slices(n)["dm"].stop:] = False
+    ref = pr.radial_profile(pos, mass, mask, "equaln", 128)
+    assert np.array_equal(np.asarray(prof.bin_edges), ref["edges"])
+    assert np.array_equal(prof.npart_bins, ref["counts"])
+    perm, offsets = prof.bins.binind.csr
+    assert np.array_equal(offsets, ref["offsets"]) and np.array_equal(perm, ref["perm"])
+    np.testing.assert_allclose(np.asarray(prof["mass"]["sum"]), ref["mass_sum"], rtol=1e-12)
+    np.testing.assert_allclose(np.asarray(prof["r"]), ref["r_mean"], rtol=1e-12)
+
+
 def test_fused_equals_unfused(gpu):
     sim = plummer_snapshot(50_000, seed=9)
     filt = Sphere(5.0, cen=(0.1, 0.0, -0.2)) & FamilyFilter("gas")
