@@ -381,30 +381,36 @@ __global__ void root_init(BuildView v, double cx, double cy, double cz, double h
 
 // children ranges of every frontier node: lb[f*9 + o] = first particle with
 // digit >= o at level d (digits are sorted inside a node's range)
+// 8 lanes per frontier node: lane o finds the first index of the node's
+// (path-sorted) range with digit >= o by its own binary search (the eight
+// searches of a node run side by side instead of one after another);
+// lb[f][0..7] = those starts, lb[f][8] = end, cnt[f] = non-empty octants.
 __global__ void split_count(BuildView v, const int32_t *__restrict__ frontier, int64_t F, int d,
                             int32_t *__restrict__ lb, uint32_t *__restrict__ cnt) {
-  int64_t f = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (f >= F) return;
-  const int32_t node = frontier[f];
-  const int64_t s = v.nstart[node], e = s + v.ncount[node];
-  int64_t lo = s;
-  uint32_t c = 0;
-  int64_t prev = s;
-  for (uint32_t o = 0; o < 8; ++o) {
-    int64_t a = lo, b = e;  // first index in [lo, e) with digit >= o
-    while (a < b) {
-      int64_t mid = (a + b) >> 1;
-      if (digit_at(v, mid, d) < o) a = mid + 1;
-      else b = mid;
-    }
-    lb[f * 9 + o] = (int32_t)a;
-    if (o > 0 && a > prev) ++c;
-    prev = a;
-    lo = a;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  const int64_t f = t >> 3;
+  const uint32_t o = (uint32_t)(t & 7);
+  const bool ok = f < F;
+  int64_t s = 0, e = 0;
+  if (ok) {
+    const int32_t node = frontier[f];
+    s = v.nstart[node];
+    e = s + v.ncount[node];
   }
-  lb[f * 9 + 8] = (int32_t)e;
-  if (e > prev) ++c;
-  cnt[f] = c;
+  int64_t a = s, b = e;  // first index in [s, e) with digit >= o
+  while (a < b) {
+    const int64_t mid = (a + b) >> 1;
+    if (digit_at(v, mid, d) < o) a = mid + 1;
+    else b = mid;
+  }
+  // start of the next octant (lane o + 1; the end for o = 7), same 8-lane group
+  const int64_t an = __shfl_down(a, 1, 8);
+  const int64_t nxt = o == 7 ? e : an;
+  const uint64_t nonempty = __ballot(ok && nxt > a);
+  if (!ok) return;
+  lb[f * 9 + o] = (int32_t)a;
+  if (o == 7) lb[f * 9 + 8] = (int32_t)e;
+  if (o == 0) cnt[f] = (uint32_t)__popcll((nonempty >> (threadIdx.x & 56)) & 0xffull);
 }
 
 // create the children of every frontier node (ids base + exclusive scan);
@@ -562,14 +568,34 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
   const int32_t nc = v.nchild[k];
   if (nc == 0) {
     const int32_t s = v.nstart[k], c = v.ncount[k];
+    // leaves of up to PL particles: every record in flight at once, then the
+    // same ordered sums as the general loop (identical results)
+    constexpr int PL = 8;
+    double4 rr[PL];
+    const bool small = c <= PL;
+    if (small) {
+#pragma unroll
+      for (int q = 0; q < PL; ++q) rr[q] = v.rec[q < c ? s + q : s];
+    }
     {
 #pragma clang fp contract(off)
-      for (int32_t j = s; j < s + c; ++j) {
-        const double4 r = v.rec[j];
-        mass += r.w;
-        cx += r.x * r.w;
-        cy += r.y * r.w;
-        cz += r.z * r.w;
+      if (small) {
+#pragma unroll
+        for (int q = 0; q < PL; ++q) {
+          if (q >= c) break;
+          mass += rr[q].w;
+          cx += rr[q].x * rr[q].w;
+          cy += rr[q].y * rr[q].w;
+          cz += rr[q].z * rr[q].w;
+        }
+      } else {
+        for (int32_t j = s; j < s + c; ++j) {
+          const double4 r = v.rec[j];
+          mass += r.w;
+          cx += r.x * r.w;
+          cy += r.y * r.w;
+          cz += r.z * r.w;
+        }
       }
       if (mass > 0.0) {
         cx /= mass;
@@ -582,24 +608,37 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
     if (P >= 2 && mass != 0.0) {
       double M[ncoef(P)];
       static_for<ncoef(P)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
-      for (int32_t j = s; j < s + c; ++j) {
-        const double4 r = v.rec[j];
-        p2m_add<P>(M, r.w, r.x - cx, r.y - cy, r.z - cz);
+      if (small) {
+#pragma unroll
+        for (int q = 0; q < PL; ++q) {
+          if (q >= c) break;
+          p2m_add<P>(M, rr[q].w, rr[q].x - cx, rr[q].y - cy, rr[q].z - cz);
+        }
+      } else {
+        for (int32_t j = s; j < s + c; ++j) {
+          const double4 r = v.rec[j];
+          p2m_add<P>(M, r.w, r.x - cx, r.y - cy, r.z - cz);
+        }
       }
       static_for<ncoef(P)>(
           [&](auto qc) { v.mom[(int64_t)k * ncoef(P) + decltype(qc)::value] = M[decltype(qc)::value]; });
     }
   } else {
     const int32_t f = v.nfirst[k];
+    double4 cq[8];  // an octree node has at most 8 children: all in flight at once
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cq[q] = v.com[q < nc ? f + q : f];
     {
 #pragma clang fp contract(off)
-      for (int32_t ch = f; ch < f + nc; ++ch) {
-        const double4 q = v.com[ch];
-        if (q.w == 0.0) continue;
-        mass += q.w;
-        cx += q.x * q.w;
-        cy += q.y * q.w;
-        cz += q.z * q.w;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (q >= nc) break;
+        const double4 c4 = cq[q];
+        if (c4.w == 0.0) continue;
+        mass += c4.w;
+        cx += c4.x * c4.w;
+        cy += c4.y * c4.w;
+        cz += c4.z * c4.w;
       }
       if (mass > 0.0) {
         cx /= mass;
@@ -612,10 +651,12 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
     if (P >= 2 && mass != 0.0) {
       double M[ncoef(P)];
       static_for<ncoef(P)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
-      for (int32_t ch = f; ch < f + nc; ++ch) {
-        const double4 q = v.com[ch];
-        if (q.w == 0.0) continue;
-        m2m_add<P>(M, v.mom + (int64_t)ch * ncoef(P), cx - q.x, cy - q.y, cz - q.z);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (q >= nc) break;
+        const double4 c4 = cq[q];
+        if (c4.w == 0.0) continue;
+        m2m_add<P>(M, v.mom + (int64_t)(f + q) * ncoef(P), cx - c4.x, cy - c4.y, cz - c4.z);
       }
       static_for<ncoef(P)>(
           [&](auto qc) { v.mom[(int64_t)k * ncoef(P) + decltype(qc)::value] = M[decltype(qc)::value]; });
@@ -1229,7 +1270,7 @@ static bool split_levels(Octree &T, hipStream_t st) {
     int32_t *lb = (int32_t *)T.lb.get(4 * 9 * (size_t)F);
     uint32_t *cnt = (uint32_t *)T.cnt.get(4 * (size_t)(F + 1));
     PBX_HIP(hipMemsetAsync(cnt + F, 0, 4, st));
-    hipLaunchKernelGGL(split_count, dim3(nblk(F)), dim3(TPB), 0, st, v, front, F, d, lb, cnt);
+    hipLaunchKernelGGL(split_count, dim3(nblk(8 * F)), dim3(TPB), 0, st, v, front, F, d, lb, cnt);
     scan_u32(T.tsum, st, cnt, F + 1);
     const int64_t C = read_u32(cnt + F, st);
     if (T.nn + C >= ((int64_t)1 << 31)) fail(PBX_ERR_VALUE, "octree too large (%lld nodes)", (long long)(T.nn + C));
