@@ -385,12 +385,17 @@ __global__ void root_init(BuildView v, double cx, double cy, double cz, double h
 // (path-sorted) range with digit >= o by its own binary search (the eight
 // searches of a node run side by side instead of one after another);
 // lb[f][0..7] = those starts, lb[f][8] = end, cnt[f] = non-empty octants.
+// Also zeroes the scan sentinel cnt[F] and the child flags (8F + 1 words,
+// the most children the level can create) for split_make.
 __global__ void split_count(BuildView v, const int32_t *__restrict__ frontier, int64_t F, int d,
-                            int32_t *__restrict__ lb, uint32_t *__restrict__ cnt) {
+                            int32_t *__restrict__ lb, uint32_t *__restrict__ cnt,
+                            uint32_t *__restrict__ flags) {
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
   const int64_t f = t >> 3;
   const uint32_t o = (uint32_t)(t & 7);
   const bool ok = f < F;
+  if (t <= 8 * F) flags[t] = 0u;
+  if (t == 0) cnt[F] = 0u;
   int64_t s = 0, e = 0;
   if (ok) {
     const int32_t node = frontier[f];
@@ -454,9 +459,18 @@ __global__ void split_make(BuildView v, const int32_t *__restrict__ frontier, in
   }
 }
 
-__global__ void compact_frontier(const uint32_t *__restrict__ scanned, int64_t C,
-                                 int32_t level_base, int32_t *__restrict__ out) {
-  int64_t c = (int64_t)blockIdx.x * TPB + threadIdx.x;
+// the next frontier; C (children made this level) is the scanned child
+// count total cnt[F]; (C, next frontier size) go to sizes[0..1] for the
+// level's single host read-back
+__global__ void compact_frontier(const uint32_t *__restrict__ scanned,
+                                 const uint32_t *__restrict__ cnt, int64_t F, int32_t level_base,
+                                 int32_t *__restrict__ out, uint32_t *__restrict__ sizes) {
+  const int64_t C = cnt[F];
+  const int64_t c = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (c == 0) {
+    sizes[0] = (uint32_t)C;
+    sizes[1] = scanned[C];
+  }
   if (c >= C) return;
   if (scanned[c + 1] != scanned[c]) out[scanned[c]] = level_base + (int32_t)c;
 }
@@ -1267,26 +1281,32 @@ static bool split_levels(Octree &T, hipStream_t st) {
   while (F > 0) {
     if (d >= LPW * T.nwords) return false;
     int32_t *front = T.front0.as<int32_t>();
+    // one host read-back per level: the node arrays, flags and next frontier
+    // are sized for the most children the level can make (8F); the actual
+    // count C and next frontier size come back together at the end
+    const int64_t Cmax = 8 * F;
+    if (T.nn + Cmax >= ((int64_t)1 << 31))
+      fail(PBX_ERR_VALUE, "octree too large (%lld nodes)", (long long)(T.nn + Cmax));
     int32_t *lb = (int32_t *)T.lb.get(4 * 9 * (size_t)F);
     uint32_t *cnt = (uint32_t *)T.cnt.get(4 * (size_t)(F + 1));
-    PBX_HIP(hipMemsetAsync(cnt + F, 0, 4, st));
-    hipLaunchKernelGGL(split_count, dim3(nblk(8 * F)), dim3(TPB), 0, st, v, front, F, d, lb, cnt);
-    scan_u32(T.tsum, st, cnt, F + 1);
-    const int64_t C = read_u32(cnt + F, st);
-    if (T.nn + C >= ((int64_t)1 << 31)) fail(PBX_ERR_VALUE, "octree too large (%lld nodes)", (long long)(T.nn + C));
-    ensure_nodes(T, T.nn + C, st);
+    uint32_t *flags = (uint32_t *)T.flags.get(4 * (size_t)(Cmax + 1));
+    ensure_nodes(T, T.nn + Cmax, st);
     bind();
-    uint32_t *flags = (uint32_t *)T.flags.get(4 * (size_t)(C + 1));
-    PBX_HIP(hipMemsetAsync(flags + C, 0, 4, st));
+    hipLaunchKernelGGL(split_count, dim3(nblk(Cmax + 1)), dim3(TPB), 0, st, v, front, F, d, lb,
+                       cnt, flags);
+    scan_u32(T.tsum, st, cnt, F + 1);
     hipLaunchKernelGGL(split_make, dim3(nblk(F)), dim3(TPB), 0, st, v, front, F, lb, cnt,
                        (int32_t)T.nn, flags);
-    scan_u32(T.tsum, st, flags, C + 1);
-    const int64_t F2 = read_u32(flags + C, st);
-    int32_t *front2 = (int32_t *)T.front1.get(4 * (size_t)std::max<int64_t>(F2, 1));
-    if (F2 > 0)
-      hipLaunchKernelGGL(compact_frontier, dim3(nblk(C)), dim3(TPB), 0, st, flags, C,
-                         (int32_t)T.nn, front2);
+    scan_u32(T.tsum, st, flags, Cmax + 1);
+    int32_t *front2 = (int32_t *)T.front1.get(4 * (size_t)std::max<int64_t>(Cmax, 1));
+    uint32_t *sizes = (uint32_t *)T.small.get(64);
+    hipLaunchKernelGGL(compact_frontier, dim3(nblk(Cmax)), dim3(TPB), 0, st, flags, cnt, F,
+                       (int32_t)T.nn, front2, sizes);
     PBX_HIP(hipGetLastError());
+    uint32_t hs[2];
+    PBX_HIP(hipMemcpyAsync(hs, sizes, 8, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    const int64_t C = hs[0], F2 = hs[1];
     T.nn += C;
     T.lvl.push_back((int32_t)T.nn);
     std::swap(T.front0, T.front1);
