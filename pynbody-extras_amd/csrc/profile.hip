@@ -955,19 +955,36 @@ __global__ void __launch_bounds__(FR_TPB)
 }
 
 // the step's results in one contiguous staging block (one D2H copy):
-// [ctl][edges nq][counts nb][monomial sums nm x nb]; the sums are the last
-// stage of the slab reduction (reduce_slab_final's fixed g order over the
-// SLAB_G partial rows `part`)
-constexpr int SLAB_G = 64;
+// [ctl][edges nq][counts nb][monomial sums nm x nb].  Blocks [0, nhead)
+// copy the head; block nhead + j sums column j of the assign slab (`rows`
+// block rows, fixed order: thread t takes rows t, t + TPB, ... in turn,
+// then a fixed LDS tree) — the slab reduction and the packing in one launch.
 // offs (optional): the CSR pass's scanned [bin][tile] histogram (ntiles
 // columns); the bin counts are then its row-start differences, and are
 // also stored to `counts` (assign_bins skipped its global count atomics).
-__global__ void fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges,
-                           int nq, unsigned long long *__restrict__ counts, int nb,
-                           const double *__restrict__ part, int nsum, double *__restrict__ out,
-                           const uint32_t *__restrict__ offs, uint32_t ntiles) {
-  const int t = blockIdx.x * TPB + threadIdx.x;
+constexpr int SLAB_G = 64;  // partial groups of the general (moments) path
+__global__ void __launch_bounds__(TPB)
+    fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges, int nq,
+               unsigned long long *__restrict__ counts, int nb, const double *__restrict__ slab,
+               int64_t rows, int nsum, double *__restrict__ out, const uint32_t *__restrict__ offs,
+               uint32_t ntiles, int nhead) {
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+  if ((int)blockIdx.x >= nhead) {
+    __shared__ double red[TPB];
+    const int j = (int)blockIdx.x - nhead;
+    double v = 0.0;
+    for (int64_t r = threadIdx.x; r < rows; r += TPB) v += slab[r * nsum + j];
+    red[threadIdx.x] = v;
+    __syncthreads();
+#pragma unroll
+    for (int h = TPB / 2; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[NC + nq + nb + j] = red[0];
+    return;
+  }
+  const int t = blockIdx.x * TPB + threadIdx.x;
   if (t < NC) out[t] = ((const double *)ctl)[t];
   else if (t < NC + nq) out[t] = edges[t - NC];
   else if (t < NC + nq + nb) {
@@ -980,13 +997,6 @@ __global__ void fused_pack(const FusedCtl *__restrict__ ctl, const double *__res
       c = counts[b];
     }
     out[t] = __builtin_bit_cast(double, c);
-  }
-  else if (t < NC + nq + nb + nsum) {
-    const int j = t - NC - nq - nb;
-    double s = 0.0;
-#pragma unroll 8
-    for (int g = 0; g < SLAB_G; ++g) s += part[(int64_t)g * nsum + j];
-    out[t] = s;
   }
 }
 
@@ -2544,13 +2554,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                              nt, tpbk, n_dev, nullptr, fs, nullptr);
       PBX_HIP(hipGetLastError());
       P.csrh_ready = th != nullptr;
-      if (fs.nm) {
-        // partial rows here, their fixed-order sum inside fused_pack
-        maccs = (double *)P.slabp.get(sizeof(double) * (size_t)SLAB_G * macc);
-        hipLaunchKernelGGL(reduce_slab_part, dim3(ceil_div(macc, TPB), SLAB_G), dim3(TPB), 0, st,
-                           (const double *)slab, (int64_t)ablocks, macc, maccs);
-        PBX_HIP(hipGetLastError());
-      }
+      if (fs.nm) maccs = slab;  // its rows are summed inside fused_pack
       if (build_csr) {  // stable counting sort of the bin ids, device length
         int bits = 0;
         while (((int64_t)1 << bits) <= nb) ++bits;
@@ -2585,9 +2589,10 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     const int nsum = maccs ? fs.nm * (int)nb : 0;
     const int ntot = NC + nq + (int)nb + nsum;
     double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)ntot);
-    hipLaunchKernelGGL(fused_pack, dim3(ceil_div(ntot, TPB)), dim3(TPB), 0, st,
-                       (const FusedCtl *)ctl, (const double *)de, nq,
-                       cnt, (int)nb, (const double *)maccs, nsum, dpk, cnt_offs, nt);
+    const int nhead = (int)ceil_div(NC + nq + (int)nb, TPB);
+    hipLaunchKernelGGL(fused_pack, dim3(nhead + nsum), dim3(TPB), 0, st, (const FusedCtl *)ctl,
+                       (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
+                       (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead);
     double *hp = (double *)P.pin.get(sizeof(double) * (size_t)ntot);
     PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * ntot, hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
