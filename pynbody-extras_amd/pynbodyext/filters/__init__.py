@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .._pyn import get_family
+from .._pyn import filt, get_family
 from ..calculate import AndFilter, FilterBase, NotFilter, OrFilter, resolve_value_in_units
 
 __all__ = ["FilterBase", "Sphere", "FamilyFilter", "AndFilter", "OrFilter", "NotFilter"]
@@ -56,32 +56,47 @@ class Sphere(FilterBase):
         return f"Sphere(radius={self.radius!r}, cen={self.cen!r})"
 
 
+def _family_slice(sim, fam):
+    """The family's contiguous index range in ``sim`` through pynbody's own
+    snapshot interface (``SimSnap._get_family_slice``, as the reference's
+    chunk.py:186,232 uses it), or None when the members do not form one
+    range (e.g. an index-list sub-snapshot) or ``sim`` has no families."""
+    get = getattr(sim, "_get_family_slice", None)
+    if get is None:
+        return None
+    sl = get(fam)
+    if not isinstance(sl, slice) or sl.step not in (None, 1):
+        return None
+    start, stop, _ = sl.indices(len(sim))
+    return slice(start, max(start, stop))
+
+
 class FamilyFilter(FilterBase):
-    """Particles of one family (dm, gas, star, ...)."""
+    """Particles of one family (dm, gas, star, ...).  The mask is pynbody's
+    own ``filt.FamilyFilter(family)(sim)`` (reference filt.py:84-86 delegates
+    to it); the device selection takes the family's index range."""
 
     def __init__(self, family):
         if isinstance(family, str):
             family = get_family(family, False)
         self.family = family
 
+    def _family(self, sim):
+        fam = self.family
+        if callable(fam) and not hasattr(fam, "name"):
+            fam = fam(sim)
+        return get_family(fam, False) if isinstance(fam, str) else fam
+
     def build_mask(self, sim, params=None):
-        mask = np.zeros(len(sim), dtype=bool)
-        fam = get_family(self.family(sim) if callable(self.family) and not hasattr(self.family, "name")
-                         else self.family)
-        slices = getattr(sim, "_family_slices", {})
-        sl = slices.get(fam)
-        if sl is not None:
-            mask[sl] = True
-        return mask
+        return np.asarray(filt.FamilyFilter(self._family(sim))(sim), dtype=bool)
 
     def device_spec(self, sim):
-        slices = getattr(sim, "_family_slices", None)
-        if slices is None or callable(self.family) and not hasattr(self.family, "name"):
+        if callable(self.family) and not hasattr(self.family, "name"):
             return None
-        sl = slices.get(get_family(self.family))
+        sl = _family_slice(sim, self._family(sim))
         if sl is None:
-            return {"families": []}
-        return {"families": [(int(sl.start), int(sl.stop))]}
+            return None
+        return {"families": [(sl.start, sl.stop)] if sl.stop > sl.start else []}
 
     def __repr__(self):
         return f"FamilyFilter({getattr(self.family, 'name', self.family)!r})"

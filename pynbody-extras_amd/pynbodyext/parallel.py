@@ -347,7 +347,15 @@ def distributed_equaln(dev, comm, nbins: int, bin_min=None, bin_max=None) -> np.
     radix select (DeviceBins.key_range / msel_*); ``comm`` the all-reduces
     (Communicator: allreduce_host for the key range, allreduce in place on
     the device histogram).  The histograms are summed before every resolve,
-    so each rank picks the same digits and no particle moves."""
+    so each rank picks the same digits and no particle moves.
+
+    The digit histograms (and the window counts the resolve derives from
+    them) are u32: the global kept count is all-reduced in i64 first and a
+    total that does not fit u32 is rejected instead of silently wrapping."""
+    total = int(comm.allreduce_host(np.array([int(dev.n)], dtype=np.int64))[0])
+    if total >= 1 << 32:
+        raise ValueError(f"distributed equaln over {total} particles: the u32 radix-select "
+                         "histograms hold at most 2**32 - 1")
     kmin, kmax = dev.key_range()
     kmin = int(comm.allreduce_host(np.array([kmin], dtype=np.uint64), OP_MIN)[0])
     kmax = int(comm.allreduce_host(np.array([kmax], dtype=np.uint64), OP_MAX)[0])

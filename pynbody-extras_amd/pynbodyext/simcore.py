@@ -249,9 +249,9 @@ class SimSnap:
         units_map = units_map or {}
         self._units = {k: as_unit(u) for k, u in units_map.items()}
         # family name -> slice of the particle index range
-        self._family_slices: dict[Family, slice] = {}
+        self._family_slice: dict[Family, slice] = {}
         for name, sl in (families or {}).items():
-            self._family_slices[get_family(name, True)] = sl
+            self._family_slice[get_family(name, True)] = sl
         self._derived: dict[str, np.ndarray] = {}
 
     # ---- basic protocol ----------------------------------------------------
@@ -259,10 +259,15 @@ class SimSnap:
         return self._n
 
     def families(self) -> list[Family]:
-        return [f for f, sl in self._family_slices.items() if sl.stop > sl.start]
+        return [f for f, sl in self._family_slice.items() if sl.stop > sl.start]
 
     def family_slice(self, fam) -> slice:
-        return self._family_slices[get_family(fam)]
+        return self._family_slice[get_family(fam)]
+
+    def _get_family_slice(self, fam) -> slice:
+        """pynbody's SimSnap._get_family_slice: the family's index range, or
+        an empty slice when the snapshot has no such particles."""
+        return self._family_slice.get(get_family(fam), slice(0, 0))
 
     def keys(self):
         return list(self._arrays)
@@ -314,7 +319,7 @@ class SimSnap:
             a.sim = self
             return a
         if isinstance(key, Family):
-            return SubSnap(self, np.arange(self._n)[self._family_slices.get(key, slice(0, 0))])
+            return SubSnap(self, np.arange(self._n)[self._family_slice.get(key, slice(0, 0))])
         if isinstance(key, slice):
             return SubSnap(self, np.arange(self._n)[key])
         if callable(key) and hasattr(key, "__call__") and not isinstance(key, np.ndarray):
@@ -329,7 +334,7 @@ class SimSnap:
     def __getattr__(self, name):
         if name.startswith("_"):
             raise AttributeError(name)
-        fams = self.__dict__.get("_family_slices", {})
+        fams = self.__dict__.get("_family_slice", {})
         for f in fams:
             if f.name == name:
                 return self[f]
@@ -358,15 +363,25 @@ class SubSnap(SimSnap):
         self._derived = {}
         root = base.ancestor
         # family slices of the view: families of the root restricted to index
-        self._family_slices = {}
+        self._family_slice = {}
         self._root_index = base._root_index[self._index] if isinstance(base, SubSnap) else self._index
-        for f, sl in root._family_slices.items():
+        for f, sl in root._family_slice.items():
             lo = np.searchsorted(self._root_index, sl.start, side="left")
             hi = np.searchsorted(self._root_index, sl.stop, side="left")
             if np.all(np.diff(self._root_index) > 0):
-                self._family_slices[f] = slice(int(lo), int(hi))
+                self._family_slice[f] = slice(int(lo), int(hi))
         self._arrays = {}
         self._units = {}
+
+    def _get_family_slice(self, fam):
+        """Index range of the family in this view; for a view whose root
+        indices are not increasing (families need not be contiguous) the
+        positions of its members as an index array."""
+        fam = get_family(fam)
+        if fam in self._family_slice or np.all(np.diff(self._root_index) > 0):
+            return self._family_slice.get(fam, slice(0, 0))
+        sl = self.ancestor._get_family_slice(fam)
+        return np.nonzero((self._root_index >= sl.start) & (self._root_index < sl.stop))[0]
 
     @property
     def ancestor(self) -> SimSnap:
@@ -473,9 +488,7 @@ class FamilyFilter(Filter):
 
     def __call__(self, sim):
         mask = np.zeros(len(sim), dtype=bool)
-        sl = sim._family_slices.get(self.family)
-        if sl is not None:
-            mask[sl] = True
+        mask[sim._get_family_slice(self.family)] = True
         return mask
 
 

@@ -28,6 +28,7 @@ def dkey_inv(k):
 class NumpyMsel:
     def __init__(self, x):
         self.k = dkey(x)
+        self.n = self.k.size
 
     def key_range(self):
         if self.k.size == 0:

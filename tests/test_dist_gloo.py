@@ -259,3 +259,22 @@ def test_distributed_equaln_world4_protocol():
     for _, out in res:
         for key in want:
             assert np.array_equal(out[key], want[key], equal_nan=True), key
+
+
+def test_distributed_equaln_rejects_u32_overflow():
+    """The digit histograms are u32: a global kept count of 2**32 or more is
+    refused before any histogram is summed (it would wrap silently)."""
+    from pynbodyext.parallel import distributed_equaln
+
+    class Dev:
+        n = 1 << 31
+
+        def key_range(self):
+            raise AssertionError("must not be reached")
+
+    class Comm:  # three ranks of 2**31 kept particles each
+        def allreduce_host(self, a, op=0):
+            return a * 3
+
+    with pytest.raises(ValueError, match="u32"):
+        distributed_equaln(Dev(), Comm(), 128)
