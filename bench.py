@@ -100,12 +100,24 @@ class Dist:
             self.comm = None
 
 
-def cpu_baseline(pos, mass, seconds: float):
+def host_cores() -> int:
+    """Threads for the multi-core CPU baseline: every core this process may
+    use (sched_getaffinity), capped by the box's CPU share when the launcher
+    states it in OMP_NUM_THREADS (16 per GPU on the gpurun boxes, where the
+    affinity mask shows the whole machine)."""
+    cores = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        cores = min(cores, int(omp))
+    return max(1, cores)
+
+
+def cpu_baseline(pos, mass, seconds: float, cores: int | None = None):
     """Oracle restatement of direct.rs (per-target loop, :160-182 / :293-310)
     on a bounded random target sample; returns pairs/s on the host cores."""
     from oracle import gravity as og
 
-    cores = min(16, os.cpu_count() or 1)
+    cores = host_cores() if cores is None else int(cores)
     og.set_num_threads(cores)
     n = len(pos)
     rng = np.random.default_rng(0)
@@ -135,6 +147,7 @@ def cpu_baseline(pos, mass, seconds: float):
         "kind": "port",
         "sample": f"{k} random targets x {n} sources (all-particles Newtonian force+potential, "
                   f"oracle/gravity_ref.c, OpenMP {cores} threads, {dt:.1f} s)",
+        **cpu_host(),
     }
 
 
@@ -231,7 +244,8 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
             row["cpu_baseline"] = {
                 "value": reps * n / tc, "unit": "particles/s", "cores": 1, "kind": "port",
                 "sample": f"full {n}-particle workload x {reps}, oracle/profile_ref.py (numpy "
-                          f"restatement of bins.py/proarray.py), 1 thread, {tc:.1f} s"}
+                          f"restatement of bins.py/proarray.py), 1 thread, {tc:.1f} s",
+                **cpu_host()}
             edges, msum, _ = res
             row["parity_vs_oracle"] = {
                 "edges_bit_exact": bool(np.array_equal(edges, ref["edges"])),
@@ -248,7 +262,8 @@ TREE_FLOP_NODE = 94   # order-3 force+potential node interaction incl. opening t
 TREE_FLOP_PP = 22     # leaf pair, same algorithmic count as the direct sum
 
 
-def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc):
+def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc,
+                      cores: int | None = None):
     """Oracle restatement of tree.rs (serial build + payload like the
     reference, OpenMP walk over a bounded random target sample); returns the
     extrapolated full-solve rate in effective pairs/s and the parity of the
@@ -256,7 +271,7 @@ def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc)
     from oracle import gravity as og
     from oracle import tree as ot
 
-    cores = min(16, os.cpu_count() or 1)
+    cores = host_cores() if cores is None else int(cores)
     og.set_num_threads(cores)
     n = len(pos)
     rng = np.random.default_rng(0)
@@ -283,6 +298,7 @@ def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc)
         "sample": f"oracle/tree_ref.c: serial build+payload of all {n} particles ({t_build:.1f} s) + "
                   f"walk of {k} random targets on {cores} OpenMP threads ({t_walk:.1f} s), "
                   f"full solve extrapolated to {t_full:.1f} s",
+        **cpu_host(),
     }, {"targets_checked": k, "pot_max_rel": rp, "acc_max_rel": ra}
 
 
@@ -306,19 +322,23 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
     edges = np.logspace(np.log10(0.01), np.log10(50.0), 257)
     prof = DeviceBins()
     solver = ShardedTree(dist.comm, n, d_pos, d_mass, 8, 3, theta)
-    solver.build()
-    if dist.active:
-        solver.balance()
-    ev = [nat.Event() for _ in range(4)]
+    ev = [nat.Event() for _ in range(6)]
 
     def step():
+        # everything a step needs is inside it: build, the cost-balanced
+        # ranges (costs carried from the previous step's walk), the walk and
+        # its cost all-gather, the profile and its all-reduce
         ev[0].record()
         solver.build()
         ev[1].record()
-        solver.walk()
+        solver.balance()
         ev[2].record()
-        mom = solver.profile(prof, edges)
+        solver.walk(share=False)
         ev[3].record()
+        solver.share_costs()
+        ev[4].record()
+        mom = solver.profile(prof, edges)
+        ev[5].record()
         return mom
 
     for _ in range(warmup):
@@ -332,9 +352,10 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
         nat.synchronize()
         dist.barrier()
         wall.append(dist.max(time.perf_counter() - t0))
-        parts.append([ev[i].elapsed_ms(ev[i + 1]) for i in range(3)])
+        parts.append([ev[i].elapsed_ms(ev[i + 1]) for i in range(5)])
     t = float(np.median(wall))
-    build_ms, walk_ms, prof_ms = (float(np.median([p[i] for p in parts])) for i in range(3))
+    build_ms, bal_ms, walk_ms, share_ms, prof_ms = (float(np.median([p[i] for p in parts]))
+                                                    for i in range(5))
     info = solver.info
     first, count = solver.ranges[dist.rank] if solver.ranges else (0, n)
     flops = info["node_interactions"] * TREE_FLOP_NODE + info["leaf_pairs"] * TREE_FLOP_PP
@@ -355,8 +376,11 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
                    "n_particles": n, "nodes": info["nodes"], "levels": info["levels"],
                    "parallelism": f"tree replicated, leaf-ordered targets cost-balanced x{dist.world}"
                                   + (", RCCL all-reduce of profile partials" if dist.world > 1 else "")},
-        "phases_ms": {"build_and_payload": build_ms, "walk": walk_ms, "walk_max_over_ranks": walk_max,
+        "phases_ms": {"build_and_payload": build_ms, "balance": bal_ms,
+                      "walk": walk_ms, "walk_max_over_ranks": walk_max, "cost_share": share_ms,
                       "profile": prof_ms},
+        "balance": "timed in every step: ranges from the previous step's per-target interaction "
+                   "counts, carried in original particle order (no extra walk)",
         "interactions": {"node": info["node_interactions"], "leaf_pairs": info["leaf_pairs"],
                          "per_target": (info["node_interactions"] + info["leaf_pairs"]) / max(count, 1),
                          "simd_lane_efficiency": info["active_lane_steps"] /
@@ -387,6 +411,8 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
         idx.free()
         out["cpu_baseline"], out["parity_vs_oracle"] = tree_cpu_baseline(
             pos, mass, cpu_seconds, theta, pot, acc)
+        one, _ = tree_cpu_baseline(pos, mass, cpu_seconds / 2, theta, pot, acc, cores=1)
+        out["cpu_baseline"]["single_core"] = {k: one[k] for k in ("value", "cores", "sample")}
     solver.close()
     prof.close()
     d_pos.free()
@@ -418,8 +444,70 @@ def pmc_traffic(which: str = "direct"):
         return None, None
 
 
+def launch_ranks(args) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start N rank processes of this
+    same command under torch.distributed.run (one process per GPU) BEFORE
+    this process touches the GPU, and return their exit status."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def cpu_host() -> dict:
+    """Host CPU model and the cores this process may use."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity_cores": len(os.sched_getaffinity(0))}
+
+
+# The symmetric kernel evaluates each UNORDERED pair once: 18 FP64 VALU
+# instructions + 1 v_rsq_f64 (csrc/direct_sym.hip, fast mode), i.e. half the
+# instructions of two ordered pairs.  The FP64 vector pipe issues one wave64
+# FP64 instruction per 4 cycles per SIMD: 256 CUs x 4 SIMDs x 16 lanes x
+# 2.4 GHz = 39.3e12 lane-instructions/s (78.6 TF counts an FMA as 2).
+SYM_INSTR_PER_UNORDERED_PAIR = 19
+FP64_LANE_INSTR_PEAK = 256 * 4 * 16 * 2.4e9
+
+
+def executed_issue(symmetric: bool, pairs_launch: float, kern_ms: float) -> dict:
+    if not symmetric:
+        return {}
+    instr = pairs_launch / 2 * SYM_INSTR_PER_UNORDERED_PAIR
+    rate = instr / (kern_ms * 1e-3)
+    return {"executed_fp64_instr_per_unordered_pair": SYM_INSTR_PER_UNORDERED_PAIR,
+            "executed_issue_frac": rate / FP64_LANE_INSTR_PEAK,
+            "executed_issue_note": "FP64 lane-instructions the kernel actually issues / the "
+                                   "FP64 VALU issue peak (39.3e12/s)"}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE {world_env}", file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("PBX_BENCH_DRYRUN") == "1":  # launcher test: no GPU call
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": world_env,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+        return
     # Load libpbx (ROCm 7.2 HIP runtime + RCCL from /opt/rocm) BEFORE torch is
     # imported for the gloo control plane, so torch binds to the same runtime
     # instead of loading its bundled copies under the same sonames.
@@ -427,8 +515,6 @@ def main():
     nat.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     dist = Dist()
     world, rank = dist.world, dist.rank
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     from pynbodyext.parallel import ShardedDirect, shard_bounds
 
@@ -484,6 +570,8 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(pos, mass, args.cpu_seconds)
+        one = cpu_baseline(pos, mass, args.cpu_seconds / 2, cores=1)
+        cpu["single_core"] = {k: one[k] for k in ("value", "cores", "sample")}
     out = {
         "metric": "particle-pairs/sec (direct-sum gravity, force+potential)",
         "value": value,
@@ -517,6 +605,8 @@ def main():
             "kernel": "sym_kernel<pot+acc> (each unordered pair once)" if solver.symmetric else "direct_kernel<Newtonian, pot+acc, self-skip>",
             "flop_per_pair": FLOP_PER_PAIR,
             "kernel_ms": kern_avg_ms,
+            "frac_is": "algorithmic: 22 flop per ORDERED pair delivered (SURVEY.md §8d)",
+            **executed_issue(solver.symmetric, pairs_launch, kern_avg_ms),
         },
         "cpu_baseline": cpu,
     }

@@ -203,6 +203,16 @@ int pbx_octree_compute_range(pbx_octree *tree, double theta, int want, int64_t f
  * particles [first, first + count), into device buffers (any may be NULL) */
 int pbx_octree_leaf_particles(pbx_octree *tree, int64_t first, int64_t count, double *d_pos,
                               double *d_mass, int64_t *d_idx);
+/* Multi-GPU load balance without an extra walk (the reference has one
+ * process; its rayon pool splits targets dynamically, tree.rs:1443-1556):
+ * cost_to_orig scatters per-target costs held in leaf order (n int32, e.g.
+ * the d_cost of every rank's compute_range, all-gathered) to original
+ * particle order; balance reads such costs through the CURRENT build's leaf
+ * order and writes to host cuts[world + 1] the contiguous leaf-order ranges
+ * [cuts[r], cuts[r+1]) of about equal summed max(cost, 1) — the split of
+ * pynbodyext.parallel.balanced_ranges.  Device pointers; balance syncs. */
+int pbx_octree_cost_to_orig(pbx_octree *tree, const int32_t *d_cost_leaf, int32_t *d_cost_orig);
+int pbx_octree_balance(pbx_octree *tree, const int32_t *d_cost_orig, int world, int64_t *cuts);
 /* out[13] = {n, nodes, levels, has_mass_payload, has_hmax,
  *            accepted node interactions and leaf pairs of the last walk,
  *            path words, wave steps and active-lane steps of the last walk

@@ -1129,6 +1129,147 @@ __global__ void leaf_particles_kernel(const double4 *__restrict__ rec, const int
   if (idx) idx[t] = perm[first + t];
 }
 
+// ------------------------------------------------- cost-balanced target ranges
+// Multi-GPU walks split the leaf-ordered targets into contiguous ranges of
+// about equal cost (interactions per target).  The costs of one walk are
+// carried to the next step in ORIGINAL particle order (the leaf order of the
+// next build may differ), so no extra walk is needed to balance a step.
+constexpr int BAL_TPB = 1024;
+constexpr int BAL_PER = 4;
+constexpr int BAL_CHUNK = BAL_TPB * BAL_PER;  // targets per block-sum entry
+
+__global__ void cost_to_orig(const int32_t *__restrict__ cost_leaf, const int32_t *__restrict__ perm,
+                             int64_t n, int32_t *__restrict__ cost_orig) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) cost_orig[perm[i]] = cost_leaf[i];
+}
+
+__device__ __forceinline__ int64_t bal_cost(const int32_t *cost_orig, const int32_t *perm, int64_t i,
+                                            int64_t n) {
+  // balanced_ranges (parallel.py) counts every target as at least 1
+  return i < n ? (int64_t)max(cost_orig[perm[i]], 1) : 0;
+}
+
+// per chunk of BAL_CHUNK leaf positions: sum of max(cost, 1)
+__global__ __launch_bounds__(BAL_TPB) void bal_chunk_sums(const int32_t *__restrict__ cost_orig,
+                                                          const int32_t *__restrict__ perm, int64_t n,
+                                                          int64_t *__restrict__ sums) {
+  __shared__ int64_t part[BAL_TPB / 64];
+  const int64_t base = (int64_t)blockIdx.x * BAL_CHUNK;
+  int64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < BAL_PER; ++k) s += bal_cost(cost_orig, perm, base + k * BAL_TPB + threadIdx.x, n);
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < BAL_TPB / 64; ++w) t += part[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// inclusive block scan of one int64 per thread (BAL_TPB threads)
+__device__ int64_t bal_block_scan(int64_t v, int64_t *lds, int64_t *total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) lds[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int w = 0; w < BAL_TPB / 64; ++w) {
+      const int64_t x = lds[w];
+      lds[w] = run;
+      run += x;
+    }
+    lds[BAL_TPB / 64] = run;
+  }
+  __syncthreads();
+  v += lds[wv];
+  *total = lds[BAL_TPB / 64];
+  __syncthreads();
+  return v;
+}
+
+// One block: cuts[r] = 1 + first leaf position whose inclusive cost prefix
+// reaches total * r / world (the same float comparison as balanced_ranges:
+// searchsorted(cum, total * r / world, 'left') + 1), made monotone, <= n.
+__global__ __launch_bounds__(BAL_TPB) void bal_cuts(const int32_t *__restrict__ cost_orig,
+                                                    const int32_t *__restrict__ perm, int64_t n,
+                                                    const int64_t *__restrict__ sums, int64_t nchunks,
+                                                    int world, int64_t *__restrict__ cuts) {
+  __shared__ int64_t lds[BAL_TPB / 64 + 1];
+  __shared__ int64_t found;
+  // pass 1: the grand total
+  int64_t total = 0;
+  for (int64_t b0 = 0; b0 < nchunks; b0 += BAL_TPB) {
+    int64_t t;
+    bal_block_scan(b0 + threadIdx.x < nchunks ? sums[b0 + threadIdx.x] : 0, lds, &t);
+    total += t;
+  }
+  int64_t prev = 0;
+  if (threadIdx.x == 0) cuts[0] = 0;
+  for (int r = 1; r < world; ++r) {
+    const double target = (double)total * (double)r / (double)world;
+    // the chunk holding the crossing: scan the chunk sums again
+    if (threadIdx.x == 0) found = -1;
+    __syncthreads();
+    int64_t run = 0, chunk = -1, before = 0;
+    for (int64_t b0 = 0; b0 < nchunks; b0 += BAL_TPB) {
+      const int64_t b = b0 + threadIdx.x;
+      const int64_t v = b < nchunks ? sums[b] : 0;
+      int64_t t;
+      const int64_t inc = run + bal_block_scan(v, lds, &t);
+      if (b < nchunks && (double)inc >= target && (double)(inc - v) < target) found = b;
+      __syncthreads();
+      if (found >= 0) {
+        chunk = found;
+        break;
+      }
+      run += t;
+    }
+    int64_t cut = n;  // target beyond the total (rounding): everything
+    if (chunk >= 0) {
+      // prefix before the chunk
+      for (int64_t b0 = 0; b0 < chunk; b0 += BAL_TPB) {
+        const int64_t b = b0 + threadIdx.x;
+        int64_t t;
+        bal_block_scan(b < chunk ? sums[b] : 0, lds, &t);
+        before += t;
+      }
+      // inside the chunk: BAL_PER consecutive leaf positions per thread
+      const int64_t base = chunk * BAL_CHUNK + (int64_t)threadIdx.x * BAL_PER;
+      int64_t c[BAL_PER], s = 0;
+#pragma unroll
+      for (int k = 0; k < BAL_PER; ++k) {
+        c[k] = bal_cost(cost_orig, perm, base + k, n);
+        s += c[k];
+      }
+      int64_t t;
+      int64_t inc = before + bal_block_scan(s, lds, &t) - s;
+      if (threadIdx.x == 0) found = -1;
+      __syncthreads();
+      int64_t mine = -1;
+#pragma unroll
+      for (int k = 0; k < BAL_PER; ++k) {
+        inc += c[k];
+        if (mine < 0 && base + k < n && (double)inc >= target) mine = base + k;
+      }
+      if (mine >= 0) atomicMin((unsigned long long *)&found, (unsigned long long)mine);
+      __syncthreads();
+      if (found >= 0 && found != -1) cut = found + 1;
+    }
+    cut = cut < prev ? prev : (cut > n ? n : cut);
+    prev = cut;
+    if (threadIdx.x == 0) cuts[r] = cut;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cuts[world] = n;
+}
+
 // ------------------------------------------------------------------- host
 struct Octree {
   int device = -1;
@@ -1150,11 +1291,12 @@ struct Octree {
   Buf nstart, ncount, nfirst, nnext, nchild, ncen, pre, size;
   Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
+  Buf bal;                   // cost-balanced ranges: chunk sums + cuts
   ~Octree() {
     Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
                    &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &keys, &ktmp0,
                    &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
-                   &counters, &trace};
+                   &counters, &trace, &bal};
     for (Buf *b : bufs) b->release();
   }
   // accepted nodes, leaf pairs, fault flag, wave steps, active-lane steps
@@ -1831,6 +1973,42 @@ int pbx_octree_leaf_particles(pbx_octree *t, int64_t first, int64_t count, doubl
                          d_idx);
     PBX_HIP(hipGetLastError());
     PBX_HIP(hipStreamSynchronize(dev.stream));
+  });
+}
+
+int pbx_octree_cost_to_orig(pbx_octree *t, const int32_t *d_cost_leaf, int32_t *d_cost_orig) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (T.n > 0 && (!d_cost_leaf || !d_cost_orig)) fail(PBX_ERR_VALUE, "null cost array");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    if (T.n > 0)
+      hipLaunchKernelGGL(cost_to_orig, dim3(nblk(T.n)), dim3(TPB), 0, dev.stream, d_cost_leaf,
+                         T.perm.as<int32_t>(), T.n, d_cost_orig);
+    PBX_HIP(hipGetLastError());
+  });
+}
+
+int pbx_octree_balance(pbx_octree *t, const int32_t *d_cost_orig, int world, int64_t *cuts) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (world < 1 || world > 4096) fail(PBX_ERR_VALUE, "world must be in [1, 4096]");
+    if (!cuts) fail(PBX_ERR_VALUE, "null cuts");
+    if (T.n > 0 && !d_cost_orig) fail(PBX_ERR_VALUE, "null cost array");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    hipStream_t st = dev.stream;
+    const int64_t nchunks = (T.n + BAL_CHUNK - 1) / BAL_CHUNK;
+    int64_t *sums = (int64_t *)T.bal.get(8 * (size_t)(nchunks + world + 1));
+    int64_t *dcuts = sums + nchunks;
+    if (nchunks > 0)
+      hipLaunchKernelGGL(bal_chunk_sums, dim3((unsigned)nchunks), dim3(BAL_TPB), 0, st, d_cost_orig,
+                         T.perm.as<int32_t>(), T.n, sums);
+    hipLaunchKernelGGL(bal_cuts, dim3(1), dim3(BAL_TPB), 0, st, d_cost_orig, T.perm.as<int32_t>(),
+                       T.n, sums, nchunks, world, dcuts);
+    PBX_HIP(hipGetLastError());
+    PBX_HIP(hipMemcpyAsync(cuts, dcuts, 8 * (size_t)(world + 1), hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
   });
 }
 

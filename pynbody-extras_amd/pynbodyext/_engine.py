@@ -293,6 +293,18 @@ class Octree:
         nat.call("pbx_octree_leaf_particles", self._h, int(first), int(count), d_pos, d_mass,
                  d_idx)
 
+    def _cost_to_orig_device(self, d_cost_leaf, d_cost_orig) -> None:
+        """Per-target costs in this build's leaf order -> original order."""
+        nat.call("pbx_octree_cost_to_orig", self._h, d_cost_leaf, d_cost_orig)
+
+    def _balance_device(self, d_cost_orig, world: int) -> list[tuple[int, int]]:
+        """[(first, count)] per rank: contiguous leaf-order ranges of equal
+        summed cost (costs in original order, e.g. from the previous step)."""
+        cuts = np.zeros(int(world) + 1, dtype=np.int64)
+        nat.call("pbx_octree_balance", self._h, d_cost_orig, int(world),
+                 cuts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+        return [(int(cuts[r]), int(cuts[r + 1] - cuts[r])) for r in range(int(world))]
+
     # -- introspection -----------------------------------------------------
     def info(self) -> dict:
         out = np.zeros(13, dtype=np.int64)

@@ -96,6 +96,8 @@ _SIGNATURES: dict[str, tuple] = {
                                          c_void_p, c_void_p, c_void_p]),
     "pbx_octree_leaf_particles": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                           c_void_p]),
+    "pbx_octree_cost_to_orig": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "pbx_octree_balance": (c_int, [c_void_p, c_void_p, c_int, _i64p]),
     "pbx_octree_info": (c_int, [c_void_p, _i64p]),
     "pbx_octree_export": (c_int, [c_void_p, _dp, _dp, _dp, _i64p, _i64p, _i64p, _dp]),
     "pbx_profile_create": (c_int, [POINTER(c_void_p)]),

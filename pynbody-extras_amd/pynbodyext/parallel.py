@@ -268,11 +268,25 @@ class ShardedTree:
     """Barnes-Hut solve + radial potential profile, one rank per GPU.
 
     Every rank builds the full octree from the (replicated, HBM-resident)
-    particle set — the build is ~10 % of a single-GPU step — and walks its own
-    contiguous range of the leaf-ordered targets (cost-balanced after the
-    first walk).  Each rank reduces its targets into per-bin partial moments
-    (sum m, sum m phi, ...) and one RCCL all-reduce of nbins x 7 doubles gives
-    every rank the profile.  Strong scaling: the particle set is fixed.
+    particle set and walks its own contiguous range of the leaf-ordered
+    targets.  One step (all of it timed by bench.py) =
+
+    * ``build()``   — device octree + payloads (identical on every rank);
+    * ``balance()`` — the ranges: contiguous leaf-order pieces of equal
+      summed cost, where a target's cost is its interaction count in the
+      PREVIOUS step's walk, carried in original particle order (so a
+      changed snapshot / leaf order still maps); before any walk, equal
+      target counts.  Device-side (two small kernels, one (world+1)-int
+      read-back) — no extra walk;
+    * ``walk()``    — this rank's targets, writing their costs; the costs are
+      all-gathered (RCCL, 4 bytes per particle) and moved to original order
+      for the next step's balance;
+    * ``profile()`` — per-bin partial moments of this rank's targets, one
+      RCCL all-reduce of nbins x 7 doubles.
+
+    Strong scaling: the particle set is fixed.  The reference has no
+    multi-process path; its rayon pool splits the targets of one process
+    (tree.rs:1443-1556).
     """
 
     def __init__(self, comm, n: int, d_pos, d_mass, leaf_capacity: int = 8,
@@ -289,7 +303,9 @@ class ShardedTree:
         self.d_acc = nat.DeviceArray(24 * max(cap, 1))
         self.d_spos = nat.DeviceArray(24 * max(cap, 1))
         self.d_smass = nat.DeviceArray(8 * max(cap, 1))
-        self.d_cost = nat.DeviceArray(4 * max(cap, 1))
+        self.d_cost = nat.DeviceArray(4 * max(cap, 1))       # leaf order, last walk
+        self.d_cost_orig = nat.DeviceArray(4 * max(cap, 1))  # original order, carried
+        self.have_costs = False
         self.info = None
 
     def build(self):
@@ -302,19 +318,38 @@ class ShardedTree:
             self.tree._rebuild_device(self.d_pos.ptr, self.n, self.d_mass.ptr)
 
     def balance(self):
-        """One full walk (every rank, untimed) -> per-target costs -> ranges."""
-        self.tree._compute_range_device(self.theta, nat.WANT_POT, 0, self.n, 1,
-                                        self.d_pot.ptr, None, self.d_cost.ptr)
-        cost = np.empty(self.n, dtype=np.int32)
-        self.d_cost.download(cost)
-        self.ranges = balanced_ranges(cost, self.world)
+        """This step's target ranges (see the class docstring)."""
+        if self.world == 1:
+            self.ranges = [(0, self.n)]
+        elif self.have_costs:
+            self.ranges = self.tree._balance_device(self.d_cost_orig.ptr, self.world)
+        else:
+            self.ranges = [(lo, hi - lo) for lo, hi in all_shards(self.n, self.world)]
+        return self.ranges
 
-    def walk(self, want: int = nat.WANT_POT | nat.WANT_ACC):
-        first, count = self.ranges[self.rank] if self.ranges else (0, self.n)
+    def walk(self, want: int = nat.WANT_POT | nat.WANT_ACC, share: bool = True):
+        """This rank's targets; ``share`` then runs share_costs()."""
+        if self.ranges is None:
+            self.balance()
+        first, count = self.ranges[self.rank]
+        multi = self.world > 1
         self.tree._compute_range_device(self.theta, want, first, count, 1, self.d_pot.ptr,
-                                        self.d_acc.ptr, None)
+                                        self.d_acc.ptr,
+                                        self.d_cost.offset(4 * first) if multi else None)
         self.info = self.tree.info()
+        if multi and share:
+            self.share_costs()
         return first, count
+
+    def share_costs(self):
+        """All-gather every rank's walk costs, then to original order."""
+        if self.world == 1:
+            return
+        if self.comm is not None and self.world > 1:
+            self.comm.allgatherv(self.d_cost.ptr, [4 * c for _, c in self.ranges],
+                                 [4 * f for f, _ in self.ranges])
+        self.tree._cost_to_orig_device(self.d_cost.ptr, self.d_cost_orig.ptr)
+        self.have_costs = True
 
     def profile(self, dev_bins, edges) -> np.ndarray:
         """Per-bin moments (nbins, 7) of this rank's targets, summed over ranks."""
@@ -326,18 +361,24 @@ class ShardedTree:
                           into=dev_bins)
         dev_bins.assign(edges)
         mom = dev_bins.moments(self.d_pot, SRC_W)
-        if self.comm is not None:
+        if self.comm is not None and self.world > 1:
             buf = nat.DeviceArray.from_host(np.ascontiguousarray(mom))
             self.comm.allreduce_sum_f64(buf.ptr, buf.ptr, mom.size)
             buf.download(mom)
             buf.free()
         return mom
 
+    def step(self, dev_bins, edges, want: int = nat.WANT_POT | nat.WANT_ACC) -> np.ndarray:
+        self.build()
+        self.balance()
+        self.walk(want)
+        return self.profile(dev_bins, edges)
+
     def close(self):
         if self.tree is not None:
             self.tree.close()
             self.tree = None
-        for a in (self.d_pot, self.d_acc, self.d_spos, self.d_smass, self.d_cost):
+        for a in (self.d_pot, self.d_acc, self.d_spos, self.d_smass, self.d_cost, self.d_cost_orig):
             a.free()
 
 
