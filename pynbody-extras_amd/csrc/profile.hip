@@ -47,6 +47,7 @@ struct SelectParams {
   int use_sphere;
   int ndim;  // 3 -> r, 2 -> rxy
   int nfam;  // 0 -> no family filter
+  int64_t base;  // first particle of the tiles (the families' span; 0 without families)
   double cx, cy, cz, r2max;
   int64_t fam_lo[MAX_FAM];
   int64_t fam_hi[MAX_FAM];
@@ -94,12 +95,18 @@ constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 6
 // BT threads per block, one 4096-element tile each: 256 (16 items per
 // lane) on big inputs; 1024 (4 per lane) when there are few tiles, so a
 // small input still puts 16 waves on each CU.
-template <int BT>
+// LAZY: no weights / original indices are written; instead one keep word
+// per 64 particles (kw, the wave ballots: word j of tile t covers particles
+// base + 64 * (64 t + j) ...) and the tile's output offset (toff[t]), from
+// which the weights and indices are materialised only when needed
+// (sel_materialize) and the assignment reads the masses directly.
+template <int BT, bool LAZY>
 __global__ void __launch_bounds__(BT)
     select_onepass(const double *__restrict__ pos, const double *__restrict__ mass, int64_t n,
                    SelectParams p, uint64_t *__restrict__ status, uint32_t *__restrict__ ctrl,
                    double *__restrict__ xo, double *__restrict__ wo, int32_t *__restrict__ io,
-                   unsigned long long *__restrict__ minmax) {
+                   unsigned long long *__restrict__ minmax, uint64_t *__restrict__ kw,
+                   uint32_t *__restrict__ toff) {
   constexpr int NW = BT / 64, SI = TILE / BT;  // waves, items per lane
   __shared__ uint32_t wcnt[NW];
   __shared__ unsigned long long wmin[NW], wmax[NW];
@@ -113,7 +120,7 @@ __global__ void __launch_bounds__(BT)
   const uint32_t tile = s_tile;
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
-  const int64_t wbase = (int64_t)tile * TILE + (int64_t)w * (TILE / NW);
+  const int64_t wbase = p.base + (int64_t)tile * TILE + (int64_t)w * (TILE / NW);
   double xv[SI];
   uint32_t keepbits = 0, c = 0;
   unsigned long long kmin = ~0ull, kmax = 0ull;
@@ -144,7 +151,7 @@ __global__ void __launch_bounds__(BT)
   }
   // the kept particles' weights: loads issued now, consumed after the look-back
   double mv[SI];
-  if (wo) {
+  if (!LAZY && wo) {
 #pragma unroll
     for (int k = 0; k < SI; ++k) {
       const int64_t i = wbase + k * 64 + lane;
@@ -213,6 +220,7 @@ __global__ void __launch_bounds__(BT)
         __hip_atomic_store(&status[tile], kStPre | (excl + tot), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       s_excl = (uint32_t)excl;
+      if (LAZY) toff[tile] = (uint32_t)excl;
     }
   }
   __syncthreads();
@@ -222,14 +230,62 @@ __global__ void __launch_bounds__(BT)
   for (int k = 0; k < SI; ++k) {
     bool keep = (keepbits >> k) & 1u;
     uint64_t b = __ballot(keep);
+    if (LAZY && lane == 0) kw[(int64_t)tile * (TILE / 64) + w * SI + k] = b;
     if (keep) {
       int64_t i = wbase + k * 64 + lane;
       uint32_t pos_out = run + rank_below(b);
       xo[pos_out] = xv[k];
-      if (wo) wo[pos_out] = mv[k];
-      io[pos_out] = (int32_t)i;
+      if (!LAZY) {
+        if (wo) wo[pos_out] = mv[k];
+        io[pos_out] = (int32_t)i;
+      }
     }
     run += (uint32_t)__popcll(b);
+  }
+}
+
+// Positions of a lazy selection's tile (TPB threads, the select layout:
+// item (wave w, k, lane) = particle base + 64 (64 t + 16 w + k) + lane):
+// the tile's 64 keep words into LDS with the kept count before each word.
+__device__ __forceinline__ void sel_tile_words(const uint64_t *__restrict__ kw,
+                                               const uint32_t *__restrict__ toff, uint32_t t,
+                                               uint64_t *wrd, uint32_t *wpre) {
+  if (threadIdx.x < 64) {
+    const uint64_t word = kw[(int64_t)t * 64 + threadIdx.x];
+    const uint32_t c = (uint32_t)__popcll(word);
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (threadIdx.x >= (uint32_t)o) x += y;
+    }
+    wrd[threadIdx.x] = word;
+    wpre[threadIdx.x] = toff[t] + x - c;
+  }
+}
+
+// weights and original indices of a lazy selection, materialised on demand
+__global__ void __launch_bounds__(TPB)
+    sel_materialize(const uint64_t *__restrict__ kw, const uint32_t *__restrict__ toff,
+                    int64_t base, const double *__restrict__ mass, double *__restrict__ wo,
+                    int32_t *__restrict__ io) {
+  __shared__ uint64_t wrd[64];
+  __shared__ uint32_t wpre[64];
+  const uint32_t t = blockIdx.x;
+  sel_tile_words(kw, toff, t, wrd, wpre);
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
+    const int j = w * 16 + k;
+    const uint64_t word = wrd[j];
+    if ((word >> lane) & 1ull) {
+      const uint32_t pos = wpre[j] + rank_below(word);
+      const int64_t i = base + 64 * ((int64_t)t * 64 + j) + lane;
+      if (wo) wo[pos] = mass ? mass[i] : 1.0;
+      if (io) io[pos] = (int32_t)i;
+    }
   }
 }
 
@@ -570,6 +626,19 @@ __global__ void msel_edges(const MsRank *__restrict__ R, int nq, uint64_t base,
   if (q < nq) out[q] = dkey_inv(base + R[q].prefix);
 }
 
+// x[i], x[i + 1] with one 16-byte load when both exist (i even: aligned)
+__device__ __forceinline__ void load_pair(const double *__restrict__ x, int64_t i, int64_t n,
+                                          double *v) {
+  if (i + 1 < n) {
+    const double2 q = *(const double2 *)(x + i);
+    v[0] = q.x;
+    v[1] = q.y;
+  } else {
+    v[0] = i < n ? x[i] : 0.0;
+    v[1] = 0.0;
+  }
+}
+
 // ------------------------------------- one-sync equaln (select -> sums)
 // pbx_profile_radial_equaln: selection, equaln edges, assignment, CSR and
 // per-bin sums back to back on the stream with ONE host round trip at the
@@ -654,17 +723,15 @@ __global__ void __launch_bounds__(MS0_TPB)
   const int64_t n = (ctl.err & 2) ? 0 : ctl.n;
   const uint64_t base = ctl.lo;
   const int s = ctl.s0;
-  constexpr int U = 8;
-  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * U; i0 < n; i0 += (int64_t)gridDim.x * MS0_TPB * U) {
-    double v[U];
+  constexpr int U = 4;  // 16-byte loads: two consecutive keys per lane each
+  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * 2 * U; i0 < n;
+       i0 += (int64_t)gridDim.x * MS0_TPB * 2 * U) {
+    double v[2 * U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
-      v[u] = i < n ? x[i] : 0.0;
-    }
+    for (int u = 0; u < U; ++u) load_pair(x, i0 + 2 * (u * MS0_TPB + threadIdx.x), n, v + 2 * u);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+    for (int u = 0; u < 2 * U; ++u) {
+      const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
       const uint64_t k = dkey(v[u]);
       if (i < n && k >= ka && k <= kb) atomicAdd(&lh[(uint32_t)((k - base) >> s)], 1u);
     }
@@ -831,17 +898,15 @@ __global__ void __launch_bounds__(MS0_TPB)
     slot[i] = boff[(int64_t)blockIdx.x * MS_MAXQ + i];
   }
   __syncthreads();
-  constexpr int U = 8;
-  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * U; i0 < n; i0 += (int64_t)gridDim.x * MS0_TPB * U) {
-    double v[U];
+  constexpr int U = 4;  // 16-byte loads: two consecutive keys per lane each
+  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * 2 * U; i0 < n;
+       i0 += (int64_t)gridDim.x * MS0_TPB * 2 * U) {
+    double v[2 * U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
-      v[u] = i < n ? x[i] : 0.0;
-    }
+    for (int u = 0; u < U; ++u) load_pair(x, i0 + 2 * (u * MS0_TPB + threadIdx.x), n, v + 2 * u);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + u * MS0_TPB + threadIdx.x;
+    for (int u = 0; u < 2 * U; ++u) {
+      const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
       const uint64_t key = dkey(v[u]);
       if (i < n && key >= ka && key <= kb) {
         const uint64_t off = key - base;
@@ -1198,6 +1263,223 @@ static void launch_assign(uint32_t blocks, size_t lds, hipStream_t st, const dou
   }
 }
 
+// ------------------------------------- assignment over a lazy selection
+// The one-sync radial path (pbx_profile_radial_equaln) keeps the selection
+// lazy: x compacted, one keep word per 64 particles and each tile's output
+// offset.  Assignment and the CSR pass then walk the SELECTION's tiles
+// (4096 particles of the families' span each): a lane finds its kept
+// particles' compacted positions from the keep words, reads x there and the
+// caller's masses at the particle itself (coalesced), so no weight / index
+// array is written or read.  Per-tile bin counts ([bin][tile], bins < 256)
+// are the CSR pass's histogram; the per-bin sums go to one slab row per
+// block (fixed-order final sum in fused_pack).
+template <bool MOM, bool LDSE, int BT>
+__global__ void __launch_bounds__(BT)
+    assign_sel(const double *__restrict__ x, const uint64_t *__restrict__ kw,
+               const uint32_t *__restrict__ toff, int64_t base, uint32_t ntiles, uint32_t tpbk,
+               const double *__restrict__ mass, const double *__restrict__ edges, int nb,
+               uint32_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
+               double *__restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t th[AS_TILES][RADIX];
+  const int macc = MOM ? fs.nm * nb : 0;
+  double *acc = (double *)smem;
+  double *e = acc + macc;
+  constexpr int NW = BT / 64;
+  if (MOM)
+    for (int k = threadIdx.x; k < macc; k += BT) acc[k] = 0.0;
+  if (LDSE)
+    for (int k = threadIdx.x; k <= nb; k += BT) e[k] = edges[k];
+  for (int k = threadIdx.x; k < AS_TILES * RADIX; k += BT) (&th[0][0])[k] = 0;
+  __syncthreads();
+  const uint32_t t0 = blockIdx.x * tpbk;
+  const uint32_t t1 = min(ntiles, t0 + tpbk);
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  const bool wneed = MOM && mass;
+#ifndef PBX_AS_CH
+#define PBX_AS_CH 4
+#endif
+  constexpr int CH = PBX_AS_CH;  // words (64-particle groups) per chunk: CH items per lane
+  // every wave streams whole tiles on its own (no block barrier per tile):
+  // the tile's 64 keep words, one per lane, scanned across the wave; chunk
+  // c + 1's loads are in flight while chunk c is binned
+  // G waves share a tile (all of the block's when it has a single tile:
+  // small inputs still put every wave to work), each taking (64 / CH) / G
+  // consecutive chunks
+  const int G = (t1 - t0 <= 1) ? NW : 1;
+  const int c0 = (w % G) * ((64 / CH) / G), c1 = c0 + (64 / CH) / G;
+  for (uint32_t t = t0 + w / G; t < t1; t += NW / G) {
+    const uint64_t word = kw[(int64_t)t * 64 + lane];
+    const uint32_t cw = (uint32_t)__popcll(word);
+    uint32_t incl = cw;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    const uint32_t pre = toff[t] + incl - cw;
+    const int64_t pbase = base + (int64_t)t * TILE + lane;
+    uint32_t *hrow = th[t - t0];
+    double nv[CH], nw[CH];
+    uint32_t npos[CH], nkeep = 0;
+    auto load = [&](int c, double *v, double *wv, uint32_t *pos, uint32_t &keep) {
+      keep = 0;
+#pragma unroll
+      for (int kk = 0; kk < CH; ++kk) {
+        const int j = c * CH + kk;
+        const uint64_t wj = __shfl(word, j, 64);
+        const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
+        const bool kp = (wj >> lane) & 1ull;
+        keep |= (uint32_t)kp << kk;
+        pos[kk] = pj + rank_below(wj);
+        v[kk] = kp ? x[pos[kk]] : 0.0;
+        wv[kk] = (kp && wneed) ? mass[pbase + 64 * j] : 1.0;
+      }
+    };
+    load(c0, nv, nw, npos, nkeep);
+#pragma unroll 1
+    for (int c = c0; c < c1; ++c) {
+      double v[CH], wv[CH];
+      uint32_t pos[CH], keep = nkeep;
+#pragma unroll
+      for (int kk = 0; kk < CH; ++kk) {
+        v[kk] = nv[kk];
+        wv[kk] = nw[kk];
+        pos[kk] = npos[kk];
+      }
+      if (c + 1 < c1) load(c + 1, nv, nw, npos, nkeep);
+      uint32_t b[CH];
+#pragma unroll
+      for (int kk = 0; kk < CH; ++kk)
+        b[kk] = ((keep >> kk) & 1u) ? (LDSE ? bin_of(v[kk], e, nb) : bin_of(v[kk], edges, nb))
+                                    : (uint32_t)nb + 1;
+#ifndef PBX_DIAG_NO_HIST
+#pragma unroll
+      for (int kk = 0; kk < CH; ++kk)
+        if (b[kk] <= (uint32_t)nb) atomicAdd(&hrow[b[kk]], 1u);
+#endif
+#pragma unroll
+      for (int kk = 0; kk < CH; ++kk)
+        if ((keep >> kk) & 1u) bins[pos[kk]] = b[kk];
+#ifdef PBX_DIAG_NO_MOM_ATOMICS
+      if (MOM) {
+        double sacc = 0.0;
+        for (int kk = 0; kk < CH; ++kk) sacc += v[kk] * wv[kk];
+        if (sacc == 1234.5) acc[0] = 0.0;
+      }
+      if (false) {
+#else
+      if (MOM) {
+#endif
+        for (int q = 0; q < fs.nm; ++q) {  // uniform
+          const int col = fs.col[q], fq = fs.f[q], wq = fs.w[q];
+          double *aq = acc + (int64_t)q * nb;
+#pragma unroll
+          for (int kk = 0; kk < CH; ++kk) {
+            if (b[kk] >= (uint32_t)nb) continue;
+            const double f = fq == 0 ? v[kk] : wv[kk];
+            const double ww = wq == 0 ? v[kk] : wv[kk];
+            atomicAdd(&aq[b[kk]], monomial(col, f, ww));
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (MOM) {
+    double *dst = slab + (int64_t)blockIdx.x * macc;
+    for (int k = threadIdx.x; k < macc; k += BT) dst[k] = acc[k];
+  }
+  const int d = threadIdx.x;  // thread d < RADIX owns digit d
+  if (d < RADIX)
+    for (uint32_t t = t0; t < t1; ++t) tile_hist[(int64_t)d * ntiles + t] = th[t - t0][d];
+}
+
+// Stable CSR scatter over a lazy selection's tiles: radix_scatter's scheme
+// (per-wave peer ranks, tile sorted by bin in LDS, runs written out
+// coalesced) with the elements = the tile's kept particles in particle
+// order, key = bin, value = compacted position.  offs = the exclusive scan
+// of assign_sel's [bin][tile] counts.
+__global__ void __launch_bounds__(TPB)
+    csr_sel(const uint64_t *__restrict__ kw, const uint32_t *__restrict__ toff,
+            const uint32_t *__restrict__ bins, const uint32_t *__restrict__ offs, uint32_t ntiles,
+            int32_t *__restrict__ perm) {
+  __shared__ uint32_t run[NWAVE][RADIX];
+  __shared__ uint32_t dstart[RADIX];
+  __shared__ uint32_t gofs[RADIX];
+  __shared__ uint32_t wsum[NWAVE];
+  __shared__ uint32_t sk[TILE];
+  __shared__ int32_t sv[TILE];
+  __shared__ uint64_t wrd[64];
+  __shared__ uint32_t wpre[64];
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  const uint32_t t = blockIdx.x;
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
+  sel_tile_words(kw, toff, t, wrd, wpre);
+  __syncthreads();
+  uint32_t key[16], pos[16];
+  uint64_t okm[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int j = w * 16 + k;
+    const uint64_t word = wrd[j];
+    okm[k] = word;
+    pos[k] = wpre[j] + rank_below(word);
+    key[k] = ((word >> lane) & 1ull) ? bins[pos[k]] : 0u;
+  }
+  uint32_t ret[16], lp[16];
+  uint64_t pm[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const bool ok = (okm[k] >> lane) & 1ull;
+    const uint32_t dgt = key[k] & 255u;
+    const uint64_t m = peers8(dgt, okm[k]);
+    pm[k] = ok ? m : 0ull;
+    ret[k] = (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
+    const uint32_t before = (uint32_t)__shfl((int)ret[k], leader, 64);
+    lp[k] = before + rank_below(pm[k]);
+  }
+  __syncthreads();
+  {
+    const int d = threadIdx.x;  // TPB == RADIX
+    uint32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) tot += run[ww][d];
+    const uint32_t st = block_excl_scan(tot, wsum, nullptr);
+    dstart[d] = st;
+    gofs[d] = offs[(int64_t)d * ntiles + t];
+    uint32_t a = st;
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) {
+      const uint32_t c = run[ww][d];
+      run[ww][d] = a;
+      a += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if ((okm[k] >> lane) & 1ull) {
+      const uint32_t dgt = key[k] & 255u;
+      const uint32_t q = run[w][dgt] + lp[k];
+      sk[q] = dgt;
+      sv[q] = (int32_t)pos[k];
+    }
+  }
+  __syncthreads();
+  const int tn = (int)(wpre[63] + (uint32_t)__popcll(wrd[63]) - toff[t]);
+  for (int j = threadIdx.x; j < tn; j += TPB) {
+    const uint32_t dgt = sk[j];
+    perm[gofs[dgt] + ((uint32_t)j - dstart[dgt])] = sv[j];
+  }
+}
+
 // ----------------------------------------------------------------- moments
 // LDS: accumulators in LDS (nb <= LDS_MOM_BINS), one slab row per block;
 // else straight to global_acc.  Templated so the LDS path indexes the
@@ -1514,6 +1796,12 @@ struct Profile {
       field, weight, ranks, bounds;
   Buf pk0, pk1, pv0, pv1, pbk, pcdf, poff, pq, pout;  // order statistics
   Buf fctl, fseg, fgrp, fslab, fpack;                // one-sync equaln path
+  // lazy selection (select_launch): keep words, tile offsets, staged masses
+  Buf kw, toff, mstage;
+  bool lazy = false, w_ready = false, idx_ready = false;
+  int64_t sel_base = 0, sel_span = 0;
+  uint32_t sel_nt = 0;
+  const double *sel_mass = nullptr;
 };
 
 // exclusive scan of len u32 in place
@@ -1771,10 +2059,14 @@ static void csr_device(Profile &P, hipStream_t st) {
 
 // Launch the fused selection (mask + x + compaction + key range) of n
 // particles into P.x / P.w / P.idx; the kept count and key range stay on
-// the device (status words / selst).  Returns the tile count.
+// the device (status words / selst).  Only the families' span is tiled.
+// lazy: P.w / P.idx are not written (keep words + tile offsets instead, see
+// select_onepass); the masses are then read from `mass` (the caller's device
+// array, or a handle-owned staged copy) when the weights are needed.
+// Returns the tile count.
 static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, const double *mass,
                               int64_t n, int on_device, int use_sphere, const double *sphere,
-                              const int64_t *fam, int nfam, int ndim) {
+                              const int64_t *fam, int nfam, int ndim, bool lazy = false) {
   check_n(n);
   if (ndim != 2 && ndim != 3) fail(PBX_ERR_VALUE, "ndim must be either 2 or 3");
   if (nfam < 0 || nfam > MAX_FAM) fail(PBX_ERR_VALUE, "at most %d family ranges", MAX_FAM);
@@ -1788,46 +2080,102 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, con
     sp.cz = sphere[2];
     sp.r2max = sphere[3];
   }
-  for (int f = 0; f < nfam; ++f) {
-    sp.fam_lo[f] = fam[2 * f];
-    sp.fam_hi[f] = fam[2 * f + 1];
+  int64_t lo = 0, hi = n;  // the span holding every family member
+  if (nfam > 0) {
+    lo = n;
+    hi = 0;
+    for (int f = 0; f < nfam; ++f) {
+      sp.fam_lo[f] = fam[2 * f];
+      sp.fam_hi[f] = fam[2 * f + 1];
+      const int64_t a = std::max<int64_t>(0, fam[2 * f]), b = std::min<int64_t>(n, fam[2 * f + 1]);
+      if (b > a) {
+        lo = std::min(lo, a);
+        hi = std::max(hi, b);
+      }
+    }
+    if (hi <= lo) lo = hi = 0;
   }
+  sp.base = lo;
+  const int64_t span = hi - lo;
   const double *d_pos = pos, *d_mass = mass;
   if (!on_device && n) {
     double *tp = (double *)P.keys0.get(sizeof(double) * 3 * (size_t)n);
     PBX_HIP(hipMemcpyAsync(tp, pos, sizeof(double) * 3 * n, hipMemcpyHostToDevice, st));
     d_pos = tp;
     if (mass) {
-      double *tm2 = (double *)P.keys1.get(sizeof(double) * (size_t)n);
+      Buf &mb = lazy ? P.mstage : P.keys1;  // lazy: kept for the selection's lifetime
+      double *tm2 = (double *)mb.get(sizeof(double) * (size_t)n);
       PBX_HIP(hipMemcpyAsync(tm2, mass, sizeof(double) * n, hipMemcpyHostToDevice, st));
       d_mass = tm2;
     }
   }
-  const uint32_t nt = ntiles_of(n);
+  const uint32_t nt = ntiles_of(span);
   // per-tile look-back status words + ticket / watchdog (selection scratch)
   // [stat nt][ctrl: ticket, watchdog][MM_SLOTS x (~min key, max key)]: one zero fill
   const size_t nst = (size_t)nt + 1 + 2 * MM_SLOTS;
   uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * nst);
   uint32_t *ctrl = (uint32_t *)(stat + nt);
-  double *xo = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
-  double *wo = (double *)P.w.get(sizeof(double) * (size_t)(n ? n : 1));
-  int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(n ? n : 1));
+  double *xo = (double *)P.x.get(sizeof(double) * (size_t)(span ? span : 1));
+  double *wo = nullptr;
+  int32_t *io = nullptr;
+  uint64_t *kw = nullptr;
+  uint32_t *toff = nullptr;
+  if (lazy) {
+    kw = (uint64_t *)P.kw.get(sizeof(uint64_t) * (TILE / 64) * (size_t)std::max<uint32_t>(nt, 1));
+    toff = (uint32_t *)P.toff.get(sizeof(uint32_t) * (size_t)std::max<uint32_t>(nt, 1));
+  } else {
+    wo = (double *)P.w.get(sizeof(double) * (size_t)(span ? span : 1));
+    io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(span ? span : 1));
+  }
   unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
   PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * nst, st));
-  if (n) {
-    if (nt < 1024)
-      hipLaunchKernelGGL(select_onepass<1024>, dim3(nt), dim3(1024), 0, st, d_pos, d_mass, n, sp,
-                         stat, ctrl, xo, wo, io, mm);
-    else
-      hipLaunchKernelGGL(select_onepass<TPB>, dim3(nt), dim3(TPB), 0, st, d_pos, d_mass, n, sp,
-                         stat, ctrl, xo, wo, io, mm);
+  if (span) {
+    auto go = [&](auto kern, int bt) {
+      hipLaunchKernelGGL(kern, dim3(nt), dim3(bt), 0, st, d_pos, d_mass, hi, sp, stat, ctrl, xo,
+                         wo, io, mm, kw, toff);
+    };
+    if (nt < 1024) {
+      if (lazy) go(select_onepass<1024, true>, 1024);
+      else go(select_onepass<1024, false>, 1024);
+    } else {
+      if (lazy) go(select_onepass<TPB, true>, TPB);
+      else go(select_onepass<TPB, false>, TPB);
+    }
     PBX_HIP(hipGetLastError());
   }
+  P.lazy = lazy;
+  P.sel_base = lo;
+  P.sel_span = span;
+  P.sel_nt = nt;
+  P.sel_mass = lazy ? d_mass : nullptr;
   return nt;
+}
+
+// materialise a lazy selection's weights / original indices
+static void ensure_w(Profile &P, hipStream_t st) {
+  if (!P.lazy || P.w_ready) return;
+  double *wo = (double *)P.w.get(sizeof(double) * (size_t)std::max<int64_t>(P.n, 1));
+  if (P.sel_nt)
+    hipLaunchKernelGGL(sel_materialize, dim3(P.sel_nt), dim3(TPB), 0, st, (const uint64_t *)P.kw.p,
+                       (const uint32_t *)P.toff.p, P.sel_base, P.sel_mass, wo, (int32_t *)nullptr);
+  PBX_HIP(hipGetLastError());
+  P.w_ready = true;
+}
+
+static void ensure_idx(Profile &P, hipStream_t st) {
+  if (!P.lazy || P.idx_ready) return;
+  int32_t *io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)std::max<int64_t>(P.n, 1));
+  if (P.sel_nt)
+    hipLaunchKernelGGL(sel_materialize, dim3(P.sel_nt), dim3(TPB), 0, st, (const uint64_t *)P.kw.p,
+                       (const uint32_t *)P.toff.p, P.sel_base, (const double *)nullptr,
+                       (double *)nullptr, io);
+  PBX_HIP(hipGetLastError());
+  P.idx_ready = true;
 }
 
 // the handle's state after a selection of `kept` particles (key range in P.mm)
 static void select_commit(Profile &P, int64_t kept) {
+  P.w_ready = P.idx_ready = !P.lazy;
   P.mm_valid = true;
   P.n = kept;
   P.has_w = true;
@@ -1846,6 +2194,7 @@ static const double *resolve_src(Profile &P, hipStream_t st, int which, const do
   if (which == 0) return (const double *)P.x.p;
   if (which == 1) {
     if (!P.has_w) fail(PBX_ERR_VALUE, "profile has no selection weights");
+    ensure_w(P, st);
     return (const double *)P.w.p;
   }
   if (which == 2) {
@@ -1857,6 +2206,7 @@ static const double *resolve_src(Profile &P, hipStream_t st, int which, const do
   if (which == 3) {  // device array per ORIGINAL particle (e.g. a tree potential)
     if (!hp && n) fail(PBX_ERR_VALUE, "device array is NULL");
     if (!P.has_idx) return hp;
+    ensure_idx(P, st);
     double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
     if (n)
       hipLaunchKernelGGL(gather_by_idx, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st, hp,
@@ -2011,6 +2361,7 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
     P.n = n;
     P.has_w = false;
     P.has_idx = false;
+    P.lazy = false;
     P.csr_ready = false;
     P.csrh_ready = false;
     P.ms.active = false;
@@ -2031,7 +2382,7 @@ int pbx_profile_select(void *handle, const double *pos, const double *mass, int6
     const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
                                       nfam, ndim);
     int64_t kept = 0;
-    if (n) {
+    if (nt) {
       uint64_t *stat = (uint64_t *)P.selst.p;
       const size_t nh = 2 + 2 * MM_SLOTS;
       uint64_t *h = (uint64_t *)P.pin.get(sizeof(uint64_t) * nh);
@@ -2061,6 +2412,8 @@ int pbx_profile_get_selection(void *handle, int64_t *h_idx, double *h_x, double 
     if (!P.has_idx) fail(PBX_ERR_VALUE, "profile has no selection");
     const int64_t n = P.n;
     if (n == 0) return;
+    if (h_idx) ensure_idx(P, st);
+    if (h_w) ensure_w(P, st);
     if (h_idx) {
       int64_t *tmp = (int64_t *)P.vtmp.get(sizeof(int64_t) * (size_t)n);
       hipLaunchKernelGGL(widen_perm, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st,
@@ -2439,8 +2792,15 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     std::lock_guard<std::mutex> lk(d.mu);
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.radial_equaln");
+    // bins < 256: the lazy selection + tile-walking assignment / CSR passes
+    static const bool eager_env = [] {  // A/B diagnostic: the eager selection path
+      const char *v = std::getenv("PBX_RADIAL_EAGER");
+      return v && v[0] == '1';
+    }();
+    const bool lazy = nbins < RADIX && !eager_env;
     const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
-                                      nfam, ndim);
+                                      nfam, ndim, lazy);
+    const int64_t n_sel = nt ? P.sel_span : 0;  // tiled particles (the families' span)
     const int nq = (int)nbins + 1;
     // the window of bins.py:734-737 as key bounds (msel_begin)
     bool empty_bounds = false;
@@ -2465,9 +2825,9 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     const double *x = (const double *)P.x.p;
     // level 0 (rows -> H), resolve + groups, per-block offsets, gather,
     // per-group finish -> edges
-    const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
+    const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n_sel / (MS0_TPB * 16)));
     uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
-    const FusedSetup fsu{(const uint64_t *)stat, nt, n, ka, kb, (int)empty_bounds};
+    const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds};
     hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
                        rows);
     hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
@@ -2480,7 +2840,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                        goff, gq);
     hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
                        (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff);
-    uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n ? n : 1));
+    uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n_sel ? n_sel : 1));
     hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
                        (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff, seg);
     double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
@@ -2489,7 +2849,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                        (const uint64_t *)seg, de);
     PBX_HIP(hipGetLastError());
     // assignment (+ the statistics' distinct sums) with the device edges
-    uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n ? n : 1));
+    uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n_sel ? n_sel : 1));
     // distinct monomials of the requested columns (x^a w^b |x|^c |w|^d);
     // mono[k][c] = its slot, -1 = column not accumulated (0)
     FusedStats fs{};
@@ -2531,7 +2891,50 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     P.csrh_ready = false;
     uint32_t ablocks = 0;
     const uint32_t *cnt_offs = nullptr;  // scanned CSR histogram the counts come from
-    if (n) {
+    if (n_sel && lazy) {
+      // tile-walking assignment over the lazy selection + its CSR pass
+      const int64_t macc = (int64_t)fs.nm * nb;
+      const bool ldse = (nb + 1) <= LDS_EDGES;
+      const size_t lds = sizeof(double) * (size_t)macc + (ldse ? sizeof(double) * (nb + 1) : 0);
+      uint32_t *th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX);
+      const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
+      ablocks = ceil_div(nt, tpbk);
+      double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
+      const uint64_t *kwp = (const uint64_t *)P.kw.p;
+      const uint32_t *tof = (const uint32_t *)P.toff.p;
+      // few tiles: one tile per 1024-thread block, every wave a piece of it
+      const bool wide = tpbk == 1 && nt < 1024;
+      auto go = [&](auto kern, int bt) {
+        hipLaunchKernelGGL(kern, dim3(ablocks), dim3(bt), lds, st, x, kwp, tof, P.sel_base, nt,
+                           tpbk, P.sel_mass, (const double *)de, (int)nb, bins, th, fs, slab);
+      };
+      if (wide) {
+        if (fs.nm) {
+          if (ldse) go(assign_sel<true, true, 1024>, 1024);
+          else go(assign_sel<true, false, 1024>, 1024);
+        } else {
+          if (ldse) go(assign_sel<false, true, 1024>, 1024);
+          else go(assign_sel<false, false, 1024>, 1024);
+        }
+      } else if (fs.nm) {
+        if (ldse) go(assign_sel<true, true, TPB>, TPB);
+        else go(assign_sel<true, false, TPB>, TPB);
+      } else {
+        if (ldse) go(assign_sel<false, true, TPB>, TPB);
+        else go(assign_sel<false, false, TPB>, TPB);
+      }
+      PBX_HIP(hipGetLastError());
+      if (fs.nm) maccs = slab;
+      // the counts are row-start differences of the scanned [bin][tile] table
+      scan_u32(P, st, th, (int64_t)nt * RADIX);
+      cnt_offs = th;
+      if (build_csr) {
+        int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
+        hipLaunchKernelGGL(csr_sel, dim3(nt), dim3(TPB), 0, st, kwp, tof, (const uint32_t *)bins,
+                           (const uint32_t *)th, nt, perm);
+        PBX_HIP(hipGetLastError());
+      }
+    } else if (n_sel) {
       const int64_t macc = (int64_t)fs.nm * nb;
       size_t lds = sizeof(double) * (size_t)macc +
                    ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
@@ -2547,10 +2950,10 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       if (th && build_csr) cnt_offs = th;
       unsigned long long *acnt = cnt_offs ? nullptr : cnt;
       if (fs.nm)
-        launch_assign<true>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, acnt, th,
+        launch_assign<true>(ablocks, lds, st, x, n_sel, (const double *)de, (int)nb, bins, acnt, th,
                             nt, tpbk, n_dev, (const double *)P.w.p, fs, slab);
       else
-        launch_assign<false>(ablocks, lds, st, x, n, (const double *)de, (int)nb, bins, acnt, th,
+        launch_assign<false>(ablocks, lds, st, x, n_sel, (const double *)de, (int)nb, bins, acnt, th,
                              nt, tpbk, n_dev, nullptr, fs, nullptr);
       PBX_HIP(hipGetLastError());
       P.csrh_ready = th != nullptr;
@@ -2558,21 +2961,21 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       if (build_csr) {  // stable counting sort of the bin ids, device length
         int bits = 0;
         while (((int64_t)1 << bits) <= nb) ++bits;
-        uint32_t *ka2 = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n);
-        uint32_t *kb2 = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n);
-        int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n);
-        int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n);
+        uint32_t *ka2 = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n_sel);
+        uint32_t *kb2 = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n_sel);
+        int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
+        int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n_sel);
         const uint32_t *kin = bins;
         bool first = true;
         for (int shift = 0; shift < bits; shift += 8) {
           const bool last = shift + 8 >= bits;
           if (first) {
             prim::radix_pass<uint32_t>(P.csrh_ready ? P.csrh : P.hist, P.tsum, st, kin, nullptr,
-                                       VAL_IOTA, n, shift, last ? nullptr : ka2, va, P.csrh_ready,
+                                       VAL_IOTA, n_sel, shift, last ? nullptr : ka2, va, P.csrh_ready,
                                        n_dev);
             first = false;
           } else {
-            prim::radix_pass<uint32_t>(P.hist, P.tsum, st, ka2, va, VAL_ARRAY, n, shift,
+            prim::radix_pass<uint32_t>(P.hist, P.tsum, st, ka2, va, VAL_ARRAY, n_sel, shift,
                                        last ? nullptr : kb2, vb, false, n_dev);
             std::swap(ka2, kb2);
             std::swap(va, vb);
@@ -2580,7 +2983,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
         }
         P.csrh_ready = false;
         if ((void *)va != P.perm.p)
-          PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+          PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n_sel, hipMemcpyDeviceToDevice, st));
       }
     }
     // the results packed on the device, one copy, one sync

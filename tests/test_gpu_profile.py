@@ -495,7 +495,9 @@ def test_profile_median_uses_device(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["plummer", "sphere_family", "clip", "nan", "single", "dups",
-                                  "skewed", "empty_window", "nothing_kept", "many_stats"])
+                                  "skewed", "empty_window", "nothing_kept", "many_stats",
+                                  "family_offset", "no_mass", "wide", "wide_family",
+                                  "empty_family"])
 def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
     """pbx_profile_radial_equaln (select + equaln + assign + CSR + sums with
     one host round trip, level-0 select + per-group LDS sort / radix finish)
@@ -530,13 +532,24 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
         lo, hi = 1e9, 2e9
     elif case == "nothing_kept":
         sphere = ((1e6, 0.0, 0.0), 1.0)
+    elif case == "family_offset":  # the tiled span starts mid-array (lazy selection base)
+        sphere, fams = ((0.0, 0.0, 0.0), 5.0), [(123_457, 300_001), (310_000, 310_003)]
+    elif case == "no_mass":  # unit weights
+        mass = None
+    elif case == "wide":  # >= 256 bins: the eager selection path
+        nb = 300
+    elif case == "wide_family":  # eager path over a families' span shorter than n
+        nb, fams = 300, [(50_000, 150_000), (200_000, 260_000)]
+        sphere = ((0.0, 0.0, 0.0), 8.0)
+    elif case == "empty_family":
+        fams = [(5, 5)]
     elif case == "many_stats":  # more statistics than the assignment pass fuses
         nb = 64
         stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11), (SRC_X, SRC_NONE, 0x7f),
                  (SRC_W, SRC_W, 0x7f), (SRC_X, SRC_W, 0x7f), (SRC_W, SRC_NONE, 0x18)]
     b = DeviceBins.select(pos, mass, sphere=sphere, families=fams, ndim=3)
     try:
-        if case in ("empty_window", "nothing_kept"):
+        if case in ("empty_window", "nothing_kept", "empty_family"):
             exc = IndexError if case == "empty_window" else ValueError
             with pytest.raises(exc) as e_ref:
                 b.binned_equaln(nb, lo, hi, stats)
@@ -558,9 +571,13 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
             p1, o1 = a.csr()
             p2, o2 = b.csr()
             assert np.array_equal(p1, p2) and np.array_equal(o1, o2)
-            # the handle is usable afterwards like a stepwise one
+            # the handle is usable afterwards like a stepwise one (a lazy
+            # selection materialises its weights / indices on demand)
             np.testing.assert_allclose(a.moments(SRC_X, SRC_W, 0x7f), b.moments(SRC_X, SRC_W, 0x7f),
                                        rtol=1e-12, atol=1e-300)
+            for u, v in zip(a.selection(idx=True, x=True, w=True),
+                            b.selection(idx=True, x=True, w=True)):
+                assert np.array_equal(u, v, equal_nan=u.dtype.kind == "f")
         finally:
             a.close()
     finally:
