@@ -46,6 +46,10 @@ extern "C" {
 #define PBX_WANT_POT 1
 #define PBX_WANT_ACC 2
 
+/* element types of pbx_profile_select_typed */
+#define PBX_F64 0
+#define PBX_F32 1
+
 /* ------------------------------------------------------------------ */
 /* runtime                                                             */
 /* ------------------------------------------------------------------ */
@@ -253,6 +257,16 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n);
 int pbx_profile_select(void *handle, const double *pos, const double *mass, int64_t n,
                        int on_device, int use_sphere, const double *sphere,
                        const int64_t *fam, int nfam, int ndim, int64_t *n_kept);
+/* The same for float32 snapshots without a host up-cast (pos_dtype /
+ * mass_dtype PBX_F64 or PBX_F32).  numpy's dtype rules for a float32 pos
+ * array: the Sphere distance against the float64 centre is evaluated in
+ * double on the exactly widened coordinates; x = sim["r"] / sim["rxy"] of the
+ * float32 array is float32 arithmetic ((x*x+y*y)+z*z, correctly rounded
+ * sqrtf) and is held widened (exactly) as double; masses are widened. */
+int pbx_profile_select_typed(void *handle, const void *pos, int pos_dtype, const void *mass,
+                             int mass_dtype, int64_t n, int on_device, int use_sphere,
+                             const double *sphere, const int64_t *fam, int nfam, int ndim,
+                             int64_t *n_kept);
 /* original indices (int64), x and weights of the selection (any may be NULL) */
 int pbx_profile_get_selection(void *handle, int64_t *h_idx, double *h_x, double *h_w);
 int pbx_profile_minmax(void *handle, double *mn, double *mx);

@@ -48,6 +48,7 @@ struct SelectParams {
   int ndim;  // 3 -> r, 2 -> rxy
   int nfam;  // 0 -> no family filter
   int64_t base;  // first particle of the tiles (the families' span; 0 without families)
+  int mass_f32;  // masses are float (else double)
   double cx, cy, cz, r2max;
   int64_t fam_lo[MAX_FAM];
   int64_t fam_hi[MAX_FAM];
@@ -63,18 +64,27 @@ __device__ __forceinline__ bool in_family(int64_t i, const SelectParams &p) {
 
 // mask and x of one particle from its loaded position (no FMA contraction:
 // numpy evaluates these as separate multiplies and adds; sqrt is correctly
-// rounded)
-__device__ __forceinline__ bool select_xyz(double px, double py, double pz, const SelectParams &p,
-                                          double &x) {
+// rounded).  float positions (T = float) follow numpy's dtype rules for a
+// float32 snapshot: the Sphere distance mixes the float64 centre in, so it
+// is evaluated in double on the exactly widened coordinates; r / rxy of the
+// float32 array stay float32 arithmetic (its float32 values are stored
+// widened, exactly).
+template <typename T>
+__device__ __forceinline__ bool select_xyz(T px, T py, T pz, const SelectParams &p, double &x) {
 #pragma clang fp contract(off)
   bool keep = true;
   if (p.use_sphere) {
-    double dx = px - p.cx, dy = py - p.cy, dz = pz - p.cz;
+    double dx = (double)px - p.cx, dy = (double)py - p.cy, dz = (double)pz - p.cz;
     keep = ((dx * dx + dy * dy) + dz * dz) < p.r2max;
   }
-  x = (p.ndim == 2) ? __builtin_sqrt(px * px + py * py)
-                    : __builtin_sqrt((px * px + py * py) + pz * pz);
+  const T r2 = (p.ndim == 2) ? (px * px + py * py) : ((px * px + py * py) + pz * pz);
+  if constexpr (std::is_same<T, float>::value) x = (double)__builtin_sqrtf(r2);
+  else x = __builtin_sqrt(r2);
   return keep;
+}
+
+__device__ __forceinline__ double load_mass(const void *mass, int64_t i, int f32) {
+  return f32 ? (double)((const float *)mass)[i] : ((const double *)mass)[i];
 }
 
 // One pass: mask + x of a tile, then the tile's output offset by a
@@ -100,9 +110,9 @@ constexpr uint64_t kStAgg = 1ull << 62, kStPre = 2ull << 62, kStVal = (1ull << 6
 // base + 64 * (64 t + j) ...) and the tile's output offset (toff[t]), from
 // which the weights and indices are materialised only when needed
 // (sel_materialize) and the assignment reads the masses directly.
-template <int BT, bool LAZY>
+template <int BT, bool LAZY, typename T>
 __global__ void __launch_bounds__(BT)
-    select_onepass(const double *__restrict__ pos, const double *__restrict__ mass, int64_t n,
+    select_onepass(const T *__restrict__ pos, const void *__restrict__ mass, int64_t n,
                    SelectParams p, uint64_t *__restrict__ status, uint32_t *__restrict__ ctrl,
                    double *__restrict__ xo, double *__restrict__ wo, int32_t *__restrict__ io,
                    unsigned long long *__restrict__ minmax, uint64_t *__restrict__ kw,
@@ -126,14 +136,14 @@ __global__ void __launch_bounds__(BT)
   unsigned long long kmin = ~0ull, kmax = 0ull;
   // all SI positions in flight at once (particles outside the range or the
   // family slices read particle 0: no branch around the loads, no extra lines)
-  double px[SI], py[SI], pz[SI];
+  T px[SI], py[SI], pz[SI];
   uint32_t inbits = 0;
 #pragma unroll
   for (int k = 0; k < SI; ++k) {
     const int64_t i = wbase + k * 64 + lane;
     const bool in = (i < n) && in_family(i, p);
     inbits |= (uint32_t)in << k;
-    const double *q = pos + 3 * (in ? i : 0);
+    const T *q = pos + 3 * (in ? i : 0);
     px[k] = q[0];
     py[k] = q[1];
     pz[k] = q[2];
@@ -155,7 +165,7 @@ __global__ void __launch_bounds__(BT)
 #pragma unroll
     for (int k = 0; k < SI; ++k) {
       const int64_t i = wbase + k * 64 + lane;
-      mv[k] = mass ? mass[((keepbits >> k) & 1u) ? i : 0] : 1.0;
+      mv[k] = mass ? load_mass(mass, ((keepbits >> k) & 1u) ? i : 0, p.mass_f32) : 1.0;
     }
   }
 #pragma unroll
@@ -2064,9 +2074,10 @@ static void csr_device(Profile &P, hipStream_t st) {
 // select_onepass); the masses are then read from `mass` (the caller's device
 // array, or a handle-owned staged copy) when the weights are needed.
 // Returns the tile count.
-static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, const double *mass,
+static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
                               int64_t n, int on_device, int use_sphere, const double *sphere,
-                              const int64_t *fam, int nfam, int ndim, bool lazy = false) {
+                              const int64_t *fam, int nfam, int ndim, bool lazy = false,
+                              int pos_f32 = 0, int mass_f32 = 0) {
   check_n(n);
   if (ndim != 2 && ndim != 3) fail(PBX_ERR_VALUE, "ndim must be either 2 or 3");
   if (nfam < 0 || nfam > MAX_FAM) fail(PBX_ERR_VALUE, "at most %d family ranges", MAX_FAM);
@@ -2097,15 +2108,19 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, con
   }
   sp.base = lo;
   const int64_t span = hi - lo;
-  const double *d_pos = pos, *d_mass = mass;
+  if (lazy && (pos_f32 || mass_f32)) fail(PBX_ERR_VALUE, "the lazy selection takes float64 arrays");
+  sp.mass_f32 = mass_f32;
+  const size_t ps = pos_f32 ? sizeof(float) : sizeof(double);
+  const size_t ms = mass_f32 ? sizeof(float) : sizeof(double);
+  const void *d_pos = pos, *d_mass = mass;
   if (!on_device && n) {
-    double *tp = (double *)P.keys0.get(sizeof(double) * 3 * (size_t)n);
-    PBX_HIP(hipMemcpyAsync(tp, pos, sizeof(double) * 3 * n, hipMemcpyHostToDevice, st));
+    void *tp = P.keys0.get(ps * 3 * (size_t)n);
+    PBX_HIP(hipMemcpyAsync(tp, pos, ps * 3 * n, hipMemcpyHostToDevice, st));
     d_pos = tp;
     if (mass) {
       Buf &mb = lazy ? P.mstage : P.keys1;  // lazy: kept for the selection's lifetime
-      double *tm2 = (double *)mb.get(sizeof(double) * (size_t)n);
-      PBX_HIP(hipMemcpyAsync(tm2, mass, sizeof(double) * n, hipMemcpyHostToDevice, st));
+      void *tm2 = mb.get(ms * (size_t)n);
+      PBX_HIP(hipMemcpyAsync(tm2, mass, ms * n, hipMemcpyHostToDevice, st));
       d_mass = tm2;
     }
   }
@@ -2130,16 +2145,20 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, con
   unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
   PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * nst, st));
   if (span) {
-    auto go = [&](auto kern, int bt) {
-      hipLaunchKernelGGL(kern, dim3(nt), dim3(bt), 0, st, d_pos, d_mass, hi, sp, stat, ctrl, xo,
-                         wo, io, mm, kw, toff);
+    auto go = [&](auto kern, int bt, auto tp) {
+      using T = decltype(tp);
+      hipLaunchKernelGGL(kern, dim3(nt), dim3(bt), 0, st, (const T *)d_pos, d_mass, hi, sp, stat,
+                         ctrl, xo, wo, io, mm, kw, toff);
     };
-    if (nt < 1024) {
-      if (lazy) go(select_onepass<1024, true>, 1024);
-      else go(select_onepass<1024, false>, 1024);
+    if (pos_f32) {  // float32 snapshots: eager only
+      if (nt < 1024) go(select_onepass<1024, false, float>, 1024, 0.0f);
+      else go(select_onepass<TPB, false, float>, TPB, 0.0f);
+    } else if (nt < 1024) {
+      if (lazy) go(select_onepass<1024, true, double>, 1024, 0.0);
+      else go(select_onepass<1024, false, double>, 1024, 0.0);
     } else {
-      if (lazy) go(select_onepass<TPB, true>, TPB);
-      else go(select_onepass<TPB, false>, TPB);
+      if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
+      else go(select_onepass<TPB, false, double>, TPB, 0.0);
     }
     PBX_HIP(hipGetLastError());
   }
@@ -2147,7 +2166,7 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const double *pos, con
   P.sel_base = lo;
   P.sel_span = span;
   P.sel_nt = nt;
-  P.sel_mass = lazy ? d_mass : nullptr;
+  P.sel_mass = lazy ? (const double *)d_mass : nullptr;
   return nt;
 }
 
@@ -2373,14 +2392,26 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
 int pbx_profile_select(void *handle, const double *pos, const double *mass, int64_t n,
                        int on_device, int use_sphere, const double *sphere, const int64_t *fam,
                        int nfam, int ndim, int64_t *n_kept) {
+  return pbx_profile_select_typed(handle, pos, PBX_F64, mass, PBX_F64, n, on_device, use_sphere,
+                                  sphere, fam, nfam, ndim, n_kept);
+}
+
+int pbx_profile_select_typed(void *handle, const void *pos, int pos_dtype, const void *mass,
+                             int mass_dtype, int64_t n, int on_device, int use_sphere,
+                             const double *sphere, const int64_t *fam, int nfam, int ndim,
+                             int64_t *n_kept) {
   return guard([&] {
     Profile &P = as_profile(handle);
+    if ((pos_dtype != PBX_F64 && pos_dtype != PBX_F32) ||
+        (mass_dtype != PBX_F64 && mass_dtype != PBX_F32))
+      fail(PBX_ERR_VALUE, "dtype must be PBX_F64 or PBX_F32");
     Device &d = current_device();
     std::lock_guard<std::mutex> lk(d.mu);
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.select");
     const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
-                                      nfam, ndim);
+                                      nfam, ndim, false, pos_dtype == PBX_F32,
+                                      mass_dtype == PBX_F32);
     int64_t kept = 0;
     if (nt) {
       uint64_t *stat = (uint64_t *)P.selst.p;

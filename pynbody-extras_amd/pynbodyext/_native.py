@@ -105,6 +105,9 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_profile_set_x": (c_int, [c_void_p, _dp, c_int64]),
     "pbx_profile_select": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, _dp, _i64p,
                                    c_int, c_int, _i64p]),
+    "pbx_profile_select_typed": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int64,
+                                         c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                         POINTER(c_int64)]),
     "pbx_profile_get_selection": (c_int, [c_void_p, _i64p, _dp, _dp]),
     "pbx_profile_minmax": (c_int, [c_void_p, _dp, _dp]),
     "pbx_profile_edges_equaln": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double, _dp,

@@ -17,6 +17,7 @@ from .. import _native as nat
 NMOM = 7  # Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|
 ALL_COLS = (1 << NMOM) - 1
 SRC_X, SRC_W, SRC_HOST, SRC_DEVICE, SRC_NONE = 0, 1, 2, 3, -1
+PBX_F64, PBX_F32 = 0, 1  # element types of pbx_profile_select_typed
 
 _i64p = ctypes.POINTER(c_int64)
 
@@ -59,34 +60,48 @@ class DeviceBins:
                into: "DeviceBins | None" = None) -> "DeviceBins":
         """Fused mask + x + compaction.
 
-        pos / mass: host (N,3) / (N,) float64 arrays, or device pointers
-        (``on_device=True``, then ``n`` is required).  sphere: (cen, radius)
+        pos / mass: host (N,3) / (N,) float64 or float32 arrays (float32 is
+        passed as is: r in float32 arithmetic, like numpy on a float32
+        snapshot), or float64 device pointers (``on_device=True``, then ``n``
+        is required).  sphere: (cen, radius)
         or None.  families: list of (start, stop) index ranges or None.
         ``into`` reuses an existing handle (and its HBM buffers).
         """
         d = into if into is not None else cls()
         d.nbins, d._csr = None, None
-        args, keep = cls._select_args(pos, mass, sphere, families, ndim, on_device, n)
+        # float32 snapshots stay float32 (no host up-cast; pbx_profile_select_typed)
+        d._pos_dt = PBX_F32 if (not on_device and np.asarray(pos).dtype == np.float32) else PBX_F64
+        d._mass_dt = (PBX_F32 if (not on_device and mass is not None and
+                                  np.asarray(mass).dtype == np.float32) else PBX_F64)
+        args, keep = cls._select_args(pos, mass, sphere, families, ndim, on_device, n,
+                                      native_f32=True)
         kept = c_int64(0)
-        nat.call("pbx_profile_select", d._h, *args, byref(kept))
+        p_pos, p_mass, n_part, *rest = args
+        nat.call("pbx_profile_select_typed", d._h, p_pos, d._pos_dt, p_mass, d._mass_dt, n_part,
+                 *rest, byref(kept))
         del keep
         d.n = kept.value
         d.has_selection = True
         return d
 
     @staticmethod
-    def _select_args(pos, mass, sphere, families, ndim, on_device, n):
+    def _select_args(pos, mass, sphere, families, ndim, on_device, n, native_f32=False):
         """ctypes arguments of a selection (pbx_profile_select order) and the
         host arrays to keep alive during the call."""
         if on_device:
             p_pos, p_mass, n_part = pos, mass, int(n)
             keep = ()
         else:
-            pos = np.ascontiguousarray(pos, dtype=np.float64)
+            pos = np.asarray(pos)
+            f32 = native_f32 and pos.dtype == np.float32
+            pos = np.ascontiguousarray(pos, dtype=np.float32 if f32 else np.float64)
             if pos.ndim != 2 or pos.shape[1] != 3:
                 raise ValueError("pos must be (N,3)")
             n_part = pos.shape[0]
-            mass = None if mass is None else np.ascontiguousarray(mass, dtype=np.float64)
+            if mass is not None:
+                mass = np.asarray(mass)
+                mf32 = native_f32 and mass.dtype == np.float32
+                mass = np.ascontiguousarray(mass, dtype=np.float32 if mf32 else np.float64)
             p_pos = pos.ctypes.data_as(c_void_p)
             p_mass = None if mass is None else mass.ctypes.data_as(c_void_p)
             keep = (pos, mass)

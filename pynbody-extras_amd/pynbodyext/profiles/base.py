@@ -28,6 +28,12 @@ from .spatial_profile import RadialProfile
 __all__ = ["ProfileBuilderBase", "RadialProfileBuilder"]
 
 
+def _native_float(a) -> np.ndarray:
+    """float32 stays float32; anything else is taken as float64."""
+    a = np.asarray(a)
+    return a if a.dtype in (np.float32, np.float64) else a.astype(np.float64)
+
+
 class ProfileBuilderBase(CalculatorBase):
     """Calculator building a profile from the active snapshot."""
 
@@ -91,15 +97,18 @@ class RadialProfileBuilder(ProfileBuilderBase):
             return NotImplemented
         params = self.resolve_dynamic_params(ctx, input)
         with ctx.phase(self, "device select"):
-            pos = np.asarray(source["pos"], dtype=np.float64)
-            mass = np.asarray(source["mass"], dtype=np.float64) if "mass" in source.keys() else None
+            # float32 snapshots go to the device as float32 (no host copy):
+            # r / rxy are then float32 values, exactly pynbody's derived array
+            pos = _native_float(source["pos"])
+            mass = _native_float(source["mass"]) if "mass" in source.keys() else None
             dev = DeviceBins.select(pos, mass, sphere=spec.get("sphere"),
                                     families=spec.get("families"), ndim=self.ndim)
             idx, x, _ = dev.selection(idx=True, x=True, w=False)
         sub = source[idx]
         key = "r" if self.ndim == 3 else "rxy"
         if hasattr(sub, "_derived"):
-            sub._derived[key] = x   # the device computed the same values
+            # the device computed the same values (in the positions' precision)
+            sub._derived[key] = x.astype(pos.dtype) if pos.dtype != x.dtype else x
         xs = sub[key]
         bins_area = "spherical_shell" if self.ndim == 3 else "annulus"
         with ctx.phase(self, "device bins"):

@@ -184,8 +184,76 @@ def edge_cases(bins_mod):
     return out
 
 
+def spatial_cases(bins_mod, pa_mod):
+    """RadialProfile's two spatial forms (spatial_profile.py:30-35):
+    * ann_*: ndim=2 — bins_by "rxy", bins_area "annulus" (bins.py:759-765)
+      on a thin disk; rxy = sqrt(x*x + y*y) (pynbody's derived rxy, which
+      pynbody is absent to confirm: parity with pynbody unpinned);
+    * f32_*: a float32 snapshot behind Sphere & FamilyFilter, ndim=3 equaln
+      128 weight mass — numpy's dtype rules: the Sphere distance against the
+      float64 centre is float64, r of the float32 positions is float32, and
+      the reference's binning / statistics then run on float32 arrays.
+    Only inputs and the reference's outputs are stored."""
+    BinsSet = bins_mod.BinsSet
+    out = {}
+    rng = np.random.default_rng(2101)
+    n = 20000
+    pos = np.column_stack([rng.normal(scale=3.0, size=n), rng.normal(scale=3.0, size=n),
+                           rng.normal(scale=0.3, size=n)])
+    mass = rng.uniform(0.5, 1.5, n)
+    out["ann/pos"], out["ann/mass"] = pos, mass
+    rxy = np.sqrt(pos[:, 0] * pos[:, 0] + pos[:, 1] * pos[:, 1])
+    for tag, bt, nb, lo, hi in (("lin_64", "lin", 64, None, None),
+                                ("log_64", "log", 64, 0.05, 15.0),
+                                ("equaln_100", "equaln", 100, None, None)):
+        bs = BinsSet(bins_by="rxy", bins_area="annulus", bins_type=bt, nbins=nb, bin_min=lo,
+                     bin_max=hi)
+        edges = np.asarray(BinsSet._bins_algorithm_registry[bt](bs, rxy), dtype=np.float64)
+        binind, counts = bs._assign_particles(rxy, edges)
+        area = BinsSet._bins_area_registry["annulus"](bs, edges)
+        prof = SimpleNamespace(nbins=len(edges) - 1, _weight=mass, binind=binind)
+        msum, _ = pa_mod.ProfileArray._compute(prof, mass, "sum")
+        out[f"ann/{tag}/edges"] = edges
+        out[f"ann/{tag}/counts"] = np.asarray(counts, dtype=np.int64)
+        out[f"ann/{tag}/perm"] = np.concatenate(binind).astype(np.int64)
+        out[f"ann/{tag}/area"] = np.asarray(area, dtype=np.float64)
+        out[f"ann/{tag}/mass_sum"] = np.asarray(msum, dtype=np.float64)
+    # float32 snapshot
+    x = rng.random(n)
+    r = np.minimum((x ** (-2.0 / 3.0) - 1.0) ** -0.5, 50.0)
+    ct, ph = rng.uniform(-1.0, 1.0, n), rng.uniform(0.0, 2 * np.pi, n)
+    st = np.sqrt(1.0 - ct * ct)
+    pos32 = np.column_stack([r * st * np.cos(ph), r * st * np.sin(ph), r * ct]).astype(np.float32)
+    mass32 = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    cen, radius, fam = np.array([0.5, -0.25, 0.125]), 10.0, (0, 12000)
+    dx, dy, dz = (pos32[:, 0] - cen[0], pos32[:, 1] - cen[1], pos32[:, 2] - cen[2])
+    mask = ((dx * dx + dy * dy) + dz * dz) < radius * radius
+    mask[fam[1]:] = False
+    kept = np.nonzero(mask)[0]
+    p = pos32[kept]
+    r32 = np.sqrt((p[:, 0] * p[:, 0] + p[:, 1] * p[:, 1]) + p[:, 2] * p[:, 2])
+    assert r32.dtype == np.float32 and dx.dtype == np.float64
+    m32 = mass32[kept]
+    bs = BinsSet(bins_by="r", bins_area="spherical_shell", bins_type="equaln", nbins=128)
+    edges = BinsSet._bins_algorithm_registry["equaln"](bs, r32)
+    binind, counts = bs._assign_particles(r32, edges)
+    prof = SimpleNamespace(nbins=len(edges) - 1, _weight=m32, binind=binind)
+    msum, _ = pa_mod.ProfileArray._compute(prof, m32, "sum")
+    rmean, _ = pa_mod.ProfileArray._compute(prof, r32, "mean")
+    out.update({"f32/pos": pos32, "f32/mass": mass32, "f32/cen": cen,
+                "f32/radius": np.array(radius), "f32/fam": np.array(fam, dtype=np.int64),
+                "f32/kept": kept.astype(np.int64), "f32/r": r32,
+                "f32/edges": np.asarray(edges), "f32/counts": np.asarray(counts, dtype=np.int64),
+                "f32/perm": np.concatenate(binind).astype(np.int64),
+                "f32/mass_sum": np.asarray(msum), "f32/r_mean": np.asarray(rmean)})
+    return out
+
+
 def main():
     bins_mod, pa_mod = load_reference()
+    np.savez_compressed(OUT / "profile_spatial.npz", numpy_version=np.array(np.__version__),
+                        **spatial_cases(bins_mod, pa_mod))
+    print("wrote profile_spatial.npz")
     meta = {"numpy_version": np.array(np.__version__)}
     for n, seed, full in ((1000, 2001, True), (10000, 2002, True), (100000, 2003, False)):
         x, w, f = dataset(n, seed)

@@ -4,6 +4,7 @@ GPU, torch.distributed.run, before any GPU call), and a rank whose
 WORLD_SIZE differs from ``--gpus`` exits non-zero."""
 import json
 import os
+import re
 import subprocess
 import sys
 from pathlib import Path
@@ -22,7 +23,8 @@ def test_bench_gpus2_spawns_two_ranks():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=_env(),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    ranks = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    # the ranks print concurrently: their lines may interleave
+    ranks = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
     assert sorted(x["rank"] for x in ranks) == [0, 1]
     assert all(x["world"] == 2 for x in ranks)
     assert sorted(x["local_rank"] for x in ranks) == [0, 1]

@@ -97,3 +97,44 @@ def test_edge_cases():
     with pytest.raises(ValueError) as e:
         pr.edges_log(np.array([0.0, 1.0]), 4)
     assert str(e.value) == str(g["log_error/message"])
+
+
+SPATIAL = np.load(GOLD / "profile_spatial.npz")
+
+
+@pytest.mark.parametrize("tag,bt,nb,lo,hi", [("lin_64", "lin", 64, None, None),
+                                             ("log_64", "log", 64, 0.05, 15.0),
+                                             ("equaln_100", "equaln", 100, None, None)])
+def test_oracle_annulus_fixture(tag, bt, nb, lo, hi):
+    """ndim=2 (rxy, annulus areas, bins.py:759-765) against the reference."""
+    pos, mass = SPATIAL["ann/pos"], SPATIAL["ann/mass"]
+    rxy = np.sqrt(pos[:, 0] * pos[:, 0] + pos[:, 1] * pos[:, 1])
+    edges = pr.EDGE_ALGORITHMS[bt](rxy, nb, lo, hi)
+    assert np.array_equal(edges, SPATIAL[f"ann/{tag}/edges"])
+    perm, offsets, counts = pr.assign(rxy, edges)
+    assert np.array_equal(counts, SPATIAL[f"ann/{tag}/counts"])
+    assert np.array_equal(perm, SPATIAL[f"ann/{tag}/perm"])
+    assert np.array_equal(pr.area_annulus(edges), SPATIAL[f"ann/{tag}/area"])
+    msum, _ = pr.compute(mass, mass, perm, offsets, "sum")
+    assert np.array_equal(msum, SPATIAL[f"ann/{tag}/mass_sum"], equal_nan=True)
+
+
+def test_oracle_float32_fixture():
+    """A float32 snapshot: numpy's dtype rules (float64 Sphere distance,
+    float32 r) and the reference's binning of the float32 r array."""
+    pos, mass = SPATIAL["f32/pos"], SPATIAL["f32/mass"]
+    lo, hi = (int(v) for v in SPATIAL["f32/fam"])
+    mask = pr.sphere_mask(pos, float(SPATIAL["f32/radius"]), SPATIAL["f32/cen"])
+    mask[hi:] = False
+    mask[:lo] = False
+    kept = np.nonzero(mask)[0]
+    assert np.array_equal(kept, SPATIAL["f32/kept"])
+    r = pr.radial_r(pos[kept])
+    assert r.dtype == np.float32 and np.array_equal(r, SPATIAL["f32/r"])
+    edges = pr.edges_equaln(r, 128)
+    assert edges.dtype == np.float32 and np.array_equal(edges, SPATIAL["f32/edges"])
+    perm, offsets, counts = pr.assign(r, edges)
+    assert np.array_equal(counts, SPATIAL["f32/counts"])
+    assert np.array_equal(perm, SPATIAL["f32/perm"])
+    msum, _ = pr.compute(mass[kept], mass[kept], perm, offsets, "sum")
+    assert np.array_equal(msum, SPATIAL["f32/mass_sum"], equal_nan=True)
