@@ -281,11 +281,15 @@ __global__ void __launch_bounds__(TPB) bbox_kernel(const double *__restrict__ po
 // LPW levels per word (level 0 in the top bits of word 0).
 __global__ void __launch_bounds__(TPB)
     path_keys(const double *__restrict__ pos, int64_t n, double cx0, double cy0, double cz0,
-              double half0, int nwords, uint64_t *__restrict__ keys) {
+              double half0, int nwords, uint64_t *__restrict__ keys,
+              const double *__restrict__ mass, double4 *__restrict__ rec0) {
 #pragma clang fp contract(off)
   int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= n) return;
   const double x = pos[3 * i], y = pos[3 * i + 1], z = pos[3 * i + 2];
+  // {x, y, z, m} in original order while the positions are in registers:
+  // pack_records then gathers one 32-byte record per particle
+  if (rec0) rec0[i] = make_double4(x, y, z, mass ? mass[i] : 1.0);
   double cx = cx0, cy = cy0, cz = cz0, h = half0;
   for (int w = 0; w < nwords; ++w) {
     uint64_t word = 0;
@@ -494,13 +498,16 @@ __global__ void leaf_sort(const int32_t *__restrict__ nchild, const int32_t *__r
   }
 }
 
-__global__ void pack_records(const double *__restrict__ pos, const double *__restrict__ mass,
-                             const int32_t *__restrict__ perm, int64_t n,
-                             double4 *__restrict__ rec) {
+__global__ void pack_records(const double4 *__restrict__ rec0, const int32_t *__restrict__ perm,
+                             int64_t n, double4 *__restrict__ rec) {
   int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (i >= n) return;
-  const int64_t p = perm[i];
-  rec[i] = make_double4(pos[3 * p], pos[3 * p + 1], pos[3 * p + 2], mass ? mass[p] : 1.0);
+  if (i < n) rec[i] = rec0[perm[i]];
+}
+
+__global__ void interleave_records(const double *__restrict__ pos, const double *__restrict__ mass,
+                                   int64_t n, double4 *__restrict__ rec0) {
+  int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i < n) rec0[i] = make_double4(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2], mass ? mass[i] : 1.0);
 }
 
 __global__ void gather_f64(const double *__restrict__ src, const int32_t *__restrict__ perm,
@@ -564,6 +571,48 @@ __device__ __forceinline__ void m2m_add(double (&M)[ncoef(P)], const double *__r
   });
 }
 
+// One record per node in DFS preorder, read by a wave with a single burst of
+// scalar loads:  [cx cy cz mass | size2 hmax | next first | leaf_start count]
+// (64 B) followed by the node's evaluation coefficients (orders 2-3: the
+// detraced Q', K'; orders 4-5: raw moments).
+template <int P> __host__ __device__ constexpr int rec_stride() {
+  return P <= 1 ? 8 : (P == 2 ? 16 : (P == 3 ? 24 : (P == 4 ? 48 : 64)));
+}
+
+template <int P>
+__device__ __forceinline__ void detraced_coef(const double *M, double *C) {
+  const double sxx = 2.0 * M[4], syy = 2.0 * M[5], szz = 2.0 * M[6];
+  const double tr3 = (sxx + syy + szz) * (1.0 / 3.0);
+  C[0] = 1.5 * (sxx - tr3);
+  C[1] = 1.5 * (syy - tr3);
+  C[2] = 1.5 * (szz - tr3);
+  C[3] = 1.5 * M[7];  // xy
+  C[4] = 1.5 * M[8];  // xz
+  C[5] = 1.5 * M[9];  // yz
+  if constexpr (P == 3) {
+    // S_ijk = l! m! n! M_lmn
+    const double sxxx = 6.0 * M[10], syyy = 6.0 * M[11], szzz = 6.0 * M[12];
+    const double sxxy = 2.0 * M[13], sxxz = 2.0 * M[14], sxyy = 2.0 * M[15];
+    const double sxzz = 2.0 * M[16], syyz = 2.0 * M[17], syzz = 2.0 * M[18];
+    const double sxyz = M[19];
+    const double tx = sxxx + sxyy + sxzz, ty = sxxy + syyy + syzz, tz = sxxz + syyz + szzz;
+    // T[S3]_ijk = S_ijk - (d_ij t_k + d_ik t_j + d_jk t_i) / 5
+    const double oxxx = sxxx - 0.6 * tx, oyyy = syyy - 0.6 * ty, ozzz = szzz - 0.6 * tz;
+    const double oxxy = sxxy - 0.2 * ty, oxxz = sxxz - 0.2 * tz, oxyy = sxyy - 0.2 * tx;
+    const double oxzz = sxzz - 0.2 * tx, oyyz = syyz - 0.2 * tz, oyzz = syzz - 0.2 * ty;
+    C[6] = 2.5 * oxxx;         // x^3
+    C[7] = 2.5 * 3.0 * oxxy;   // x^2 y
+    C[8] = 2.5 * 3.0 * oxxz;   // x^2 z
+    C[9] = 2.5 * 3.0 * oxyy;   // x y^2
+    C[10] = 2.5 * 6.0 * sxyz;  // x y z
+    C[11] = 2.5 * 3.0 * oxzz;  // x z^2
+    C[12] = 2.5 * oyyy;        // y^3
+    C[13] = 2.5 * 3.0 * oyyz;  // y^2 z
+    C[14] = 2.5 * 3.0 * oyzz;  // y z^2
+    C[15] = 2.5 * ozzz;        // z^3
+  }
+}
+
 struct PayloadView {
   const int32_t *nstart, *ncount, *nfirst, *nchild;
   const double4 *rec;
@@ -571,6 +620,11 @@ struct PayloadView {
   double4 *com;        // com xyz + mass
   double *hmax;        // or null
   double *mom;         // ncoef(P) per node (P >= 2) or null
+  // the node's walk record, written here too (DFS preorder pre[k])
+  const int32_t *pre, *size;
+  const double4 *ncen;
+  int64_t nn;
+  double *walk;
 };
 
 // one level of the bottom-up payload pass (tree.rs:866-1067)
@@ -685,6 +739,39 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
   }
   v.com[k] = make_double4(cx, cy, cz, mass);
   if (v.hmax) v.hmax[k] = hm;
+  {  // the walk record (was pack_walk / pack_coef / pack_moments)
+#pragma clang fp contract(off)
+    const int32_t pk = v.pre[k];
+    double *r = v.walk + (int64_t)pk * rec_stride<P>();
+    r[0] = cx;
+    r[1] = cy;
+    r[2] = cz;
+    r[3] = mass;
+    const double sz = v.ncen[k].w * 2.0;  // tree.rs:794-798
+    r[4] = sz * sz;
+    r[5] = v.hmax ? hm : 0.0;
+    // DFS preorder ids: first child = k + 1, next_branch = k + subtree size
+    // (the same threading as tree.rs:736-776, renumbered)
+    const int64_t after = (int64_t)pk + v.size[k];
+    const bool leaf = nc == 0;
+    int32_t *ir = (int32_t *)(r + 6);
+    ir[0] = after < v.nn ? (int32_t)after : -1;
+    ir[1] = leaf ? -1 : pk + 1;
+    ir[2] = leaf ? v.nstart[k] : 0;
+    ir[3] = leaf ? v.ncount[k] : 0;
+    if constexpr (P >= 2) {
+      const double *Mk = v.mom + (int64_t)k * ncoef(P);  // just written by this thread
+      if constexpr (P == 2 || P == 3) {
+        double Mc[ncoef(P)];
+#pragma unroll
+        for (int q = 0; q < ncoef(P); ++q) Mc[q] = Mk[q];
+        detraced_coef<P>(Mc, r + 8);
+      } else {
+#pragma unroll
+        for (int q = 0; q < ncoef(P); ++q) r[8 + q] = Mk[q];
+      }
+    }
+  }
 }
 
 // Detraced evaluation coefficients (orders 2 and 3).  With raw moments
@@ -698,85 +785,13 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
 //        (x^3, x^2y, x^2z, xy^2, xyz, xz^2, y^3, y^2z, yz^2, z^3)
 // so phi = -M/r - q2'/r^5 + q3'/r^7 with q2' = R.Q'.R and q3' = K'(R).
 __host__ __device__ constexpr int ncoef_fast(int P) { return P == 3 ? 16 : (P == 2 ? 6 : 0); }
-template <int P> __host__ __device__ constexpr int rec_stride();
-
-template <int P>
-__global__ void pack_coef(const double *__restrict__ mom, const int32_t *__restrict__ pre,
-                          int64_t nn, double *__restrict__ coef) {
-  int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (k >= nn) return;
-  const double *M = mom + k * ncoef(P);
-  double *C = coef + (int64_t)pre[k] * rec_stride<P>() + 8;
-  const double sxx = 2.0 * M[4], syy = 2.0 * M[5], szz = 2.0 * M[6];
-  const double tr3 = (sxx + syy + szz) * (1.0 / 3.0);
-  C[0] = 1.5 * (sxx - tr3);
-  C[1] = 1.5 * (syy - tr3);
-  C[2] = 1.5 * (szz - tr3);
-  C[3] = 1.5 * M[7];  // xy
-  C[4] = 1.5 * M[8];  // xz
-  C[5] = 1.5 * M[9];  // yz
-  if constexpr (P == 3) {
-    // S_ijk = l! m! n! M_lmn
-    const double sxxx = 6.0 * M[10], syyy = 6.0 * M[11], szzz = 6.0 * M[12];
-    const double sxxy = 2.0 * M[13], sxxz = 2.0 * M[14], sxyy = 2.0 * M[15];
-    const double sxzz = 2.0 * M[16], syyz = 2.0 * M[17], syzz = 2.0 * M[18];
-    const double sxyz = M[19];
-    const double tx = sxxx + sxyy + sxzz, ty = sxxy + syyy + syzz, tz = sxxz + syyz + szzz;
-    // T[S3]_ijk = S_ijk - (d_ij t_k + d_ik t_j + d_jk t_i) / 5
-    const double oxxx = sxxx - 0.6 * tx, oyyy = syyy - 0.6 * ty, ozzz = szzz - 0.6 * tz;
-    const double oxxy = sxxy - 0.2 * ty, oxxz = sxxz - 0.2 * tz, oxyy = sxyy - 0.2 * tx;
-    const double oxzz = sxzz - 0.2 * tx, oyyz = syyz - 0.2 * tz, oyzz = syzz - 0.2 * ty;
-    C[6] = 2.5 * oxxx;         // x^3
-    C[7] = 2.5 * 3.0 * oxxy;   // x^2 y
-    C[8] = 2.5 * 3.0 * oxxz;   // x^2 z
-    C[9] = 2.5 * 3.0 * oxyy;   // x y^2
-    C[10] = 2.5 * 6.0 * sxyz;  // x y z
-    C[11] = 2.5 * 3.0 * oxzz;  // x z^2
-    C[12] = 2.5 * oyyy;        // y^3
-    C[13] = 2.5 * 3.0 * oyyz;  // y^2 z
-    C[14] = 2.5 * 3.0 * oyzz;  // y z^2
-    C[15] = 2.5 * ozzz;        // z^3
-  }
-}
 
 // ------------------------------------------------------------------- walk
 // One record per node in DFS preorder, read by a wave with a single burst of
 // scalar loads:  [cx cy cz mass | size2 hmax | next first | leaf_start count]
 // (64 B) followed by the node's evaluation coefficients (orders 2-3: the
 // detraced Q', K'; orders 4-5: raw moments).
-template <int P> __host__ __device__ constexpr int rec_stride() {
-  return P <= 1 ? 8 : (P == 2 ? 16 : (P == 3 ? 24 : (P == 4 ? 48 : 64)));
-}
-
-template <int P>
-__global__ void pack_walk(const double4 *__restrict__ com, const double4 *__restrict__ ncen,
-                          const double *__restrict__ hmax, const int32_t *__restrict__ nchild,
-                          const int32_t *__restrict__ nstart, const int32_t *__restrict__ ncount,
-                          const int32_t *__restrict__ pre, const int32_t *__restrict__ size,
-                          int64_t nn, double *__restrict__ walk) {
-#pragma clang fp contract(off)
-  int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (k >= nn) return;
-  const int32_t pk = pre[k];
-  double *r = walk + (int64_t)pk * rec_stride<P>();
-  const double4 c = com[k];
-  r[0] = c.x;
-  r[1] = c.y;
-  r[2] = c.z;
-  r[3] = c.w;
-  const double s = ncen[k].w * 2.0;  // tree.rs:794-798
-  r[4] = s * s;
-  r[5] = hmax ? hmax[k] : 0.0;
-  // DFS preorder ids: first child = k + 1, next_branch = k + subtree size
-  // (the same threading as tree.rs:736-776, renumbered)
-  const int64_t after = (int64_t)pk + size[k];
-  const bool leaf = nchild[k] == 0;
-  int32_t *ir = (int32_t *)(r + 6);
-  ir[0] = after < nn ? (int32_t)after : -1;
-  ir[1] = leaf ? -1 : pk + 1;
-  ir[2] = leaf ? nstart[k] : 0;
-  ir[3] = leaf ? ncount[k] : 0;
-}
+// (rec_stride: defined with the payload, which writes the walk records)
 
 // subtree sizes, one level bottom-up
 __global__ void subtree_size(const int32_t *__restrict__ nfirst, const int32_t *__restrict__ nchild,
@@ -801,16 +816,6 @@ __global__ void preorder_ids(const int32_t *__restrict__ nfirst, const int32_t *
     pre[c] = run;
     run += size[c];
   }
-}
-
-// raw moments in preorder (orders >= 4 evaluate them directly)
-template <int P>
-__global__ void pack_moments(const double *__restrict__ mom, const int32_t *__restrict__ pre,
-                             int64_t nn, double *__restrict__ walk) {
-  int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (k >= nn) return;
-  double *out = walk + (int64_t)pre[k] * rec_stride<P>() + 8;
-  for (int q = 0; q < ncoef(P); ++q) out[q] = mom[k * ncoef(P) + q];
 }
 
 struct WalkParams {
@@ -1129,6 +1134,238 @@ __global__ void leaf_particles_kernel(const double4 *__restrict__ rec, const int
   if (idx) idx[t] = perm[first + t];
 }
 
+// ------------------------------------------ parallel structure (sorted paths)
+// The level-synchronous split (split_count / split_make, one host read-back
+// per level) rebuilt from the sorted octant paths in a fixed number of
+// launches.  With the paths sorted, the particles of any node form one run
+// of a common path prefix, and a node at level d exists iff its parent's
+// run holds more than leaf_capacity particles (tree.rs:847-864).  For
+// particle i let m(i) = the deepest level whose run containing i still has
+// > cap particles: some window of cap + 1 consecutive sorted particles
+// around i shares that prefix, so m(i) = max over the windows [k, k + cap]
+// that contain i of lcp(path k, path k + cap).  i's leaf sits at level
+// L(i) = m(i) + 1, and the nodes that START at i are the levels
+// fd(i) .. L(i), fd(i) = 1 + lcp(path i - 1, path i) (fd(0) = 0).  Their
+// DFS preorder ids are S(i) + d - fd(i) with S the exclusive scan of the
+// per-particle node counts (the shallower node of a shared start comes
+// first); a stable sort of the nodes by level gives the breadth-first ids
+// of split_make (children contiguous, in octant order); every other field
+// (range end, subtree size, threaded next, first child, centre replayed
+// with the same additions as split_make, parent's child count) follows
+// from these.  Inputs the rule cannot decide (a run of > cap particles on
+// one full path: identical points, or deeper than the key words) fall back
+// to the level-synchronous builder.
+constexpr int BP_MAX_LEVEL = 200;
+
+// common leading octant digits of sorted paths a and b (multi-word)
+__device__ __forceinline__ int path_lcp(const uint64_t *__restrict__ keys, int64_t n, int nw,
+                                        int64_t a, int64_t b) {
+  for (int w = 0; w < nw; ++w) {
+    const uint64_t x = keys[(int64_t)w * n + a] ^ keys[(int64_t)w * n + b];
+    if (x) return w * LPW + (__builtin_clzll(x) - 1) / 3;  // bit 63 is never used
+  }
+  return nw * LPW;
+}
+
+// lcp of every window [k, k + cap] of cap + 1 consecutive sorted paths
+// (u8; 255 where the window does not exist) and of each path with its
+// predecessor
+__global__ void __launch_bounds__(TPB)
+    bp_lcp(const uint64_t *__restrict__ keys, int64_t n, int nw, int64_t cap,
+           uint8_t *__restrict__ eq, uint8_t *__restrict__ win) {
+  const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k >= n) return;
+  const int e = k ? path_lcp(keys, n, nw, k - 1, k) : 0;
+  eq[k] = (uint8_t)(e < 254 ? e : 254);
+  int l = 255;
+  if (k + cap < n) {
+    l = path_lcp(keys, n, nw, k, k + cap);
+    l = l < 254 ? l : 254;
+  }
+  win[k] = (uint8_t)l;
+}
+
+// fd(i), L(i) and the node count of every sorted position; level
+// histogram (LDS per block, one global add per level and block: the grid
+// is bounded, so those adds stay few — every block adds to the same words)
+constexpr int BP_DEPTH_BLOCKS = 1024;
+__global__ void __launch_bounds__(TPB)
+    bp_depth(const uint8_t *__restrict__ eq, const uint8_t *__restrict__ win, int64_t n, int D,
+             int64_t cap, uint8_t *__restrict__ fd, uint8_t *__restrict__ lv,
+             uint32_t *__restrict__ cnt, unsigned int *__restrict__ flag) {
+  __shared__ unsigned int h[BP_MAX_LEVEL + 1];
+  __shared__ uint8_t sw[TPB + 64];  // the windows [i - cap, i] of the chunk, cap <= 64
+  for (int d = threadIdx.x; d <= BP_MAX_LEVEL; d += TPB) h[d] = 0u;
+  bool over = false;
+  for (int64_t base = (int64_t)blockIdx.x * TPB; base < n; base += (int64_t)gridDim.x * TPB) {
+    __syncthreads();  // the previous chunk's windows are read
+    for (int j = threadIdx.x; j < TPB + cap; j += TPB) {
+      const int64_t k = base - cap + j;
+      sw[j] = (k >= 0 && k < n) ? win[k] : (uint8_t)255;
+    }
+    __syncthreads();
+    const int64_t i = base + threadIdx.x;
+    const bool ok = i < n;
+    int f = 1, L = 0;
+    if (ok) {  // D: levels whose prefix runs are contiguous (sorted)
+      f = i ? eq[i] + 1 : 0;
+      f = f < 255 ? f : 255;
+      int m = -1;
+      for (int j = 0; j <= cap; ++j) {
+        const int l = sw[threadIdx.x + j];
+        if (l != 255) m = l > m ? l : m;
+      }
+      over |= (m >= D || m + 1 > BP_MAX_LEVEL);  // undecidable: fall back
+      L = m + 1 < BP_MAX_LEVEL ? m + 1 : BP_MAX_LEVEL;
+      fd[i] = (uint8_t)f;
+      lv[i] = (uint8_t)L;
+      cnt[i] = (uint32_t)(L >= f ? L - f + 1 : 0);
+    }
+    // nodes per level: one ballot per level and wave
+    int dmax = ok ? L : -1;
+    for (int o = 32; o > 0; o >>= 1) {
+      const int y = __shfl_xor(dmax, o, 64);
+      dmax = y > dmax ? y : dmax;
+    }
+    for (int d = 0; d <= dmax; ++d) {
+      const uint32_t c = (uint32_t)__popcll(__ballot(ok && f <= d && d <= L));
+      if ((threadIdx.x & 63) == 0 && c) atomicAdd(&h[d], c);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[n] = 0u;  // scan sentinel: S[n] = nodes
+  if (__ballot(over) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+  __syncthreads();
+  for (int d = threadIdx.x; d <= BP_MAX_LEVEL; d += TPB)
+    if (h[d]) atomicAdd(&flag[1 + d], h[d]);
+}
+
+// every node in preorder: its level and start
+__global__ void __launch_bounds__(TPB)
+    bp_nodes_pre(const uint8_t *__restrict__ fd, const uint8_t *__restrict__ lv,
+                 const uint32_t *__restrict__ S, int64_t n, uint32_t *__restrict__ level,
+                 int32_t *__restrict__ start) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  const int f = fd[i], L = lv[i];
+  uint32_t pre = S[i];
+  for (int d = f; d <= L; ++d, ++pre) {
+    level[pre] = (uint32_t)d;
+    start[pre] = (int32_t)i;
+  }
+}
+
+__global__ void bp_inverse(const int32_t *__restrict__ b2p, int64_t nn, int32_t *__restrict__ p2b) {
+  const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k < nn) p2b[b2p[k]] = (int32_t)k;
+}
+
+// every node: range, centre, links, subtree size (in its breadth-first
+// slot); its parent's child count
+__global__ void __launch_bounds__(TPB)
+    bp_nodes_bfs(const uint64_t *__restrict__ keys, int64_t n, int nw, const uint8_t *__restrict__ eq,
+                 const uint8_t *__restrict__ fd,
+                 const uint8_t *__restrict__ lv, const uint32_t *__restrict__ S,
+                 const uint32_t *__restrict__ level, const int32_t *__restrict__ start,
+                 const int32_t *__restrict__ b2p, const int32_t *__restrict__ p2b, int64_t nn,
+                 double4 root, BuildView v, int32_t *__restrict__ size) {
+#pragma clang fp contract(off)
+  // threads walk the nodes in preorder (their start / level loads coalesce,
+  // neighbouring threads scan neighbouring paths); outputs go to the
+  // breadth-first slot
+  const int32_t pre = (int32_t)((int64_t)blockIdx.x * TPB + threadIdx.x);
+  if (pre >= nn) return;
+  const int64_t k = p2b[pre];
+  const int64_t i = start[pre];
+  const int d = (int)level[pre];
+  const int f = fd[i];
+  // range end: the first later path whose level-d prefix differs (eq of
+  // that path < d): the next 16 eq bytes first (leaves and the levels
+  // above them), then galloping over the paths
+  int64_t lo = i + 1, hi = n;
+  {
+    uint8_t e[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) e[q] = (i + 1 + q < n) ? eq[i + 1 + q] : (uint8_t)0;
+    int q0 = 16;
+#pragma unroll
+    for (int q = 15; q >= 0; --q)
+      if ((int)e[q] < d) q0 = q;
+    if (q0 < 16 || i + 17 >= n) hi = lo = (i + 1 + q0 < n) ? i + 1 + q0 : n;
+    else lo = i + 17;
+  }
+  for (int64_t step = 1; lo < hi;) {
+    const int64_t probe = lo + step - 1 < hi ? lo + step - 1 : hi - 1;
+    if (path_lcp(keys, n, nw, i, probe) >= d) {
+      lo = probe + 1;
+      step <<= 1;
+    } else {
+      hi = probe;
+      break;
+    }
+  }
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (path_lcp(keys, n, nw, i, mid) >= d) lo = mid + 1;
+    else hi = mid;
+  }
+  const int64_t end = lo;
+  const int32_t sz = (int32_t)((S[end] - S[i]) - (uint32_t)(d - f));
+  v.nstart[k] = (int32_t)i;
+  v.ncount[k] = (int32_t)(end - i);
+  v.nfirst[k] = (d == (int)lv[i]) ? -1 : p2b[pre + 1];
+  v.nnext[k] = (pre + sz < nn) ? p2b[pre + sz] : -1;
+  size[k] = sz;
+  // centre: the path's digits from the root, split_make's additions
+  double cx = root.x, cy = root.y, cz = root.z, h = root.w;
+  uint64_t word = 0;
+  for (int l = 0; l < d; ++l) {
+    if (l % LPW == 0) word = keys[(int64_t)(l / LPW) * n + i];
+    const uint32_t o = (uint32_t)(word >> (3 * (LPW - 1 - l % LPW))) & 7u;
+    const double off = h / 2.0;
+    cx = cx + ((o & 1u) ? off : -off);
+    cy = cy + ((o & 2u) ? off : -off);
+    cz = cz + ((o & 4u) ? off : -off);
+    h = off;
+  }
+  v.ncen[k] = make_double4(cx, cy, cz, h);
+  if (d > 0) {
+    int32_t ppre;
+    if (f <= d - 1) {
+      ppre = pre - 1;  // the parent starts at i too
+    } else {  // the parent's start: the first path sharing the level-(d-1) prefix
+      int64_t a = 0, b = i;
+      {  // the 16 eq bytes up to i first: b = the last p <= i with eq(p) < d - 1
+        uint8_t e[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) e[q] = (i - q > 0) ? eq[i - q] : (uint8_t)0;
+        int q0 = 16;
+#pragma unroll
+        for (int q = 15; q >= 0; --q)
+          if ((int)e[q] < d - 1) q0 = q;
+        if (q0 < 16) a = b = (i - q0 > 0) ? i - q0 : 0;
+        else b = i - 16;
+      }
+      for (int64_t step = 1; a < b;) {  // galloping back
+        const int64_t probe = b - step > a ? b - step : a;
+        if (path_lcp(keys, n, nw, probe, i) >= d - 1) {
+          b = probe;
+          step <<= 1;
+        } else {
+          a = probe + 1;
+          break;
+        }
+      }
+      while (a < b) {
+        const int64_t mid = (a + b) >> 1;
+        if (path_lcp(keys, n, nw, mid, i) >= d - 1) b = mid;
+        else a = mid + 1;
+      }
+      ppre = (int32_t)(S[a] + (uint32_t)(d - 1 - fd[a]));
+    }
+    atomicAdd(&v.nchild[p2b[ppre]], 1);
+  }
+}
+
 // ------------------------------------------------- cost-balanced target ranges
 // Multi-GPU walks split the leaf-ordered targets into contiguous ranges of
 // about equal cost (interactions per target).  The costs of one walk are
@@ -1292,11 +1529,15 @@ struct Octree {
   Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
   Buf bal;                   // cost-balanced ranges: chunk sums + cuts
+  Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
+  Buf rec0;                  // {x, y, z, m} in original order (path_keys)
+  bool rec0_valid = false;   // rec0 holds the current masses
   ~Octree() {
     Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
                    &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &keys, &ktmp0,
                    &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
-                   &counters, &trace, &bal};
+                   &counters, &trace, &bal, &bp_fl, &bp_eq, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
+                   &bp_p2b};
     for (Buf *b : bufs) b->release();
   }
   // accepted nodes, leaf pairs, fault flag, wave steps, active-lane steps
@@ -1341,8 +1582,12 @@ static uint32_t read_u32(const void *dptr, hipStream_t st) {
   return v;
 }
 
-// sort perm by the multi-word paths (LSD over words, last word first)
-static void sort_paths(Octree &T, hipStream_t st) {
+// sort perm by the multi-word paths (LSD over words, last word first).
+// min_shift > 0 (one path word): only the bytes from bit min_shift up are
+// sorted, with no read-back of the varying bits — the runs of a common
+// prefix are then contiguous down to level (62 - min_shift) / 3 only,
+// which split_parallel checks (levels deeper than that need the full sort).
+static void sort_paths(Octree &T, hipStream_t st, int min_shift = 0) {
   const int64_t n = T.n;
   uint64_t *keys = T.keys.as<uint64_t>();
   uint64_t *k0 = (uint64_t *)T.ktmp0.get(8 * (size_t)n);
@@ -1351,19 +1596,22 @@ static void sort_paths(Octree &T, hipStream_t st) {
   int32_t *v1 = (int32_t *)T.vtmp.get(4 * (size_t)n);
   unsigned long long *oa = (unsigned long long *)T.small.get(64);
   bool have_perm = false;
+  const bool partial = min_shift > 0 && T.nwords == 1;
   for (int w = T.nwords - 1; w >= 0; --w) {
-    // bits that vary across all paths of this word
-    unsigned long long h[2] = {0ull, ~0ull};
-    PBX_HIP(hipMemcpyAsync(oa, h, 16, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(key_or_and, dim3(std::min<unsigned>(1024, nblk(n))), dim3(TPB), 0, st,
-                       keys + (int64_t)w * n, n, oa);
-    PBX_HIP(hipMemcpyAsync(h, oa, 16, hipMemcpyDeviceToHost, st));
-    PBX_HIP(hipStreamSynchronize(st));
-    const uint64_t vary = h[0] ^ h[1];
-    if (!vary) continue;
+    uint64_t vary = ~0ull;
+    if (!partial) {  // bits that vary across all paths of this word
+      unsigned long long h[2] = {0ull, ~0ull};
+      PBX_HIP(hipMemcpyAsync(oa, h, 16, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(key_or_and, dim3(std::min<unsigned>(1024, nblk(n))), dim3(TPB), 0, st,
+                         keys + (int64_t)w * n, n, oa);
+      PBX_HIP(hipMemcpyAsync(h, oa, 16, hipMemcpyDeviceToHost, st));
+      PBX_HIP(hipStreamSynchronize(st));
+      vary = h[0] ^ h[1];
+      if (!vary) continue;
+    }
     hipLaunchKernelGGL(gather_u64, dim3(nblk(n)), dim3(TPB), 0, st, keys + (int64_t)w * n,
                        have_perm ? v0 : (const int32_t *)nullptr, n, k0);
-    for (int shift = 0; shift < 64; shift += 8) {
+    for (int shift = partial ? min_shift : 0; shift < 64; shift += 8) {
       if (!((vary >> shift) & 0xffull)) continue;
       radix_pass<uint64_t>(T.hist, T.tsum, st, k0, v0, have_perm ? VAL_ARRAY : VAL_IOTA, n,
                            shift, k1, v1);
@@ -1382,13 +1630,97 @@ static void sort_paths(Octree &T, hipStream_t st) {
     // result landed in the scratch buffer: swap the allocations
     std::swap(T.perm, T.vtmp);
   }
-  // sorted paths (structure pass reads them in leaf order)
+  // sorted paths (structure pass reads them in leaf order): one word that
+  // went through a pass is sorted already in k0
+  if (T.nwords == 1 && have_perm) {
+    Buf &b = (k0 == T.ktmp0.as<uint64_t>()) ? T.ktmp0 : T.ktmp1;
+    std::swap(T.keys, b);
+    return;
+  }
   uint64_t *sorted = (uint64_t *)T.ktmp1.get(8 * (size_t)n * T.nwords);
   for (int w = 0; w < T.nwords; ++w)
     hipLaunchKernelGGL(gather_u64, dim3(nblk(n)), dim3(TPB), 0, st, keys + (int64_t)w * n,
                        T.perm.as<int32_t>(), n, sorted + (int64_t)w * n);
   PBX_HIP(hipGetLastError());
   std::swap(T.keys, T.ktmp1);
+}
+
+// The whole structure from the sorted paths (bp_* kernels), one host
+// read-back; also the DFS preorder ids and subtree sizes (T.pre, T.size).
+// Returns false where the rule cannot decide (see bp_depth) or the leaf
+// capacity makes the windows long: the level-synchronous split then runs.
+static bool split_parallel(Octree &T, hipStream_t st, int sorted_levels) {
+  const int64_t n = T.n;
+  if (n <= 0 || T.leaf_capacity > 64 || !(T.root[3] > 1e-290) || n >= ((int64_t)1 << 31) - 1)
+    return false;
+  static const bool off = [] {  // A/B diagnostic: the level-synchronous builder
+    const char *e = std::getenv("PBX_TREE_LEVEL_BUILD");
+    return e && e[0] == '1';
+  }();
+  if (off) return false;
+  const uint64_t *keys = T.keys.as<uint64_t>();
+  uint8_t *fd = (uint8_t *)T.bp_fl.get(2 * (size_t)n + 16);
+  uint8_t *lv = fd + n;
+  uint32_t *S = (uint32_t *)T.bp_s.get(4 * (size_t)(n + 1));
+  const size_t nctl = 2 + BP_MAX_LEVEL + 1;
+  unsigned int *ctl = (unsigned int *)T.bp_ctl.get(4 * nctl);
+  PBX_HIP(hipMemsetAsync(ctl, 0, 4 * nctl, st));
+  uint8_t *eq = (uint8_t *)T.bp_eq.get(2 * (size_t)n + 16), *win = eq + n;
+  hipLaunchKernelGGL(bp_lcp, dim3(nblk(n)), dim3(TPB), 0, st, keys, n, T.nwords, T.leaf_capacity,
+                     eq, win);
+  hipLaunchKernelGGL(bp_depth, dim3(std::min<unsigned>(BP_DEPTH_BLOCKS, nblk(n))), dim3(TPB), 0,
+                     st, (const uint8_t *)eq,
+                     (const uint8_t *)win, n, sorted_levels, T.leaf_capacity, fd, lv, S, ctl);
+  scan_u32(T.tsum, st, S, n + 1);
+  PBX_HIP(hipMemcpyAsync(ctl + (nctl - 1), S + n, 4, hipMemcpyDeviceToDevice, st));  // nn
+  std::vector<unsigned int> h(nctl);
+  PBX_HIP(hipMemcpyAsync(h.data(), ctl, 4 * nctl, hipMemcpyDeviceToHost, st));
+  PBX_HIP(hipStreamSynchronize(st));
+  if (h[0]) return false;
+  const int64_t nn = h[nctl - 1];
+  // levels: nodes per level -> breadth-first id ranges
+  T.lvl.assign(1, 0);
+  int64_t tot = 0;
+  for (int d = 0; d <= BP_MAX_LEVEL && tot < nn; ++d) {
+    tot += h[1 + d];
+    T.lvl.push_back((int32_t)tot);
+  }
+  if (tot != nn || nn < 1) fail(PBX_ERR_RUNTIME, "parallel octree build: %lld nodes by level, %lld in all",
+                                (long long)tot, (long long)nn);
+  T.nn = 0;
+  ensure_nodes(T, nn, st);
+  uint32_t *level = (uint32_t *)T.bp_level.get(4 * (size_t)nn);
+  int32_t *startp = (int32_t *)T.bp_start.get(4 * (size_t)nn);
+  hipLaunchKernelGGL(bp_nodes_pre, dim3(nblk(n)), dim3(TPB), 0, st, (const uint8_t *)fd,
+                     (const uint8_t *)lv, (const uint32_t *)S, n, level, startp);
+  // breadth-first order = preorder stably sorted by level
+  int32_t *b2p = (int32_t *)T.pre.get(4 * (size_t)nn);
+  radix_pass<uint32_t>(T.hist, T.tsum, st, level, nullptr, VAL_IOTA, nn, 0, nullptr, b2p);
+  int32_t *p2b = (int32_t *)T.bp_p2b.get(4 * (size_t)nn);
+  hipLaunchKernelGGL(bp_inverse, dim3(nblk(nn)), dim3(TPB), 0, st, (const int32_t *)b2p, nn, p2b);
+  PBX_HIP(hipMemsetAsync(T.nchild.p, 0, 4 * (size_t)nn, st));
+  BuildView v;
+  v.keys = keys;
+  v.perm = T.perm.as<int32_t>();
+  v.pos = T.pos.as<double>();
+  v.n = n;
+  v.nwords = T.nwords;
+  v.cap = T.leaf_capacity;
+  v.nstart = T.nstart.as<int32_t>();
+  v.ncount = T.ncount.as<int32_t>();
+  v.nfirst = T.nfirst.as<int32_t>();
+  v.nnext = T.nnext.as<int32_t>();
+  v.nchild = T.nchild.as<int32_t>();
+  v.ncen = T.ncen.as<double4>();
+  int32_t *size = (int32_t *)T.size.get(4 * (size_t)nn);
+  hipLaunchKernelGGL(bp_nodes_bfs, dim3(nblk(nn)), dim3(TPB), 0, st, keys, n, T.nwords,
+                     (const uint8_t *)eq, (const uint8_t *)fd, (const uint8_t *)lv, (const uint32_t *)S,
+                     (const uint32_t *)level, (const int32_t *)startp, (const int32_t *)b2p,
+                     (const int32_t *)p2b, nn,
+                     make_double4(T.root[0], T.root[1], T.root[2], T.root[3]), v, size);
+  PBX_HIP(hipGetLastError());
+  T.nn = nn;
+  return true;
 }
 
 // levels of the tree; returns false when the paths are too short
@@ -1525,19 +1857,38 @@ static void build_structure(Octree &T, hipStream_t st) {
     preorder(T, st);
     return;
   }
+  bool parallel = false;
   for (T.nwords = 1;; ++T.nwords) {
     if (T.nwords > MAX_WORDS) fail(PBX_ERR_RUNTIME, "octree deeper than %d levels", LPW * MAX_WORDS);
-    uint64_t *keys = (uint64_t *)T.keys.get(8 * (size_t)n * T.nwords);
-    hipLaunchKernelGGL(path_keys, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(), n,
-                       T.root[0], T.root[1], T.root[2], T.root[3], T.nwords, keys);
-    PBX_HIP(hipGetLastError());
+    auto make_keys = [&] {
+      uint64_t *keys = (uint64_t *)T.keys.get(8 * (size_t)n * T.nwords);
+      double4 *rec0 = (double4 *)T.rec0.get(sizeof(double4) * (size_t)n);
+      hipLaunchKernelGGL(path_keys, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(), n,
+                         T.root[0], T.root[1], T.root[2], T.root[3], T.nwords, keys,
+                         T.user_mass ? T.mass.as<double>() : (const double *)nullptr, rec0);
+      T.rec0_valid = true;
+      PBX_HIP(hipGetLastError());
+    };
+    make_keys();
+    if (T.nwords == 1) {  // the top 6 bytes first: levels 0..14 (enough for most trees)
+      sort_paths(T, st, 16);
+      if (split_parallel(T, st, 15)) {
+        parallel = true;
+        break;
+      }
+      make_keys();  // the sort replaced the keys: start over with the full sort
+    }
     sort_paths(T, st);
+    if (split_parallel(T, st, LPW * T.nwords)) {
+      parallel = true;
+      break;
+    }
     if (split_levels(T, st)) break;
   }
   hipLaunchKernelGGL(leaf_sort, dim3(nblk(T.nn)), dim3(TPB), 0, st, T.nchild.as<int32_t>(),
                      T.nstart.as<int32_t>(), T.ncount.as<int32_t>(), T.nn, T.perm.as<int32_t>());
   PBX_HIP(hipGetLastError());
-  preorder(T, st);
+  if (!parallel) preorder(T, st);  // (the parallel build made pre / size already)
 }
 
 // softenings in leaf order (+ 4 zero pad entries, read 4 at a time)
@@ -1554,8 +1905,12 @@ static void pack_particles(Octree &T, hipStream_t st) {
   double4 *rec = (double4 *)T.rec.get(sizeof(double4) * (size_t)(n + 4));
   PBX_HIP(hipMemsetAsync(rec + n, 0, sizeof(double4) * 4, st));
   if (n > 0) {
-    hipLaunchKernelGGL(pack_records, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(),
-                       T.user_mass ? T.mass.as<double>() : (const double *)nullptr,
+    double4 *rec0 = (double4 *)T.rec0.get(sizeof(double4) * (size_t)n);
+    if (!T.rec0_valid)  // masses changed since the build (build_mass)
+      hipLaunchKernelGGL(interleave_records, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(),
+                         T.user_mass ? T.mass.as<double>() : (const double *)nullptr, n, rec0);
+    T.rec0_valid = true;
+    hipLaunchKernelGGL(pack_records, dim3(nblk(n)), dim3(TPB), 0, st, (const double4 *)rec0,
                        T.perm.as<int32_t>(), n, rec);
     if (T.soft_set) gather_softenings(T, st);
   }
@@ -1587,34 +1942,33 @@ static void build_payload(Octree &T, hipStream_t st) {
   v.hmax = T.has_hmax ? (double *)T.hmax.get(8 * (size_t)T.nn) : nullptr;
   const int P = T.moment_order();
   v.mom = P >= 2 ? (double *)T.mom.get(8 * (size_t)T.nn * ncoef(P)) : nullptr;
+  v.pre = T.pre.as<int32_t>();
+  v.size = T.size.as<int32_t>();
+  v.ncen = T.ncen.as<double4>();
+  v.nn = T.nn;
+  auto walk_buf = [&](int stride) { return (double *)T.walk.get(8 * (size_t)T.nn * stride); };
   switch (P) {
     case 0:
-    case 1: run_payload<0>(T, st, v); break;
-    case 2: run_payload<2>(T, st, v); break;
-    case 3: run_payload<3>(T, st, v); break;
-    case 4: run_payload<4>(T, st, v); break;
-    default: run_payload<5>(T, st, v); break;
-  }
-  const int32_t *pre = T.pre.as<int32_t>();
-  const dim3 g(nblk(T.nn)), b(TPB);
-  auto pack = [&](auto pc) {
-    constexpr int PP = decltype(pc)::value;
-    double *wk = (double *)T.walk.get(8 * (size_t)T.nn * rec_stride<PP>());
-    hipLaunchKernelGGL(pack_walk<PP>, g, b, 0, st, T.com.as<double4>(), T.ncen.as<double4>(),
-                       v.hmax, T.nchild.as<int32_t>(), T.nstart.as<int32_t>(),
-                       T.ncount.as<int32_t>(), pre, T.size.as<int32_t>(), T.nn, wk);
-    if constexpr (PP == 2 || PP == 3)
-      hipLaunchKernelGGL(pack_coef<PP>, g, b, 0, st, v.mom, pre, T.nn, wk);
-    else if constexpr (PP >= 4)
-      hipLaunchKernelGGL(pack_moments<PP>, g, b, 0, st, v.mom, pre, T.nn, wk);
-  };
-  switch (P) {
-    case 0: pack(std::integral_constant<int, 0>{}); break;
-    case 1: pack(std::integral_constant<int, 1>{}); break;
-    case 2: pack(std::integral_constant<int, 2>{}); break;
-    case 3: pack(std::integral_constant<int, 3>{}); break;
-    case 4: pack(std::integral_constant<int, 4>{}); break;
-    default: pack(std::integral_constant<int, 5>{}); break;
+    case 1:
+      v.walk = walk_buf(rec_stride<0>());
+      run_payload<0>(T, st, v);
+      break;
+    case 2:
+      v.walk = walk_buf(rec_stride<2>());
+      run_payload<2>(T, st, v);
+      break;
+    case 3:
+      v.walk = walk_buf(rec_stride<3>());
+      run_payload<3>(T, st, v);
+      break;
+    case 4:
+      v.walk = walk_buf(rec_stride<4>());
+      run_payload<4>(T, st, v);
+      break;
+    default:
+      v.walk = walk_buf(rec_stride<5>());
+      run_payload<5>(T, st, v);
+      break;
   }
   PBX_HIP(hipGetLastError());
   T.has_bh = true;
@@ -1836,6 +2190,7 @@ int pbx_octree_build_mass(pbx_octree *t, const double *masses, int on_device) {
     if (masses) {
       upload(T.mass, masses, T.n, on_device, dev.stream);
       T.user_mass = true;
+      T.rec0_valid = false;
     }
     build_payload(T, dev.stream);
     PBX_HIP(hipStreamSynchronize(dev.stream));
