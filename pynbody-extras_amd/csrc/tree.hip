@@ -945,59 +945,38 @@ __global__ void __launch_bounds__(WALK_TPB)
   }
   const bool has_th = SOFT && self_mode && wp.soft != nullptr;
   double ph = 0.0, ax = 0.0, ay = 0.0, az = 0.0;
+  int32_t cost = 0;  // this lane's accepted nodes + leaf pairs
+  // wave-uniform counters (ballot popcounts, kept in SGPRs)
   unsigned long long n_node = 0, n_pp = 0, n_active = 0;
-  unsigned long long leaf_steps = 0, leaf_active = 0, open_steps = 0;  // wave-uniform
+  unsigned long long leaf_steps = 0, leaf_active = 0, open_steps = 0;
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
-  int64_t steps = 0;           // the wave moves strictly forward in DFS order
-  while (w >= 0) {
-    if (++steps > wp.max_steps) {  // corrupted links: stop instead of hanging
-      if (lane0) atomicOr(wp.fault, 1u);
-      break;
-    }
+  uint32_t steps = 0;          // the wave moves strictly forward in DFS order
+  // One path through the body, no `continue`: every exit of a divergent
+  // region merges into the same accumulator registers, and p takes one
+  // select at the bottom (a body with three early exits to the latch made
+  // the register allocator copy the accumulators and counters through
+  // phi registers: ~20 v_mov_b64 per wave step, as many VALU issues as the
+  // opening test itself).
+  const uint32_t max_steps = (uint32_t)wp.max_steps;
+  while (w >= 0 && steps < max_steps) {  // corrupted links: stop instead of hanging
+    ++steps;
     w = __builtin_amdgcn_readfirstlane(w);  // uniform: keep it (and the address math) scalar
     u32x16 c[NCH];
     load_chunks<NCH>(wp.walk + (int64_t)w * RS, c);
     const double mass = chunk_d(c[0], 3);
     const int32_t next = chunk_i(c[0], 12), first = chunk_i(c[0], 13);
     const bool act = (p == w);
-    n_active += (unsigned long long)__popcll(__ballot(act));  // SIMD efficiency counter
-    if (mass == 0.0) {  // tree.rs:1087-1090
-      if (act) p = next;
-      w = next;
-      continue;
-    }
-    if (first < 0) {  // leaf: direct sum in ascending index order
-      ++leaf_steps;
-      leaf_active += (unsigned long long)__popcll(__ballot(act));
-      if (act) {
-        const int32_t s = chunk_i(c[0], 14), e = s + chunk_i(c[0], 15);
-        n_pp += (unsigned long long)(e - s);
-#ifndef PBX_DIAG_SKIP_LEAF  // timing diagnostic: leaves visited, pairs not evaluated
-        for (int32_t j = s; j < e; j += 4) {  // 4 records (128 B) per round trip
-          u32x16 r[2];
-          load_chunks<2>((const double *)(wp.rec + j), r);
-          double4 hs = make_double4(0.0, 0.0, 0.0, 0.0);
-          if (SOFT && wp.soft) hs = *(const double4 *)(wp.soft + j);
-          const double hv[4] = {hs.x, hs.y, hs.z, hs.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (j + q < e)
-              leaf_pair<WANT, SOFT, RAW>(wp, chunk_d(r[q / 2], 4 * (q & 1)),
-                                    chunk_d(r[q / 2], 4 * (q & 1) + 1),
-                                    chunk_d(r[q / 2], 4 * (q & 1) + 2),
-                                    chunk_d(r[q / 2], 4 * (q & 1) + 3), hv[q], j + q == self, tx,
-                                    ty, tz, th, ph, ax, ay, az);
-          }
-        }
-#endif
-        p = next;
-      }
-      w = next;
-      continue;
-    }
+    const unsigned na = (unsigned)__popcll(__ballot(act));
+    n_active += na;  // SIMD efficiency counter
     bool open = false;
-    if (act) {
+    int32_t nw = next;
+    const bool live = mass != 0.0;  // tree.rs:1087-1090: empty nodes are skipped
+    // two independent uniform ifs, not an if / else chain (the chain made a
+    // flow block through which the internal path's values were copied)
+    if (live && first >= 0) {
+    {  // the test runs on every lane (some lane is always active at w, so an
+       // `if (act)` would never skip it; as a branch it doubled the phis)
       const double dx = chunk_d(c[0], 0) - tx, dy = chunk_d(c[0], 1) - ty,
                    dz = chunk_d(c[0], 2) - tz;
       const double dist2 = dist2_fma(dx, dy, dz) + kR2Tiny;  // tree.rs:1117
@@ -1010,8 +989,10 @@ __global__ void __launch_bounds__(WALK_TPB)
           soft_ok = dist2 > ch * ch;
         }
       }
-      if (soft_ok && chunk_d(c[0], 4) < wp.theta2 * dist2) {
-        ++n_node;
+      const bool accept = act && soft_ok && chunk_d(c[0], 4) < wp.theta2 * dist2;
+      open = act && !accept;
+      cost += accept ? 1 : 0;
+      if (accept) {
         if constexpr (P == 0) {  // monopole without multipoles (tree.rs:1126-1129, 1284-1291)
           const double y = rsq_walk<RAW>(dist2 + kR2Tiny);
           if (WANT & PBX_WANT_POT) ph = __builtin_fma(-mass, y, ph);
@@ -1076,16 +1057,44 @@ __global__ void __launch_bounds__(WALK_TPB)
             eval_multipole<P, WANT>(wp.walk + (int64_t)w * RS + 8, D, ph, ax, ay, az);
           }
         }
-        p = next;
-      } else {
-        open = true;
-        p = first;
       }
     }
-    const bool descend = __ballot(open) != 0ull;
-    open_steps += descend ? 1ull : 0ull;
-    w = descend ? first : next;
+    const unsigned no = (unsigned)__popcll(__ballot(open));
+    n_node += na - no;  // active lanes accept or open
+    open_steps += (no + 63u) >> 6;  // no in [0, 64]: integer, stays scalar
+    nw = no ? first : next;
+    }
+    if (live && first < 0) {  // leaf: direct sum in ascending index order
+      const int32_t s = chunk_i(c[0], 14), e = s + chunk_i(c[0], 15);
+      ++leaf_steps;
+      leaf_active += na;
+      n_pp += (unsigned long long)na * (unsigned long long)(e - s);
+      if (act) {
+        cost += e - s;
+#ifndef PBX_DIAG_SKIP_LEAF  // timing diagnostic: leaves visited, pairs not evaluated
+        for (int32_t j = s; j < e; j += 4) {  // 4 records (128 B) per round trip
+          u32x16 r[2];
+          load_chunks<2>((const double *)(wp.rec + j), r);
+          double4 hs = make_double4(0.0, 0.0, 0.0, 0.0);
+          if (SOFT && wp.soft) hs = *(const double4 *)(wp.soft + j);
+          const double hv[4] = {hs.x, hs.y, hs.z, hs.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (j + q < e)
+              leaf_pair<WANT, SOFT, RAW>(wp, chunk_d(r[q / 2], 4 * (q & 1)),
+                                    chunk_d(r[q / 2], 4 * (q & 1) + 1),
+                                    chunk_d(r[q / 2], 4 * (q & 1) + 2),
+                                    chunk_d(r[q / 2], 4 * (q & 1) + 3), hv[q], j + q == self, tx,
+                                    ty, tz, th, ph, ax, ay, az);
+          }
+        }
+#endif
+      }
+    }
+    p = act ? (open ? first : next) : p;
+    w = nw;
   }
+  if (w >= 0 && lane0) atomicOr(wp.fault, 1u);
   if (wp.trace && lane0) {
     const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     wp.trace[3 * wv] = t_start;
@@ -1094,7 +1103,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   }
   if (!valid) return;
   const int64_t o = (self_mode && !wp.compact) ? (int64_t)wp.perm[wp.first + t] : t;
-  if (wp.cost) wp.cost[t] = (int32_t)(n_node + n_pp);
+  if (wp.cost) wp.cost[t] = cost;
   if (WANT & PBX_WANT_POT) wp.pot[o] = ph;
   if (WANT & PBX_WANT_ACC) {
     wp.acc[3 * o] = ax;
@@ -1102,11 +1111,6 @@ __global__ void __launch_bounds__(WALK_TPB)
     wp.acc[3 * o + 2] = az;
   }
   if (wp.counters) {
-#pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-      n_node += __shfl_xor(n_node, sh, 64);
-      n_pp += __shfl_xor(n_pp, sh, 64);
-    }
     if (lane0) {
       atomicAdd(&wp.counters[0], n_node);
       atomicAdd(&wp.counters[1], n_pp);
