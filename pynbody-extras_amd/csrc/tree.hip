@@ -908,6 +908,30 @@ __device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, doubl
   }
 }
 
+// the pairs of one leaf [s, e) for this lane's target, ascending index
+// order (tree.rs:1093-1110); SELF: the leaf may hold the target itself
+template <int WANT, bool SOFT, bool RAW, bool SELF>
+__device__ __forceinline__ void leaf_sum(const WalkParams &wp, int32_t s, int32_t e, int32_t self,
+                                         double tx, double ty, double tz, double th, double &ph,
+                                         double &ax, double &ay, double &az) {
+  for (int32_t j = s; j < e; j += 4) {  // 4 records (128 B) per round trip
+    u32x16 r[2];
+    load_chunks<2>((const double *)(wp.rec + j), r);
+    double4 hs = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (SOFT && wp.soft) hs = *(const double4 *)(wp.soft + j);
+    const double hv[4] = {hs.x, hs.y, hs.z, hs.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (j + q < e)
+        leaf_pair<WANT, SOFT, RAW>(wp, chunk_d(r[q / 2], 4 * (q & 1)),
+                                   chunk_d(r[q / 2], 4 * (q & 1) + 1),
+                                   chunk_d(r[q / 2], 4 * (q & 1) + 2),
+                                   chunk_d(r[q / 2], 4 * (q & 1) + 3), hv[q],
+                                   SELF && j + q == self, tx, ty, tz, th, ph, ax, ay, az);
+    }
+  }
+}
+
 // SOFT: h_max guard and/or softened leaf sums are live.  The walk hides
 // its scalar-load latency with other waves: orders <= 3 without softening
 // are held to 7 waves per SIMD (~100 SGPRs would leave room for only 6; at
@@ -927,7 +951,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   const bool valid = t < wp.m;
   const bool self_mode = wp.tgt == nullptr;
   double tx = 0.0, ty = 0.0, tz = 0.0, th = 0.0;
-  int64_t self = -1;
+  int32_t self32 = -1;  // this target's own record (self mode)
   if (valid) {
     if (self_mode) {
       const int64_t ts = wp.first + t;
@@ -935,7 +959,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       tx = r.x;
       ty = r.y;
       tz = r.z;
-      self = ts;
+      self32 = (int32_t)ts;
       if (SOFT && wp.soft) th = __builtin_fmax(wp.soft[ts], 0.0);
     } else {
       tx = wp.tgt[3 * t];
@@ -971,7 +995,9 @@ __global__ void __launch_bounds__(WALK_TPB)
     n_active += na;  // SIMD efficiency counter
     bool open = false;
     int32_t nw = next;
-    const bool live = mass != 0.0;  // tree.rs:1087-1090: empty nodes are skipped
+    // tree.rs:1087-1090: empty nodes are skipped (mass != 0.0 on the bits,
+    // so the test stays on the scalar unit: SALU has no f64 compare)
+    const bool live = ((c[0][7] & 0x7fffffffu) | c[0][6]) != 0u;
     // two independent uniform ifs, not an if / else chain (the chain made a
     // flow block through which the internal path's values were copied)
     if (live && first >= 0) {
@@ -1072,22 +1098,13 @@ __global__ void __launch_bounds__(WALK_TPB)
       if (act) {
         cost += e - s;
 #ifndef PBX_DIAG_SKIP_LEAF  // timing diagnostic: leaves visited, pairs not evaluated
-        for (int32_t j = s; j < e; j += 4) {  // 4 records (128 B) per round trip
-          u32x16 r[2];
-          load_chunks<2>((const double *)(wp.rec + j), r);
-          double4 hs = make_double4(0.0, 0.0, 0.0, 0.0);
-          if (SOFT && wp.soft) hs = *(const double4 *)(wp.soft + j);
-          const double hv[4] = {hs.x, hs.y, hs.z, hs.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            if (j + q < e)
-              leaf_pair<WANT, SOFT, RAW>(wp, chunk_d(r[q / 2], 4 * (q & 1)),
-                                    chunk_d(r[q / 2], 4 * (q & 1) + 1),
-                                    chunk_d(r[q / 2], 4 * (q & 1) + 2),
-                                    chunk_d(r[q / 2], 4 * (q & 1) + 3), hv[q], j + q == self, tx,
-                                    ty, tz, th, ph, ax, ay, az);
-          }
-        }
+        // only a target's own leaf needs the self-pair mask (an int compare
+        // and four selects per pair): every other leaf takes the plain loop
+        const bool own = (uint32_t)(self32 - s) < (uint32_t)(e - s);
+        if (__ballot(own) == 0ull)
+          leaf_sum<WANT, SOFT, RAW, false>(wp, s, e, -1, tx, ty, tz, th, ph, ax, ay, az);
+        else
+          leaf_sum<WANT, SOFT, RAW, true>(wp, s, e, self32, tx, ty, tz, th, ph, ax, ay, az);
 #endif
       }
     }
