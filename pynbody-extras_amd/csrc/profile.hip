@@ -49,6 +49,7 @@ struct SelectParams {
   int nfam;  // 0 -> no family filter
   int64_t base;  // first particle of the tiles (the families' span; 0 without families)
   int mass_f32;  // masses are float (else double)
+  int tiled;     // lazy + tiled: x of tile t at xo[t * TILE ..], no look-back
   double cx, cy, cz, r2max;
   int64_t fam_lo[MAX_FAM];
   int64_t fam_hi[MAX_FAM];
@@ -202,7 +203,12 @@ __global__ void __launch_bounds__(BT)
     uint32_t spins = 0;
     // lane l inspects tile (hi - l): lane 0 is the nearest predecessor;
     // tiles before 0 read as an inclusive prefix of 0
-    for (int64_t hi = (int64_t)tile - 1; tile != 0 && hi >= -1;) {
+#ifdef PBX_DIAG_SEL_NOLB  // timing diagnostic only: no look-back (offsets wrong)
+    excl = (uint64_t)tile * (TILE / 2);
+    for (int64_t hi = -2; false;) {
+#else
+    for (int64_t hi = (int64_t)tile - 1; tile != 0 && !p.tiled && hi >= -1;) {
+#endif
       const int64_t q = hi - (int64_t)lane;
       const uint64_t s = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT)
@@ -226,22 +232,27 @@ __global__ void __launch_bounds__(BT)
       hi -= 64;
     }
     if (lane == 0) {
-      if (tile != 0)
+      if (tile != 0 && !p.tiled)
         __hip_atomic_store(&status[tile], kStPre | (excl + tot), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       s_excl = (uint32_t)excl;
-      if (LAZY) toff[tile] = (uint32_t)excl;
+      if (LAZY && !p.tiled) toff[tile] = (uint32_t)excl;
     }
   }
   __syncthreads();
   uint32_t run = s_excl;
   for (int ww = 0; ww < w; ++ww) run += wcnt[ww];
+  if (LAZY && p.tiled) xo += (int64_t)tile * TILE;  // the tile's own slots
 #pragma unroll
   for (int k = 0; k < SI; ++k) {
     bool keep = (keepbits >> k) & 1u;
     uint64_t b = __ballot(keep);
     if (LAZY && lane == 0) kw[(int64_t)tile * (TILE / 64) + w * SI + k] = b;
+#ifdef PBX_DIAG_SEL_NOWRITE  // timing diagnostic only: r not written
+    if (keep && xv[k] == -1.0) {
+#else
     if (keep) {
+#endif
       int64_t i = wbase + k * 64 + lane;
       uint32_t pos_out = run + rank_below(b);
       xo[pos_out] = xv[k];
@@ -272,6 +283,63 @@ __device__ __forceinline__ void sel_tile_words(const uint64_t *__restrict__ kw,
     wrd[threadIdx.x] = word;
     wpre[threadIdx.x] = toff[t] + x - c;
   }
+}
+
+// Tiled lazy selection (large inputs): the select kernel skips the
+// decoupled look-back and writes each tile's kept x into the tile's own
+// TILE slots; block 0 of fused_hist0 then turns the tiles' published
+// counts into the exclusive tile offsets (toff) and the kept count.
+// (At 64M the look-back held every select block until its predecessors'
+// prefixes arrived: 309 -> 211 us of select without it.)
+constexpr int TS_TPB = 1024;
+constexpr int TS_PT = 16;  // tiles per thread per round (one round up to 16384 tiles = 64M slots)
+// (a block of TS_TPB threads; returns the total in every thread)
+__device__ uint32_t tile_scan_block(const uint64_t *__restrict__ status, uint32_t nt,
+                                    uint32_t *__restrict__ toff, uint32_t *wsum) {
+  const uint32_t lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint32_t r0 = 0; r0 < nt; r0 += TS_TPB * TS_PT) {
+    // thread t owns tiles r0 + t * TS_PT .. + TS_PT - 1: all loads in flight together
+    const uint32_t t0 = r0 + threadIdx.x * TS_PT;
+    uint32_t c[TS_PT], tot = 0;
+#pragma unroll
+    for (int k = 0; k < TS_PT; ++k) c[k] = t0 + k < nt ? (uint32_t)(status[t0 + k] & kStVal) : 0u;
+#pragma unroll
+    for (int k = 0; k < TS_PT; ++k) tot += c[k];
+    uint32_t x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t ex = carry + x - tot, all = carry;
+    for (int k = 0; k < TS_TPB / 64; ++k) {
+      if (k < wv) ex += wsum[k];
+      all += wsum[k];
+    }
+#pragma unroll
+    for (int k = 0; k < TS_PT; ++k) {
+      if (t0 + k < nt) toff[t0 + k] = ex;
+      ex += c[k];
+    }
+    carry = all;
+    __syncthreads();
+  }
+  return carry;
+}
+
+// a tiled selection's x compacted (for the consumers that read x by
+// selection index)
+__global__ void __launch_bounds__(TPB)
+    tile_compact(const double *__restrict__ xt, const uint32_t *__restrict__ toff, uint32_t nt,
+                 int64_t n, double *__restrict__ xc) {
+  const uint32_t t = blockIdx.x;
+  const uint32_t o = toff[t];
+  const uint32_t c = (uint32_t)((t + 1 < nt ? (int64_t)toff[t + 1] : n) - o);
+  for (uint32_t j = threadIdx.x; j < c; j += TPB) xc[o + j] = xt[(int64_t)t * TILE + j];
 }
 
 // weights and original indices of a lazy selection, materialised on demand
@@ -683,13 +751,45 @@ struct FusedSetup {
   int64_t n_in;
   uint64_t ka, kb;
   int empty_bounds;
+  int tiled;  // tiled selection: x of tile t at x[t * TILE ..], its count in stat[t]
+  uint32_t *toff;  // tiled: the tile offsets block 0 writes
 };
+
+// Element range of fused_hist0 / fused_gather: the kept x [0, n), or with
+// a tiled selection the tiles' slots [0, nt * TILE) of which slot j of
+// tile t holds a key iff j < its count.  One block step covers EL_STEP
+// slots = two whole tiles, so the two counts are wave-uniform.
+constexpr int EL_U = 4;  // 16-byte loads per lane per step (two keys each)
+constexpr int64_t EL_STEP = (int64_t)MS0_TPB * 2 * EL_U;
+static_assert(EL_STEP == 2 * TILE, "a step is two tiles");
+struct ElRange {
+  const uint64_t *stat;  // tiled: the select's status words (count in the low bits)
+  uint32_t nt;
+  int64_t n;    // kept keys
+  int64_t lim;  // slots
+  __device__ uint32_t count(int64_t t) const {
+    return t < (int64_t)nt ? (uint32_t)(stat[t] & kStVal) : 0u;
+  }
+};
+__device__ __forceinline__ ElRange el_range(const uint64_t *stat, uint32_t nt, int64_t n) {
+  return stat ? ElRange{stat, nt, n, (int64_t)nt * TILE} : ElRange{nullptr, 0u, n, n};
+}
+// key slot i of the step starting at i0 holds a key
+__device__ __forceinline__ bool el_valid(const ElRange &r, int64_t i0, int64_t i, uint32_t c0,
+                                         uint32_t c1) {
+  if (!r.stat) return i < r.n;
+  const int64_t j = i - i0;
+  return (j < TILE) ? j < (int64_t)c0 : (j - TILE) < (int64_t)c1;
+}
 
 __device__ FusedCtl fused_ctl(const FusedSetup &f) {
   FusedCtl c{};
   const uint32_t *ctrl = (const uint32_t *)(f.stat + f.nt);
   const unsigned long long *mm = (const unsigned long long *)(f.stat + f.nt + 1);
-  if (f.n_in > 0) {
+  if (f.tiled) {  // the kept count comes from fused_hist0's block 0 (tile_scan_block)
+    c.n = -1;
+    if (ctrl[1]) c.err |= 1;
+  } else if (f.n_in > 0) {  // the last tile's inclusive prefix
     const uint64_t last = f.stat[f.nt - 1];
     if (ctrl[1] || (last >> 62) != 2) c.err |= 1;
     c.n = (int64_t)(last & kStVal);
@@ -715,6 +815,34 @@ __device__ FusedCtl fused_ctl(const FusedSetup &f) {
   return c;
 }
 
+// every key slot of this block (grid-stride by EL_STEP): f(x value, valid).
+// (Issuing the next step's loads before this step's keys are processed made
+// fused_gather slower at 64M, 71 -> 91 us: kept single-step.)
+// With a tiled selection block 0 runs the tile scan instead (fused_hist0),
+// so the slots are spread over blocks 1.. (the same in fused_gather).
+template <class F>
+__device__ __forceinline__ void el_for_each(const double *__restrict__ x, const ElRange &er,
+                                            int64_t lim, F &&f) {
+  constexpr int U = EL_U;
+  const int b0 = (er.stat && gridDim.x > 1) ? 1 : 0;
+  if ((int)blockIdx.x < b0) return;
+  for (int64_t i0 = (int64_t)(blockIdx.x - b0) * EL_STEP; i0 < lim;
+       i0 += (int64_t)(gridDim.x - b0) * EL_STEP) {
+    double v[2 * U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_pair(x, i0 + 2 * (u * MS0_TPB + threadIdx.x), lim, v + 2 * u);
+    const uint32_t c0 = er.stat ? er.count(i0 / TILE) : 0u;
+    const uint32_t c1 = er.stat ? er.count(i0 / TILE + 1) : 0u;
+#pragma unroll
+    for (int u = 0; u < 2 * U; ++u) {
+      const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
+      f(v[u], el_valid(er, i0, i, c0, c1));
+    }
+  }
+}
+
+static_assert(MS0_TPB == TS_TPB, "fused_hist0's block 0 runs the tile scan");
+
 // level-0 histogram rows (msel_hist0 with the base / shift / length from ctl)
 __global__ void __launch_bounds__(MS0_TPB)
     fused_hist0(const double *__restrict__ x, FusedSetup fsu, FusedCtl *__restrict__ ctl_out,
@@ -724,28 +852,30 @@ __global__ void __launch_bounds__(MS0_TPB)
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
   const FusedCtl ctl = fused_ctl(fsu);
   if (blockIdx.x == 0) {  // the step's shared state: control record, zeroed counts / H
-    if (threadIdx.x == 0) *ctl_out = ctl;
+    if (fsu.tiled) {  // tiled selection: tile offsets and the kept count (no keys: lo > hi above)
+      __shared__ uint32_t wsum[MS0_TPB / 64];
+      const uint32_t total = tile_scan_block(fsu.stat, fsu.nt, fsu.toff, wsum);
+      if (threadIdx.x == 0) {
+        FusedCtl c = ctl;
+        c.n = total;
+        *ctl_out = c;
+      }
+    } else if (threadIdx.x == 0) {
+      *ctl_out = ctl;
+    }
     for (int k = threadIdx.x; k <= nb; k += MS0_TPB) counts[k] = 0;  // for assign_bins
     for (int k = threadIdx.x; k < MS0_DIG; k += MS0_TPB) H[k] = 0;   // for msel_reduce0
   }
   __syncthreads();
   const uint64_t ka = fsu.ka, kb = fsu.kb;
-  const int64_t n = (ctl.err & 2) ? 0 : ctl.n;
+  const ElRange er = el_range(fsu.tiled ? fsu.stat : nullptr, fsu.nt, (ctl.err & 2) ? 0 : ctl.n);
+  const int64_t lim = (ctl.err & 2) ? 0 : er.lim;
   const uint64_t base = ctl.lo;
   const int s = ctl.s0;
-  constexpr int U = 4;  // 16-byte loads: two consecutive keys per lane each
-  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * 2 * U; i0 < n;
-       i0 += (int64_t)gridDim.x * MS0_TPB * 2 * U) {
-    double v[2 * U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) load_pair(x, i0 + 2 * (u * MS0_TPB + threadIdx.x), n, v + 2 * u);
-#pragma unroll
-    for (int u = 0; u < 2 * U; ++u) {
-      const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
-      const uint64_t k = dkey(v[u]);
-      if (i < n && k >= ka && k <= kb) atomicAdd(&lh[(uint32_t)((k - base) >> s)], 1u);
-    }
-  }
+  el_for_each(x, er, lim, [&](double xv, bool ok) {
+    const uint64_t k = dkey(xv);
+    if (ok && k >= ka && k <= kb) atomicAdd(&lh[(uint32_t)((k - base) >> s)], 1u);
+  });
   __syncthreads();
   uint32_t *row = rows + (int64_t)blockIdx.x * MS0_DIG;
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) row[i] = lh[i];
@@ -893,7 +1023,8 @@ __global__ void __launch_bounds__(TPB)
 __global__ void __launch_bounds__(MS0_TPB)
     fused_gather(const double *__restrict__ x, uint64_t ka, uint64_t kb,
                  const FusedCtl *__restrict__ ctl, const uint32_t *__restrict__ gdig,
-                 const uint32_t *__restrict__ boff, uint64_t *__restrict__ seg) {
+                 const uint32_t *__restrict__ boff, uint64_t *__restrict__ seg,
+                 const uint64_t *__restrict__ tstat, uint32_t nt) {
   __shared__ uint16_t gidx[MS0_DIG];
   __shared__ uint32_t slot[MS_MAXQ];
   if (ctl->err & 2) return;
@@ -908,23 +1039,16 @@ __global__ void __launch_bounds__(MS0_TPB)
     slot[i] = boff[(int64_t)blockIdx.x * MS_MAXQ + i];
   }
   __syncthreads();
-  constexpr int U = 4;  // 16-byte loads: two consecutive keys per lane each
-  for (int64_t i0 = (int64_t)blockIdx.x * MS0_TPB * 2 * U; i0 < n;
-       i0 += (int64_t)gridDim.x * MS0_TPB * 2 * U) {
-    double v[2 * U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) load_pair(x, i0 + 2 * (u * MS0_TPB + threadIdx.x), n, v + 2 * u);
-#pragma unroll
-    for (int u = 0; u < 2 * U; ++u) {
-      const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
-      const uint64_t key = dkey(v[u]);
-      if (i < n && key >= ka && key <= kb) {
-        const uint64_t off = key - base;
-        const uint32_t g = gidx[(uint32_t)(off >> s)];
-        if (g != 0xffffu) seg[atomicAdd(&slot[g], 1u)] = off;
-      }
+  const ElRange er = el_range(tstat, nt, n);
+  const int64_t lim = er.lim;
+  el_for_each(x, er, lim, [&](double xv, bool ok) {
+    const uint64_t key = dkey(xv);
+    if (ok && key >= ka && key <= kb) {
+      const uint64_t off = key - base;
+      const uint32_t g = gidx[(uint32_t)(off >> s)];
+      if (g != 0xffffu) seg[atomicAdd(&slot[g], 1u)] = off;
     }
-  }
+  });
 }
 
 // One block (FR_TPB threads) per group: for each of its ranks, an MSD radix
@@ -1289,7 +1413,7 @@ __global__ void __launch_bounds__(BT)
                const uint32_t *__restrict__ toff, int64_t base, uint32_t ntiles, uint32_t tpbk,
                const double *__restrict__ mass, const double *__restrict__ edges, int nb,
                uint32_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
-               double *__restrict__ slab) {
+               double *__restrict__ slab, int xtiled) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t th[AS_TILES][RADIX];
   const int macc = MOM ? fs.nm * nb : 0;
@@ -1329,6 +1453,8 @@ __global__ void __launch_bounds__(BT)
       if (lane >= (uint32_t)o) incl += y;
     }
     const uint32_t pre = toff[t] + incl - cw;
+    // x of a tiled selection sits in the tile's own slots
+    const double *xt = xtiled ? x + ((int64_t)t * TILE - (int64_t)toff[t]) : x;
     const int64_t pbase = base + (int64_t)t * TILE + lane;
     uint32_t *hrow = th[t - t0];
     double nv[CH], nw[CH];
@@ -1343,7 +1469,7 @@ __global__ void __launch_bounds__(BT)
         const bool kp = (wj >> lane) & 1ull;
         keep |= (uint32_t)kp << kk;
         pos[kk] = pj + rank_below(wj);
-        v[kk] = kp ? x[pos[kk]] : 0.0;
+        v[kk] = kp ? xt[pos[kk]] : 0.0;
         wv[kk] = (kp && wneed) ? mass[pbase + 64 * j] : 1.0;
       }
     };
@@ -1807,12 +1933,15 @@ struct Profile {
   Buf pk0, pk1, pv0, pv1, pbk, pcdf, poff, pq, pout;  // order statistics
   Buf fctl, fseg, fgrp, fslab, fpack;                // one-sync equaln path
   // lazy selection (select_launch): keep words, tile offsets, staged masses
-  Buf kw, toff, mstage;
+  Buf kw, toff, mstage, xc;
   bool lazy = false, w_ready = false, idx_ready = false;
+  bool x_tiled = false;  // x holds a tiled selection (tile t at x[t * TILE ..]): ensure_x
   int64_t sel_base = 0, sel_span = 0;
   uint32_t sel_nt = 0;
   const double *sel_mass = nullptr;
 };
+
+static void ensure_x(Profile &P, hipStream_t st);
 
 // exclusive scan of len u32 in place
 static void scan_u32(Profile &P, hipStream_t st, uint32_t *a, int64_t len) {
@@ -1840,6 +1969,7 @@ static void minmax_of(Profile &P, hipStream_t st, uint64_t out[2]) {
     PBX_HIP(hipMemcpyAsync(mm, h, 16, hipMemcpyHostToDevice, st));
     if (P.n) {
       unsigned grid = (unsigned)std::min<int64_t>(1024, (P.n + TPB - 1) / TPB);
+      ensure_x(P, st);
       hipLaunchKernelGGL(minmax_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, P.n, mm);
       PBX_HIP(hipGetLastError());
     }
@@ -1930,6 +2060,7 @@ static int64_t msel_hist(Profile &P, hipStream_t st, int level) {
     const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n / (MS0_TPB * 16)));
     uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
     if (n) {
+      ensure_x(P, st);
       hipLaunchKernelGGL(msel_hist0, dim3(g0), dim3(MS0_TPB), 0, st, (const double *)P.x.p, n,
                          S.ka, S.kb, S.lo, s, rows);
       hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st, rows, g0, H);
@@ -1945,6 +2076,7 @@ static int64_t msel_hist(Profile &P, hipStream_t st, int level) {
   uint64_t *list = (uint64_t *)P.msL0.get(sizeof(uint64_t) * (size_t)(nw * cap));
   uint32_t *wc = (uint32_t *)P.msL1.get(sizeof(uint32_t) * (size_t)(nw * MS_MAXL));
   const int keep = level + 1 < S.L ? 1 : 0;
+  ensure_x(P, st);
   if (level == 1)
     hipLaunchKernelGGL(msel_filter<true>, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n,
                        S.ka, S.kb, S.lo, list, (const uint32_t *)nullptr, cap, s, S.wd[level], G,
@@ -2025,6 +2157,7 @@ static void assign_device(Profile &P, hipStream_t st, const double *de, int64_t 
                                 : nullptr;
     // >= ~1024 blocks where the input allows it
     const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
+    ensure_x(P, st);
     launch_assign<false>(ceil_div(nt, tpbk), lds, st, (const double *)P.x.p, n, de, (int)nb, bins,
                          cnt, th, nt, tpbk, nullptr, nullptr, FusedStats{}, nullptr);
     P.csrh_ready = th != nullptr;
@@ -2077,7 +2210,7 @@ static void csr_device(Profile &P, hipStream_t st) {
 static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
                               int64_t n, int on_device, int use_sphere, const double *sphere,
                               const int64_t *fam, int nfam, int ndim, bool lazy = false,
-                              int pos_f32 = 0, int mass_f32 = 0) {
+                              int pos_f32 = 0, int mass_f32 = 0, bool tiled = false) {
   check_n(n);
   if (ndim != 2 && ndim != 3) fail(PBX_ERR_VALUE, "ndim must be either 2 or 3");
   if (nfam < 0 || nfam > MAX_FAM) fail(PBX_ERR_VALUE, "at most %d family ranges", MAX_FAM);
@@ -2125,12 +2258,16 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
     }
   }
   const uint32_t nt = ntiles_of(span);
+  // large lazy selections: tiled output, no look-back (tile offsets: fused_hist0)
+  tiled = tiled && lazy && nt >= 1024;
+  sp.tiled = tiled ? 1 : 0;
   // per-tile look-back status words + ticket / watchdog (selection scratch)
   // [stat nt][ctrl: ticket, watchdog][MM_SLOTS x (~min key, max key)]: one zero fill
   const size_t nst = (size_t)nt + 1 + 2 * MM_SLOTS;
   uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * nst);
   uint32_t *ctrl = (uint32_t *)(stat + nt);
-  double *xo = (double *)P.x.get(sizeof(double) * (size_t)(span ? span : 1));
+  const int64_t xlen = tiled ? (int64_t)nt * TILE : span;
+  double *xo = (double *)P.x.get(sizeof(double) * (size_t)(xlen ? xlen : 1));
   double *wo = nullptr;
   int32_t *io = nullptr;
   uint64_t *kw = nullptr;
@@ -2163,6 +2300,7 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
     PBX_HIP(hipGetLastError());
   }
   P.lazy = lazy;
+  P.x_tiled = tiled && span;
   P.sel_base = lo;
   P.sel_span = span;
   P.sel_nt = nt;
@@ -2192,6 +2330,18 @@ static void ensure_idx(Profile &P, hipStream_t st) {
   P.idx_ready = true;
 }
 
+// compact a tiled selection's x (consumers that index x by selection index)
+static void ensure_x(Profile &P, hipStream_t st) {
+  if (!P.x_tiled) return;
+  double *xc = (double *)P.xc.get(sizeof(double) * (size_t)std::max<int64_t>(P.n, 1));
+  if (P.sel_nt && P.n)
+    hipLaunchKernelGGL(tile_compact, dim3(P.sel_nt), dim3(TPB), 0, st, (const double *)P.x.p,
+                       (const uint32_t *)P.toff.p, P.sel_nt, P.n, xc);
+  PBX_HIP(hipGetLastError());
+  std::swap(P.x, P.xc);
+  P.x_tiled = false;
+}
+
 // the handle's state after a selection of `kept` particles (key range in P.mm)
 static void select_commit(Profile &P, int64_t kept) {
   P.w_ready = P.idx_ready = !P.lazy;
@@ -2210,7 +2360,10 @@ static void select_commit(Profile &P, int64_t kept) {
 static const double *resolve_src(Profile &P, hipStream_t st, int which, const double *hp,
                                  Buf &stage) {
   const int64_t n = P.n;
-  if (which == 0) return (const double *)P.x.p;
+  if (which == 0) {
+    ensure_x(P, st);
+    return (const double *)P.x.p;
+  }
   if (which == 1) {
     if (!P.has_w) fail(PBX_ERR_VALUE, "profile has no selection weights");
     ensure_w(P, st);
@@ -2381,6 +2534,7 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
     P.has_w = false;
     P.has_idx = false;
     P.lazy = false;
+    P.x_tiled = false;
     P.csr_ready = false;
     P.csrh_ready = false;
     P.ms.active = false;
@@ -2451,7 +2605,10 @@ int pbx_profile_get_selection(void *handle, int64_t *h_idx, double *h_x, double 
                          (const int32_t *)P.idx.p, n, tmp);
       PBX_HIP(hipMemcpyAsync(h_idx, tmp, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
     }
-    if (h_x) PBX_HIP(hipMemcpyAsync(h_x, P.x.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    if (h_x) {
+      ensure_x(P, st);
+      PBX_HIP(hipMemcpyAsync(h_x, P.x.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    }
     if (h_w && P.has_w)
       PBX_HIP(hipMemcpyAsync(h_w, P.w.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
@@ -2548,6 +2705,7 @@ int pbx_profile_edges_equaln(void *handle, int64_t nbins, int has_min, double bi
     uint64_t *k0 = (uint64_t *)P.keys0.get(sizeof(uint64_t) * (size_t)n);
     uint64_t *k1 = (uint64_t *)P.keys1.get(sizeof(uint64_t) * (size_t)n);
     unsigned grid = (unsigned)std::min<int64_t>(4096, (n + TPB - 1) / TPB);
+    ensure_x(P, st);
     hipLaunchKernelGGL(make_keys, dim3(grid), dim3(TPB), 0, st, (const double *)P.x.p, n, k0);
     PBX_HIP(hipGetLastError());
     // only the bits where min and max keys differ need sorting
@@ -2830,8 +2988,9 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     }();
     const bool lazy = nbins < RADIX && !eager_env;
     const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
-                                      nfam, ndim, lazy);
+                                      nfam, ndim, lazy, 0, 0, /*tiled=*/true);
     const int64_t n_sel = nt ? P.sel_span : 0;  // tiled particles (the families' span)
+    const bool tiled = P.x_tiled;  // x by tile (large inputs): tile offsets from fused_hist0
     const int nq = (int)nbins + 1;
     // the window of bins.py:734-737 as key bounds (msel_begin)
     bool empty_bounds = false;
@@ -2858,7 +3017,8 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     // per-group finish -> edges
     const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n_sel / (MS0_TPB * 16)));
     uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
-    const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds};
+    const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
+                         (uint32_t *)P.toff.p};
     hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
                        rows);
     hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
@@ -2873,7 +3033,8 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                        (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff);
     uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n_sel ? n_sel : 1));
     hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
-                       (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff, seg);
+                       (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff, seg,
+                       tiled ? (const uint64_t *)stat : nullptr, nt);
     double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
     hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
                        (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
@@ -2937,7 +3098,8 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       const bool wide = tpbk == 1 && nt < 1024;
       auto go = [&](auto kern, int bt) {
         hipLaunchKernelGGL(kern, dim3(ablocks), dim3(bt), lds, st, x, kwp, tof, P.sel_base, nt,
-                           tpbk, P.sel_mass, (const double *)de, (int)nb, bins, th, fs, slab);
+                           tpbk, P.sel_mass, (const double *)de, (int)nb, bins, th, fs, slab,
+                           tiled ? 1 : 0);
       };
       if (wide) {
         if (fs.nm) {

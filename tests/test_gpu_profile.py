@@ -497,7 +497,7 @@ def test_profile_median_uses_device(gpu, monkeypatch):
 @pytest.mark.parametrize("case", ["plummer", "sphere_family", "clip", "nan", "single", "dups",
                                   "skewed", "empty_window", "nothing_kept", "many_stats",
                                   "family_offset", "no_mass", "wide", "wide_family",
-                                  "empty_family"])
+                                  "empty_family", "tiled", "tiled_family"])
 def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
     """pbx_profile_radial_equaln (select + equaln + assign + CSR + sums with
     one host round trip, level-0 select + per-group LDS sort / radix finish)
@@ -543,6 +543,12 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
         sphere = ((0.0, 0.0, 0.0), 8.0)
     elif case == "empty_family":
         fams = [(5, 5)]
+    elif case in ("tiled", "tiled_family"):  # >= 1024 selection tiles: tiled x, tile_scan
+        n = 4_400_000
+        pos = rng.normal(scale=3.0, size=(n, 3))
+        mass = rng.uniform(0.5, 1.5, n)
+        if case == "tiled_family":
+            sphere, fams = ((0.2, 0.0, 0.1), 7.0), [(3_001, 4_300_000)]
     elif case == "many_stats":  # more statistics than the assignment pass fuses
         nb = 64
         stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11), (SRC_X, SRC_NONE, 0x7f),
