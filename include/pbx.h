@@ -207,6 +207,17 @@ int pbx_octree_compute_range(pbx_octree *tree, double theta, int want, int64_t f
  * particles [first, first + count), into device buffers (any may be NULL) */
 int pbx_octree_leaf_particles(pbx_octree *tree, int64_t first, int64_t count, double *d_pos,
                               double *d_mass, int64_t *d_idx);
+/* 3-D radial profile of a per-target field over the leaf-order targets
+ * [first, first + count): d_f (device, count doubles in leaf order, e.g. the
+ * potential of compute_range with compact = 1), nbins + 1 increasing host
+ * edges; r = sqrt((x*x + y*y) + z*z) of the tree's own positions, bin as
+ * BinsSet._assign_particles (bins.py:346-395).  Outputs (host): counts[nbins]
+ * and moments[nbins][7] = {Σw, Σf·w, Σf²·w, Σf, Σf², Σ|f|·w, Σ|f|} with w =
+ * the mass (pbx_profile_moments' columns, proarray.py:272-334).  Replaces
+ * the select / assign / moments round trips of a tree's potential profile. */
+int pbx_octree_radial_moments(pbx_octree *tree, int64_t first, int64_t count, const double *d_f,
+                              const double *h_edges, int64_t nbins, int64_t *h_counts,
+                              double *h_moments);
 /* Multi-GPU load balance without an extra walk (the reference has one
  * process; its rayon pool splits targets dynamically, tree.rs:1443-1556):
  * cost_to_orig scatters per-target costs held in leaf order (n int32, e.g.

@@ -57,6 +57,29 @@ __device__ __forceinline__ uint64_t peers8(uint32_t d, uint64_t valid) {
   return m;
 }
 
+// bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
+// x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379).
+// Branchless lower bound over the nb+1 edges: the trip count depends on nb
+// only (uniform), so a wave's searches never diverge.  "e[k] < v" is
+// monotone in k for sorted edges (a NaN edge, sorted last by numpy, compares
+// false like +inf), so this is the first k with !(e[k] < v) exactly as the
+// classic bisection finds it.
+template <class E>
+__device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
+  int base = 0, len = nb + 1;
+  while (len > 1) {
+    const int half = len >> 1;
+    base = (e[base + half] < v) ? base + half : base;
+    len -= half;
+  }
+  const int lo = base + (e[base] < v ? 1 : 0);  // first k with e[k] >= v  (NaN: 0)
+  int b = lo - 1;
+  if (v == e[0]) b = 0;
+  if (v == e[nb]) b = nb - 1;
+  if (v != v) b = nb;  // searchsorted puts NaN past every edge
+  return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
+}
+
 // exclusive scan of one u32 per thread over the block
 __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t *lds_wave, uint32_t *total) {
   const uint32_t lane = lane_id();

@@ -1059,7 +1059,7 @@ constexpr int FS_BITS = 11;
 constexpr int FS_DIG = 1 << FS_BITS;
 constexpr int FS_LDS = 8192;
 
-template <bool IN_LDS>
+template <bool IN_LDS, bool SC1 = false>  // SC1: keys handed over in-launch (radial_mono)
 __device__ void finish_group(const uint64_t *__restrict__ keys, int64_t S, uint64_t pref0, int s,
                              int64_t rr, uint32_t *hist, uint32_t *wsum, uint64_t *pick,
                              uint64_t &out) {
@@ -1076,7 +1076,8 @@ __device__ void finish_group(const uint64_t *__restrict__ keys, int64_t S, uint6
     for (int d = tid; d < FS_DIG; d += FR_TPB) hist[d] = 0;
     __syncthreads();
     for (int64_t i = tid; i < S; i += FR_TPB) {
-      const uint64_t k = keys[i];
+      const uint64_t k = SC1 ? __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : keys[i];
       if ((k & hmask) == pref) atomicAdd(&hist[(uint32_t)(k >> sh) & dm], 1u);
     }
     __syncthreads();
@@ -1200,28 +1201,7 @@ __global__ void __launch_bounds__(TPB)
 }
 
 // ----------------------------------------------------------------- assign
-// bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
-// x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379).
-// Branchless lower bound over the nb+1 edges: the trip count depends on nb
-// only (uniform), so a wave's searches never diverge.  "e[k] < v" is
-// monotone in k for sorted edges (a NaN edge, sorted last by numpy, compares
-// false like +inf), so this is the first k with !(e[k] < v) exactly as the
-// classic bisection finds it.
-template <class E>
-__device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
-  int base = 0, len = nb + 1;
-  while (len > 1) {
-    const int half = len >> 1;
-    base = (e[base + half] < v) ? base + half : base;
-    len -= half;
-  }
-  const int lo = base + (e[base] < v ? 1 : 0);  // first k with e[k] >= v  (NaN: 0)
-  int b = lo - 1;
-  if (v == e[0]) b = 0;
-  if (v == e[nb]) b = nb - 1;
-  if (v != v) b = nb;  // searchsorted puts NaN past every edge
-  return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
-}
+// bin_of (prims.h): bins.py:368-379 bin assignment
 
 // One block takes `tpbk` (<= AS_TILES) consecutive 4096-element tiles:
 // AS_TILES on big inputs (LDS init and the tile_hist rows amortised), fewer
@@ -1616,6 +1596,626 @@ __global__ void __launch_bounds__(TPB)
   }
 }
 
+// ---------------------------- one-launch radial equaln (small selections)
+// A selection of at most one tile per CU (<= MONO_MAXT tiles of 4096
+// particles: ~1M) runs the whole pbx_profile_radial_equaln step as ONE
+// persistent launch: block t = selection tile t (select_onepass<1024>'s
+// layout, 4 particles per lane), every block resident, five grid barriers.
+// A tile's particles stay in registers from the selection to the CSR
+// scatter (x, mass, compacted position): the kept x is written once and
+// never re-read, and the 11 dependent launches of the multi-kernel path
+// (each ~5 us at this size) become phases of one.  Results are those of
+// the multi-kernel path (same rank rules, same selection code, same
+// stable CSR order); the per-bin sums differ by float-add order only.
+//   1 select: mask, x, keep words; the tile's count and key range -> rec[t]
+//   2 every block: totals, key range, window geometry (fused_ctl's rules),
+//     this tile's offset; compacted x; level-0 histogram of the tile's
+//     window keys in LDS, its non-zero bins added to H
+//   3 every block: scan of H, each rank's level-0 digit and residual rank
+//     (fused_resolve0's rules), the groups; the tile's keys of chosen
+//     buckets -> the group segments (one global atomic per tile and group)
+//   4 block g (and g + grid, ...): group g's ranks (fused_finish) -> edges
+//   5 bins (bin_of), per-bin monomial sums in LDS (one slab row per tile),
+//     the tile's bin counts -> th[bin][tile], in-tile CSR ranks (csr_sel)
+//   6 every block: its CSR offsets from the th table, perm scatter; block 0
+//     packs ctl / edges / counts; slab columns summed in fixed order
+constexpr int MONO_BT = 1024;
+constexpr int MONO_NW = MONO_BT / 64;
+constexpr int MONO_SI = TILE / MONO_BT;  // particles per lane
+constexpr uint32_t MONO_MAXT = 256;
+constexpr int BAR_LINE = 16;             // u64 words per 128-B line
+// lines 0-7 group counters, 8 top counter, 9 generation, 10 completions
+constexpr size_t BAR_WORDS = (size_t)BAR_LINE * 11;
+
+// Hand-off loads / stores of the one-launch path: sc1 (relaxed agent-scope
+// atomics: global_load / global_store ... sc1), so no fence is needed at a
+// barrier — the measured-valid form of MI355X_MICROARCH.md's hand-off table
+// (every handed-off word stored sc1 by its producer and loaded sc1 by every
+// consumer; the producer waves drain vmcnt(0) before the arrival).  An
+// agent-scope release writes back the whole XCD L2 (~2-6 us per wave that
+// issues it): with one per wave per phase the first version spent ~40 us
+// per phase in fences.
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1d(const double *p) {
+  return __builtin_bit_cast(double, ld_sc1((const uint64_t *)p));
+}
+__device__ __forceinline__ void st_sc1d(double *p, double v) {
+  st_sc1((uint64_t *)p, __builtin_bit_cast(uint64_t, v));
+}
+
+// Grid barrier of a co-resident grid, XCD-hierarchical: a block arrives on
+// the counter of its group (block % 8, the dispatcher's XCD round robin:
+// a speed hint only), the last block of a group on the top counter, and the
+// last group publishes generation `gen`.  Counters are monotonic across
+// calls: the host carries the generation and zeroes them when the grid size
+// changes or a call failed.  Every wave drains its stores (vmcnt(0)) before
+// the block's arrival; the data handed over a barrier is stored and loaded
+// sc1 (ld_sc1 / st_sc1).  Bounded spin: false when the generation did not
+// come (the host discards the call).
+__device__ bool grid_sync(uint64_t *bar, uint64_t gen, uint32_t nblk, int *ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t g = blockIdx.x % 8, ngrp = nblk < 8 ? nblk : 8;
+    const uint64_t gs = nblk / 8 + (g < nblk % 8 ? 1 : 0);
+    const uint64_t old = __hip_atomic_fetch_add(bar + BAR_LINE * g, 1ull, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == gen * gs) {
+      const uint64_t o2 = __hip_atomic_fetch_add(bar + BAR_LINE * 8, 1ull, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if (o2 + 1 == gen * ngrp) st_sc1(bar + BAR_LINE * 9, gen);
+    }
+    uint32_t spins = 0;
+    while (ld_sc1(bar + BAR_LINE * 9) < gen) {
+      if (++spins > (1u << 22)) {
+        *ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  return *ok != 0;
+}
+
+struct MonoRec {  // a tile's selection result (phase 1)
+  uint64_t cnt, kmin, kmax, pad;
+};
+
+struct MonoArgs {
+  const double *pos;
+  const double *mass;  // null: unit weights
+  int64_t n_hi;        // particles [sp.base, n_hi) are tiled
+  SelectParams sp;
+  uint64_t ka, kb;     // equaln window keys (bins.py:734-737)
+  int empty_bounds;
+  int nb, nq;
+  int64_t nbins;
+  FusedStats fs;
+  MonoRec *rec;
+  uint32_t *H;      // level-0 histogram (MS0_DIG)
+  uint32_t *gcnt;   // per-group segment fill (MS_MAXQ)
+  uint64_t *seg;    // group segments (keys - lo)
+  double *x;        // compacted kept x
+  uint64_t *kw;
+  uint32_t *toff;
+  uint32_t *bins;
+  int32_t *perm;
+  double *edges;
+  uint32_t *th;     // [RADIX][nt] bin counts per tile
+  double *slab;     // [nt][nm * nb] per-tile monomial sums
+  unsigned long long *counts;
+  double *pack;     // [ctl][edges nq][counts nb][sums nm x nb][tag]
+  uint64_t *bar;
+  uint64_t gen0;         // generations gen0 + 1 .. gen0 + 5; tag of this call
+  uint64_t done_target;  // the completion counter's value once every block is done
+  uint64_t *trace;       // PBX_MONO_TRACE diagnostic: 8 wall-clock stamps per block, or null
+};
+
+// End of a block's part of the call: the block whose completion brings the
+// (monotonic) counter to its target writes the pack's tag.  A call in which
+// a block gave up at a barrier never reaches the target: no tag, and the
+// host discards the call.
+__device__ void mono_done(const MonoArgs &a, int tagpos) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t old = __hip_atomic_fetch_add(a.bar + BAR_LINE * 10, 1ull, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == a.done_target) a.pack[tagpos] = __builtin_bit_cast(double, a.gen0);
+  }
+}
+
+#define MONO_STAMP(k)                                                       \
+  do {                                                                      \
+    if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x * 8 + (k)] = wall_clock64(); \
+  } while (0)
+__global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
+  static_assert(MONO_SI == 4 && MONO_NW == 16, "4 particles per lane, 16 waves");
+  MONO_STAMP(0);
+  __shared__ __attribute__((aligned(16))) uint32_t L0[MS0_DIG];  // hist / scan; keys; th partials
+  __shared__ __attribute__((aligned(16))) uint16_t L1[MS0_DIG];  // digit -> group; finish hist; runs + sums
+  __shared__ int64_t q_rr[RADIX];
+  __shared__ uint32_t q_dig[RADIX];
+  __shared__ uint32_t g_start[RADIX + 1], g_off[RADIX + 1], g_lcnt[RADIX], g_base[RADIX];
+  __shared__ double e_lds[RADIX];
+  __shared__ uint32_t wcnt[MONO_NW], wsum[MONO_NW];
+  __shared__ unsigned long long wmin[MONO_NW], wmax[MONO_NW];
+  __shared__ uint32_t s_gofs[RADIX];
+  __shared__ uint64_t pick[2];
+  __shared__ FusedCtl s_ctl;
+  __shared__ uint32_t s_toff;
+  __shared__ int s_ok;
+  const uint32_t t = blockIdx.x, nt = gridDim.x;
+  const int tid = threadIdx.x, w = tid >> 6;
+  const uint32_t lane = lane_id();
+  const int nb = a.nb, nq = a.nq;
+  if (tid == 0) s_ok = 1;
+  for (int i = tid; i < MS0_DIG; i += MONO_BT) L0[i] = 0;
+  if (t == 0) {  // zeroed here, used after barrier 1
+    for (int i = tid; i < MS0_DIG; i += MONO_BT) st_sc1(&a.H[i], 0u);
+    for (int i = tid; i < RADIX; i += MONO_BT) st_sc1(&a.gcnt[i], 0u);
+  }
+  // ---- 1: selection (select_onepass) -------------------------------------
+  const int64_t wbase = a.sp.base + (int64_t)t * TILE + (int64_t)w * (TILE / MONO_NW);
+  double xv[MONO_SI], mv[MONO_SI];
+  uint64_t bal[MONO_SI];
+  uint32_t keepbits = 0;
+  unsigned long long kmin = ~0ull, kmax = 0ull;
+  {
+    double px[MONO_SI], py[MONO_SI], pz[MONO_SI];
+    uint32_t inbits = 0;
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      const int64_t i = wbase + k * 64 + lane;
+      const bool in = (i < a.n_hi) && in_family(i, a.sp);
+      inbits |= (uint32_t)in << k;
+      const double *q = a.pos + 3 * (in ? i : 0);
+      px[k] = q[0];
+      py[k] = q[1];
+      pz[k] = q[2];
+    }
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      const bool keep = ((inbits >> k) & 1u) && select_xyz(px[k], py[k], pz[k], a.sp, xv[k]);
+      keepbits |= (uint32_t)keep << k;
+      bal[k] = __ballot(keep);
+      if (keep) {
+        const unsigned long long kk = dkey(xv[k]);
+        kmin = kk < kmin ? kk : kmin;
+        kmax = kk > kmax ? kk : kmax;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      const int64_t i = wbase + k * 64 + lane;
+      mv[k] = (a.mass && ((keepbits >> k) & 1u)) ? a.mass[i] : 1.0;
+    }
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < MONO_SI; ++k) {
+    c += (uint32_t)__popcll(bal[k]);
+    if (lane == 0) a.kw[(int64_t)t * (TILE / 64) + w * MONO_SI + k] = bal[k];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long p = __shfl_xor(kmin, o, 64), q = __shfl_xor(kmax, o, 64);
+    kmin = p < kmin ? p : kmin;
+    kmax = q > kmax ? q : kmax;
+  }
+  if (lane == 0) {
+    wcnt[w] = c;
+    wmin[w] = kmin;
+    wmax[w] = kmax;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    MonoRec r{0, ~0ull, 0ull, 0};
+    for (int k = 0; k < MONO_NW; ++k) {
+      r.cnt += wcnt[k];
+      r.kmin = wmin[k] < r.kmin ? wmin[k] : r.kmin;
+      r.kmax = wmax[k] > r.kmax ? wmax[k] : r.kmax;
+    }
+    st_sc1(&a.rec[t].cnt, r.cnt);
+    st_sc1(&a.rec[t].kmin, r.kmin);
+    st_sc1(&a.rec[t].kmax, r.kmax);
+  }
+  if (!grid_sync(a.bar, a.gen0 + 1, nt, &s_ok)) return;
+  MONO_STAMP(1);
+
+  // ---- 2: totals, this tile's offset, compacted x, level-0 histogram -----
+  {
+    uint32_t cc = 0;
+    unsigned long long mn = ~0ull, mx = 0ull;
+    if ((uint32_t)tid < nt) {
+      cc = (uint32_t)ld_sc1(&a.rec[tid].cnt);
+      mn = ld_sc1(&a.rec[tid].kmin);
+      mx = ld_sc1(&a.rec[tid].kmax);
+    }
+    uint32_t xs = cc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(xs, o, 64);
+      if (lane >= (uint32_t)o) xs += y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long p = __shfl_xor(mn, o, 64), q = __shfl_xor(mx, o, 64);
+      mn = p < mn ? p : mn;
+      mx = q > mx ? q : mx;
+    }
+    if (lane == 63) wsum[w] = xs;
+    if (lane == 0) {
+      wmin[w] = mn;
+      wmax[w] = mx;
+    }
+    __syncthreads();
+    uint32_t ex = xs - cc;
+    for (int k = 0; k < w; ++k) ex += wsum[k];
+    if ((uint32_t)tid == t) s_toff = ex;
+    if (tid == 0) {
+      FusedCtl cl{};
+      uint64_t tot = 0;
+      cl.kmin = ~0ull;
+      cl.kmax = 0ull;
+      for (int k = 0; k < MONO_NW; ++k) {
+        tot += wsum[k];
+        cl.kmin = wmin[k] < cl.kmin ? wmin[k] : cl.kmin;
+        cl.kmax = wmax[k] > cl.kmax ? wmax[k] : cl.kmax;
+      }
+      cl.n = (int64_t)tot;
+      const uint64_t lo = a.ka > cl.kmin ? a.ka : cl.kmin;
+      const uint64_t hi = a.kb < cl.kmax ? a.kb : cl.kmax;
+      if (cl.n == 0 || a.empty_bounds || lo > hi) {
+        cl.err |= 2;
+        cl.w0 = 1;
+      } else {
+        const uint64_t span = hi - lo;
+        const int B = span ? 64 - __builtin_clzll(span) : 1;
+        cl.w0 = B < MS0_BITS ? B : MS0_BITS;
+        cl.s0 = B - cl.w0;
+        cl.lo = lo;
+      }
+      s_ctl = cl;
+    }
+  }
+  __syncthreads();
+  const FusedCtl ctl0 = s_ctl;
+  const bool ok2 = !(ctl0.err & 2);
+  uint32_t pos[MONO_SI];
+  {
+    uint32_t run = s_toff;
+    for (int k = 0; k < w; ++k) run += wcnt[k];
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      pos[k] = run + rank_below(bal[k]);
+      if ((keepbits >> k) & 1u) a.x[pos[k]] = xv[k];
+      run += (uint32_t)__popcll(bal[k]);
+    }
+    if (tid == 0) a.toff[t] = s_toff;
+  }
+  if (ok2) {
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      const uint64_t key = dkey(xv[k]);
+      if (((keepbits >> k) & 1u) && key >= a.ka && key <= a.kb)
+        atomicAdd(&L0[(uint32_t)((key - ctl0.lo) >> ctl0.s0)], 1u);
+    }
+  }
+  __syncthreads();
+  if (ok2)
+    for (int i = tid; i < MS0_DIG; i += MONO_BT) {
+      const uint32_t v = L0[i];
+      if (v) atomicAdd(&a.H[i], v);
+    }
+  if (!grid_sync(a.bar, a.gen0 + 2, nt, &s_ok)) return;
+  MONO_STAMP(2);
+
+  // ---- 3: ranks -> level-0 digits and groups; keys -> group segments -----
+  int ng = 0;
+  if (ok2) {
+    constexpr int PT = MS0_DIG / MONO_BT;
+    uint32_t v[PT], tot = 0;
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      v[k] = ld_sc1(&a.H[tid * PT + k]);
+      tot += v[k];
+    }
+    uint32_t xs = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(xs, o, 64);
+      if (lane >= (uint32_t)o) xs += y;
+    }
+    if (lane == 63) wsum[w] = xs;
+    __syncthreads();
+    uint32_t run = xs - tot;
+    for (int k = 0; k < w; ++k) run += wsum[k];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      run += v[k];
+      L0[tid * PT + k] = run;  // inclusive counts
+    }
+    for (int i = tid; i < MS0_DIG / 2; i += MONO_BT) ((uint32_t *)L1)[i] = ~0u;
+    __syncthreads();
+    MONO_STAMP(7);
+    const int64_t m = (int64_t)L0[MS0_DIG - 1];
+    const int top = (1 << ctl0.w0) - 1;
+    for (int q = tid; q < nq; q += MONO_BT) {
+      int64_t r = 0;
+      if (m >= 2) r = (q == nq - 1) ? m - 1 : (int64_t)((double)(q * m) / (double)a.nbins);
+      int lo = 0, hi = top;  // first digit whose inclusive count exceeds r
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)L0[mid] <= r) lo = mid + 1; else hi = mid;
+      }
+      q_dig[q] = (uint32_t)lo;
+      q_rr[q] = r - (lo ? (int64_t)L0[lo - 1] : 0);
+    }
+    __syncthreads();
+    if (w == 0) {  // groups = run starts of the non-decreasing digits; sizes, offsets
+      uint32_t cnt = 0;
+      for (int q0 = 0; q0 < nq; q0 += 64) {
+        const int q = q0 + (int)lane;
+        const bool st = q < nq && (q == 0 || q_dig[q - 1] != q_dig[q]);
+        const uint64_t b = __ballot(st);
+        if (st) g_start[cnt + rank_below(b)] = (uint32_t)q;
+        cnt += (uint32_t)__popcll(b);
+      }
+      if (lane == 0) g_start[cnt] = (uint32_t)nq;
+      uint32_t base = 0;
+      for (uint32_t g0 = 0; g0 < cnt; g0 += 64) {
+        const uint32_t g = g0 + lane;
+        uint32_t sz = 0;
+        if (g < cnt) {
+          const uint32_t d = q_dig[g_start[g]];
+          sz = L0[d] - (d ? L0[d - 1] : 0u);
+          L1[d] = (uint16_t)g;
+          g_lcnt[g] = 0;
+        }
+        uint32_t ys = sz;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(ys, o, 64);
+          if (lane >= (uint32_t)o) ys += y;
+        }
+        if (g < cnt) g_off[g] = base + ys - sz;
+        base += __shfl(ys, 63, 64);
+      }
+      if (lane == 0) {
+        g_off[cnt] = base;
+        s_ctl.m = m;
+        s_ctl.ng = (int32_t)cnt;
+        s_ctl.total = base;
+      }
+    }
+    __syncthreads();
+    ng = s_ctl.ng;
+    // this tile's keys of chosen buckets: LDS slots per group, then one
+    // global atomic per non-empty group for the tile's place in its segment
+    uint32_t gg[MONO_SI], ls[MONO_SI];
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      gg[k] = 0xffffu;
+      const uint64_t key = dkey(xv[k]);
+      if (((keepbits >> k) & 1u) && key >= a.ka && key <= a.kb)
+        gg[k] = L1[(uint32_t)((key - ctl0.lo) >> ctl0.s0)];
+      ls[k] = gg[k] != 0xffffu ? atomicAdd(&g_lcnt[gg[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (tid < ng && g_lcnt[tid]) g_base[tid] = atomicAdd(&a.gcnt[tid], g_lcnt[tid]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k)
+      if (gg[k] != 0xffffu)
+        st_sc1(&a.seg[g_off[gg[k]] + g_base[gg[k]] + ls[k]], dkey(xv[k]) - ctl0.lo);
+  }
+  if (!grid_sync(a.bar, a.gen0 + 3, nt, &s_ok)) return;
+  MONO_STAMP(3);
+
+  // ---- 4: each group's ranks (fused_finish) -> edges ---------------------
+  if (ok2) {
+    uint64_t *sk = (uint64_t *)L0;
+    uint32_t *hist = (uint32_t *)L1;
+    const uint64_t lo = ctl0.lo;
+    const int s = ctl0.s0;
+    for (int g = (int)t; g < ng; g += (int)nt) {
+      const int64_t o = g_off[g], S = (int64_t)g_off[g + 1] - o;
+      const bool in_lds = S <= FS_LDS;
+      if (in_lds)
+        for (int64_t i = tid; i < S; i += MONO_BT) sk[i] = ld_sc1(&a.seg[o + i]);
+      __syncthreads();
+      if (S <= MONO_BT) {  // small group: each key's rank by counting
+        const uint64_t k = tid < S ? sk[tid] : ~0ull;
+        uint32_t less = 0, eq = 0;
+        for (int j = 0; j < (int)S; ++j) {
+          const uint64_t kj = sk[j];
+          less += kj < k ? 1u : 0u;
+          eq += kj == k ? 1u : 0u;
+        }
+        for (int q = (int)g_start[g]; q < (int)g_start[g + 1]; ++q) {
+          const int64_t rr = q_rr[q];
+          if (tid < S && (int64_t)less <= rr && rr < (int64_t)(less + eq))
+            st_sc1d(&a.edges[q], dkey_inv(lo + k));  // tied threads write the same value
+        }
+      } else {
+        for (int q = (int)g_start[g]; q < (int)g_start[g + 1]; ++q) {
+          uint64_t key;
+          const uint64_t pref0 = (uint64_t)q_dig[q] << s;
+          if (in_lds) finish_group<true>(sk, S, pref0, s, q_rr[q], hist, wsum, pick, key);
+          else finish_group<false, true>(a.seg + o, S, pref0, s, q_rr[q], hist, wsum, pick, key);
+          if (tid == 0) st_sc1d(&a.edges[q], dkey_inv(lo + key));
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (!grid_sync(a.bar, a.gen0 + 4, nt, &s_ok)) return;
+  MONO_STAMP(4);
+  if (!ok2) {  // nothing to bin: the control record tells the host
+    constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+    if (t == 0 && tid < NC) a.pack[tid] = ((const double *)&s_ctl)[tid];
+    mono_done(a, NC + nq + nb + a.fs.nm * nb);
+    return;
+  }
+
+  // ---- 5: bins, per-bin sums, the tile's counts and in-tile CSR ranks ----
+  uint32_t *runs = (uint32_t *)L1;                         // [MONO_NW][RADIX]
+  double *acc = (double *)((char *)L1 + sizeof(uint32_t) * MONO_NW * RADIX);
+  const int nm = a.fs.nm, macc = nm * nb;
+  for (int i = tid; i < nq; i += MONO_BT) e_lds[i] = ld_sc1d(&a.edges[i]);
+  for (int i = tid; i < MONO_NW * RADIX; i += MONO_BT) runs[i] = 0;
+  for (int i = tid; i < macc; i += MONO_BT) acc[i] = 0.0;
+  __syncthreads();
+  uint32_t bk[MONO_SI], lp[MONO_SI];
+  {
+    uint32_t ret[MONO_SI];
+    uint64_t pm[MONO_SI];
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      const bool kp = (keepbits >> k) & 1u;
+      bk[k] = kp ? bin_of(xv[k], e_lds, nb) : (uint32_t)nb + 1;
+      if (kp) a.bins[pos[k]] = bk[k];
+    }
+    for (int q = 0; q < nm; ++q) {  // uniform
+      const int col = a.fs.col[q], fq = a.fs.f[q], wq = a.fs.w[q];
+      double *aq = acc + q * nb;
+#pragma unroll
+      for (int k = 0; k < MONO_SI; ++k) {
+        if (bk[k] >= (uint32_t)nb) continue;
+        const double f = fq == 0 ? xv[k] : mv[k];
+        const double ww = wq == 0 ? xv[k] : mv[k];
+        atomicAdd(&aq[bk[k]], monomial(col, f, ww));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {  // element order (wave, k, lane) = particle order
+      const bool kp = (keepbits >> k) & 1u;
+      const uint32_t dgt = bk[k] & 255u;
+      const uint64_t m = peers8(dgt, bal[k]);
+      pm[k] = kp ? m : 0ull;
+      ret[k] = (kp && rank_below(m) == 0) ? atomicAdd(&runs[w * RADIX + dgt], (uint32_t)__popcll(m))
+                                          : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k) {
+      const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
+      lp[k] = (uint32_t)__shfl((int)ret[k], leader, 64) + rank_below(pm[k]);
+    }
+  }
+  __syncthreads();
+  if (tid < RADIX) {  // the tile's count of bin d; runs -> offsets over the waves
+    uint32_t s = 0;
+    for (int k = 0; k < MONO_NW; ++k) {
+      const uint32_t v = runs[k * RADIX + tid];
+      runs[k * RADIX + tid] = s;
+      s += v;
+    }
+    st_sc1(&a.th[(int64_t)tid * nt + t], s);
+  }
+  for (int i = tid; i < macc; i += MONO_BT) st_sc1d(&a.slab[(int64_t)t * macc + i], acc[i]);
+  if (!grid_sync(a.bar, a.gen0 + 5, nt, &s_ok)) return;
+  MONO_STAMP(5);
+
+  // ---- 6: CSR offsets, perm, counts, packed results ----------------------
+  {
+    // bin d: its count in the tiles before t and in all tiles.  Wave w reads
+    // rows d = w, w + 16, ... of the [bin][tile] table coalesced (lane = tile,
+    // nt <= 256: 4 loads per lane and row), four rows (16 loads) in flight
+    uint32_t *pb = L0, *pa = L0 + RADIX;
+    static_assert(MONO_MAXT <= 256, "4 tiles per lane and row");
+    for (int d0 = w; d0 < RADIX; d0 += 4 * MONO_NW) {
+      uint32_t v[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t u = lane + 64 * j;
+          v[r][j] = u < nt ? ld_sc1(&a.th[(int64_t)(d0 + r * MONO_NW) * nt + u]) : 0u;
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint32_t al = 0, be = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          al += v[r][j];
+          be += (lane + 64 * j) < t ? v[r][j] : 0u;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          al += __shfl_xor(al, o, 64);
+          be += __shfl_xor(be, o, 64);
+        }
+        if (lane == 0) {
+          pa[d0 + r * MONO_NW] = al;
+          pb[d0 + r * MONO_NW] = be;
+        }
+      }
+    }
+    __syncthreads();
+    const int d = tid & (RADIX - 1);
+    // bins d < RADIX on waves 0-3: total, tiles-before-t count, bin start
+    uint32_t bl = 0, tot = 0, xs = 0;
+    if (tid < RADIX) {
+      bl = pb[d];
+      tot = pa[d];
+      xs = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(xs, o, 64);
+        if (lane >= (uint32_t)o) xs += y;
+      }
+      if (lane == 63) wsum[w] = xs;
+    }
+    __syncthreads();
+    if (tid < RADIX) {
+      uint32_t ex = 0;
+      for (int k = 0; k < w; ++k) ex += wsum[k];
+      if (t == 0 && d < nb) {
+        a.counts[d] = tot;
+        constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+        a.pack[NC + nq + d] = __builtin_bit_cast(double, (unsigned long long)tot);
+      }
+      s_gofs[d] = ex + xs - tot + bl;  // bin start + this bin's keys in tiles before t
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MONO_SI; ++k)
+      if ((keepbits >> k) & 1u) {
+        const uint32_t dgt = bk[k] & 255u;
+        a.perm[s_gofs[dgt] + runs[w * RADIX + dgt] + lp[k]] = (int32_t)pos[k];
+      }
+  }
+  constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+  if (t == 0) {
+    if (tid < NC) a.pack[tid] = ((const double *)&s_ctl)[tid];
+    for (int i = tid; i < nq; i += MONO_BT) a.pack[NC + i] = e_lds[i];
+  }
+  // per-bin sums: column j summed over the tiles in a fixed order by one wave
+  const int nsum = macc;
+  for (int j = (int)t * MONO_NW + w; j < nsum; j += (int)nt * MONO_NW) {
+    double v[4];  // nt <= 256: four rows per lane, loads in flight together
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t r = lane + 64 * k;
+      v[k] = r < nt ? ld_sc1d(&a.slab[(int64_t)r * macc + j]) : 0.0;
+    }
+    double s = ((v[0] + v[1]) + v[2]) + v[3];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) a.pack[NC + nq + nb + j] = s;
+  }
+  MONO_STAMP(6);
+  mono_done(a, NC + nq + nb + nsum);
+}
+
 // ----------------------------------------------------------------- moments
 // LDS: accumulators in LDS (nb <= LDS_MOM_BINS), one slab row per block;
 // else straight to global_acc.  Templated so the LDS path indexes the
@@ -1939,6 +2539,11 @@ struct Profile {
   int64_t sel_base = 0, sel_span = 0;
   uint32_t sel_nt = 0;
   const double *sel_mass = nullptr;
+  // one-launch radial path (radial_mono): tile records + group fill, grid
+  // barrier words; barrier generation / completion count carried across calls
+  Buf mono, bar, mono_trace;
+  uint64_t bar_gen = 0, bar_done = 0;
+  uint32_t bar_n = 0;  // grid size the barrier words were counted for (0: reset)
 };
 
 static void ensure_x(Profile &P, hipStream_t st);
@@ -2207,10 +2812,21 @@ static void csr_device(Profile &P, hipStream_t st) {
 // select_onepass); the masses are then read from `mass` (the caller's device
 // array, or a handle-owned staged copy) when the weights are needed.
 // Returns the tile count.
-static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
-                              int64_t n, int on_device, int use_sphere, const double *sphere,
-                              const int64_t *fam, int nfam, int ndim, bool lazy = false,
-                              int pos_f32 = 0, int mass_f32 = 0, bool tiled = false) {
+struct SelPrep {  // a selection's parameters and output buffers (select_prep)
+  SelectParams sp;
+  int64_t hi = 0, span = 0;
+  uint32_t nt = 0;
+  const void *d_pos = nullptr, *d_mass = nullptr;
+  double *xo = nullptr;
+  uint64_t *kw = nullptr;
+  uint32_t *toff = nullptr;
+};
+
+// parameters, host staging and output buffers of a selection (no launch)
+static SelPrep select_prep(Profile &P, hipStream_t st, const void *pos, const void *mass,
+                           int64_t n, int on_device, int use_sphere, const double *sphere,
+                           const int64_t *fam, int nfam, int ndim, bool lazy, int pos_f32,
+                           int mass_f32, bool tiled) {
   check_n(n);
   if (ndim != 2 && ndim != 3) fail(PBX_ERR_VALUE, "ndim must be either 2 or 3");
   if (nfam < 0 || nfam > MAX_FAM) fail(PBX_ERR_VALUE, "at most %d family ranges", MAX_FAM);
@@ -2261,21 +2877,49 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
   // large lazy selections: tiled output, no look-back (tile offsets: fused_hist0)
   tiled = tiled && lazy && nt >= 1024;
   sp.tiled = tiled ? 1 : 0;
+  const int64_t xlen = tiled ? (int64_t)nt * TILE : span;
+  SelPrep r;
+  r.xo = (double *)P.x.get(sizeof(double) * (size_t)(xlen ? xlen : 1));
+  if (lazy) {
+    r.kw = (uint64_t *)P.kw.get(sizeof(uint64_t) * (TILE / 64) * (size_t)std::max<uint32_t>(nt, 1));
+    r.toff = (uint32_t *)P.toff.get(sizeof(uint32_t) * (size_t)std::max<uint32_t>(nt, 1));
+  }
+  r.sp = sp;
+  r.hi = hi;
+  r.span = span;
+  r.nt = nt;
+  r.d_pos = d_pos;
+  r.d_mass = d_mass;
+  P.lazy = lazy;
+  P.x_tiled = tiled && span;
+  P.sel_base = lo;
+  P.sel_span = span;
+  P.sel_nt = nt;
+  P.sel_mass = lazy ? (const double *)d_mass : nullptr;
+  return r;
+}
+
+static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
+                              int64_t n, int on_device, int use_sphere, const double *sphere,
+                              const int64_t *fam, int nfam, int ndim, bool lazy = false,
+                              int pos_f32 = 0, int mass_f32 = 0, bool tiled = false) {
+  const SelPrep r = select_prep(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
+                                lazy, pos_f32, mass_f32, tiled);
+  const SelectParams &sp = r.sp;
+  const uint32_t nt = r.nt;
+  const int64_t hi = r.hi, span = r.span;
+  const void *d_pos = r.d_pos, *d_mass = r.d_mass;
   // per-tile look-back status words + ticket / watchdog (selection scratch)
   // [stat nt][ctrl: ticket, watchdog][MM_SLOTS x (~min key, max key)]: one zero fill
   const size_t nst = (size_t)nt + 1 + 2 * MM_SLOTS;
   uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * nst);
   uint32_t *ctrl = (uint32_t *)(stat + nt);
-  const int64_t xlen = tiled ? (int64_t)nt * TILE : span;
-  double *xo = (double *)P.x.get(sizeof(double) * (size_t)(xlen ? xlen : 1));
+  double *xo = r.xo;
   double *wo = nullptr;
   int32_t *io = nullptr;
-  uint64_t *kw = nullptr;
-  uint32_t *toff = nullptr;
-  if (lazy) {
-    kw = (uint64_t *)P.kw.get(sizeof(uint64_t) * (TILE / 64) * (size_t)std::max<uint32_t>(nt, 1));
-    toff = (uint32_t *)P.toff.get(sizeof(uint32_t) * (size_t)std::max<uint32_t>(nt, 1));
-  } else {
+  uint64_t *kw = r.kw;
+  uint32_t *toff = r.toff;
+  if (!lazy) {
     wo = (double *)P.w.get(sizeof(double) * (size_t)(span ? span : 1));
     io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(span ? span : 1));
   }
@@ -2299,12 +2943,6 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
     }
     PBX_HIP(hipGetLastError());
   }
-  P.lazy = lazy;
-  P.x_tiled = tiled && span;
-  P.sel_base = lo;
-  P.sel_span = span;
-  P.sel_nt = nt;
-  P.sel_mass = lazy ? (const double *)d_mass : nullptr;
   return nt;
 }
 
@@ -2478,6 +3116,143 @@ static void percentiles_device(Profile &P, hipStream_t st, int f_src, const doub
                        w, absval, (const double *)dq, nq, cdf, out);
     PBX_HIP(hipGetLastError());
   }
+}
+
+// ---- one-launch radial path (radial_mono) -------------------------------
+// PBX_RADIAL_MONO=0 turns it off (A/B: the multi-kernel path)
+static bool mono_enabled() {
+  static const bool on = [] {
+    const char *v = std::getenv("PBX_RADIAL_MONO");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+// Tiles (= blocks) the one-launch path may use on a device: every block must
+// be resident at once, one 1024-thread block per CU (0: never)
+static uint32_t mono_max_tiles(int dev) {
+  static std::mutex mu;
+  static std::vector<int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)cache.size() <= dev) cache.resize((size_t)dev + 1, -1);
+  if (cache[(size_t)dev] < 0) {
+    int cus = 0, per = 0;
+    PBX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    PBX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per, reinterpret_cast<const void *>(&radial_mono), MONO_BT, 0));
+    cache[(size_t)dev] = per >= 1 ? std::min<int>(cus, (int)MONO_MAXT) : 0;
+  }
+  return (uint32_t)cache[(size_t)dev];
+}
+
+// the families' span of n particles (select_prep's rule)
+static int64_t family_span(int64_t n, const int64_t *fam, int nfam) {
+  if (nfam <= 0) return n;
+  int64_t lo = n, hi = 0;
+  for (int f = 0; f < nfam; ++f) {
+    const int64_t a = std::max<int64_t>(0, fam[2 * f]), b = std::min<int64_t>(n, fam[2 * f + 1]);
+    if (b > a) {
+      lo = std::min(lo, a);
+      hi = std::max(hi, b);
+    }
+  }
+  return hi > lo ? hi - lo : 0;
+}
+
+// Runs the step as one launch when the selection fits (<= one tile per CU,
+// bins < 256, the fused sums in LDS); returns the pinned results pack
+// ([ctl][edges][counts][sums], the fused_pack layout) after ONE sync, or
+// null when the path does not apply or the call was discarded (a block gave
+// up at a barrier: the barrier words are reset and the caller runs the
+// multi-kernel path, which recomputes everything).
+static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, const void *mass,
+                               int64_t n, int on_device, int use_sphere, const double *sphere,
+                               const int64_t *fam, int nfam, int ndim, int64_t nbins, uint64_t ka,
+                               uint64_t kb, bool empty_bounds, const FusedStats &fs, int *nsum) {
+  check_n(n);
+  const int nb = (int)nbins, nq = nb + 1, macc = fs.nm * nb;
+  if (nb >= RADIX || ndim < 2 || ndim > 3 || nfam < 0 || nfam > MAX_FAM) return nullptr;
+  if (sizeof(double) * (size_t)macc + sizeof(uint32_t) * MONO_NW * RADIX > sizeof(uint16_t) * MS0_DIG)
+    return nullptr;
+  const uint32_t nt = ntiles_of(family_span(n, fam, nfam));
+  if (nt == 0 || nt > mono_max_tiles(P.device)) return nullptr;
+  const SelPrep r = select_prep(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
+                                /*lazy=*/true, 0, 0, /*tiled=*/false);
+  const int64_t ns = std::max<int64_t>(r.span, 1);
+  MonoArgs a{};
+  a.pos = (const double *)r.d_pos;
+  a.mass = (const double *)r.d_mass;
+  a.n_hi = r.hi;
+  a.sp = r.sp;
+  a.ka = ka;
+  a.kb = kb;
+  a.empty_bounds = empty_bounds ? 1 : 0;
+  a.nb = nb;
+  a.nq = nq;
+  a.nbins = nbins;
+  a.fs = fs;
+  char *scr = (char *)P.mono.get(sizeof(MonoRec) * MONO_MAXT + sizeof(uint32_t) * RADIX);
+  a.rec = (MonoRec *)scr;
+  a.gcnt = (uint32_t *)(scr + sizeof(MonoRec) * MONO_MAXT);
+  a.H = (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG);
+  a.seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)ns);
+  a.x = r.xo;
+  a.kw = r.kw;
+  a.toff = r.toff;
+  a.bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)ns);
+  a.perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)ns);
+  a.edges = (double *)P.edges.get(sizeof(double) * (size_t)nq);
+  a.th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * RADIX * (size_t)nt);
+  a.slab = macc ? (double *)P.fslab.get(sizeof(double) * (size_t)nt * macc) : nullptr;
+  a.counts = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
+  constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+  const int ntot = NC + nq + nb + macc;
+  a.pack = (double *)P.fpack.get(sizeof(double) * (size_t)(ntot + 1));
+  if (P.bar_n != nt || !P.bar.p) {  // counters are counted for one grid size
+    P.bar.get(sizeof(uint64_t) * BAR_WORDS);
+    PBX_HIP(hipMemsetAsync(P.bar.p, 0, sizeof(uint64_t) * BAR_WORDS, st));
+    P.bar_gen = P.bar_done = 0;
+    P.bar_n = nt;
+  }
+  a.bar = (uint64_t *)P.bar.p;
+  static const bool trace_env = [] {
+    const char *v = std::getenv("PBX_MONO_TRACE");
+    return v && v[0] == '1';
+  }();
+  a.trace = trace_env ? (uint64_t *)P.mono_trace.get(sizeof(uint64_t) * 8 * nt) : nullptr;
+  a.gen0 = P.bar_gen;
+  a.done_target = P.bar_done + nt;
+  hipLaunchKernelGGL(radial_mono, dim3(nt), dim3(MONO_BT), 0, st, a);
+  PBX_HIP(hipGetLastError());
+  P.bar_gen += 5;
+  P.bar_done += nt;
+  double *hp = (double *)P.pin.get(sizeof(double) * (size_t)(ntot + 1));
+  hp[ntot] = __builtin_bit_cast(double, ~0ull);
+  PBX_HIP(hipMemcpyAsync(hp, a.pack, sizeof(double) * (ntot + 1), hipMemcpyDeviceToHost, st));
+  PBX_HIP(hipStreamSynchronize(st));
+  if (__builtin_bit_cast(uint64_t, hp[ntot]) != a.gen0) {
+    P.bar_n = 0;  // discarded: zero the barrier words before the next call
+    return nullptr;
+  }
+  if (a.trace) {  // per phase: min / max over blocks of the stamp, relative to the earliest start
+    std::vector<uint64_t> tr((size_t)8 * nt);
+    PBX_HIP(hipMemcpy(tr.data(), a.trace, sizeof(uint64_t) * 8 * nt, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull;
+    for (uint32_t b = 0; b < nt; ++b) t0 = std::min(t0, tr[(size_t)b * 8]);
+    std::fprintf(stderr, "[mono] nt=%u", nt);
+    for (int k = 0; k < 8; ++k) {
+      uint64_t lo = ~0ull, hi = 0;
+      for (uint32_t b = 0; b < nt; ++b) {
+        lo = std::min(lo, tr[(size_t)b * 8 + k] - t0);
+        hi = std::max(hi, tr[(size_t)b * 8 + k] - t0);
+      }
+      std::fprintf(stderr, " p%d %.2f-%.2fus", k, lo / 100.0, hi / 100.0);
+    }
+    std::fprintf(stderr, "\n");
+  }
+  P.csrh_ready = false;
+  *nsum = macc;
+  return hp;
 }
 
 static Profile &as_profile(void *h) {
@@ -2905,6 +3680,7 @@ int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double b
     if (m == 0) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
     if (m < 2) {  // the reference's degenerate [s0, s0]: one bin, redo with 2 edges
       h_edges[1] = h_edges[0];
+      double *de = (double *)P.edges.get(sizeof(double) * 2);
       PBX_HIP(hipMemcpyAsync(de, h_edges, sizeof(double) * 2, hipMemcpyHostToDevice, st));
       assign_device(P, st, de, 1);
       if (build_csr) csr_device(P, st);
@@ -2987,10 +3763,6 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       return v && v[0] == '1';
     }();
     const bool lazy = nbins < RADIX && !eager_env;
-    const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
-                                      nfam, ndim, lazy, 0, 0, /*tiled=*/true);
-    const int64_t n_sel = nt ? P.sel_span : 0;  // tiled particles (the families' span)
-    const bool tiled = P.x_tiled;  // x by tile (large inputs): tile offsets from fused_hist0
     const int nq = (int)nbins + 1;
     // the window of bins.py:734-737 as key bounds (msel_begin)
     bool empty_bounds = false;
@@ -3006,42 +3778,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
         else kb = std::min<uint64_t>(kb, dkey(bin_max));
       }
     }
-    uint64_t *stat = (uint64_t *)P.selst.p;
-    FusedCtl *ctl = (FusedCtl *)P.fctl.get(sizeof(FusedCtl));
     const int64_t nb = nbins;
-    unsigned long long *cnt = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
-    uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG);
-    const int64_t *n_dev = &ctl->n;
-    const double *x = (const double *)P.x.p;
-    // level 0 (rows -> H), resolve + groups, per-block offsets, gather,
-    // per-group finish -> edges
-    const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n_sel / (MS0_TPB * 16)));
-    uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
-    const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
-                         (uint32_t *)P.toff.p};
-    hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
-                       rows);
-    hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
-                       (const uint32_t *)rows, g0, H);
-    MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
-    uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)g0) * (MS_MAXQ + 1));
-    uint32_t *goff = gdig + (MS_MAXQ + 1), *gq = goff + (MS_MAXQ + 1);
-    uint32_t *boff = gq + (MS_MAXQ + 1);
-    hipLaunchKernelGGL(fused_resolve0, dim3(1), dim3(FR_TPB), 0, st, H, ctl, nbins, nq, R, gdig,
-                       goff, gq);
-    hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
-                       (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff);
-    uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n_sel ? n_sel : 1));
-    hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
-                       (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff, seg,
-                       tiled ? (const uint64_t *)stat : nullptr, nt);
-    double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
-    hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
-                       (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
-                       (const uint64_t *)seg, de);
-    PBX_HIP(hipGetLastError());
-    // assignment (+ the statistics' distinct sums) with the device edges
-    uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n_sel ? n_sel : 1));
     // distinct monomials of the requested columns (x^a w^b |x|^c |w|^d);
     // mono[k][c] = its slot, -1 = column not accumulated (0)
     FusedStats fs{};
@@ -3079,119 +3816,166 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
         mono[(size_t)k * NMOM + c] = slot;
       }
     if (!fuse) fs.nm = 0;
-    double *maccs = nullptr;
-    P.csrh_ready = false;
-    uint32_t ablocks = 0;
-    const uint32_t *cnt_offs = nullptr;  // scanned CSR histogram the counts come from
-    if (n_sel && lazy) {
-      // tile-walking assignment over the lazy selection + its CSR pass
-      const int64_t macc = (int64_t)fs.nm * nb;
-      const bool ldse = (nb + 1) <= LDS_EDGES;
-      const size_t lds = sizeof(double) * (size_t)macc + (ldse ? sizeof(double) * (nb + 1) : 0);
-      uint32_t *th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX);
-      const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
-      ablocks = ceil_div(nt, tpbk);
-      double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
-      const uint64_t *kwp = (const uint64_t *)P.kw.p;
-      const uint32_t *tof = (const uint32_t *)P.toff.p;
-      // few tiles: one tile per 1024-thread block, every wave a piece of it
-      const bool wide = tpbk == 1 && nt < 1024;
-      auto go = [&](auto kern, int bt) {
-        hipLaunchKernelGGL(kern, dim3(ablocks), dim3(bt), lds, st, x, kwp, tof, P.sel_base, nt,
-                           tpbk, P.sel_mass, (const double *)de, (int)nb, bins, th, fs, slab,
-                           tiled ? 1 : 0);
-      };
-      if (wide) {
-        if (fs.nm) {
-          if (ldse) go(assign_sel<true, true, 1024>, 1024);
-          else go(assign_sel<true, false, 1024>, 1024);
-        } else {
-          if (ldse) go(assign_sel<false, true, 1024>, 1024);
-          else go(assign_sel<false, false, 1024>, 1024);
-        }
-      } else if (fs.nm) {
-        if (ldse) go(assign_sel<true, true, TPB>, TPB);
-        else go(assign_sel<true, false, TPB>, TPB);
-      } else {
-        if (ldse) go(assign_sel<false, true, TPB>, TPB);
-        else go(assign_sel<false, false, TPB>, TPB);
-      }
-      PBX_HIP(hipGetLastError());
-      if (fs.nm) maccs = slab;
-      // the counts are row-start differences of the scanned [bin][tile] table
-      scan_u32(P, st, th, (int64_t)nt * RADIX);
-      cnt_offs = th;
-      if (build_csr) {
-        int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
-        hipLaunchKernelGGL(csr_sel, dim3(nt), dim3(TPB), 0, st, kwp, tof, (const uint32_t *)bins,
-                           (const uint32_t *)th, nt, perm);
-        PBX_HIP(hipGetLastError());
-      }
-    } else if (n_sel) {
-      const int64_t macc = (int64_t)fs.nm * nb;
-      size_t lds = sizeof(double) * (size_t)macc +
-                   ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
-                   sizeof(uint32_t) * (nb + 1);
-      if (lds > 150 * 1024) fail(PBX_ERR_VALUE, "too many bins for the device histogram (%lld)", (long long)nb);
-      uint32_t *th = (nb < RADIX) ? (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX)
-                                  : nullptr;
-      const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
-      ablocks = ceil_div(nt, tpbk);
-      double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
-      // with the CSR pass, the bin counts are differences of its scanned
-      // [bin][tile] histogram: no global count atomics in assign_bins
-      if (th && build_csr) cnt_offs = th;
-      unsigned long long *acnt = cnt_offs ? nullptr : cnt;
-      if (fs.nm)
-        launch_assign<true>(ablocks, lds, st, x, n_sel, (const double *)de, (int)nb, bins, acnt, th,
-                            nt, tpbk, n_dev, (const double *)P.w.p, fs, slab);
-      else
-        launch_assign<false>(ablocks, lds, st, x, n_sel, (const double *)de, (int)nb, bins, acnt, th,
-                             nt, tpbk, n_dev, nullptr, fs, nullptr);
-      PBX_HIP(hipGetLastError());
-      P.csrh_ready = th != nullptr;
-      if (fs.nm) maccs = slab;  // its rows are summed inside fused_pack
-      if (build_csr) {  // stable counting sort of the bin ids, device length
-        int bits = 0;
-        while (((int64_t)1 << bits) <= nb) ++bits;
-        uint32_t *ka2 = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n_sel);
-        uint32_t *kb2 = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n_sel);
-        int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
-        int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n_sel);
-        const uint32_t *kin = bins;
-        bool first = true;
-        for (int shift = 0; shift < bits; shift += 8) {
-          const bool last = shift + 8 >= bits;
-          if (first) {
-            prim::radix_pass<uint32_t>(P.csrh_ready ? P.csrh : P.hist, P.tsum, st, kin, nullptr,
-                                       VAL_IOTA, n_sel, shift, last ? nullptr : ka2, va, P.csrh_ready,
-                                       n_dev);
-            first = false;
-          } else {
-            prim::radix_pass<uint32_t>(P.hist, P.tsum, st, ka2, va, VAL_ARRAY, n_sel, shift,
-                                       last ? nullptr : kb2, vb, false, n_dev);
-            std::swap(ka2, kb2);
-            std::swap(va, vb);
-          }
-        }
-        P.csrh_ready = false;
-        if ((void *)va != P.perm.p)
-          PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n_sel, hipMemcpyDeviceToDevice, st));
-      }
-    }
-    // the results packed on the device, one copy, one sync
     constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
     static_assert(sizeof(FusedCtl) % sizeof(double) == 0, "FusedCtl packs as doubles");
-    const int nsum = maccs ? fs.nm * (int)nb : 0;
-    const int ntot = NC + nq + (int)nb + nsum;
-    double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)ntot);
-    const int nhead = (int)ceil_div(NC + nq + (int)nb, TPB);
-    hipLaunchKernelGGL(fused_pack, dim3(nhead + nsum), dim3(TPB), 0, st, (const FusedCtl *)ctl,
-                       (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
-                       (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead);
-    double *hp = (double *)P.pin.get(sizeof(double) * (size_t)ntot);
-    PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * ntot, hipMemcpyDeviceToHost, st));
-    PBX_HIP(hipStreamSynchronize(st));
+    // small selections: the whole step as one persistent launch (radial_mono)
+    double *hp = nullptr;
+    int nsum = 0;
+    if (lazy && mono_enabled())
+      hp = radial_mono_run(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
+                           nbins, ka, kb, empty_bounds, fs, &nsum);
+    if (!hp) {  // the multi-kernel path
+      const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
+                                        nfam, ndim, lazy, 0, 0, /*tiled=*/true);
+      const int64_t n_sel = nt ? P.sel_span : 0;  // tiled particles (the families' span)
+      const bool tiled = P.x_tiled;  // x by tile (large inputs): tile offsets from fused_hist0
+      uint64_t *stat = (uint64_t *)P.selst.p;
+      FusedCtl *ctl = (FusedCtl *)P.fctl.get(sizeof(FusedCtl));
+      unsigned long long *cnt = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
+      uint32_t *H = (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG);
+      const int64_t *n_dev = &ctl->n;
+      const double *x = (const double *)P.x.p;
+      // level 0 (rows -> H), resolve + groups, per-block offsets, gather,
+      // per-group finish -> edges
+      const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n_sel / (MS0_TPB * 16)));
+      uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
+      const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
+                           (uint32_t *)P.toff.p};
+      hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
+                         rows);
+      hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
+                         (const uint32_t *)rows, g0, H);
+      MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
+      uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)g0) * (MS_MAXQ + 1));
+      uint32_t *goff = gdig + (MS_MAXQ + 1), *gq = goff + (MS_MAXQ + 1);
+      uint32_t *boff = gq + (MS_MAXQ + 1);
+      hipLaunchKernelGGL(fused_resolve0, dim3(1), dim3(FR_TPB), 0, st, H, ctl, nbins, nq, R, gdig,
+                         goff, gq);
+      hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
+                         (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff);
+      uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n_sel ? n_sel : 1));
+      hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
+                         (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff, seg,
+                         tiled ? (const uint64_t *)stat : nullptr, nt);
+      double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
+      hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
+                         (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
+                         (const uint64_t *)seg, de);
+      PBX_HIP(hipGetLastError());
+      // assignment (+ the statistics' distinct sums) with the device edges
+      uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n_sel ? n_sel : 1));
+      double *maccs = nullptr;
+      P.csrh_ready = false;
+      uint32_t ablocks = 0;
+      const uint32_t *cnt_offs = nullptr;  // scanned CSR histogram the counts come from
+      if (n_sel && lazy) {
+        // tile-walking assignment over the lazy selection + its CSR pass
+        const int64_t macc = (int64_t)fs.nm * nb;
+        const bool ldse = (nb + 1) <= LDS_EDGES;
+        const size_t lds = sizeof(double) * (size_t)macc + (ldse ? sizeof(double) * (nb + 1) : 0);
+        uint32_t *th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX);
+        const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
+        ablocks = ceil_div(nt, tpbk);
+        double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
+        const uint64_t *kwp = (const uint64_t *)P.kw.p;
+        const uint32_t *tof = (const uint32_t *)P.toff.p;
+        // few tiles: one tile per 1024-thread block, every wave a piece of it
+        const bool wide = tpbk == 1 && nt < 1024;
+        auto go = [&](auto kern, int bt) {
+          hipLaunchKernelGGL(kern, dim3(ablocks), dim3(bt), lds, st, x, kwp, tof, P.sel_base, nt,
+                             tpbk, P.sel_mass, (const double *)de, (int)nb, bins, th, fs, slab,
+                             tiled ? 1 : 0);
+        };
+        if (wide) {
+          if (fs.nm) {
+            if (ldse) go(assign_sel<true, true, 1024>, 1024);
+            else go(assign_sel<true, false, 1024>, 1024);
+          } else {
+            if (ldse) go(assign_sel<false, true, 1024>, 1024);
+            else go(assign_sel<false, false, 1024>, 1024);
+          }
+        } else if (fs.nm) {
+          if (ldse) go(assign_sel<true, true, TPB>, TPB);
+          else go(assign_sel<true, false, TPB>, TPB);
+        } else {
+          if (ldse) go(assign_sel<false, true, TPB>, TPB);
+          else go(assign_sel<false, false, TPB>, TPB);
+        }
+        PBX_HIP(hipGetLastError());
+        if (fs.nm) maccs = slab;
+        // the counts are row-start differences of the scanned [bin][tile] table
+        scan_u32(P, st, th, (int64_t)nt * RADIX);
+        cnt_offs = th;
+        if (build_csr) {
+          int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
+          hipLaunchKernelGGL(csr_sel, dim3(nt), dim3(TPB), 0, st, kwp, tof, (const uint32_t *)bins,
+                             (const uint32_t *)th, nt, perm);
+          PBX_HIP(hipGetLastError());
+        }
+      } else if (n_sel) {
+        const int64_t macc = (int64_t)fs.nm * nb;
+        size_t lds = sizeof(double) * (size_t)macc +
+                     ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
+                     sizeof(uint32_t) * (nb + 1);
+        if (lds > 150 * 1024) fail(PBX_ERR_VALUE, "too many bins for the device histogram (%lld)", (long long)nb);
+        uint32_t *th = (nb < RADIX) ? (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * RADIX)
+                                    : nullptr;
+        const uint32_t tpbk = std::min<uint32_t>(AS_TILES, std::max<uint32_t>(1, nt / 1024));
+        ablocks = ceil_div(nt, tpbk);
+        double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)ablocks * macc) : nullptr;
+        // with the CSR pass, the bin counts are differences of its scanned
+        // [bin][tile] histogram: no global count atomics in assign_bins
+        if (th && build_csr) cnt_offs = th;
+        unsigned long long *acnt = cnt_offs ? nullptr : cnt;
+        if (fs.nm)
+          launch_assign<true>(ablocks, lds, st, x, n_sel, (const double *)de, (int)nb, bins, acnt, th,
+                              nt, tpbk, n_dev, (const double *)P.w.p, fs, slab);
+        else
+          launch_assign<false>(ablocks, lds, st, x, n_sel, (const double *)de, (int)nb, bins, acnt, th,
+                               nt, tpbk, n_dev, nullptr, fs, nullptr);
+        PBX_HIP(hipGetLastError());
+        P.csrh_ready = th != nullptr;
+        if (fs.nm) maccs = slab;  // its rows are summed inside fused_pack
+        if (build_csr) {  // stable counting sort of the bin ids, device length
+          int bits = 0;
+          while (((int64_t)1 << bits) <= nb) ++bits;
+          uint32_t *ka2 = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n_sel);
+          uint32_t *kb2 = (uint32_t *)P.keys1.get(sizeof(uint32_t) * (size_t)n_sel);
+          int32_t *va = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
+          int32_t *vb = (int32_t *)P.vtmp.get(sizeof(int32_t) * (size_t)n_sel);
+          const uint32_t *kin = bins;
+          bool first = true;
+          for (int shift = 0; shift < bits; shift += 8) {
+            const bool last = shift + 8 >= bits;
+            if (first) {
+              prim::radix_pass<uint32_t>(P.csrh_ready ? P.csrh : P.hist, P.tsum, st, kin, nullptr,
+                                         VAL_IOTA, n_sel, shift, last ? nullptr : ka2, va, P.csrh_ready,
+                                         n_dev);
+              first = false;
+            } else {
+              prim::radix_pass<uint32_t>(P.hist, P.tsum, st, ka2, va, VAL_ARRAY, n_sel, shift,
+                                         last ? nullptr : kb2, vb, false, n_dev);
+              std::swap(ka2, kb2);
+              std::swap(va, vb);
+            }
+          }
+          P.csrh_ready = false;
+          if ((void *)va != P.perm.p)
+            PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n_sel, hipMemcpyDeviceToDevice, st));
+        }
+      }
+      // the results packed on the device, one copy, one sync
+      nsum = maccs ? fs.nm * (int)nb : 0;
+      const int ntot = NC + nq + (int)nb + nsum;
+      double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)ntot);
+      const int nhead = (int)ceil_div(NC + nq + (int)nb, TPB);
+      hipLaunchKernelGGL(fused_pack, dim3(nhead + nsum), dim3(TPB), 0, st, (const FusedCtl *)ctl,
+                         (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
+                         (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead);
+      hp = (double *)P.pin.get(sizeof(double) * (size_t)ntot);
+      PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * ntot, hipMemcpyDeviceToHost, st));
+      PBX_HIP(hipStreamSynchronize(st));
+    }
     const FusedCtl *hc = (const FusedCtl *)hp;
     const double *he = hp + NC;
     const int64_t *hcn = (const int64_t *)(he + nq);
@@ -3208,6 +3992,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     std::memcpy(h_edges, he, sizeof(double) * nq);
     if (m < 2) {  // the reference's degenerate [s0, s0]: one bin, stepwise
       h_edges[1] = h_edges[0];
+      double *de = (double *)P.edges.get(sizeof(double) * 2);
       PBX_HIP(hipMemcpyAsync(de, h_edges, sizeof(double) * 2, hipMemcpyHostToDevice, st));
       assign_device(P, st, de, 1);
       if (build_csr) csr_device(P, st);

@@ -1553,6 +1553,7 @@ struct Octree {
   Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
   Buf rec0;                  // {x, y, z, m} in original order (path_keys)
   bool rec0_valid = false;   // rec0 holds the current masses
+  prim::HostBuf rm_pin;      // radial_moments readback staging
   ~Octree() {
     Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
                    &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &keys, &ktmp0,
@@ -1560,6 +1561,7 @@ struct Octree {
                    &counters, &trace, &bal, &bp_fl, &bp_eq, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
                    &bp_p2b};
     for (Buf *b : bufs) b->release();
+    rm_pin.release();
   }
   // accepted nodes, leaf pairs, fault flag, wave steps, active-lane steps
   // + leaf wave steps, their active lanes, descending wave steps
@@ -2150,6 +2152,107 @@ static const char *method_name(int want, bool at_points) {
   return want == PBX_WANT_POT ? "compute_potentials" : "compute_accelerations";
 }
 
+// ---------------------------------------- radial profile of walk outputs
+// The 3-D radial profile of a per-target field (the potential of config 5)
+// over a range of the leaf-ordered targets, straight from the tree's
+// records: RadialProfile(ndim=3) with explicit edges — r = sqrt((x*x+y*y)+z*z)
+// (the selection's expression, no FMA), bins.py:346-395 assignment (bin_of),
+// and the seven per-bin columns of pbx_profile_moments with f = the field,
+// w = the mass (proarray.py:272-334 statistics read them) + the bin counts.
+// It replaces select + assign + gather + moments (and their host syncs).
+// Every thread takes RM_PT consecutive targets — neighbours in leaf order,
+// mostly one bin — and adds a run's sums to LDS when the bin changes, so
+// the LDS atomics are few and rarely contended; one slab row per block and
+// a fixed-order sum over the rows (radial_moments_reduce).
+constexpr int RM_PT = 8;
+constexpr int RM_CHUNK = TPB * RM_PT;
+constexpr int RM_MAXB = 1024;
+__global__ void __launch_bounds__(TPB)
+    radial_moments_kernel(const double4 *__restrict__ rec, const double *__restrict__ f,
+                          int64_t first, int64_t count, const double *__restrict__ edges, int nb,
+                          double *__restrict__ slab, uint32_t *__restrict__ cslab) {
+  extern __shared__ __attribute__((aligned(16))) double rm_sm[];
+  double *e = rm_sm, *acc = rm_sm + (nb + 1);
+  uint32_t *cnt = (uint32_t *)(acc + 7 * (int64_t)nb);
+  for (int k = threadIdx.x; k <= nb; k += TPB) e[k] = edges[k];
+  for (int k = threadIdx.x; k < 7 * nb; k += TPB) acc[k] = 0.0;
+  for (int k = threadIdx.x; k < nb; k += TPB) cnt[k] = 0u;
+  __syncthreads();
+  for (int64_t c0 = (int64_t)blockIdx.x * RM_CHUNK; c0 < count; c0 += (int64_t)gridDim.x * RM_CHUNK) {
+    const int64_t i0 = c0 + (int64_t)threadIdx.x * RM_PT;
+    double4 q[RM_PT];
+    double v[RM_PT];
+#pragma unroll
+    for (int k = 0; k < RM_PT; ++k) {  // all loads in flight before use
+      const int64_t i = i0 + k < count ? i0 + k : 0;
+      q[k] = rec[first + i];
+      v[k] = f[i];
+    }
+    uint32_t cur = (uint32_t)nb, c = 0;
+    double s[7] = {0, 0, 0, 0, 0, 0, 0};
+    auto flush = [&]() {
+      if (cur < (uint32_t)nb && c) {
+#pragma unroll
+        for (int j = 0; j < 7; ++j) atomicAdd(&acc[cur * 7 + j], s[j]);
+        atomicAdd(&cnt[cur], c);
+      }
+#pragma unroll
+      for (int j = 0; j < 7; ++j) s[j] = 0.0;
+      c = 0;
+    };
+#pragma unroll
+    for (int k = 0; k < RM_PT; ++k) {
+      if (i0 + k >= count) break;
+      double r;
+      {
+#pragma clang fp contract(off)
+        r = __builtin_sqrt((q[k].x * q[k].x + q[k].y * q[k].y) + q[k].z * q[k].z);
+      }
+      const uint32_t b = bin_of(r, e, nb);
+      if (b != cur) {
+        flush();
+        cur = b;
+      }
+      if (b < (uint32_t)nb) {
+#pragma clang fp contract(off)
+        const double x = v[k], w = q[k].w, a = __builtin_fabs(x);
+        s[0] += w;
+        s[1] += x * w;
+        s[2] += (x * x) * w;
+        s[3] += x;
+        s[4] += x * x;
+        s[5] += a * w;
+        s[6] += a;
+        ++c;
+      }
+    }
+    flush();
+  }
+  __syncthreads();
+  double *dst = slab + (int64_t)blockIdx.x * 7 * nb;
+  for (int k = threadIdx.x; k < 7 * nb; k += TPB) dst[k] = acc[k];
+  uint32_t *cd = cslab + (int64_t)blockIdx.x * nb;
+  for (int k = threadIdx.x; k < nb; k += TPB) cd[k] = cnt[k];
+}
+
+// out = [counts nb (u64)][moments nb x 7]: column j summed over the rows in
+// a fixed order (thread j, rows 0, 1, ...)
+__global__ void radial_moments_reduce(const double *__restrict__ slab,
+                                      const uint32_t *__restrict__ cslab, int rows, int nb,
+                                      double *__restrict__ out) {
+  const int j = blockIdx.x * TPB + threadIdx.x;
+  if (j < nb) {
+    unsigned long long c = 0;
+    for (int r = 0; r < rows; ++r) c += cslab[(int64_t)r * nb + j];
+    out[j] = __builtin_bit_cast(double, c);
+  } else if (j < 8 * nb) {
+    const int k = j - nb;
+    double s = 0.0;
+    for (int r = 0; r < rows; ++r) s += slab[(int64_t)r * 7 * nb + k];
+    out[j] = s;
+  }
+}
+
 }  // namespace tree
 }  // namespace pbx
 
@@ -2349,6 +2452,47 @@ int pbx_octree_leaf_particles(pbx_octree *t, int64_t first, int64_t count, doubl
                          d_idx);
     PBX_HIP(hipGetLastError());
     PBX_HIP(hipStreamSynchronize(dev.stream));
+  });
+}
+
+int pbx_octree_radial_moments(pbx_octree *t, int64_t first, int64_t count, const double *d_f,
+                              const double *h_edges, int64_t nbins, int64_t *h_counts,
+                              double *h_moments) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (first < 0 || count < 0 || first + count > T.n) fail(PBX_ERR_VALUE, "range outside the tree");
+    if (!T.has_bh) fail(PBX_ERR_VALUE, "mass payload not built; call build_mass() first");
+    if (nbins < 1 || nbins > RM_MAXB) fail(PBX_ERR_VALUE, "nbins must be in [1, %d]", RM_MAXB);
+    for (int64_t k = 0; k < nbins; ++k)
+      if (!(h_edges[k] <= h_edges[k + 1]))
+        fail(PBX_ERR_VALUE, "bin edges must be increasing");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    hipStream_t st = dev.stream;
+    ScopedTimer tm("octree.radial_moments");
+    const int nb = (int)nbins;
+    const int rows = (int)std::max<int64_t>(1, std::min<int64_t>(512, (count + RM_CHUNK - 1) / RM_CHUNK));
+    const size_t eb = sizeof(double) * (size_t)(nb + 1);
+    const size_t sb = sizeof(double) * 7 * (size_t)nb * rows, cb = sizeof(uint32_t) * (size_t)nb * rows;
+    const size_t ob = sizeof(double) * 8 * (size_t)nb;
+    char *w = (char *)dev.slot(kSlotProf7).ensure(eb + sb + cb + ob + 64);
+    double *de = (double *)w;
+    double *slab = (double *)(w + ((eb + 15) & ~(size_t)15));
+    uint32_t *cslab = (uint32_t *)((char *)slab + sb);
+    double *out = (double *)(((uintptr_t)((char *)cslab + cb) + 15) & ~(uintptr_t)15);
+    prim::HostBuf &hb = T.rm_pin;
+    double *hp = (double *)hb.get(ob);
+    PBX_HIP(hipMemcpyAsync(de, h_edges, eb, hipMemcpyHostToDevice, st));
+    const size_t lds = eb + sizeof(double) * 7 * nb + sizeof(uint32_t) * nb;
+    hipLaunchKernelGGL(radial_moments_kernel, dim3(rows), dim3(TPB), lds, st, T.rec.as<double4>(),
+                       d_f, first, count, (const double *)de, nb, slab, cslab);
+    hipLaunchKernelGGL(radial_moments_reduce, dim3(nblk(8 * (int64_t)nb)), dim3(TPB), 0, st,
+                       (const double *)slab, (const uint32_t *)cslab, rows, nb, out);
+    PBX_HIP(hipGetLastError());
+    PBX_HIP(hipMemcpyAsync(hp, out, ob, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    std::memcpy(h_counts, hp, sizeof(int64_t) * nb);
+    std::memcpy(h_moments, hp + nb, sizeof(double) * 7 * nb);
   });
 }
 

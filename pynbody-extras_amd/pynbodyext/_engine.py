@@ -293,6 +293,19 @@ class Octree:
         nat.call("pbx_octree_leaf_particles", self._h, int(first), int(count), d_pos, d_mass,
                  d_idx)
 
+    def _radial_moments_device(self, first, count, d_f, edges):
+        """(counts (nbins,) int64, moments (nbins, 7)) of the 3-D radial
+        profile of a leaf-order field over the targets [first, first + count)
+        (pbx_octree_radial_moments: the pbx_profile_moments columns with the
+        mass as weight)."""
+        edges = np.ascontiguousarray(edges, dtype=np.float64)
+        nb = len(edges) - 1
+        counts = np.zeros(nb, dtype=np.int64)
+        mom = np.zeros((nb, 7))
+        nat.call("pbx_octree_radial_moments", self._h, int(first), int(count), d_f,
+                 nat.dptr(edges), nb, counts.ctypes.data_as(nat._i64p), nat.dptr(mom))
+        return counts, mom
+
     def _cost_to_orig_device(self, d_cost_leaf, d_cost_orig) -> None:
         """Per-target costs in this build's leaf order -> original order."""
         nat.call("pbx_octree_cost_to_orig", self._h, d_cost_leaf, d_cost_orig)

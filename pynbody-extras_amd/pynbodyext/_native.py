@@ -96,6 +96,8 @@ _SIGNATURES: dict[str, tuple] = {
                                          c_void_p, c_void_p, c_void_p]),
     "pbx_octree_leaf_particles": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                           c_void_p]),
+    "pbx_octree_radial_moments": (c_int, [c_void_p, c_int64, c_int64, c_void_p, _dp, c_int64,
+                                          _i64p, _dp]),
     "pbx_octree_cost_to_orig": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pbx_octree_balance": (c_int, [c_void_p, c_void_p, c_int, _i64p]),
     "pbx_octree_info": (c_int, [c_void_p, _i64p]),

@@ -301,8 +301,6 @@ class ShardedTree:
         cap = self.n  # worst-case shard
         self.d_pot = nat.DeviceArray(8 * max(cap, 1))
         self.d_acc = nat.DeviceArray(24 * max(cap, 1))
-        self.d_spos = nat.DeviceArray(24 * max(cap, 1))
-        self.d_smass = nat.DeviceArray(8 * max(cap, 1))
         self.d_cost = nat.DeviceArray(4 * max(cap, 1))       # leaf order, last walk
         self.d_cost_orig = nat.DeviceArray(4 * max(cap, 1))  # original order, carried
         self.have_costs = False
@@ -352,20 +350,24 @@ class ShardedTree:
         self.have_costs = True
 
     def profile(self, dev_bins, edges) -> np.ndarray:
-        """Per-bin moments (nbins, 7) of this rank's targets, summed over ranks."""
-        from .profiles._device import SRC_W, DeviceBins
-
+        """Per-bin moments (nbins, 7) of this rank's targets, summed over ranks
+        (RadialProfile ndim=3 of the potential with the mass as weight: the
+        pbx_profile_moments columns, f = potential).  One fused device pass
+        over the leaf-ordered records and this rank's potentials
+        (pbx_octree_radial_moments); the summed bin counts are left in
+        ``dev_bins.counts`` when a DeviceBins is given."""
         first, count = self.ranges[self.rank] if self.ranges else (0, self.n)
-        self.tree._leaf_particles_device(first, count, self.d_spos.ptr, self.d_smass.ptr, None)
-        DeviceBins.select(self.d_spos.ptr, self.d_smass.ptr, ndim=3, on_device=True, n=count,
-                          into=dev_bins)
-        dev_bins.assign(edges)
-        mom = dev_bins.moments(self.d_pot, SRC_W)
+        counts, mom = self.tree._radial_moments_device(first, count, self.d_pot.ptr, edges)
         if self.comm is not None and self.world > 1:
-            buf = nat.DeviceArray.from_host(np.ascontiguousarray(mom))
-            self.comm.allreduce_sum_f64(buf.ptr, buf.ptr, mom.size)
-            buf.download(mom)
+            buf = nat.DeviceArray.from_host(np.concatenate([mom.ravel(), counts.astype(np.float64)]))
+            self.comm.allreduce_sum_f64(buf.ptr, buf.ptr, mom.size + counts.size)
+            flat = buf.download(np.empty(mom.size + counts.size))
             buf.free()
+            mom = flat[:mom.size].reshape(mom.shape)
+            counts = np.rint(flat[mom.size:]).astype(np.int64)
+        if dev_bins is not None:
+            dev_bins.counts = counts
+            dev_bins.nbins = len(counts)
         return mom
 
     def step(self, dev_bins, edges, want: int = nat.WANT_POT | nat.WANT_ACC) -> np.ndarray:
@@ -378,7 +380,7 @@ class ShardedTree:
         if self.tree is not None:
             self.tree.close()
             self.tree = None
-        for a in (self.d_pot, self.d_acc, self.d_spos, self.d_smass, self.d_cost, self.d_cost_orig):
+        for a in (self.d_pot, self.d_acc, self.d_cost, self.d_cost_orig):
             a.free()
 
 

@@ -588,3 +588,47 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
             a.close()
     finally:
         b.close()
+
+
+def test_radial_equaln_one_launch_reused_handle_and_size_boundary(gpu):
+    """The one-launch path (radial_mono: one persistent block per selection
+    tile, grid barriers whose counters carry over from call to call) on ONE
+    handle over changing grid sizes, including the largest selection it takes
+    (256 tiles = 1,048,576 particles) and the first it leaves to the
+    multi-kernel path (257 tiles): every call equals the stepwise
+    select + binned_equaln (edges, counts, CSR bit-identical, sums to
+    rounding), and a repeated call on unchanged input gives the same edges
+    and counts."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(33)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    sizes = [400_000, 100_000, 400_000, 1_048_576, 1_048_577, 5_000, 1_048_576]
+    data = {}
+    h = DeviceBins()
+    try:
+        for rep, n in enumerate(sizes):
+            if n not in data:
+                data[n] = (rng.normal(scale=2.0, size=(n, 3)), rng.uniform(0.5, 1.5, n))
+            pos, mass = data[n]
+            nb = 128 if rep % 2 == 0 else 100
+            _, e1, c1, m1 = DeviceBins.radial_equaln(pos, mass, nbins=nb, stats=stats, into=h)
+            b = DeviceBins.select(pos, mass, ndim=3)
+            try:
+                e2, c2, m2 = b.binned_equaln(nb, None, None, stats)
+                assert np.array_equal(e1, e2), (n, rep)
+                assert np.array_equal(c1, c2), (n, rep)
+                for got, ref in zip(m1, m2):
+                    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-300)
+                p1, o1 = h.csr()
+                p2, o2 = b.csr()
+                assert np.array_equal(p1, p2) and np.array_equal(o1, o2), (n, rep)
+                # the same call again on the same handle: identical results
+                _, e3, c3, m3 = DeviceBins.radial_equaln(pos, mass, nbins=nb, stats=stats, into=h)
+                assert np.array_equal(e3, e1) and np.array_equal(c3, c1)
+                for u, v in zip(m3, m1):  # LDS float atomics: order-dependent last bits
+                    np.testing.assert_allclose(u, v, rtol=1e-13, atol=1e-300)
+            finally:
+                b.close()
+    finally:
+        h.close()

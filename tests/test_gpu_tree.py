@@ -346,6 +346,7 @@ def test_range_walk_shards_equal_full(gpu):
     full.assign(edges)
     mom_full = full.moments(pot_full, SRC_W)
     mom_sum = np.zeros_like(mom_full)
+    mom_fused = np.zeros_like(mom_full)
     d_spos, d_smass = nat.DeviceArray(24 * n), nat.DeviceArray(8 * n)
     for first, count in balanced_ranges(cost, 3):
         dev._compute_range_device(0.5, nat.WANT_POT | nat.WANT_ACC, first, count, 1, d_pot.ptr,
@@ -358,10 +359,20 @@ def test_range_walk_shards_equal_full(gpu):
         assert np.array_equal(p, pot_full[ids]) and np.array_equal(a, acc_full[ids])
         dev._leaf_particles_device(first, count, d_spos.ptr, d_smass.ptr, None)
         part = DeviceBins.select(d_spos.ptr, d_smass.ptr, ndim=3, on_device=True, n=count)
-        part.assign(edges)
-        mom_sum += part.moments(d_pot, SRC_W)
+        counts_part = part.assign(edges)
+        mom_part = part.moments(d_pot, SRC_W)
+        mom_sum += mom_part
+        # the fused pass over the tree's records (pbx_octree_radial_moments)
+        # = select + assign + moments of the same leaf-order range
+        c_f, m_f = dev._radial_moments_device(first, count, d_pot.ptr, edges)
+        assert np.array_equal(c_f, counts_part)
+        np.testing.assert_allclose(m_f, mom_part, rtol=1e-12, atol=1e-300)
+        mom_fused += m_f
     np.testing.assert_array_equal(mom_sum[:, 0] > 0, mom_full[:, 0] > 0)
     np.testing.assert_allclose(mom_sum, mom_full, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(mom_fused, mom_full, rtol=1e-12, atol=1e-300)
+    with pytest.raises(ValueError, match="increasing"):
+        dev._radial_moments_device(0, n, d_pot.ptr, edges[::-1])
     with pytest.raises(ValueError, match="outside"):
         dev._compute_range_device(0.5, nat.WANT_POT, n - 5, 10, 1, d_pot.ptr, None, None)
 
