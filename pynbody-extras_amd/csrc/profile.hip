@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(BT)
                    SelectParams p, uint64_t *__restrict__ status, uint32_t *__restrict__ ctrl,
                    double *__restrict__ xo, double *__restrict__ wo, int32_t *__restrict__ io,
                    unsigned long long *__restrict__ minmax, uint64_t *__restrict__ kw,
-                   uint32_t *__restrict__ toff) {
+                   uint32_t *__restrict__ toff, uint16_t *__restrict__ kpre) {
   constexpr int NW = BT / 64, SI = TILE / BT;  // waves, items per lane
   __shared__ uint32_t wcnt[NW];
   __shared__ unsigned long long wmin[NW], wmax[NW];
@@ -247,7 +247,10 @@ __global__ void __launch_bounds__(BT)
   for (int k = 0; k < SI; ++k) {
     bool keep = (keepbits >> k) & 1u;
     uint64_t b = __ballot(keep);
-    if (LAZY && lane == 0) kw[(int64_t)tile * (TILE / 64) + w * SI + k] = b;
+    if (LAZY && lane == 0) {  // keep word + its in-tile prefix (kept particles before it)
+      kw[(int64_t)tile * (TILE / 64) + w * SI + k] = b;
+      kpre[(int64_t)tile * (TILE / 64) + w * SI + k] = (uint16_t)(run - s_excl);
+    }
 #ifdef PBX_DIAG_SEL_NOWRITE  // timing diagnostic only: r not written
     if (keep && xv[k] == -1.0) {
 #else
@@ -753,6 +756,8 @@ struct FusedSetup {
   int empty_bounds;
   int tiled;  // tiled selection: x of tile t at x[t * TILE ..], its count in stat[t]
   uint32_t *toff;  // tiled: the tile offsets block 0 writes
+  uint32_t *zero;  // words block 0 zeroes for later kernels (fused_boff's per-block counts)
+  int nzero;
 };
 
 // Element range of fused_hist0 / fused_gather: the kept x [0, n), or with
@@ -818,16 +823,65 @@ __device__ FusedCtl fused_ctl(const FusedSetup &f) {
 // every key slot of this block (grid-stride by EL_STEP): f(x value, valid).
 // (Issuing the next step's loads before this step's keys are processed made
 // fused_gather slower at 64M, 71 -> 91 us: kept single-step.)
-// With a tiled selection block 0 runs the tile scan instead (fused_hist0),
-// so the slots are spread over blocks 1.. (the same in fused_gather).
+// With a tiled selection block 0 runs the tile scan instead (fused_hist0)
+// and blocks 1.. each take a contiguous range of tiles (tile_range), two
+// per step: assign_gather walks the same ranges, so a block's gathered keys
+// are exactly those it counted here.
+__device__ __forceinline__ void tile_range(uint32_t nt, uint32_t &ta, uint32_t &tb) {
+  const uint32_t b0 = gridDim.x > 1 ? 1u : 0u;
+  if (blockIdx.x < b0) {
+    ta = tb = 0;
+    return;
+  }
+  const uint64_t G = gridDim.x - b0, b = blockIdx.x - b0;
+  ta = (uint32_t)((uint64_t)nt * b / G);
+  tb = (uint32_t)((uint64_t)nt * (b + 1) / G);
+}
+
 template <class F>
 __device__ __forceinline__ void el_for_each(const double *__restrict__ x, const ElRange &er,
                                             int64_t lim, F &&f) {
   constexpr int U = EL_U;
-  const int b0 = (er.stat && gridDim.x > 1) ? 1 : 0;
-  if ((int)blockIdx.x < b0) return;
-  for (int64_t i0 = (int64_t)(blockIdx.x - b0) * EL_STEP; i0 < lim;
-       i0 += (int64_t)(gridDim.x - b0) * EL_STEP) {
+  if (er.stat) {
+    uint32_t ta, tb;
+    tile_range(er.nt, ta, tb);
+    if (lim == 0 || ta >= tb) return;
+    // unconditional 16-B loads (a lone last tile re-reads itself for its
+    // missing partner: no branch around a load), the next step's in flight
+    // while this one is processed (ping-pong, no register copies)
+    auto ld = [&](uint32_t t, double *v) {
+      const int64_t i0 = (int64_t)t * TILE;
+      const int64_t end = (int64_t)(t + 1 < tb ? t + 2 : t + 1) * TILE;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + 2 * (u * MS0_TPB + threadIdx.x);
+        const double2 q = *(const double2 *)(x + (i < end ? i : i - TILE));
+        v[2 * u] = q.x;
+        v[2 * u + 1] = q.y;
+      }
+    };
+    auto use = [&](uint32_t t, const double *v) {
+      const int64_t i0 = (int64_t)t * TILE;
+      const uint32_t c0 = er.count(t);
+      const uint32_t c1 = t + 1 < tb ? er.count(t + 1) : 0u;
+#pragma unroll
+      for (int u = 0; u < 2 * U; ++u) {
+        const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
+        f(v[u], el_valid(er, i0, i, c0, c1));
+      }
+    };
+    double va[2 * U], vb[2 * U];
+    ld(ta, va);
+    for (uint32_t t = ta; t < tb; t += 4) {
+      if (t + 2 < tb) ld(t + 2, vb);
+      use(t, va);
+      if (t + 2 >= tb) break;
+      if (t + 4 < tb) ld(t + 4, va);
+      use(t + 2, vb);
+    }
+    return;
+  }
+  for (int64_t i0 = (int64_t)blockIdx.x * EL_STEP; i0 < lim; i0 += (int64_t)gridDim.x * EL_STEP) {
     double v[2 * U];
 #pragma unroll
     for (int u = 0; u < U; ++u) load_pair(x, i0 + 2 * (u * MS0_TPB + threadIdx.x), lim, v + 2 * u);
@@ -865,6 +919,7 @@ __global__ void __launch_bounds__(MS0_TPB)
     }
     for (int k = threadIdx.x; k <= nb; k += MS0_TPB) counts[k] = 0;  // for assign_bins
     for (int k = threadIdx.x; k < MS0_DIG; k += MS0_TPB) H[k] = 0;   // for msel_reduce0
+    for (int k = threadIdx.x; k < fsu.nzero; k += MS0_TPB) fsu.zero[k] = 0;
   }
   __syncthreads();
   const uint64_t ka = fsu.ka, kb = fsu.kb;
@@ -1005,7 +1060,7 @@ __global__ void __launch_bounds__(FR_TPB)
 __global__ void __launch_bounds__(TPB)
     fused_boff(const uint32_t *__restrict__ rows, int g0, const FusedCtl *__restrict__ ctl,
                const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ goff,
-               uint32_t *__restrict__ boff) {
+               uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt) {
   __shared__ uint32_t wsum[NWAVE];
   const int g = blockIdx.x;
   if ((ctl->err & 2) || g >= ctl->ng) return;
@@ -1013,6 +1068,7 @@ __global__ void __launch_bounds__(TPB)
   const uint32_t c = b < g0 ? rows[(int64_t)b * MS0_DIG + gdig[g]] : 0u;
   const uint32_t ex = block_excl_scan(c, wsum, nullptr);
   if (b < g0) boff[(int64_t)b * MS_MAXQ + g] = goff[g] + ex;
+  if (bcnt && b < g0 && c) atomicAdd(&bcnt[b], c);  // keys block b gathers, all groups
 }
 
 // keys of the chosen level-0 buckets -> their group's segment (key - base).
@@ -1049,6 +1105,31 @@ __global__ void __launch_bounds__(MS0_TPB)
       if (g != 0xffffu) seg[atomicAdd(&slot[g], 1u)] = off;
     }
   });
+}
+
+// Per-bin sums fused into the assignment pass (the one-sync equaln path):
+// the distinct per-element values ("monomials") the requested statistics'
+// columns sum — e.g. Sum of the mass and the weights column of a
+// mass-weighted Mean are the same Σw, accumulated once.  Monomial q is
+// column col[q] of pbx_profile_moments_cols for field f[q] (0 = x, 1 =
+// weights) and weights w[q] (0 = x, 1 = weights, -1 = none); block sums in
+// LDS, one slab row (nm x nb) per block.
+constexpr int AS_MAXM = 8;
+struct FusedStats {
+  int nm;
+  int f[AS_MAXM];
+  int w[AS_MAXM];
+  int col[AS_MAXM];
+};
+
+// monomial value of column `col` (the expression moments_kernel sums):
+// a(f) in {1, f, f*f, |f|} times b in {1, ww}; x*1.0 is exact, so this is
+// bit-identical to the per-column expressions
+__device__ __forceinline__ double monomial(int col, double f, double ww) {
+  const int am = (col == 0) ? 0 : (col == 1 || col == 3) ? 1 : (col == 2 || col == 4) ? 2 : 3;
+  const bool wb = (col == 0 || col == 1 || col == 2 || col == 5);
+  const double a = am == 0 ? 1.0 : am == 1 ? f : am == 2 ? f * f : __builtin_fabs(f);
+  return wb ? a * ww : a;
 }
 
 // One block (FR_TPB threads) per group: for each of its ranks, an MSD radix
@@ -1157,8 +1238,9 @@ __global__ void __launch_bounds__(FR_TPB)
 // the step's results in one contiguous staging block (one D2H copy):
 // [ctl][edges nq][counts nb][monomial sums nm x nb].  Blocks [0, nhead)
 // copy the head; block nhead + j sums column j of the assign slab (`rows`
-// block rows, fixed order: thread t takes rows t, t + TPB, ... in turn,
-// then a fixed LDS tree) — the slab reduction and the packing in one launch.
+// block rows, then the rows2 rows of slab2, fixed order: thread
+// t takes rows t, t + TPB, ... in turn, then a fixed LDS tree) — the slab
+// reduction and the packing in one launch.
 // offs (optional): the CSR pass's scanned [bin][tile] histogram (ntiles
 // columns); the bin counts are then its row-start differences, and are
 // also stored to `counts` (assign_bins skipped its global count atomics).
@@ -1167,13 +1249,14 @@ __global__ void __launch_bounds__(TPB)
     fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges, int nq,
                unsigned long long *__restrict__ counts, int nb, const double *__restrict__ slab,
                int64_t rows, int nsum, double *__restrict__ out, const uint32_t *__restrict__ offs,
-               uint32_t ntiles, int nhead) {
+               uint32_t ntiles, int nhead, const double *__restrict__ slab2, int64_t rows2) {
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
   if ((int)blockIdx.x >= nhead) {
     __shared__ double red[TPB];
     const int j = (int)blockIdx.x - nhead;
     double v = 0.0;
     for (int64_t r = threadIdx.x; r < rows; r += TPB) v += slab[r * nsum + j];
+    for (int64_t r = threadIdx.x; r < rows2; r += TPB) v += slab2[r * nsum + j];  // fix_deferred
     red[threadIdx.x] = v;
     __syncthreads();
 #pragma unroll
@@ -1212,31 +1295,6 @@ __global__ void __launch_bounds__(TPB)
 // words); else tile_hist is null.  Block totals go to `counts` with one
 // contiguous atomic per bin.
 constexpr int AS_TILES = 8;
-
-// Per-bin sums fused into the assignment pass (the one-sync equaln path):
-// the distinct per-element values ("monomials") the requested statistics'
-// columns sum — e.g. Sum of the mass and the weights column of a
-// mass-weighted Mean are the same Σw, accumulated once.  Monomial q is
-// column col[q] of pbx_profile_moments_cols for field f[q] (0 = x, 1 =
-// weights) and weights w[q] (0 = x, 1 = weights, -1 = none); block sums in
-// LDS, one slab row (nm x nb) per block.
-constexpr int AS_MAXM = 8;
-struct FusedStats {
-  int nm;
-  int f[AS_MAXM];
-  int w[AS_MAXM];
-  int col[AS_MAXM];
-};
-
-// monomial value of column `col` (the expression moments_kernel sums):
-// a(f) in {1, f, f*f, |f|} times b in {1, ww}; x*1.0 is exact, so this is
-// bit-identical to the per-column expressions
-__device__ __forceinline__ double monomial(int col, double f, double ww) {
-  const int am = (col == 0) ? 0 : (col == 1 || col == 3) ? 1 : (col == 2 || col == 4) ? 2 : 3;
-  const bool wb = (col == 0 || col == 1 || col == 2 || col == 5);
-  const double a = am == 0 ? 1.0 : am == 1 ? f : am == 2 ? f * f : __builtin_fabs(f);
-  return wb ? a * ww : a;
-}
 
 // LDSE: the edges sit in LDS (nb + 1 <= LDS_EDGES); else they are read from
 // global memory (L2-resident).  Loads of tile t+1 (x and weights) are in
@@ -1449,8 +1507,9 @@ __global__ void __launch_bounds__(BT)
         const bool kp = (wj >> lane) & 1ull;
         keep |= (uint32_t)kp << kk;
         pos[kk] = pj + rank_below(wj);
-        v[kk] = kp ? xt[pos[kk]] : 0.0;
-        wv[kk] = (kp && wneed) ? mass[pbase + 64 * j] : 1.0;
+        v[kk] = xt[kp ? pos[kk] : toff[t]];  // unconditional loads (see assign_gather)
+        const double mv = (wneed ? mass : xt)[(kp && wneed) ? pbase + 64 * j : (wneed ? base : toff[t])];
+        wv[kk] = wneed ? mv : 1.0;
       }
     };
     load(c0, nv, nw, npos, nkeep);
@@ -1512,39 +1571,334 @@ __global__ void __launch_bounds__(BT)
     for (uint32_t t = t0; t < t1; ++t) tile_hist[(int64_t)d * ntiles + t] = th[t - t0][d];
 }
 
+// ------------------------------ assignment fused with the level-0 gather
+// Tiled (large) selections: after the level-0 resolve ONE more read of x
+// both gathers the keys of the chosen level-0 buckets (fused_gather's job)
+// and assigns every other kept particle.  The edges' level-0 digits are
+// known (R[q].prefix, non-decreasing in q), so a key whose digit holds no
+// edge lies strictly between the edges of smaller and of larger digits: its
+// bin is #{q : digit_q < digit} - 1 (bins.py:368-379, searchsorted - 1;
+// neither extremum can equal it; < 0 or >= nb -> invalid), a per-digit
+// table (lut).  A key in a digit that does hold edges (a group's) goes to
+// the group's segment (for fused_finish) and, with its weight and position,
+// to this block's list of deferred keys (fix_deferred bins them once the
+// edges are known, block by block, so its writes stay inside the block's
+// own tiles).  NaN is invalid either way.  Blocks walk fused_hist0's tile
+// ranges (tile_range), so block b fills exactly the segment slots fused_boff
+// gave it, and its list lies at the exclusive sum of the earlier blocks'
+// gathered counts (bcnt).  Bins are bytes (nb < 256; invalid = nb).
+// Per-tile counts for the CSR pass ([bin][tile], nb + 1 rows) stay in LDS
+// for up to AG_TR tiles and leave as contiguous row pieces; per-bin sums:
+// one slab row per block.
+constexpr int AG_TR = 64;
+#ifndef PBX_AG_W
+#define PBX_AG_W 4
+#endif
+constexpr int AG_W = PBX_AG_W;                // keep words of a tile per wave
+constexpr int AG_TPS = AG_W * (MS0_TPB / 64) / 64;  // tiles per step (the block's waves)
+struct AgRec {  // a deferred key: key - window base, weight, compacted position, tile
+  uint64_t off;
+  double w;
+  uint32_t pos, t;
+};
+struct GatherOut {
+  uint64_t *seg;          // key - window base, by segment slot
+  AgRec *rec;             // deferred keys, block by block
+  const uint32_t *bcnt;   // per block: keys gathered (fused_boff)
+  uint32_t *rbase, *rn;   // per block: list start, deferred keys written
+};
+
+// exclusive sum of v[0 .. k) over a block (k <= blockDim.x)
+__device__ __forceinline__ uint32_t block_prefix(const uint32_t *__restrict__ v, int k,
+                                                 uint32_t *red) {
+  uint32_t x = (int)threadIdx.x < k ? v[threadIdx.x] : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+  return t;
+}
+
+template <bool MOM>
+__global__ void __launch_bounds__(MS0_TPB)
+    assign_gather(const double *__restrict__ x, const uint64_t *__restrict__ kw,
+                  const uint16_t *__restrict__ kpre, const uint32_t *__restrict__ toff,
+                  int64_t base, uint32_t nt,
+                  const double *__restrict__ mass, const FusedCtl *__restrict__ ctl, uint64_t ka,
+                  uint64_t kb, const MsRank *__restrict__ R, int nq,
+                  const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ boff, int nb,
+                  uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
+                  double *__restrict__ slab, GatherOut go) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint16_t gidx[MS0_DIG];
+  __shared__ uint8_t lut[MS0_DIG];
+  __shared__ uint32_t sslot[RADIX];
+  __shared__ uint32_t qd[RADIX];
+  __shared__ uint32_t red[MS0_TPB / 64];
+  __shared__ uint32_t dk;
+  const int macc = MOM ? fs.nm * nb : 0;
+  double *acc = (double *)smem;
+  const int nr = nb + 1, nrs = nr | 1;  // th row stride odd: flush reads bank-conflict free
+  uint32_t *th = (uint32_t *)(acc + macc);  // [tile][bin]: a wave's atomics hit distinct banks
+  const int tid = threadIdx.x;
+  const bool win = !(ctl->err & 2);
+  const int ng = win ? ctl->ng : 0;
+  const uint64_t lo = ctl->lo;
+  const int s = ctl->s0;
+  const uint32_t rb = block_prefix(go.bcnt, (int)blockIdx.x, red);
+  for (int k = tid; k < MS0_DIG / 2; k += MS0_TPB) ((uint32_t *)gidx)[k] = ~0u;
+  for (int q = tid; q < nq; q += MS0_TPB) qd[q] = (uint32_t)R[q].prefix;
+  for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
+  for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
+  if (tid == 0) dk = 0;
+  __syncthreads();
+  for (int g = tid; g < ng; g += MS0_TPB) {
+    gidx[gdig[g]] = (uint16_t)g;
+    sslot[g] = boff[(int64_t)blockIdx.x * MS_MAXQ + g];
+  }
+  for (int d = tid; d < MS0_DIG; d += MS0_TPB) {  // #{q : digit_q < d}, lower bound
+    int a = 0, len = nq;
+    while (len > 0) {
+      const int h = len >> 1;
+      if (qd[a + h] < (uint32_t)d) {
+        a += h + 1;
+        len -= h + 1;
+      } else {
+        len = h;
+      }
+    }
+    const int b = a - 1;
+    lut[d] = (uint8_t)((b < 0 || b >= nb) ? nb : b);
+  }
+  __syncthreads();
+  uint32_t ta, tb;
+  tile_range(nt, ta, tb);
+  // wave w: words [AG_W wl, AG_W (wl + 1)) of tiles r0 + sub, r0 + sub + AG_TPS, ...
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wl = w % (64 / AG_W), sub = w / (64 / AG_W);
+  const uint32_t lane = lane_id();
+  const bool wneed = mass != nullptr;
+  // one tile's share of a wave: loads issued (issue) one tile before they
+  // are binned (bin), ping-pong buffers so no register copy waits on them
+  struct Part {
+    double v[AG_W], m[AG_W];
+    uint32_t pos[AG_W];
+    uint32_t keep;
+  };
+  // a wave's AG_W keep words of tile t and their in-tile prefixes come in as
+  // scalar loads (lgkmcnt): the vector-load queue (vmcnt, in order) holds
+  // only x / mass, so tile t + 1's stay in flight while tile t is binned
+  auto issue = [&](uint32_t t, Part &P) {
+    const int64_t j0 = (int64_t)t * 64 + wl * AG_W;
+    const uint32_t to = toff[t];
+    const double *xt = x + ((int64_t)t * TILE - (int64_t)to);  // x of tile t by position
+    const int64_t pb = base + (int64_t)t * TILE + lane;
+    // every load unconditional (a lane without a particle reads the tile's
+    // first slot / the span's first mass): no branch around a load
+    const double *mp = wneed ? mass : xt + to;
+    P.keep = 0;
+#pragma unroll
+    for (int kk = 0; kk < AG_W; ++kk) {
+      const int j = wl * AG_W + kk;
+      const uint64_t wj = kw[j0 + kk];
+      const uint32_t pj = to + kpre[j0 + kk];
+      const bool kp = (wj >> lane) & 1ull;
+      P.keep |= (uint32_t)kp << kk;
+      P.pos[kk] = pj + rank_below(wj);
+      P.v[kk] = xt[kp ? P.pos[kk] : to];
+      const double mv = mp[(kp && wneed) ? pb + 64 * j : (wneed ? base : 0)];
+      P.m[kk] = wneed ? mv : 1.0;
+    }
+  };
+  auto bin = [&](uint32_t t, uint32_t tl, const Part &P) {
+#pragma unroll
+    for (int kk = 0; kk < AG_W; ++kk) {
+      if (!((P.keep >> kk) & 1u)) continue;
+      const double xv = P.v[kk];
+      const uint64_t key = dkey(xv);
+      uint32_t b = (uint32_t)nb;
+      bool defer = false;
+      if (win && key >= ka && key <= kb) {  // fused_hist0's window
+        const uint32_t d = (uint32_t)((key - lo) >> s);
+#ifdef PBX_DIAG_AG_NOLDS
+        const uint32_t g = (d & 0xff) == 0x77 ? (d >> 8) & 127 : 0xffffu;
+#else
+        const uint32_t g = gidx[d];
+#endif
+        if (g != 0xffffu) {
+          go.seg[atomicAdd(&sslot[g], 1u)] = key - lo;
+          defer = xv == xv;
+          if (defer) go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{key - lo, P.m[kk], P.pos[kk], t};
+        } else if (xv == xv) {
+#ifdef PBX_DIAG_AG_NOLDS
+          b = d & 127;
+#else
+          b = lut[d];
+#endif
+        }
+      }
+      if (defer) continue;
+      bins[P.pos[kk]] = (uint8_t)b;
+      atomicAdd(&th[tl * nrs + b], 1u);
+      if (MOM && b < (uint32_t)nb)
+        for (int q = 0; q < fs.nm; ++q) {  // uniform
+          const double f = fs.f[q] == 0 ? xv : P.m[kk];
+          const double ww = fs.w[q] == 0 ? xv : P.m[kk];
+          atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
+        }
+    }
+  };
+  for (uint32_t r0 = ta; r0 < tb; r0 += AG_TR) {
+    const uint32_t r1 = min(tb, r0 + (uint32_t)AG_TR);
+    Part A, B;
+    constexpr uint32_t S1 = AG_TPS;
+    const uint32_t t0 = r0 + sub;
+    if (t0 < r1) issue(t0, A);
+    for (uint32_t t = t0; t < r1; t += 2 * S1) {
+      // the next tile's loads go out before this one is binned
+      if (t + S1 < r1) issue(t + S1, B);
+      bin(t, t - r0, A);
+      if (t + S1 >= r1) break;
+      if (t + 2 * S1 < r1) issue(t + 2 * S1, A);
+      bin(t + S1, t + S1 - r0, B);
+    }
+    __syncthreads();
+    const int nrt = (int)(r1 - r0);
+    for (int k = tid; k < nr * AG_TR; k += MS0_TPB) {
+      const int b = k / AG_TR, tl = k - b * AG_TR;
+      if (tl < nrt) tile_hist[(int64_t)b * nt + r0 + tl] = th[tl * nrs + b];
+    }
+    __syncthreads();
+    for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    go.rbase[blockIdx.x] = rb;
+    go.rn[blockIdx.x] = dk;
+  }
+  if (MOM) {
+    double *dst = slab + (int64_t)blockIdx.x * macc;
+    for (int k = tid; k < macc; k += MS0_TPB) dst[k] = acc[k];
+  }
+}
+
+// The deferred keys' bins once fused_finish has the edges (the ~1-3 % of
+// the kept particles whose level-0 digit holds an edge): block b takes
+// assign_gather block b's list, so its byte stores and [bin][tile] count
+// atomics stay inside that block's tiles; bin_of over the edges in LDS.
+// (A block's list mixes all groups, so a wave's keys spread over many bins:
+// plain LDS atomics; a per-distinct-bin wave reduction — dependent
+// ds_bpermute chains — took 316 us at 64M.)
+constexpr int FD_U = 4;          // keys per thread in flight
+constexpr int FD_LDSW = 16384;   // LDS words for the block's [tile][bin] counts
+template <bool MOM>
+__global__ void __launch_bounds__(MS0_TPB)
+    fix_deferred(const FusedCtl *__restrict__ ctl, const AgRec *__restrict__ rec,
+                 const uint32_t *__restrict__ rbase, const uint32_t *__restrict__ rn,
+                 const double *__restrict__ edges, int nb, uint8_t *__restrict__ bins,
+                 uint32_t *__restrict__ tile_hist, uint32_t nt, FusedStats fs,
+                 double *__restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int macc = MOM ? fs.nm * nb : 0;
+  double *acc = (double *)smem;
+  double *e = acc + macc;
+  // this block's tiles' counts [tile][bin] in LDS when they fit: global
+  // atomics execute at the memory side, one request per scattered lane
+  uint32_t *tc = (uint32_t *)(e + nb + 1);
+  const int tid = threadIdx.x;
+  const int nrs = (nb + 1) | 1;
+  uint32_t ta, tb;
+  tile_range(nt, ta, tb);
+  const bool in_lds = (int64_t)(tb - ta) * nrs <= FD_LDSW;
+  for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
+  for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
+  if (in_lds)
+    for (int k = tid; k < (int)(tb - ta) * nrs; k += MS0_TPB) tc[k] = 0;
+  __syncthreads();
+  const bool ok_all = !(ctl->err & 2);
+  const int64_t r0 = rbase[blockIdx.x], cnt = ok_all ? (int64_t)rn[blockIdx.x] : 0;
+  const uint64_t lo = ctl->lo;
+  for (int64_t i0 = 0; i0 < cnt; i0 += (int64_t)MS0_TPB * FD_U) {
+    AgRec r[FD_U];
+#pragma unroll
+    for (int u = 0; u < FD_U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + tid;
+      r[u] = rec[r0 + (i < cnt ? i : 0)];  // unconditional loads
+    }
+#pragma unroll
+    for (int u = 0; u < FD_U; ++u) {
+      const int64_t i = i0 + u * MS0_TPB + tid;
+      const double v = dkey_inv(lo + r[u].off);
+      const bool ok = i < cnt;  // (no NaN keys: assign_gather binned those)
+      const uint32_t b = ok ? bin_of(v, e, nb) : (uint32_t)nb;
+      if (ok) {
+        bins[r[u].pos] = (uint8_t)b;
+        if (in_lds) atomicAdd(&tc[(r[u].t - ta) * nrs + b], 1u);
+        else atomicAdd(&tile_hist[(int64_t)b * nt + r[u].t], 1u);
+      }
+      if (MOM && ok && b < (uint32_t)nb)
+        for (int q = 0; q < fs.nm; ++q) {
+          const double f = fs.f[q] == 0 ? v : r[u].w;
+          const double ww = fs.w[q] == 0 ? v : r[u].w;
+          atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
+        }
+    }
+  }
+  __syncthreads();
+  if (in_lds)  // the block owns these columns: plain read-modify-write
+    for (int k = tid; k < (int)(tb - ta) * (nb + 1); k += MS0_TPB) {
+      const int b = k / (int)(tb - ta), tl = k - b * (int)(tb - ta);
+      const uint32_t c = tc[tl * nrs + b];
+      if (c) tile_hist[(int64_t)b * nt + ta + tl] += c;
+    }
+  if (MOM) {
+    double *dst = slab + (int64_t)blockIdx.x * macc;
+    for (int k2 = tid; k2 < macc; k2 += MS0_TPB) dst[k2] = acc[k2];
+  }
+}
+
 // Stable CSR scatter over a lazy selection's tiles: radix_scatter's scheme
 // (per-wave peer ranks, tile sorted by bin in LDS, runs written out
 // coalesced) with the elements = the tile's kept particles in particle
 // order, key = bin, value = compacted position.  offs = the exclusive scan
-// of assign_sel's [bin][tile] counts.
+// of assign_sel's [bin][tile] counts (nrows rows: the digits that occur).
+// A tile's kept particles are the contiguous compacted positions
+// [toff[t], toff[t + 1]) in particle order, so the pass walks those
+// positions directly (element e = w * 1024 + k * 64 + lane: (wave,
+// iteration, lane) = position order); the tile's offsets are loaded first,
+// beside the bins.  LDS holds the digit (byte) and the in-tile position
+// (u16) of each element.
+template <typename BT>  // bins: uint32_t, or bytes (assign_gather)
 __global__ void __launch_bounds__(TPB)
-    csr_sel(const uint64_t *__restrict__ kw, const uint32_t *__restrict__ toff,
-            const uint32_t *__restrict__ bins, const uint32_t *__restrict__ offs, uint32_t ntiles,
-            int32_t *__restrict__ perm) {
+    csr_sel(const uint32_t *__restrict__ toff, const int64_t *__restrict__ n_dev,
+            const BT *__restrict__ bins, const uint32_t *__restrict__ offs, uint32_t ntiles,
+            int32_t *__restrict__ perm, uint32_t nrows) {
   __shared__ uint32_t run[NWAVE][RADIX];
   __shared__ uint32_t dstart[RADIX];
   __shared__ uint32_t gofs[RADIX];
   __shared__ uint32_t wsum[NWAVE];
-  __shared__ uint32_t sk[TILE];
-  __shared__ int32_t sv[TILE];
-  __shared__ uint64_t wrd[64];
-  __shared__ uint32_t wpre[64];
+  __shared__ uint8_t sk[TILE];
+  __shared__ uint16_t sv[TILE];
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const uint32_t t = blockIdx.x;
+  const uint32_t o = toff[t];
+  const uint32_t tn = (t + 1 < ntiles ? toff[t + 1] : (uint32_t)*n_dev) - o;
+  const int d0 = threadIdx.x;  // TPB == RADIX
+  const uint32_t go = (uint32_t)d0 < nrows ? offs[(int64_t)d0 * ntiles + t] : 0u;
   for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
-  sel_tile_words(kw, toff, t, wrd, wpre);
-  __syncthreads();
-  uint32_t key[16], pos[16];
+  uint32_t key[16];
   uint64_t okm[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const int j = w * 16 + k;
-    const uint64_t word = wrd[j];
-    okm[k] = word;
-    pos[k] = wpre[j] + rank_below(word);
-    key[k] = ((word >> lane) & 1ull) ? bins[pos[k]] : 0u;
+    const uint32_t e = (uint32_t)(w * 1024 + k * 64) + lane;
+    const bool ok = e < tn;
+    okm[k] = __ballot(ok);
+    key[k] = (uint32_t)bins[o + (ok ? e : 0u)];  // unconditional (o: this tile's or the next's first)
   }
+  __syncthreads();
   uint32_t ret[16], lp[16];
   uint64_t pm[16];
 #pragma unroll
@@ -1563,18 +1917,17 @@ __global__ void __launch_bounds__(TPB)
   }
   __syncthreads();
   {
-    const int d = threadIdx.x;  // TPB == RADIX
     uint32_t tot = 0;
 #pragma unroll
-    for (int ww = 0; ww < NWAVE; ++ww) tot += run[ww][d];
+    for (int ww = 0; ww < NWAVE; ++ww) tot += run[ww][d0];
     const uint32_t st = block_excl_scan(tot, wsum, nullptr);
-    dstart[d] = st;
-    gofs[d] = offs[(int64_t)d * ntiles + t];
+    dstart[d0] = st;
+    gofs[d0] = go;
     uint32_t a = st;
 #pragma unroll
     for (int ww = 0; ww < NWAVE; ++ww) {
-      const uint32_t c = run[ww][d];
-      run[ww][d] = a;
+      const uint32_t c = run[ww][d0];
+      run[ww][d0] = a;
       a += c;
     }
   }
@@ -1584,15 +1937,14 @@ __global__ void __launch_bounds__(TPB)
     if ((okm[k] >> lane) & 1ull) {
       const uint32_t dgt = key[k] & 255u;
       const uint32_t q = run[w][dgt] + lp[k];
-      sk[q] = dgt;
-      sv[q] = (int32_t)pos[k];
+      sk[q] = (uint8_t)dgt;
+      sv[q] = (uint16_t)(w * 1024 + k * 64 + lane);
     }
   }
   __syncthreads();
-  const int tn = (int)(wpre[63] + (uint32_t)__popcll(wrd[63]) - toff[t]);
-  for (int j = threadIdx.x; j < tn; j += TPB) {
+  for (int j = threadIdx.x; j < (int)tn; j += TPB) {
     const uint32_t dgt = sk[j];
-    perm[gofs[dgt] + ((uint32_t)j - dstart[dgt])] = sv[j];
+    perm[gofs[dgt] + ((uint32_t)j - dstart[dgt])] = (int32_t)(o + sv[j]);
   }
 }
 
@@ -2531,9 +2883,10 @@ struct Profile {
   Buf x, w, idx, bins, perm, keys0, keys1, vtmp, hist, tsum, edges, counts, minmax, slab, acc,
       field, weight, ranks, bounds;
   Buf pk0, pk1, pv0, pv1, pbk, pcdf, poff, pq, pout;  // order statistics
-  Buf fctl, fseg, fgrp, fslab, fpack;                // one-sync equaln path
+  Buf fctl, fseg, fgrp, fslab, fpack, frec, fblk, bins8;  // one-sync equaln path
+  bool bins_in8 = false;  // the last assignment's bins are bytes in bins8 (ensure_bins32)
   // lazy selection (select_launch): keep words, tile offsets, staged masses
-  Buf kw, toff, mstage, xc;
+  Buf kw, toff, mstage, xc, kpre;
   bool lazy = false, w_ready = false, idx_ready = false;
   bool x_tiled = false;  // x holds a tiled selection (tile t at x[t * TILE ..]): ensure_x
   int64_t sel_base = 0, sel_span = 0;
@@ -2547,6 +2900,23 @@ struct Profile {
 };
 
 static void ensure_x(Profile &P, hipStream_t st);
+
+__global__ void widen_bins(const uint8_t *__restrict__ b8, int64_t n, uint32_t *__restrict__ b) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
+    b[i] = b8[i];
+}
+
+// bins as uint32 for the consumers that read them (assign_gather leaves bytes)
+static void ensure_bins32(Profile &P, hipStream_t st) {
+  if (!P.bins_in8) return;
+  if (P.n > 0) {
+    uint32_t *b = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)P.n);
+    const unsigned grid = (unsigned)std::min<int64_t>(4096, (P.n + TPB - 1) / TPB);
+    hipLaunchKernelGGL(widen_bins, dim3(grid), dim3(TPB), 0, st, (const uint8_t *)P.bins8.p, P.n, b);
+    PBX_HIP(hipGetLastError());
+  }
+  P.bins_in8 = false;
+}
 
 // exclusive scan of len u32 in place
 static void scan_u32(Profile &P, hipStream_t st, uint32_t *a, int64_t len) {
@@ -2753,6 +3123,7 @@ static void assign_device(Profile &P, hipStream_t st, const double *de, int64_t 
   PBX_HIP(hipMemsetAsync(cnt, 0, sizeof(uint64_t) * (nb + 1), st));
   uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n ? n : 1));
   P.csrh_ready = false;
+  P.bins_in8 = false;
   if (n) {
     size_t lds = ((nb + 1) <= LDS_EDGES ? sizeof(double) * (nb + 1) : 0) +
                  sizeof(uint32_t) * (nb + 1);
@@ -2776,6 +3147,7 @@ static void assign_device(Profile &P, hipStream_t st, const double *de, int64_t 
 static void csr_device(Profile &P, hipStream_t st) {
   const int64_t n = P.n, nb = P.nb;
   if (P.csr_ready || !n) return;
+  ensure_bins32(P, st);
   int bits = 0;
   while (((int64_t)1 << bits) <= nb) ++bits;
   uint32_t *ka = (uint32_t *)P.keys0.get(sizeof(uint32_t) * (size_t)n);
@@ -2820,6 +3192,7 @@ struct SelPrep {  // a selection's parameters and output buffers (select_prep)
   double *xo = nullptr;
   uint64_t *kw = nullptr;
   uint32_t *toff = nullptr;
+  uint16_t *kpre = nullptr;
 };
 
 // parameters, host staging and output buffers of a selection (no launch)
@@ -2883,6 +3256,7 @@ static SelPrep select_prep(Profile &P, hipStream_t st, const void *pos, const vo
   if (lazy) {
     r.kw = (uint64_t *)P.kw.get(sizeof(uint64_t) * (TILE / 64) * (size_t)std::max<uint32_t>(nt, 1));
     r.toff = (uint32_t *)P.toff.get(sizeof(uint32_t) * (size_t)std::max<uint32_t>(nt, 1));
+    r.kpre = (uint16_t *)P.kpre.get(sizeof(uint16_t) * (TILE / 64) * (size_t)std::max<uint32_t>(nt, 1));
   }
   r.sp = sp;
   r.hi = hi;
@@ -2929,7 +3303,7 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
     auto go = [&](auto kern, int bt, auto tp) {
       using T = decltype(tp);
       hipLaunchKernelGGL(kern, dim3(nt), dim3(bt), 0, st, (const T *)d_pos, d_mass, hi, sp, stat,
-                         ctrl, xo, wo, io, mm, kw, toff);
+                         ctrl, xo, wo, io, mm, kw, toff, r.kpre);
     };
     if (pos_f32) {  // float32 snapshots: eager only
       if (nt < 1024) go(select_onepass<1024, false, float>, 1024, 0.0f);
@@ -3038,6 +3412,7 @@ static void moments_device(Profile &P, hipStream_t st, int f_src, const double *
   const double *w = (w_src < 0) ? nullptr : src(w_src, h_w, wstage);
   const int64_t len = nb * NMOM;
   PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * len, st));
+  ensure_bins32(P, st);
   if (n && nb > 0) {
     // <= 1024 blocks (4 per CU) stride over the tiles
     uint32_t nt = std::min<uint32_t>(ntiles_of(n), 1024u);
@@ -3098,6 +3473,7 @@ static void percentiles_device(Profile &P, hipStream_t st, int f_src, const doub
     // then the bin id (stable: value order kept inside each bin)
     uint32_t *ba = (uint32_t *)P.pbk.get(sizeof(uint32_t) * 2 * (size_t)n);
     uint32_t *bb = ba + n;
+    ensure_bins32(P, st);
     hipLaunchKernelGGL(gather_bin_ids, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st,
                        (const uint32_t *)P.bins.p, va, n, ba);
     int bits = 0;
@@ -3120,6 +3496,15 @@ static void percentiles_device(Profile &P, hipStream_t st, int f_src, const doub
 
 // ---- one-launch radial path (radial_mono) -------------------------------
 // PBX_RADIAL_MONO=0 turns it off (A/B: the multi-kernel path)
+// PBX_AGATHER=0: tiled selections take fused_gather + assign_sel (A/B)
+static bool agather_off() {
+  static const bool off = [] {
+    const char *v = std::getenv("PBX_AGATHER");
+    return v && v[0] == '0';
+  }();
+  return off;
+}
+
 static bool mono_enabled() {
   static const bool on = [] {
     const char *v = std::getenv("PBX_RADIAL_MONO");
@@ -3200,6 +3585,7 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   a.kw = r.kw;
   a.toff = r.toff;
   a.bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)ns);
+  P.bins_in8 = false;
   a.perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)ns);
   a.edges = (double *)P.edges.get(sizeof(double) * (size_t)nq);
   a.th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * RADIX * (size_t)nt);
@@ -3839,8 +4225,12 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       // per-group finish -> edges
       const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n_sel / (MS0_TPB * 16)));
       uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
+      // tiled selections: assignment fused with the gather (assign_gather),
+      // the deferred keys binned block by block by fix_deferred
+      const bool agath = tiled && lazy && n_sel && !agather_off();
+      uint32_t *bcnt = agath ? (uint32_t *)P.fblk.get(sizeof(uint32_t) * 3 * (size_t)g0) : nullptr;
       const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
-                           (uint32_t *)P.toff.p};
+                           (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0};
       hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
                          rows);
       hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
@@ -3852,23 +4242,76 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       hipLaunchKernelGGL(fused_resolve0, dim3(1), dim3(FR_TPB), 0, st, H, ctl, nbins, nq, R, gdig,
                          goff, gq);
       hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
-                         (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff);
+                         (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff,
+                         bcnt);
       uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n_sel ? n_sel : 1));
-      hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
-                         (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff, seg,
-                         tiled ? (const uint64_t *)stat : nullptr, nt);
       double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
+      uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n_sel ? n_sel : 1));
+      P.bins_in8 = agath;
+      double *maccs = nullptr, *maccs2 = nullptr;
+      P.csrh_ready = false;
+      uint32_t ablocks = 0;
+      const uint32_t *cnt_offs = nullptr;  // scanned CSR histogram the counts come from
+      uint32_t *th = nullptr;
+      uint8_t *bins8 = nullptr;
+      GatherOut go{};
+      if (agath) {
+        const int nr = (int)nb + 1;
+        const int64_t macc = (int64_t)fs.nm * nb;
+        th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * nr);
+        bins8 = (uint8_t *)P.bins8.get((size_t)n_sel);
+        double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)(2 * g0) * macc) : nullptr;
+        go = GatherOut{seg, (AgRec *)P.frec.get(sizeof(AgRec) * (size_t)n_sel), bcnt, bcnt + g0,
+                       bcnt + 2 * g0};
+        const size_t lds = sizeof(double) * (size_t)macc + sizeof(uint32_t) * (size_t)(nr | 1) * AG_TR;
+        auto ag = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, x, (const uint64_t *)P.kw.p,
+                             (const uint16_t *)P.kpre.p, (const uint32_t *)P.toff.p, P.sel_base,
+                             nt, P.sel_mass,
+                             (const FusedCtl *)ctl, ka, kb, (const MsRank *)R, nq,
+                             (const uint32_t *)gdig, (const uint32_t *)boff, (int)nb, bins8, th,
+                             fs, slab, go);
+        };
+        if (fs.nm) ag(assign_gather<true>);
+        else ag(assign_gather<false>);
+        PBX_HIP(hipGetLastError());
+        ablocks = (uint32_t)g0;
+        if (fs.nm) {
+          maccs = slab;
+          maccs2 = slab + (size_t)g0 * macc;
+        }
+      } else {
+        hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
+                           (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff,
+                           seg, tiled ? (const uint64_t *)stat : nullptr, nt);
+      }
       hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
                          (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
                          (const uint64_t *)seg, de);
       PBX_HIP(hipGetLastError());
       // assignment (+ the statistics' distinct sums) with the device edges
-      uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n_sel ? n_sel : 1));
-      double *maccs = nullptr;
-      P.csrh_ready = false;
-      uint32_t ablocks = 0;
-      const uint32_t *cnt_offs = nullptr;  // scanned CSR histogram the counts come from
-      if (n_sel && lazy) {
+      if (agath) {
+        const uint32_t nr = (uint32_t)nb + 1;
+        const size_t lds = sizeof(double) * ((size_t)fs.nm * nb + nb + 1) + sizeof(uint32_t) * FD_LDSW;
+        auto fd = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, (const FusedCtl *)ctl,
+                             (const AgRec *)go.rec, (const uint32_t *)go.rbase,
+                             (const uint32_t *)go.rn, (const double *)de, (int)nb, bins8, th, nt,
+                             fs, maccs2);
+        };
+        if (fs.nm) fd(fix_deferred<true>);
+        else fd(fix_deferred<false>);
+        PBX_HIP(hipGetLastError());
+        scan_u32(P, st, th, (int64_t)nt * nr);
+        cnt_offs = th;
+        if (build_csr) {
+          int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
+          hipLaunchKernelGGL(csr_sel<uint8_t>, dim3(nt), dim3(TPB), 0, st,
+                             (const uint32_t *)P.toff.p, n_dev, (const uint8_t *)bins8,
+                             (const uint32_t *)th, nt, perm, nr);
+          PBX_HIP(hipGetLastError());
+        }
+      } else if (n_sel && lazy) {
         // tile-walking assignment over the lazy selection + its CSR pass
         const int64_t macc = (int64_t)fs.nm * nb;
         const bool ldse = (nb + 1) <= LDS_EDGES;
@@ -3908,8 +4351,8 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
         cnt_offs = th;
         if (build_csr) {
           int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
-          hipLaunchKernelGGL(csr_sel, dim3(nt), dim3(TPB), 0, st, kwp, tof, (const uint32_t *)bins,
-                             (const uint32_t *)th, nt, perm);
+          hipLaunchKernelGGL(csr_sel<uint32_t>, dim3(nt), dim3(TPB), 0, st, tof, n_dev, (const uint32_t *)bins,
+                             (const uint32_t *)th, nt, perm, (uint32_t)RADIX);
           PBX_HIP(hipGetLastError());
         }
       } else if (n_sel) {
@@ -3971,7 +4414,8 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       const int nhead = (int)ceil_div(NC + nq + (int)nb, TPB);
       hipLaunchKernelGGL(fused_pack, dim3(nhead + nsum), dim3(TPB), 0, st, (const FusedCtl *)ctl,
                          (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
-                         (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead);
+                         (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead,
+                         (const double *)maccs2, maccs2 ? (int64_t)g0 : 0);
       hp = (double *)P.pin.get(sizeof(double) * (size_t)ntot);
       PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * ntot, hipMemcpyDeviceToHost, st));
       PBX_HIP(hipStreamSynchronize(st));

@@ -497,7 +497,10 @@ def test_profile_median_uses_device(gpu, monkeypatch):
 @pytest.mark.parametrize("case", ["plummer", "sphere_family", "clip", "nan", "single", "dups",
                                   "skewed", "empty_window", "nothing_kept", "many_stats",
                                   "family_offset", "no_mass", "wide", "wide_family",
-                                  "empty_family", "tiled", "tiled_family"])
+                                  "empty_family", "tiled", "tiled_family", "tiled_nan",
+                                  "tiled_dups", "tiled_skewed", "tiled_clip", "tiled_single",
+                                  "tiled_no_mass", "tiled_many_stats", "tiled_nb255", "tiled_nb1",
+                                  "tiled_empty_window", "tiled_nothing_kept"])
 def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
     """pbx_profile_radial_equaln (select + equaln + assign + CSR + sums with
     one host round trip, level-0 select + per-group LDS sort / radix finish)
@@ -513,7 +516,18 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
     sphere, fams = None, None
     nb = 128
     stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
-    if case == "sphere_family":
+    if case.startswith("tiled"):  # >= 1024 selection tiles: tiled x, tile_scan, assign_gather
+        n = 4_400_000
+        pos = rng.normal(scale=3.0, size=(n, 3))
+        mass = rng.uniform(0.5, 1.5, n)
+        case = case[6:]  # the variant, at the tiled size
+    if case == "family":
+        sphere, fams = ((0.2, 0.0, 0.1), 7.0), [(3_001, 4_300_000)]
+    elif case == "nb255":  # the most bins of the lazy path
+        nb = 255
+    elif case == "nb1":
+        nb = 1
+    elif case == "sphere_family":
         sphere, fams = ((0.5, -0.25, 0.0), 6.0), [(0, 150_000), (200_000, 390_000)]
     elif case == "clip":
         lo, hi = 0.5, 6.0
@@ -543,12 +557,6 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
         sphere = ((0.0, 0.0, 0.0), 8.0)
     elif case == "empty_family":
         fams = [(5, 5)]
-    elif case in ("tiled", "tiled_family"):  # >= 1024 selection tiles: tiled x, tile_scan
-        n = 4_400_000
-        pos = rng.normal(scale=3.0, size=(n, 3))
-        mass = rng.uniform(0.5, 1.5, n)
-        if case == "tiled_family":
-            sphere, fams = ((0.2, 0.0, 0.1), 7.0), [(3_001, 4_300_000)]
     elif case == "many_stats":  # more statistics than the assignment pass fuses
         nb = 64
         stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11), (SRC_X, SRC_NONE, 0x7f),
@@ -584,6 +592,15 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
             for u, v in zip(a.selection(idx=True, x=True, w=True),
                             b.selection(idx=True, x=True, w=True)):
                 assert np.array_equal(u, v, equal_nan=u.dtype.kind == "f")
+            if n > 1_000_000 and case == "":  # tiled, no CSR in the call: byte bins widened on demand
+                a2 = DeviceBins.radial_equaln(pos, mass, nbins=nb, sphere=sphere, families=fams,
+                                              bin_min=lo, bin_max=hi, stats=stats, csr=False)[0]
+                try:
+                    p3, o3 = a2.csr()
+                    assert np.array_equal(p3, p2) and np.array_equal(o3, o2)
+                    assert np.array_equal(a2.percentiles([10, 50, 90]), b.percentiles([10, 50, 90]))
+                finally:
+                    a2.close()
         finally:
             a.close()
     finally:
