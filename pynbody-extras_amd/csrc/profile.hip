@@ -3676,7 +3676,9 @@ int pbx_profile_destroy(void *handle) {
                   &p->field, &p->weight, &p->ranks, &p->bounds, &p->msH, &p->msR, &p->msG,
                   &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst, &p->accs,
                   &p->pk0, &p->pk1, &p->pv0, &p->pv1, &p->pbk, &p->pcdf, &p->poff, &p->pq, &p->pout,
-                  &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack};
+                  &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack, &p->frec, &p->fblk,
+                  &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->mono, &p->bar,
+                  &p->mono_trace};
     for (Buf *b : all) b->release();
     p->pin.release();
     delete p;
