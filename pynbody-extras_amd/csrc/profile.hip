@@ -2480,20 +2480,26 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   {
     // bin d: its count in the tiles before t and in all tiles.  Wave w reads
     // rows d = w, w + 16, ... of the [bin][tile] table coalesced (lane = tile,
-    // nt <= 256: 4 loads per lane and row), four rows (16 loads) in flight
+    // nt <= 256: 4 loads per lane and row), six rows (24 loads) in flight;
+    // only the nb + 1 rows a bin can occupy (nb: invalid), the rest are 0
     uint32_t *pb = L0, *pa = L0 + RADIX;
     static_assert(MONO_MAXT <= 256, "4 tiles per lane and row");
-    for (int d0 = w; d0 < RADIX; d0 += 4 * MONO_NW) {
-      uint32_t v[4][4];
+    constexpr int RR = 6;
+    const int nr = nb + 1;
+    for (int d = nr + tid; d < RADIX; d += MONO_BT) pa[d] = pb[d] = 0u;
+    for (int d0 = w; d0 < nr; d0 += RR * MONO_NW) {
+      uint32_t v[RR][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < RR; ++r)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const uint32_t u = lane + 64 * j;
-          v[r][j] = u < nt ? ld_sc1(&a.th[(int64_t)(d0 + r * MONO_NW) * nt + u]) : 0u;
+          v[r][j] = (u < nt && d0 + r * MONO_NW < nr)
+                        ? ld_sc1(&a.th[(int64_t)(d0 + r * MONO_NW) * nt + u]) : 0u;
         }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < RR; ++r) {
+        if (d0 + r * MONO_NW >= nr) continue;  // (uniform)
         uint32_t al = 0, be = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
