@@ -1140,6 +1140,30 @@ constexpr int FS_BITS = 11;
 constexpr int FS_DIG = 1 << FS_BITS;
 constexpr int FS_LDS = 8192;
 
+// keys of sk[0, S) below / equal to k: 8 keys per step from four 16-B LDS
+// reads (broadcast: every lane reads the same address), counts split over
+// two chains
+__device__ __forceinline__ void count_rank(const uint64_t *sk, int S, uint64_t k, uint32_t &less,
+                                           uint32_t &eq) {
+  uint32_t l0 = 0, l1 = 0, e0 = 0, e1 = 0;
+  int j = 0;
+  for (; j + 8 <= S; j += 8) {
+    const ulonglong2 a = *(const ulonglong2 *)(sk + j), b = *(const ulonglong2 *)(sk + j + 2);
+    const ulonglong2 c = *(const ulonglong2 *)(sk + j + 4), d = *(const ulonglong2 *)(sk + j + 6);
+    l0 += (a.x < k) + (a.y < k) + (b.x < k) + (b.y < k);
+    l1 += (c.x < k) + (c.y < k) + (d.x < k) + (d.y < k);
+    e0 += (a.x == k) + (a.y == k) + (b.x == k) + (b.y == k);
+    e1 += (c.x == k) + (c.y == k) + (d.x == k) + (d.y == k);
+  }
+  for (; j < S; ++j) {
+    const uint64_t kj = sk[j];
+    l0 += kj < k ? 1u : 0u;
+    e0 += kj == k ? 1u : 0u;
+  }
+  less = l0 + l1;
+  eq = e0 + e1;
+}
+
 template <bool IN_LDS, bool SC1 = false>  // SC1: keys handed over in-launch (radial_mono)
 __device__ void finish_group(const uint64_t *__restrict__ keys, int64_t S, uint64_t pref0, int s,
                              int64_t rr, uint32_t *hist, uint32_t *wsum, uint64_t *pick,
@@ -1193,7 +1217,7 @@ __global__ void __launch_bounds__(FR_TPB)
     fused_finish(const FusedCtl *__restrict__ ctl, const MsRank *__restrict__ R,
                  const uint32_t *__restrict__ gq, const uint32_t *__restrict__ goff,
                  const uint64_t *__restrict__ seg, double *__restrict__ edges) {
-  __shared__ uint64_t sk[FS_LDS];
+  __shared__ __attribute__((aligned(16))) uint64_t sk[FS_LDS];
   __shared__ uint32_t hist[FS_DIG];
   __shared__ uint32_t wsum[FR_TPB / 64];
   __shared__ uint64_t pick[2];
@@ -1212,11 +1236,7 @@ __global__ void __launch_bounds__(FR_TPB)
   if (S <= FR_TPB) {  // small group: each key's rank by counting (one key per thread)
     const uint64_t k = tid < S ? sk[tid] : ~0ull;
     uint32_t less = 0, eq = 0;
-    for (int j = 0; j < (int)S; ++j) {
-      const uint64_t kj = sk[j];
-      less += kj < k ? 1u : 0u;
-      eq += kj == k ? 1u : 0u;
-    }
+    count_rank(sk, (int)S, k, less, eq);
     for (int q = (int)gq[g]; q < (int)gq[g + 1]; ++q) {
       const int64_t rr = R[q].rr;
       if (tid < S && (int64_t)less <= rr && rr < (int64_t)(less + eq))
@@ -1975,6 +1995,12 @@ constexpr int MONO_BT = 1024;
 constexpr int MONO_NW = MONO_BT / 64;
 constexpr int MONO_SI = TILE / MONO_BT;  // particles per lane
 constexpr uint32_t MONO_MAXT = 256;
+// level-0 digits of the one-launch path (13 bits: the histogram flush and
+// H scan got 5.5 us faster, the finish of the twice larger groups 10 us
+// slower at 1M)
+constexpr int MONO_BITS = 14;
+constexpr int MONO_DIG = 1 << MONO_BITS;
+static_assert(MONO_DIG <= MS0_DIG, "the LDS arrays are MS0_DIG long");
 constexpr int BAR_LINE = 16;             // u64 words per 128-B line
 // lines 0-7 group counters, 8 top counter, 9 generation, 10 completions
 constexpr size_t BAR_WORDS = (size_t)BAR_LINE * 11;
@@ -2109,9 +2135,9 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   const uint32_t lane = lane_id();
   const int nb = a.nb, nq = a.nq;
   if (tid == 0) s_ok = 1;
-  for (int i = tid; i < MS0_DIG; i += MONO_BT) L0[i] = 0;
+  for (int i = tid; i < MONO_DIG; i += MONO_BT) L0[i] = 0;
   if (t == 0) {  // zeroed here, used after barrier 1
-    for (int i = tid; i < MS0_DIG; i += MONO_BT) st_sc1(&a.H[i], 0u);
+    for (int i = tid; i < MONO_DIG; i += MONO_BT) st_sc1(&a.H[i], 0u);
     for (int i = tid; i < RADIX; i += MONO_BT) st_sc1(&a.gcnt[i], 0u);
   }
   // ---- 1: selection (select_onepass) -------------------------------------
@@ -2231,7 +2257,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       } else {
         const uint64_t span = hi - lo;
         const int B = span ? 64 - __builtin_clzll(span) : 1;
-        cl.w0 = B < MS0_BITS ? B : MS0_BITS;
+        cl.w0 = B < MONO_BITS ? B : MONO_BITS;
         cl.s0 = B - cl.w0;
         cl.lo = lo;
       }
@@ -2263,7 +2289,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   }
   __syncthreads();
   if (ok2)
-    for (int i = tid; i < MS0_DIG; i += MONO_BT) {
+    for (int i = tid; i < MONO_DIG; i += MONO_BT) {
       const uint32_t v = L0[i];
       if (v) atomicAdd(&a.H[i], v);
     }
@@ -2273,7 +2299,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   // ---- 3: ranks -> level-0 digits and groups; keys -> group segments -----
   int ng = 0;
   if (ok2) {
-    constexpr int PT = MS0_DIG / MONO_BT;
+    constexpr int PT = MONO_DIG / MONO_BT;
     uint32_t v[PT], tot = 0;
 #pragma unroll
     for (int k = 0; k < PT; ++k) {
@@ -2295,10 +2321,10 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       run += v[k];
       L0[tid * PT + k] = run;  // inclusive counts
     }
-    for (int i = tid; i < MS0_DIG / 2; i += MONO_BT) ((uint32_t *)L1)[i] = ~0u;
+    for (int i = tid; i < MONO_DIG / 2; i += MONO_BT) ((uint32_t *)L1)[i] = ~0u;
     __syncthreads();
     MONO_STAMP(7);
-    const int64_t m = (int64_t)L0[MS0_DIG - 1];
+    const int64_t m = (int64_t)L0[MONO_DIG - 1];
     const int top = (1 << ctl0.w0) - 1;
     for (int q = tid; q < nq; q += MONO_BT) {
       int64_t r = 0;
@@ -2387,11 +2413,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       if (S <= MONO_BT) {  // small group: each key's rank by counting
         const uint64_t k = tid < S ? sk[tid] : ~0ull;
         uint32_t less = 0, eq = 0;
-        for (int j = 0; j < (int)S; ++j) {
-          const uint64_t kj = sk[j];
-          less += kj < k ? 1u : 0u;
-          eq += kj == k ? 1u : 0u;
-        }
+        count_rank(sk, (int)S, k, less, eq);
         for (int q = (int)g_start[g]; q < (int)g_start[g + 1]; ++q) {
           const int64_t rr = q_rr[q];
           if (tid < S && (int64_t)less <= rr && rr < (int64_t)(less + eq))
