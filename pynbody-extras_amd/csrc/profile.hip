@@ -2300,12 +2300,29 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   int ng = 0;
   if (ok2) {
     constexpr int PT = MONO_DIG / MONO_BT;
+    static_assert(PT % 4 == 0, "16-B LDS reads");
+    // H in with lane-consecutive sc1 loads (a thread's PT consecutive words
+    // loaded directly put a wave's 64 lanes 4 KB apart: ~64 L2 requests
+    // per load), through LDS to each thread's PT consecutive digits
+    {
+      uint32_t h[PT];
+#pragma unroll
+      for (int k = 0; k < PT; ++k) h[k] = ld_sc1(&a.H[k * MONO_BT + tid]);
+#pragma unroll
+      for (int k = 0; k < PT; ++k) L0[k * MONO_BT + tid] = h[k];
+    }
+    __syncthreads();
     uint32_t v[PT], tot = 0;
 #pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      v[k] = ld_sc1(&a.H[tid * PT + k]);
-      tot += v[k];
+    for (int k = 0; k < PT; k += 4) {
+      const uint4 q = *(const uint4 *)&L0[tid * PT + k];
+      v[k] = q.x;
+      v[k + 1] = q.y;
+      v[k + 2] = q.z;
+      v[k + 3] = q.w;
     }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) tot += v[k];
     uint32_t xs = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -2578,9 +2595,11 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     if (tid < NC) a.pack[tid] = ((const double *)&s_ctl)[tid];
     for (int i = tid; i < nq; i += MONO_BT) a.pack[NC + i] = e_lds[i];
   }
-  // per-bin sums: column j summed over the tiles in a fixed order by one wave
+  // per-bin sums: column j summed over the tiles in a fixed order by one
+  // wave; columns spread over the blocks first (its 4 loads per lane are 64
+  // lines apart: a few columns per CU, not 16 on each of the first CUs)
   const int nsum = macc;
-  for (int j = (int)t * MONO_NW + w; j < nsum; j += (int)nt * MONO_NW) {
+  for (int j = (int)t + w * (int)nt; j < nsum; j += (int)nt * MONO_NW) {
     double v[4];  // nt <= 256: four rows per lane, loads in flight together
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
