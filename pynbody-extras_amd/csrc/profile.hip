@@ -1652,8 +1652,9 @@ __global__ void __launch_bounds__(MS0_TPB)
                   uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
                   double *__restrict__ slab, GatherOut go) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ uint16_t gidx[MS0_DIG];
-  __shared__ uint8_t lut[MS0_DIG];
+  // per level-0 digit: the bin of its keys (#{q : digit_q < d} - 1, or nb),
+  // or 0x8000 | group when the digit holds edges — one LDS read per key
+  __shared__ uint16_t dtab[MS0_DIG];
   __shared__ uint32_t sslot[RADIX];
   __shared__ uint32_t qd[RADIX];
   __shared__ uint32_t red[MS0_TPB / 64];
@@ -1668,16 +1669,12 @@ __global__ void __launch_bounds__(MS0_TPB)
   const uint64_t lo = ctl->lo;
   const int s = ctl->s0;
   const uint32_t rb = block_prefix(go.bcnt, (int)blockIdx.x, red);
-  for (int k = tid; k < MS0_DIG / 2; k += MS0_TPB) ((uint32_t *)gidx)[k] = ~0u;
   for (int q = tid; q < nq; q += MS0_TPB) qd[q] = (uint32_t)R[q].prefix;
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
   for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
   if (tid == 0) dk = 0;
   __syncthreads();
-  for (int g = tid; g < ng; g += MS0_TPB) {
-    gidx[gdig[g]] = (uint16_t)g;
-    sslot[g] = boff[(int64_t)blockIdx.x * MS_MAXQ + g];
-  }
+  for (int g = tid; g < ng; g += MS0_TPB) sslot[g] = boff[(int64_t)blockIdx.x * MS_MAXQ + g];
   for (int d = tid; d < MS0_DIG; d += MS0_TPB) {  // #{q : digit_q < d}, lower bound
     int a = 0, len = nq;
     while (len > 0) {
@@ -1690,8 +1687,10 @@ __global__ void __launch_bounds__(MS0_TPB)
       }
     }
     const int b = a - 1;
-    lut[d] = (uint8_t)((b < 0 || b >= nb) ? nb : b);
+    dtab[d] = (uint16_t)((b < 0 || b >= nb) ? nb : b);
   }
+  __syncthreads();
+  for (int g = tid; g < ng; g += MS0_TPB) dtab[gdig[g]] = (uint16_t)(0x8000u | (uint32_t)g);
   __syncthreads();
   uint32_t ta, tb;
   tile_range(nt, ta, tb);
@@ -1742,21 +1741,14 @@ __global__ void __launch_bounds__(MS0_TPB)
       bool defer = false;
       if (win && key >= ka && key <= kb) {  // fused_hist0's window
         const uint32_t d = (uint32_t)((key - lo) >> s);
-#ifdef PBX_DIAG_AG_NOLDS
-        const uint32_t g = (d & 0xff) == 0x77 ? (d >> 8) & 127 : 0xffffu;
-#else
-        const uint32_t g = gidx[d];
-#endif
-        if (g != 0xffffu) {
+        const uint32_t e = dtab[d];
+        if (e & 0x8000u) {
+          const uint32_t g = e & 0x7fffu;
           go.seg[atomicAdd(&sslot[g], 1u)] = key - lo;
           defer = xv == xv;
           if (defer) go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{key - lo, P.m[kk], P.pos[kk], t};
         } else if (xv == xv) {
-#ifdef PBX_DIAG_AG_NOLDS
-          b = d & 127;
-#else
-          b = lut[d];
-#endif
+          b = e;
         }
       }
       if (defer) continue;
