@@ -1180,10 +1180,23 @@ __device__ void finish_group(const uint64_t *__restrict__ keys, int64_t S, uint6
     const uint32_t dm = (1u << wd) - 1;
     for (int d = tid; d < FS_DIG; d += FR_TPB) hist[d] = 0;
     __syncthreads();
-    for (int64_t i = tid; i < S; i += FR_TPB) {
-      const uint64_t k = SC1 ? __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : keys[i];
-      if ((k & hmask) == pref) atomicAdd(&hist[(uint32_t)(k >> sh) & dm], 1u);
+    // FS_U keys per thread in flight (a group of ~20k keys re-read from
+    // global memory was one latency per 1024 keys per pass)
+    constexpr int FS_U = IN_LDS ? 1 : 8;
+    for (int64_t i0 = 0; i0 < S; i0 += (int64_t)FR_TPB * FS_U) {
+      uint64_t kv[FS_U];
+#pragma unroll
+      for (int u = 0; u < FS_U; ++u) {
+        const int64_t i = i0 + (int64_t)u * FR_TPB + tid;
+        const int64_t ic = i < S ? i : 0;  // unconditional loads
+        kv[u] = SC1 ? __hip_atomic_load(&keys[ic], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : keys[ic];
+      }
+#pragma unroll
+      for (int u = 0; u < FS_U; ++u) {
+        const int64_t i = i0 + (int64_t)u * FR_TPB + tid;
+        if (i < S && (kv[u] & hmask) == pref) atomicAdd(&hist[(uint32_t)(kv[u] >> sh) & dm], 1u);
+      }
     }
     __syncthreads();
     // inclusive scan of 2 digits per thread; the thread whose digits hold rank rr picks
