@@ -122,11 +122,9 @@ __global__ void __launch_bounds__(BT)
   __shared__ uint32_t wcnt[NW];
   __shared__ unsigned long long wmin[NW], wmax[NW];
   __shared__ uint32_t s_tile, s_excl;
-#ifdef PBX_DIAG_NO_TICKET
-  if (threadIdx.x == 0) s_tile = blockIdx.x;
-#else
-  if (threadIdx.x == 0) s_tile = atomicAdd(&ctrl[0], 1u);
-#endif
+  // the ticket (a returning device atomic before any load can be issued)
+  // orders the look-back; a tiled selection has none: block = tile
+  if (threadIdx.x == 0) s_tile = (LAZY && p.tiled) ? blockIdx.x : atomicAdd(&ctrl[0], 1u);
   __syncthreads();
   const uint32_t tile = s_tile;
   const int w = threadIdx.x >> 6;
