@@ -137,17 +137,17 @@ class DeviceBins:
         nq = int(nbins) + 1
         k = len(stats)
         # The selection and statistics arguments of a repeated call on device
-        # pointers are rebuilt only when they change (host-side cost of a
-        # 1M-particle step); the output arrays are fresh every call.
+        # pointers, and the staging arrays the results land in, are rebuilt
+        # only when they change (host-side cost of a 1M-particle step); the
+        # returned arrays are fresh copies every call.
         key = None
         if on_device:
             key = (pos, mass, None if sphere is None else (tuple(sphere[0]), float(sphere[1])),
-                   None if families is None else tuple(tuple(f) for f in families), ndim, n,
-                   tuple(tuple(int(v) for v in s) for s in stats), nbins, bin_min, bin_max,
-                   bool(csr))
+                   None if families is None else tuple(map(tuple, families)), ndim, n,
+                   tuple(map(tuple, stats)), nbins, bin_min, bin_max, bool(csr))
         cached = getattr(d, "_req", None)
         if key is not None and cached is not None and cached[0] == key:
-            args, keep, fs, ws, cs, head, refs = cached[1]
+            args, keep, fs, ws, cs, head, refs, outs = cached[1]
         else:
             args, keep = cls._select_args(pos, mass, sphere, families, ndim, on_device, n)
             fs = (c_int * max(k, 1))(*[int(s[0]) for s in stats])
@@ -157,15 +157,17 @@ class DeviceBins:
                     float(bin_min) if bin_min is not None else 0.0, int(bin_max is not None),
                     float(bin_max) if bin_max is not None else 0.0, int(bool(csr)), k, fs, ws, cs)
             refs = (c_int64(0), c_int64(0), c_int64(0))
+            e_buf, c_buf = np.empty(nq), np.zeros(nbins, dtype=np.int64)
+            m_buf = np.zeros((max(k, 1), nbins, NMOM))
+            kept, ne, nv = refs
+            outs = (e_buf, c_buf, m_buf, (byref(kept), nat.dptr(e_buf), byref(ne), _i64(c_buf),
+                                          byref(nv), nat.dptr(m_buf)))
             if key is not None:
-                d._req = (key, (args, keep, fs, ws, cs, head, refs))
+                d._req = (key, (args, keep, fs, ws, cs, head, refs, outs))
         kept, ne, nv = refs
-        edges = np.empty(nq)
-        counts = np.zeros(nbins, dtype=np.int64)
-        mom = np.zeros((max(k, 1), nbins, NMOM))
+        edges, counts, mom, optrs = outs
         try:
-            nat.call("pbx_profile_radial_equaln", d._h, *args, *head, byref(kept),
-                     nat.dptr(edges), byref(ne), _i64(counts), byref(nv), nat.dptr(mom))
+            nat.call("pbx_profile_radial_equaln", d._h, *args, *head, *optrs)
         except ValueError as e:
             if str(e).startswith("index 0 is out of bounds"):
                 raise IndexError(str(e)) from None
@@ -179,9 +181,10 @@ class DeviceBins:
         d.n_valid = nv.value
         if nb != nbins:  # degenerate: one bin, compact layout [k][1][7]
             mom = mom.reshape(-1)[: max(k, 1) * NMOM].reshape(max(k, 1), 1, NMOM)
-            counts = counts[:1].copy()
+            counts = counts[:1]
+        counts = counts.copy()  # (the staging arrays are reused by the next call)
         d.counts = counts
-        return d, edges[: ne.value].copy(), counts, [mom[i] for i in range(k)]
+        return d, edges[: ne.value].copy(), counts, [mom[i].copy() for i in range(k)]
 
     def selection(self, idx=True, x=True, w=True):
         """(original indices int64, x, weights) of the fused selection."""
