@@ -3362,7 +3362,15 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
       if (lazy) go(select_onepass<1024, true, double>, 1024, 0.0);
       else go(select_onepass<1024, false, double>, 1024, 0.0);
     } else {
-      if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
+      // 512-thread tiles (8 particles per lane, 64 VGPRs: 8 waves per SIMD)
+      // for the lazy selection: 244 -> 233 us at 64M against 256 threads
+      // (16 per lane, 136 VGPRs, 3 waves); PBX_SEL_BT=256 for the A/B
+      static const bool sel512 = [] {
+        const char *v = std::getenv("PBX_SEL_BT");
+        return !(v && std::strcmp(v, "256") == 0);
+      }();
+      if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
+      else if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
       else go(select_onepass<TPB, false, double>, TPB, 0.0);
     }
     PBX_HIP(hipGetLastError());
