@@ -3371,6 +3371,7 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
       }();
       if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
       else if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
+      else if (sel512) go(select_onepass<512, false, double>, 512, 0.0);
       else go(select_onepass<TPB, false, double>, TPB, 0.0);
     }
     PBX_HIP(hipGetLastError());
