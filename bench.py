@@ -155,6 +155,27 @@ PROFILE_BYTES_PER_PARTICLE = 49  # equaln profile, algorithmic H
 HBM_PEAK_GBS = 8000.0
 
 
+def profile_parity(dev, res, ref) -> dict:
+    """The last timed step's results against oracle/profile_ref.radial_profile
+    on the same particles (outside the timed region): edges, counts and the
+    CSR (binind, bins.py:383-393) bit-exact; Σm and mass-weighted <r> per bin
+    (proarray.py:320-328) relative to the oracle's numpy sums."""
+    edges, msum, rmom = res
+    perm, offs = dev.csr()
+    with np.errstate(invalid="ignore", divide="ignore"):
+        rmean = rmom[:, 1] / rmom[:, 0]  # weighted Mean: Σ(r·m) / Σm
+        ms = np.abs(msum - ref["mass_sum"]) / np.abs(ref["mass_sum"])
+        rm = np.abs(rmean - ref["r_mean"]) / np.abs(ref["r_mean"])
+    return {
+        "edges_bit_exact": bool(np.array_equal(edges, ref["edges"])),
+        "counts_bit_exact": bool(np.array_equal(dev.counts, ref["counts"])),
+        "csr_bit_exact": bool(np.array_equal(offs, ref["offsets"]) and np.array_equal(perm, ref["perm"])),
+        "mass_sum_max_rel": float(np.nanmax(ms)),
+        "r_mean_max_rel": float(np.nanmax(rm)),
+        "n_kept": int(len(ref["x"])),
+    }
+
+
 def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
     """Config 3: RadialProfileBuilder(ndim=3, weight='mass', equaln, 128 bins)
     behind Sphere(R=10) & FamilyFilter('dm'), positions / masses resident in
@@ -228,30 +249,30 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                "hbm_gbs_algorithmic": n_all * PROFILE_BYTES_PER_PARTICLE / td / 1e9,
                "hbm_gbs_algorithmic_per_gpu": n * PROFILE_BYTES_PER_PARTICLE / td / 1e9,
                "stream_ms": td * 1e3}
+        if dist is None:
+            row["path"] = dev.path_stats()  # one-launch / discarded / multi-kernel calls
         out.append(row)
-        if cpu and n == sizes[0] and world == 1:
+        if cpu and world == 1:
             from oracle import profile_ref as pr
 
             mask = pr.sphere_mask(pos, 10.0)
             mask[dm.stop:] = False
-            # the full workload, repeated until ~10 s of CPU time
-            reps, tc = 0, 0.0
-            while tc < 10.0 and reps < 1000:
-                t0 = time.perf_counter()
+            if n == sizes[0]:
+                # the full workload, repeated until ~10 s of CPU time
+                reps, tc = 0, 0.0
+                while tc < 10.0 and reps < 1000:
+                    t0 = time.perf_counter()
+                    ref = pr.radial_profile(pos, mass, mask, "equaln", 128)
+                    tc += time.perf_counter() - t0
+                    reps += 1
+                row["cpu_baseline"] = {
+                    "value": reps * n / tc, "unit": "particles/s", "cores": 1, "kind": "port",
+                    "sample": f"full {n}-particle workload x {reps}, oracle/profile_ref.py (numpy "
+                              f"restatement of bins.py/proarray.py), 1 thread, {tc:.1f} s",
+                    **cpu_host()}
+            else:
                 ref = pr.radial_profile(pos, mass, mask, "equaln", 128)
-                tc += time.perf_counter() - t0
-                reps += 1
-            row["cpu_baseline"] = {
-                "value": reps * n / tc, "unit": "particles/s", "cores": 1, "kind": "port",
-                "sample": f"full {n}-particle workload x {reps}, oracle/profile_ref.py (numpy "
-                          f"restatement of bins.py/proarray.py), 1 thread, {tc:.1f} s",
-                **cpu_host()}
-            edges, msum, _ = res
-            row["parity_vs_oracle"] = {
-                "edges_bit_exact": bool(np.array_equal(edges, ref["edges"])),
-                "counts_bit_exact": bool(np.array_equal(dev.counts, ref["counts"])),
-                "mass_sum_max_rel": float(np.nanmax(np.abs(msum - ref["mass_sum"]) /
-                                                    np.abs(ref["mass_sum"])))}
+            row["parity_vs_oracle"] = profile_parity(dev, res, ref)
         dev.close()
         d_pos.free()
         d_mass.free()
@@ -564,6 +585,14 @@ def main():
     if not args.no_tree:
         tree = bench_tree(dist, args.tree_n, steps=max(3, args.steps), warmup=1,
                           cpu=not args.no_cpu_baseline, cpu_seconds=args.cpu_seconds)
+    sweep = None
+    if not args.no_profile:
+        # every rank: with N > 1 (or PBX_BENCH_FORCE_DIST=1) the sharded
+        # profile with global edges (distributed radix select over RCCL)
+        sizes = [int(s) for s in args.profile_sizes.split(",") if s]
+        sweep = bench_profile(sizes, steps=max(3, args.steps), warmup=1,
+                              cpu=not args.no_cpu_baseline and rank == 0 and world == 1,
+                              dist=dist if dist.comm is not None else None)
     dist.close()
     if rank != 0:
         return
@@ -610,11 +639,7 @@ def main():
         },
         "cpu_baseline": cpu,
     }
-    if not args.no_profile:
-        sizes = [int(s) for s in args.profile_sizes.split(",") if s]
-        sweep = bench_profile(sizes, steps=max(3, args.steps), warmup=1,
-                              cpu=not args.no_cpu_baseline and rank == 0,
-                              dist=dist if dist.comm is not None else None)
+    if sweep is not None:
         head = sweep[0]
         big = max(sweep, key=lambda r: r["hbm_gbs_algorithmic_per_gpu"])
         out["profile"] = {
@@ -637,6 +662,8 @@ def main():
                          "traffic": pmc_profile_step_bytes(big["n_per_gpu"]),
                          "traffic_note": "HBM bytes per 64M step (all profile kernels, PMC "
                                          "run committed in profiles/pmc_profile_latest.json)"},
+            "parity_at_roofline_point": big.get("parity_vs_oracle"),
+            "one_launch_discards": (head.get("path") or {}).get("mono_discarded"),
             "sweep": sweep,
             "cpu_baseline": head.get("cpu_baseline"),
         }

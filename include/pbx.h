@@ -335,7 +335,14 @@ int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double b
  * (the RadialProfileBuilder equaln path end to end: filters/filt.py:42-86,
  * bins.py:720-746 / :346-395, proarray.py:272-334 sums).  Same arguments,
  * results and errors as the two calls in sequence; *n_kept as
- * pbx_profile_select (also set when the binning then fails). */
+ * pbx_profile_select (also set when the binning then fails).
+ * Lifetime: with on_device = 1 the selection is lazy — the weights of the
+ * kept particles are read from the caller's `mass` device array by the
+ * first later call on this handle that needs them (pbx_profile_moments*,
+ * pbx_profile_get_selection with h_w, weighted percentiles) and held by the
+ * handle from then on, so that array must stay allocated and unchanged
+ * until that call (or the next selection).  Host inputs (on_device = 0) are
+ * staged into the handle. */
 int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mass, int64_t n,
                               int on_device, int use_sphere, const double *sphere,
                               const int64_t *fam, int nfam, int ndim, int64_t nbins, int has_min,
@@ -344,6 +351,12 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                               const uint32_t *cols, int64_t *n_kept, double *h_edges,
                               int64_t *n_edges, int64_t *h_counts, int64_t *n_valid,
                               double *h_moments);
+/* Telemetry of pbx_profile_radial_equaln on this handle (no reference
+ * counterpart): out[3] = {calls run as the one-launch persistent kernel,
+ * of those the calls discarded at a grid barrier and re-run by the
+ * multi-kernel path (a silent ~2x slowdown if non-zero), calls that took
+ * the multi-kernel path}. */
+int pbx_profile_path_stats(void *handle, int64_t *out);
 /* Per-bin percentiles of the last assignment — replaces the per-bin loop of
  * ProfileArray._compute for Percentile / Median / Abs_pXX
  * (proarray.py:272-334 + :689-722): h_out[bin*nq + k] = np.interp(q[k],
@@ -378,6 +391,10 @@ int pbx_comm_allreduce(void *comm, const void *d_send, void *d_recv, int64_t cou
                        int op);
 int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv,
                            int64_t count);
+/* all-reduce of a small HOST array in place (dtype / op as above) through
+ * the communicator's persistent device + pinned staging: no allocation per
+ * call, one stream sync (the profile partials of ShardedProfile) */
+int pbx_comm_allreduce_host(void *comm, void *h_buf, int64_t count, int dtype, int op);
 /* Control plane on the same communicator: device barrier (returns after
  * every rank reached it and the stream drained) and max over ranks of a
  * host double. */

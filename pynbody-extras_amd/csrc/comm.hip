@@ -27,7 +27,13 @@ struct Comm {
   int nranks = 0;
   int rank = 0;
   int device = -1;
+  // persistent staging of pbx_comm_allreduce_host (HBM + pinned host),
+  // grown on demand: no allocation per call
+  void *dstage = nullptr, *hstage = nullptr;
+  size_t stage_bytes = 0;
 };
+
+static size_t dtype_size(int dtype) { return dtype == 3 ? 4 : 8; }
 
 }  // namespace pbx
 
@@ -72,6 +78,8 @@ int pbx_comm_destroy(void *comm) {
     Comm *c = (Comm *)comm;
     if (!c) return;
     if (c->nccl) PBX_NCCL(ncclCommDestroy(c->nccl));
+    if (c->dstage) (void)hipFree(c->dstage);
+    if (c->hstage) (void)hipHostFree(c->hstage);
     delete c;
   });
 }
@@ -155,6 +163,42 @@ int pbx_comm_allreduce(void *comm, const void *d_send, void *d_recv, int64_t cou
     Device &d = current_device();
     PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, types[dtype], ops[op], c->nccl,
                            d.stream));
+  });
+}
+
+// All-reduce of a small host array in place (dtype / op as above): one H2D,
+// the collective and one D2H on the library stream through the
+// communicator's persistent staging, one stream sync.
+int pbx_comm_allreduce_host(void *comm, void *h_buf, int64_t count, int dtype, int op) {
+  return guard([&] {
+    Comm *c = (Comm *)comm;
+    if (!c) fail(PBX_ERR_VALUE, "null communicator");
+    static const ncclDataType_t types[] = {ncclFloat64, ncclInt64, ncclUint64, ncclUint32};
+    static const ncclRedOp_t ops[] = {ncclSum, ncclMin, ncclMax};
+    if (dtype < 0 || dtype > 3) fail(PBX_ERR_VALUE, "bad dtype %d", dtype);
+    if (op < 0 || op > 2) fail(PBX_ERR_VALUE, "bad reduction op %d", op);
+    if (count < 0) fail(PBX_ERR_VALUE, "negative count");
+    Device &d = current_device();
+    if (d.id != c->device) fail(PBX_ERR_VALUE, "communicator belongs to device %d", c->device);
+    const size_t bytes = dtype_size(dtype) * (size_t)count;
+    if (bytes == 0) return;
+    if (bytes > c->stage_bytes) {
+      if (c->dstage) (void)hipFree(c->dstage);
+      if (c->hstage) (void)hipHostFree(c->hstage);
+      c->dstage = c->hstage = nullptr;
+      c->stage_bytes = 0;
+      const size_t want = bytes < 65536 ? 65536 : bytes;
+      PBX_HIP(hipMalloc(&c->dstage, want));
+      PBX_HIP(hipHostMalloc(&c->hstage, want, hipHostMallocDefault));
+      c->stage_bytes = want;
+    }
+    std::memcpy(c->hstage, h_buf, bytes);
+    PBX_HIP(hipMemcpyAsync(c->dstage, c->hstage, bytes, hipMemcpyHostToDevice, d.stream));
+    PBX_NCCL(ncclAllReduce(c->dstage, c->dstage, (size_t)count, types[dtype], ops[op], c->nccl,
+                           d.stream));
+    PBX_HIP(hipMemcpyAsync(c->hstage, c->dstage, bytes, hipMemcpyDeviceToHost, d.stream));
+    PBX_HIP(hipStreamSynchronize(d.stream));
+    std::memcpy(h_buf, c->hstage, bytes);
   });
 }
 

@@ -58,12 +58,18 @@ __device__ __forceinline__ uint64_t peers8(uint32_t d, uint64_t valid) {
 }
 
 // bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
-// x == e[nb] -> nb-1, invalid (NaN / out of range) -> nb (bins.py:368-379).
+// x == e[nb] -> nb-1, invalid (out of range) -> nb (bins.py:368-379).
 // Branchless lower bound over the nb+1 edges: the trip count depends on nb
 // only (uniform), so a wave's searches never diverge.  "e[k] < v" is
 // monotone in k for sorted edges (a NaN edge, sorted last by numpy, compares
 // false like +inf), so this is the first k with !(e[k] < v) exactly as the
 // classic bisection finds it.
+// NaN x: numpy orders NaN after every number and equal to a NaN edge, so
+// searchsorted returns the first NaN edge (nb + 1 when there is none, then
+// the particle is dropped): with NaN edges — equaln over x holding NaN and
+// no window, bins.py:734-744 — NaN particles land in the bin below the first
+// NaN edge, as np.digitize(right=True) puts them (checked against the
+// reference's _assign_particles).
 template <class E>
 __device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
   int base = 0, len = nb + 1;
@@ -72,11 +78,22 @@ __device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
     base = (e[base + half] < v) ? base + half : base;
     len -= half;
   }
-  const int lo = base + (e[base] < v ? 1 : 0);  // first k with e[k] >= v  (NaN: 0)
+  const int lo = base + (e[base] < v ? 1 : 0);  // first k with e[k] >= v
   int b = lo - 1;
   if (v == e[0]) b = 0;
   if (v == e[nb]) b = nb - 1;
-  if (v != v) b = nb;  // searchsorted puts NaN past every edge
+  if (v != v) {  // rare: first NaN edge (NaN edges are the tail of the sorted edges)
+    int j = nb + 1;
+    if (e[nb] != e[nb]) {
+      int l = 0, h = nb;  // first k with e[k] NaN, e[nb] is
+      while (l < h) {
+        const int m = (l + h) >> 1;
+        if (e[m] != e[m]) h = m; else l = m + 1;
+      }
+      j = l;
+    }
+    b = j - 1;
+  }
   return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
 }
 
@@ -393,22 +410,27 @@ struct Buf {
 
 // Pinned host staging (hipHostMalloc), grown on demand: D2H copies into it
 // stay asynchronous, so a batch of readbacks costs one stream sync.
+// mapped = true: coherent host memory a kernel stores its (small) results
+// into directly (dev = its device address) — no copy on the stream.
 struct HostBuf {
-  void *p = nullptr;
+  void *p = nullptr, *dev = nullptr;
   size_t bytes = 0;
+  bool mapped = false;
   void *get(size_t need) {
     if (need <= bytes) return p;
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     bytes = 0;
     size_t want = need < 4096 ? 4096 : need;
-    PBX_HIP(hipHostMalloc(&p, want, hipHostMallocDefault));
+    PBX_HIP(hipHostMalloc(&p, want,
+                          mapped ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault));
+    if (mapped) PBX_HIP(hipHostGetDevicePointer(&dev, p, 0));
     bytes = want;
     return p;
   }
   void release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     bytes = 0;
   }
 };

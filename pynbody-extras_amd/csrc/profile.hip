@@ -1614,7 +1614,8 @@ __global__ void __launch_bounds__(BT)
 // the group's segment (for fused_finish) and, with its weight and position,
 // to this block's list of deferred keys (fix_deferred bins them once the
 // edges are known, block by block, so its writes stay inside the block's
-// own tiles).  NaN is invalid either way.  Blocks walk fused_hist0's tile
+// own tiles).  NaN keys are binned like the others (bin_of's NaN rule: the
+// bin below the first NaN edge, else dropped).  Blocks walk fused_hist0's tile
 // ranges (tile_range), so block b fills exactly the segment slots fused_boff
 // gave it, and its list lies at the exclusive sum of the earlier blocks'
 // gathered counts (bcnt).  Bins are bytes (nb < 256; invalid = nb).
@@ -1756,10 +1757,10 @@ __global__ void __launch_bounds__(MS0_TPB)
         if (e & 0x8000u) {
           const uint32_t g = e & 0x7fffu;
           go.seg[atomicAdd(&sslot[g], 1u)] = key - lo;
-          defer = xv == xv;
-          if (defer) go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{key - lo, P.m[kk], P.pos[kk], t};
-        } else if (xv == xv) {
-          b = e;
+          defer = true;  // NaN too: its bin is below the first NaN edge, if any (bin_of)
+          go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{key - lo, P.m[kk], P.pos[kk], t};
+        } else {
+          b = e;  // (NaN in a digit without edges: no NaN edge, dropped like the table says)
         }
       }
       if (defer) continue;
@@ -1854,7 +1855,7 @@ __global__ void __launch_bounds__(MS0_TPB)
     for (int u = 0; u < FD_U; ++u) {
       const int64_t i = i0 + u * MS0_TPB + tid;
       const double v = dkey_inv(lo + r[u].off);
-      const bool ok = i < cnt;  // (no NaN keys: assign_gather binned those)
+      const bool ok = i < cnt;
       const uint32_t b = ok ? bin_of(v, e, nb) : (uint32_t)nb;
       if (ok) {
         bins[r[u].pos] = (uint8_t)b;
@@ -2454,6 +2455,10 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   if (!grid_sync(a.bar, a.gen0 + 4, nt, &s_ok)) return;
   MONO_STAMP(4);
   if (!ok2) {  // nothing to bin: the control record tells the host
+    // every block takes this branch (ctl0 is the same in all of them); the
+    // fifth barrier keeps the counters at the generation the host carries
+    // (gen0 + 5), or the next call on this handle would wait one short
+    if (!grid_sync(a.bar, a.gen0 + 5, nt, &s_ok)) return;
     constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
     if (t == 0 && tid < NC) a.pack[tid] = ((const double *)&s_ctl)[tid];
     mono_done(a, NC + nq + nb + a.fs.nm * nb);
@@ -2947,6 +2952,10 @@ struct Profile {
   Buf mono, bar, mono_trace;
   uint64_t bar_gen = 0, bar_done = 0;
   uint32_t bar_n = 0;  // grid size the barrier words were counted for (0: reset)
+  prim::HostBuf mpin{nullptr, nullptr, 0, true};  // radial_mono's results pack (mapped host)
+  // path counters (pbx_profile_path_stats): one-launch calls, of them
+  // discarded (re-run by the multi-kernel path), multi-kernel calls
+  int64_t n_mono = 0, n_mono_discard = 0, n_multi = 0;
 };
 
 static void ensure_x(Profile &P, hipStream_t st);
@@ -3652,7 +3661,11 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   a.counts = (unsigned long long *)P.counts.get(sizeof(uint64_t) * (size_t)(nb + 1));
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
   const int ntot = NC + nq + nb + macc;
-  a.pack = (double *)P.fpack.get(sizeof(double) * (size_t)(ntot + 1));
+  // the pack lands in mapped host memory: the kernel's stores are the
+  // readback (no copy on the stream), the host reads it after the sync
+  double *hp = (double *)P.mpin.get(sizeof(double) * (size_t)(ntot + 1));
+  a.pack = (double *)P.mpin.dev;
+  hp[ntot] = __builtin_bit_cast(double, ~0ull);
   if (P.bar_n != nt || !P.bar.p) {  // counters are counted for one grid size
     P.bar.get(sizeof(uint64_t) * BAR_WORDS);
     PBX_HIP(hipMemsetAsync(P.bar.p, 0, sizeof(uint64_t) * BAR_WORDS, st));
@@ -3671,12 +3684,11 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   PBX_HIP(hipGetLastError());
   P.bar_gen += 5;
   P.bar_done += nt;
-  double *hp = (double *)P.pin.get(sizeof(double) * (size_t)(ntot + 1));
-  hp[ntot] = __builtin_bit_cast(double, ~0ull);
-  PBX_HIP(hipMemcpyAsync(hp, a.pack, sizeof(double) * (ntot + 1), hipMemcpyDeviceToHost, st));
+  ++P.n_mono;
   PBX_HIP(hipStreamSynchronize(st));
-  if (__builtin_bit_cast(uint64_t, hp[ntot]) != a.gen0) {
+  if (__builtin_bit_cast(uint64_t, ((volatile double *)hp)[ntot]) != a.gen0) {
     P.bar_n = 0;  // discarded: zero the barrier words before the next call
+    ++P.n_mono_discard;
     return nullptr;
   }
   if (a.trace) {  // per phase: min / max over blocks of the stamp, relative to the earliest start
@@ -3740,7 +3752,18 @@ int pbx_profile_destroy(void *handle) {
                   &p->mono_trace};
     for (Buf *b : all) b->release();
     p->pin.release();
+    p->mpin.release();
     delete p;
+  });
+}
+
+int pbx_profile_path_stats(void *handle, int64_t *out) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (!out) fail(PBX_ERR_VALUE, "null output");
+    out[0] = P.n_mono;
+    out[1] = P.n_mono_discard;
+    out[2] = P.n_multi;
   });
 }
 
@@ -4272,6 +4295,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       hp = radial_mono_run(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
                            nbins, ka, kb, empty_bounds, fs, &nsum);
     if (!hp) {  // the multi-kernel path
+      ++P.n_multi;
       const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
                                         nfam, ndim, lazy, 0, 0, /*tiled=*/true);
       const int64_t n_sel = nt ? P.sel_span : 0;  // tiled particles (the families' span)

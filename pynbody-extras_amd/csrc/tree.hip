@@ -2170,11 +2170,16 @@ constexpr int RM_MAXB = 1024;
 __global__ void __launch_bounds__(TPB)
     radial_moments_kernel(const double4 *__restrict__ rec, const double *__restrict__ f,
                           int64_t first, int64_t count, const double *__restrict__ edges, int nb,
-                          double *__restrict__ slab, uint32_t *__restrict__ cslab) {
+                          double *__restrict__ slab, uint32_t *__restrict__ cslab,
+                          int e_lds) {
   extern __shared__ __attribute__((aligned(16))) double rm_sm[];
-  double *e = rm_sm, *acc = rm_sm + (nb + 1);
+  // edges in LDS when everything fits the 64 KB a workgroup may allocate
+  // (nb <= 963); above that they are read from global memory (L1/L2-hot)
+  const double *e = e_lds ? rm_sm : edges;
+  double *acc = rm_sm + (e_lds ? nb + 1 : 0);
   uint32_t *cnt = (uint32_t *)(acc + 7 * (int64_t)nb);
-  for (int k = threadIdx.x; k <= nb; k += TPB) e[k] = edges[k];
+  if (e_lds)
+    for (int k = threadIdx.x; k <= nb; k += TPB) rm_sm[k] = edges[k];
   for (int k = threadIdx.x; k < 7 * nb; k += TPB) acc[k] = 0.0;
   for (int k = threadIdx.x; k < nb; k += TPB) cnt[k] = 0u;
   __syncthreads();
@@ -2483,9 +2488,11 @@ int pbx_octree_radial_moments(pbx_octree *t, int64_t first, int64_t count, const
     prim::HostBuf &hb = T.rm_pin;
     double *hp = (double *)hb.get(ob);
     PBX_HIP(hipMemcpyAsync(de, h_edges, eb, hipMemcpyHostToDevice, st));
-    const size_t lds = eb + sizeof(double) * 7 * nb + sizeof(uint32_t) * nb;
+    const size_t lds_acc = sizeof(double) * 7 * nb + sizeof(uint32_t) * nb;
+    const int e_lds = eb + lds_acc <= 65536 ? 1 : 0;
+    const size_t lds = (e_lds ? eb : 0) + lds_acc;  // <= 61,440 B at RM_MAXB
     hipLaunchKernelGGL(radial_moments_kernel, dim3(rows), dim3(TPB), lds, st, T.rec.as<double4>(),
-                       d_f, first, count, (const double *)de, nb, slab, cslab);
+                       d_f, first, count, (const double *)de, nb, slab, cslab, e_lds);
     hipLaunchKernelGGL(radial_moments_reduce, dim3(nblk(8 * (int64_t)nb)), dim3(TPB), 0, st,
                        (const double *)slab, (const uint32_t *)cslab, rows, nb, out);
     PBX_HIP(hipGetLastError());

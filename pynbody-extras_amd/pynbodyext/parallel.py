@@ -88,17 +88,13 @@ class Communicator:
                  int(op))
 
     def allreduce_host(self, a: np.ndarray, op: int = OP_SUM) -> np.ndarray:
-        """All-reduce of a small host array (f64 / i64 / u64 / u32) through HBM."""
-        a = np.ascontiguousarray(a)
+        """All-reduce of a small host array (f64 / i64 / u64 / u32) through the
+        communicator's persistent HBM staging (one call, one stream sync)."""
+        out = np.array(a, copy=True, order="C")
         dt = {np.dtype(np.float64): DT_F64, np.dtype(np.int64): DT_I64,
-              np.dtype(np.uint64): DT_U64, np.dtype(np.uint32): DT_U32}[a.dtype]
-        buf = nat.DeviceArray.from_host(a)
-        try:
-            self.allreduce(buf.ptr, buf.ptr, a.size, dt, op)
-            out = np.empty_like(a)
-            buf.download(out)
-        finally:
-            buf.free()
+              np.dtype(np.uint64): DT_U64, np.dtype(np.uint32): DT_U32}[out.dtype]
+        nat.call("pbx_comm_allreduce_host", self.handle, out.ctypes.data_as(c_void_p), out.size,
+                 dt, int(op))
         return out
 
     def barrier(self) -> None:
@@ -359,10 +355,9 @@ class ShardedTree:
         first, count = self.ranges[self.rank] if self.ranges else (0, self.n)
         counts, mom = self.tree._radial_moments_device(first, count, self.d_pot.ptr, edges)
         if self.comm is not None and self.world > 1:
-            buf = nat.DeviceArray.from_host(np.concatenate([mom.ravel(), counts.astype(np.float64)]))
-            self.comm.allreduce_sum_f64(buf.ptr, buf.ptr, mom.size + counts.size)
-            flat = buf.download(np.empty(mom.size + counts.size))
-            buf.free()
+            # one all-reduce of [moments | counts] through the communicator's
+            # persistent staging (no allocation per step)
+            flat = self.comm.allreduce_host(np.concatenate([mom.ravel(), counts.astype(np.float64)]))
             mom = flat[:mom.size].reshape(mom.shape)
             counts = np.rint(flat[mom.size:]).astype(np.int64)
         if dev_bins is not None:

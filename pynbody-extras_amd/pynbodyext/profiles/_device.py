@@ -131,7 +131,23 @@ class DeviceBins:
                       into: "DeviceBins | None" = None):
         """select() followed by binned_equaln() with ONE host round trip
         (pbx_profile_radial_equaln).  Returns (handle, edges, counts, moments)
-        with the same values and errors as the two calls."""
+        with the same values and errors as the two calls.
+
+        With ``on_device=True`` the selection is lazy: the weights of the kept
+        particles are read from the caller's ``mass`` device array by the
+        first later call that needs them (moments(), selection(w=True),
+        weighted percentiles) and held by the handle from then on, so that
+        array must stay alive and unchanged until that call or the next
+        selection on this handle (pbx.h, pbx_profile_radial_equaln).  Host
+        arrays are staged into the handle and carry no such contract."""
+        if not on_device and (np.asarray(pos).dtype == np.float32 or
+                              (mass is not None and np.asarray(mass).dtype == np.float32)):
+            # float32 snapshots: r in float32 arithmetic exactly as select()
+            # computes it (the one-sync kernels read float64 only), then the
+            # same binning pass — identical to select() + binned_equaln()
+            d = cls.select(pos, mass, sphere=sphere, families=families, ndim=ndim, into=into)
+            edges, counts, mom = d.binned_equaln(nbins, bin_min, bin_max, stats, csr)
+            return d, edges, counts, [m.copy() for m in mom]
         d = into if into is not None else cls()
         d.nbins, d._csr = None, None
         nq = int(nbins) + 1
@@ -185,6 +201,14 @@ class DeviceBins:
         counts = counts.copy()  # (the staging arrays are reused by the next call)
         d.counts = counts
         return d, edges[: ne.value].copy(), counts, [mom[i].copy() for i in range(k)]
+
+    def path_stats(self) -> dict:
+        """Which path radial_equaln took on this handle: one-launch calls,
+        of them discarded at a grid barrier (re-run by the multi-kernel path),
+        multi-kernel calls (pbx_profile_path_stats)."""
+        out = np.zeros(3, dtype=np.int64)
+        nat.call("pbx_profile_path_stats", self._h, _i64(out))
+        return {"mono": int(out[0]), "mono_discarded": int(out[1]), "multi": int(out[2])}
 
     def selection(self, idx=True, x=True, w=True):
         """(original indices int64, x, weights) of the fused selection."""

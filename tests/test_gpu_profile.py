@@ -204,12 +204,15 @@ def test_fused_builder_matches_oracle_config3(gpu):
                                rtol=1e-12)
 
 
-def test_fused_config3_large_input_path(gpu):
-    """Config 3 at 8M particles (> 1024 tiles): the 256-thread selection, the
-    8-tiles-per-block assignment and the bin counts taken from the scanned
-    CSR histogram, bit-exact against the oracle (the 1M case above runs the
-    small-input 1024-thread kernels)."""
-    n = 8_000_000
+@pytest.mark.parametrize("n", [8_000_000, 32_000_000])
+def test_fused_config3_large_input_path(gpu, n):
+    """Config 3 on the tiled path (>= 1024 selection tiles of the dm span:
+    1,172 tiles at 8M, 4,688 at 32M): the 512-thread lazy selection
+    (select_onepass<512>), fused_hist0 over tile ranges, assign_gather with
+    byte bins and the deferred edge-digit keys (fix_deferred), csr_sel and
+    the counts from the scanned [bin][tile] table — edges, counts and CSR
+    bit-exact against the oracle, sums to 1e-12 (the 1M case above runs
+    the one-launch radial_mono)."""
     sim = plummer_snapshot(n, seed=1004)
     prof = RadialProfileBuilder(ndim=3, weight="mass", bins_type="equaln", nbins=128).filter(
         Sphere(10.0) & FamilyFilter("dm"))(sim)
@@ -494,6 +497,37 @@ def test_profile_median_uses_device(gpu, monkeypatch):
     assert len(calls) == 3
 
 
+def _oracle_radial(pos, mass, sphere, fams, nb, lo, hi):
+    """oracle/profile_ref restatement of the selection (Sphere & family
+    ranges, r = sqrt((x*x+y*y)+z*z)) + equaln edges + assignment."""
+    keep = np.ones(len(pos), dtype=bool)
+    if sphere is not None:
+        keep &= pr.sphere_mask(pos, sphere[1], sphere[0])
+    if fams is not None:
+        fm = np.zeros(len(pos), dtype=bool)
+        for a0, b0 in fams:
+            fm[max(a0, 0):max(b0, 0)] = True
+        keep &= fm
+    x = pr.radial_r(pos[keep])
+    w = mass[keep] if mass is not None else np.ones(len(x))
+    edges = pr.edges_equaln(x, nb, lo, hi)
+    perm, offsets, counts = pr.assign(x, edges)
+    return {"x": x, "w": w, "edges": edges, "perm": perm, "offsets": offsets, "counts": counts}
+
+
+def _oracle_col(ref, f_src, w_src, col):
+    """Per-bin column `col` of pbx_profile_moments ({Σw, Σf·w, Σf²·w, Σf,
+    Σf², Σ|f|·w, Σ|f|}) from the oracle's CSR, numpy sums."""
+    f = ref["x"] if f_src == 0 else ref["w"]
+    w = None if w_src == -1 else (ref["x"] if w_src == 0 else ref["w"])
+    a = np.abs(f)
+    terms = [w, f * w if w is not None else None, f * f * w if w is not None else None, f, f * f,
+             a * w if w is not None else None, a]
+    t = terms[col]
+    perm, offs = ref["perm"], ref["offsets"]
+    return np.array([t[perm[offs[i]:offs[i + 1]]].sum() for i in range(len(offs) - 1)])
+
+
 @pytest.mark.parametrize("case", ["plummer", "sphere_family", "clip", "nan", "single", "dups",
                                   "skewed", "empty_window", "nothing_kept", "many_stats",
                                   "family_offset", "no_mass", "wide", "wide_family",
@@ -585,6 +619,21 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
             p1, o1 = a.csr()
             p2, o2 = b.csr()
             assert np.array_equal(p1, p2) and np.array_equal(o1, o2)
+            # and against the oracle (bins.py:720-746 / :346-395,
+            # proarray.py sums) on the same particles, not only the stepwise
+            # device path
+            ref = _oracle_radial(pos, mass, sphere, fams, nb, lo, hi)
+            assert a.n == len(ref["x"])
+            assert np.array_equal(e1, ref["edges"], equal_nan=True), (e1, ref["edges"])
+            assert np.array_equal(c1, ref["counts"])
+            assert np.array_equal(o1, ref["offsets"]) and np.array_equal(p1, ref["perm"])
+            ne = c1 > 0
+            for (f, w, cols), got in zip(stats, m1):
+                for col in range(7):
+                    if (cols >> col) & 1 and not (w == -1 and col in (0, 1, 2, 5)):
+                        want = _oracle_col(ref, f, w, col)
+                        np.testing.assert_allclose(got[ne, col], want[ne], rtol=1e-12,
+                                                   atol=1e-12 * np.nanmax(np.abs(want[ne])))
             # the handle is usable afterwards like a stepwise one (a lazy
             # selection materialises its weights / indices on demand)
             np.testing.assert_allclose(a.moments(SRC_X, SRC_W, 0x7f), b.moments(SRC_X, SRC_W, 0x7f),
@@ -647,5 +696,115 @@ def test_radial_equaln_one_launch_reused_handle_and_size_boundary(gpu):
                     np.testing.assert_allclose(u, v, rtol=1e-13, atol=1e-300)
             finally:
                 b.close()
+        st = h.path_stats()
+        # 2 calls per size, all one-launch except the 257-tile size
+        assert st["mono"] == 2 * (len(sizes) - 1) and st["mono_discarded"] == 0, st
+        assert st["multi"] == 2, st
     finally:
         h.close()
+
+
+@pytest.mark.parametrize("first", ["nothing_kept", "empty_window"])
+def test_radial_mono_empty_call_then_normal_call(gpu, first):
+    """A one-launch call that has nothing to bin (no particle kept, or an
+    empty bin_min/bin_max window) still passes all five grid barriers, so the
+    barrier generation the handle carries stays right: the next normal call
+    on the same handle runs one-launch again (no discard, no barrier-word
+    reset) and equals the oracle."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W
+
+    rng = np.random.default_rng(5)
+    n = 300_000
+    pos, mass = rng.normal(scale=2.0, size=(n, 3)), rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3)]
+    h = DeviceBins()
+    try:
+        DeviceBins.radial_equaln(pos, mass, nbins=64, stats=stats, into=h)
+        for _ in range(2):
+            if first == "nothing_kept":
+                with pytest.raises(ValueError):
+                    DeviceBins.radial_equaln(pos, mass, nbins=64, stats=stats, into=h,
+                                             sphere=((1e6, 0.0, 0.0), 1.0))
+            else:
+                with pytest.raises(IndexError):
+                    DeviceBins.radial_equaln(pos, mass, nbins=64, stats=stats, into=h,
+                                             bin_min=1e9, bin_max=2e9)
+            _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=64, stats=stats, into=h)
+            ref = _oracle_radial(pos, mass, None, None, 64, None, None)
+            assert np.array_equal(e, ref["edges"]) and np.array_equal(c, ref["counts"])
+            np.testing.assert_allclose(m[0][:, 3], _oracle_col(ref, 1, -1, 3), rtol=1e-12)
+        st = h.path_stats()
+        assert st == {"mono": 5, "mono_discarded": 0, "multi": 0}, st
+    finally:
+        h.close()
+
+
+def test_radial_equaln_float32_snapshot_equals_select(gpu):
+    """float32 pos / mass through radial_equaln: r in float32 arithmetic like
+    numpy on a float32 snapshot — the same edges, counts, CSR and sums as
+    select() (which keeps float32) + binned_equaln, and the oracle on the
+    float32 r."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(17)
+    n = 250_000
+    pos = rng.normal(scale=3.0, size=(n, 3)).astype(np.float32)
+    mass = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    a, e1, c1, m1 = DeviceBins.radial_equaln(pos, mass, nbins=100, sphere=((0.0, 0.0, 0.0), 6.0),
+                                             stats=stats)
+    b = DeviceBins.select(pos, mass, sphere=((0.0, 0.0, 0.0), 6.0))
+    try:
+        e2, c2, m2 = b.binned_equaln(100, None, None, stats)
+        assert np.array_equal(e1, e2) and np.array_equal(c1, c2)
+        for u, v in zip(m1, m2):
+            np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300)
+        assert np.array_equal(a.csr()[0], b.csr()[0])
+        keep = pr.sphere_mask(pos.astype(np.float64), 6.0)
+        p = pos[keep]
+        r = np.sqrt((p[:, 0] * p[:, 0] + p[:, 1] * p[:, 1]) + p[:, 2] * p[:, 2])  # float32
+        assert r.dtype == np.float32
+        edges = pr.edges_equaln(r.astype(np.float64), 100)
+        assert np.array_equal(e1, edges)
+        _, _, counts = pr.assign(r.astype(np.float64), edges)
+        assert np.array_equal(c1, counts)
+    finally:
+        a.close()
+        b.close()
+
+
+def test_lazy_selection_reads_device_mass_at_use(gpu):
+    """The documented lifetime contract of an on-device lazy selection
+    (pbx.h, pbx_profile_radial_equaln): the kept particles' weights are read
+    from the caller's mass array by the first later call that needs them
+    and held by the handle from then on.  Unchanged array: moments() equal
+    the oracle's, and a later overwrite no longer matters; an overwrite
+    BEFORE that first use is what the next call sees."""
+    from pynbodyext import _native as nat
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W
+
+    rng = np.random.default_rng(8)
+    n = 200_000
+    pos, mass = rng.normal(size=(n, 3)), rng.uniform(0.5, 1.5, n)
+    d_pos, d_mass = nat.DeviceArray.from_host(pos), nat.DeviceArray.from_host(mass)
+    stats = [(SRC_W, SRC_NONE, 1 << 3)]
+    ref = _oracle_radial(pos, mass, None, None, 32, None, None)
+    want = _oracle_col(ref, 1, -1, 3)
+    try:
+        h = DeviceBins.radial_equaln(d_pos.ptr, d_mass.ptr, nbins=32, on_device=True, n=n,
+                                     stats=stats)[0]
+        try:
+            np.testing.assert_allclose(h.moments(SRC_W, SRC_NONE, 1 << 3)[:, 3], want, rtol=1e-12)
+            d_mass.upload(2.0 * mass)  # after the first use: the handle holds the weights
+            np.testing.assert_allclose(h.moments(SRC_W, SRC_NONE, 1 << 3)[:, 3], want, rtol=1e-12)
+            d_mass.upload(mass)
+            DeviceBins.radial_equaln(d_pos.ptr, d_mass.ptr, nbins=32, on_device=True, n=n,
+                                     stats=stats, into=h)
+            d_mass.upload(2.0 * mass)  # before the first use: read by it
+            np.testing.assert_allclose(h.moments(SRC_W, SRC_NONE, 1 << 3)[:, 3], 2.0 * want,
+                                       rtol=1e-12)
+        finally:
+            h.close()
+    finally:
+        d_pos.free()
+        d_mass.free()

@@ -377,6 +377,37 @@ def test_range_walk_shards_equal_full(gpu):
         dev._compute_range_device(0.5, nat.WANT_POT, n - 5, 10, 1, d_pot.ptr, None, None)
 
 
+@pytest.mark.parametrize("nbins", [963, 964, 1024])
+def test_radial_moments_max_bins(gpu, nbins):
+    """pbx_octree_radial_moments at the largest bin counts: up to 963 bins the
+    edges sit in LDS next to the accumulators, above that (the LDS a
+    workgroup may allocate is 64 KB) they are read from global memory; both
+    equal select + assign + moments of the same range, up to RM_MAXB."""
+    from pynbodyext import _native as nat
+    from pynbodyext.profiles._device import SRC_W, DeviceBins
+
+    n = 200_000
+    pos, mass = plummer(n, seed=98)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    d_pot, d_spos, d_smass = nat.DeviceArray(8 * n), nat.DeviceArray(24 * n), nat.DeviceArray(8 * n)
+    try:
+        dev._compute_range_device(0.5, nat.WANT_POT, 0, n, 1, d_pot.ptr, None, None)
+        edges = np.logspace(np.log10(0.005), np.log10(60.0), nbins + 1)
+        c_f, m_f = dev._radial_moments_device(0, n, d_pot.ptr, edges)
+        dev._leaf_particles_device(0, n, d_spos.ptr, d_smass.ptr, None)
+        part = DeviceBins.select(d_spos.ptr, d_smass.ptr, ndim=3, on_device=True, n=n)
+        try:
+            assert np.array_equal(c_f, part.assign(edges))
+            np.testing.assert_allclose(m_f, part.moments(d_pot, SRC_W), rtol=1e-12, atol=1e-300)
+        finally:
+            part.close()
+        assert (c_f > 0).sum() > nbins // 2
+    finally:
+        for a in (d_pot, d_spos, d_smass):
+            a.free()
+        dev.close()
+
+
 def test_rebuild_reuses_handle(gpu):
     from pynbodyext import _native as nat
 
