@@ -176,6 +176,36 @@ def profile_parity(dev, res, ref) -> dict:
     }
 
 
+def dist_profile_parity(rank: int, world: int, n: int, res, counts):
+    """Rank 0: the global profile (edges, counts, Σm) against the oracle on
+    the concatenation of every rank's particles (regenerated from the seeds,
+    rank order), outside the timed region; other ranks return None."""
+    if rank != 0:
+        return None
+    from oracle import profile_ref as pr
+    from pynbodyext.synthetic import family_slices
+
+    dm = family_slices(n)["dm"]
+    rs, ms = [], []
+    for r in range(world):
+        pos, mass = plummer(n, seed=SEEDS.get(n, 1002) + 7919 * r)
+        keep = pr.sphere_mask(pos, 10.0)
+        keep[dm.stop:] = False
+        rs.append(pr.radial_r(pos[keep]))
+        ms.append(mass[keep])
+    x, w = np.concatenate(rs), np.concatenate(ms)
+    edges = pr.edges_equaln(x, 128)
+    perm, offs, cnt = pr.assign(x, edges)
+    msum, _ = pr.compute(w, w, perm, offs, "sum")
+    e, s, _ = res
+    with np.errstate(invalid="ignore", divide="ignore"):
+        rel = np.abs(s - msum) / np.abs(msum)
+    return {"ranks": world, "n_kept_all": int(len(x)),
+            "edges_bit_exact": bool(np.array_equal(e, edges)),
+            "counts_bit_exact": bool(np.array_equal(counts, cnt)),
+            "mass_sum_max_rel": float(np.nanmax(rel))}
+
+
 def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
     """Config 3: RadialProfileBuilder(ndim=3, weight='mass', equaln, 128 bins)
     behind Sphere(R=10) & FamilyFilter('dm'), positions / masses resident in
@@ -184,9 +214,13 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
     mass-weighted <r>.  particles/s counts every INPUT particle.
 
     With several ranks (weak scaling): every rank holds n particles of its own
-    (seed + rank), the edges are the global equaln (distributed radix select,
-    RCCL all-reduce of the digit histograms), counts and sums are
-    all-reduced; particles/s = world * n / (max-over-ranks step time)."""
+    (seed + 7919 rank), the edges are the global equaln, counts and sums are
+    global (ShardedProfile.radial_equaln: the same kernels with RCCL
+    all-reduces of the key range, the level-0 digit histogram, the gathered
+    group keys and the packed results between them; PBX_BENCH_STAGED=1: the
+    staged host-driven distributed radix select instead);
+    particles/s = world * n / (max-over-ranks step time).  Rank 0 checks the
+    first size against the oracle on all ranks' particles."""
     from pynbodyext.parallel import ShardedProfile
     from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X, DeviceBins
     from pynbodyext.synthetic import family_slices
@@ -208,6 +242,8 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
         # Mean: Σw, Σf·w) — what pynbodyext.profiles requests for them
         stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, (1 << 0) | (1 << 1))]
 
+        staged = os.environ.get("PBX_BENCH_STAGED") == "1"
+
         def step():
             if comm is None:  # selection, edges, counts, CSR and sums: one host round trip
                 _, edges, _, (msum, rmean) = DeviceBins.radial_equaln(
@@ -215,10 +251,17 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                     families=[(dm.start, dm.stop)], ndim=3, stats=stats, csr=True,
                     on_device=True, n=n, into=dev)
                 return edges, msum[:, 3], rmean
+            if not staged:  # the same pipeline with device all-reduces between its kernels
+                edges, counts, (msum, rmean) = sp.radial_equaln(
+                    d_pos.ptr, d_mass.ptr, nbins=128, sphere=((0.0, 0.0, 0.0), 10.0),
+                    families=[(dm.start, dm.stop)], ndim=3, stats=stats, csr=True,
+                    on_device=True, n=n)
+                step.counts = counts
+                return edges, msum[:, 3], rmean
             DeviceBins.select(d_pos.ptr, d_mass.ptr, sphere=((0.0, 0.0, 0.0), 10.0),
                               families=[(dm.start, dm.stop)], ndim=3, on_device=True, n=n, into=dev)
             edges = sp.edges_equaln(128)
-            sp.assign(edges)
+            step.counts = sp.assign(edges)
             dev.build_csr_on_device()
             msum = sp.moments(*stats[0])[:, 3]
             rmean = sp.moments(*stats[1])
@@ -273,6 +316,8 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
             else:
                 ref = pr.radial_profile(pos, mass, mask, "equaln", 128)
             row["parity_vs_oracle"] = profile_parity(dev, res, ref)
+        if dist is not None and n == sizes[0] and world > 1:
+            row["parity_vs_oracle"] = dist_profile_parity(rank, world, n, res, step.counts)
         dev.close()
         d_pos.free()
         d_mass.free()

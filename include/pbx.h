@@ -351,6 +351,23 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                               const uint32_t *cols, int64_t *n_kept, double *h_edges,
                               int64_t *n_edges, int64_t *h_counts, int64_t *n_valid,
                               double *h_moments);
+/* pbx_profile_radial_equaln for one rank of a profile whose particles are
+ * sharded over the ranks of `comm` (the reference is
+ * single-process): pos / mass are this rank's particles, the edges are the
+ * equaln order statistics of ALL ranks' kept x (identical on every rank),
+ * h_counts / h_moments the global per-bin counts and sums, h_counts_local
+ * (nbins, may be NULL) this rank's counts; *n_kept / *n_valid and the CSR
+ * left in the handle are this rank's.  Every rank calls it with the same
+ * nbins, window and statistics.  Device all-reduces between the kernels,
+ * two host read-backs per call. */
+int pbx_profile_radial_equaln_comm(void *comm, void *handle, const double *pos, const double *mass,
+                                   int64_t n, int on_device, int use_sphere, const double *sphere,
+                                   const int64_t *fam, int nfam, int ndim, int64_t nbins,
+                                   int has_min, double bin_min, int has_max, double bin_max,
+                                   int build_csr, int n_stats, const int *f_src, const int *w_src,
+                                   const uint32_t *cols, int64_t *n_kept, double *h_edges,
+                                   int64_t *n_edges, int64_t *h_counts, int64_t *h_counts_local,
+                                   int64_t *n_valid, double *h_moments);
 /* Telemetry of pbx_profile_radial_equaln on this handle (no reference
  * counterpart): out[3] = {calls run as the one-launch persistent kernel,
  * of those the calls discarded at a grid barrier and re-run by the

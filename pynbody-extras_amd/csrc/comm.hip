@@ -35,6 +35,26 @@ struct Comm {
 
 static size_t dtype_size(int dtype) { return dtype == 3 ? 4 : 8; }
 
+static const ncclDataType_t kTypes[] = {ncclFloat64, ncclInt64, ncclUint64, ncclUint32};
+static const ncclRedOp_t kOps[] = {ncclSum, ncclMin, ncclMax};
+
+CommRanks comm_ranks(void *comm) {
+  Comm *c = (Comm *)comm;
+  if (!c) fail(PBX_ERR_VALUE, "null communicator");
+  if (current_device().id != c->device)
+    fail(PBX_ERR_VALUE, "communicator belongs to device %d", c->device);
+  return CommRanks{c->nranks, c->rank};
+}
+
+void comm_allreduce(void *comm, const void *send, void *recv, int64_t count, int dtype, int op,
+                    hipStream_t st) {
+  Comm *c = (Comm *)comm;
+  if (dtype < 0 || dtype > 3) fail(PBX_ERR_VALUE, "bad dtype %d", dtype);
+  if (op < 0 || op > 2) fail(PBX_ERR_VALUE, "bad reduction op %d", op);
+  if (count <= 0) return;
+  PBX_NCCL(ncclAllReduce(send, recv, (size_t)count, kTypes[dtype], kOps[op], c->nccl, st));
+}
+
 }  // namespace pbx
 
 using namespace pbx;

@@ -123,6 +123,18 @@ struct ScopedTimer {
   }
 };
 
+// Collectives a device pipeline issues on the library stream between its
+// kernels, without a host round trip (comm.hip, RCCL).  `comm` is a
+// pbx_comm_init handle; comm_ranks validates it for the calling thread's
+// device and returns {nranks, rank}; dtype / op are pbx_comm_allreduce's
+// codes (dtype 0 f64, 1 i64, 2 u64, 3 u32; op 0 sum, 1 min, 2 max).
+struct CommRanks {
+  int nranks, rank;
+};
+CommRanks comm_ranks(void *comm);
+void comm_allreduce(void *comm, const void *send, void *recv, int64_t count, int dtype, int op,
+                    hipStream_t st);
+
 // Direct-sum precision mode (pbx_set_precise): true -> Newton-refined
 // 1/sqrt everywhere (~1e-16); false (default, or PBX_PRECISE=0) -> the
 // all-particles symmetric kernel uses v_rsq_f64 unrefined (~5e-8).

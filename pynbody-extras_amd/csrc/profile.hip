@@ -756,6 +756,7 @@ struct FusedSetup {
   uint32_t *toff;  // tiled: the tile offsets block 0 writes
   uint32_t *zero;  // words block 0 zeroes for later kernels (fused_boff's per-block counts)
   int nzero;
+  int dist;  // one rank of several: the key range (mm slots) is global, no keys here is no error
 };
 
 // Element range of fused_hist0 / fused_gather: the kept x [0, n), or with
@@ -805,7 +806,7 @@ __device__ FusedCtl fused_ctl(const FusedSetup &f) {
   }
   const uint64_t lo = f.ka > c.kmin ? f.ka : c.kmin;
   const uint64_t hi = f.kb < c.kmax ? f.kb : c.kmax;
-  if (c.n == 0 || f.empty_bounds || lo > hi) {
+  if ((c.n == 0 && !f.dist) || f.empty_bounds || lo > hi) {
     c.err |= 2;
     c.w0 = 1;
   } else {
@@ -1058,15 +1059,33 @@ __global__ void __launch_bounds__(FR_TPB)
 __global__ void __launch_bounds__(TPB)
     fused_boff(const uint32_t *__restrict__ rows, int g0, const FusedCtl *__restrict__ ctl,
                const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ goff,
-               uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt) {
+               uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
+               uint32_t *__restrict__ lc) {
   __shared__ uint32_t wsum[NWAVE];
   const int g = blockIdx.x;
   if ((ctl->err & 2) || g >= ctl->ng) return;
   const int b = threadIdx.x;  // g0 <= TPB
   const uint32_t c = b < g0 ? rows[(int64_t)b * MS0_DIG + gdig[g]] : 0u;
-  const uint32_t ex = block_excl_scan(c, wsum, nullptr);
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan(c, wsum, &tot);
   if (b < g0) boff[(int64_t)b * MS_MAXQ + g] = goff[g] + ex;
   if (bcnt && b < g0 && c) atomicAdd(&bcnt[b], c);  // keys block b gathers, all groups
+  if (lc && b == 0) lc[g] = tot;  // distributed: this rank's keys of group g
+}
+
+// Distributed equaln: every rank's keys of group g occupy one slice of the
+// GLOBAL segment (goff from the summed histogram), ranks in order: rank r's
+// slice starts after the keys of ranks < r (lc_all[r'][g], all-reduced), so
+// the ranks' gathers fill disjoint slots of one zeroed array and a SUM
+// all-reduce of it is the all-gather of every group's keys.
+__global__ void __launch_bounds__(TPB)
+    dist_rank_offsets(const FusedCtl *__restrict__ ctl, const uint32_t *__restrict__ lc_all,
+                      int rank, int g0, uint32_t *__restrict__ boff) {
+  const int g = blockIdx.x;
+  if ((ctl->err & 2) || g >= ctl->ng) return;
+  uint32_t before = 0;
+  for (int r = 0; r < rank; ++r) before += lc_all[(int64_t)r * MS_MAXQ + g];
+  for (int b = threadIdx.x; b < g0; b += TPB) boff[(int64_t)b * MS_MAXQ + g] += before;
 }
 
 // keys of the chosen level-0 buckets -> their group's segment (key - base).
@@ -2950,6 +2969,7 @@ struct Profile {
   // one-launch radial path (radial_mono): tile records + group fill, grid
   // barrier words; barrier generation / completion count carried across calls
   Buf mono, bar, mono_trace;
+  Buf dscal, dlc;  // distributed radial_equaln: global scalars, per-rank group counts
   uint64_t bar_gen = 0, bar_done = 0;
   uint32_t bar_n = 0;  // grid size the barrier words were counted for (0: reset)
   prim::HostBuf mpin{nullptr, nullptr, 0, true};  // radial_mono's results pack (mapped host)
@@ -3749,7 +3769,7 @@ int pbx_profile_destroy(void *handle) {
                   &p->pk0, &p->pk1, &p->pv0, &p->pv1, &p->pbk, &p->pcdf, &p->poff, &p->pq, &p->pout,
                   &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack, &p->frec, &p->fblk,
                   &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->mono, &p->bar,
-                  &p->mono_trace};
+                  &p->mono_trace, &p->dscal, &p->dlc};
     for (Buf *b : all) b->release();
     p->pin.release();
     p->mpin.release();
@@ -4207,16 +4227,29 @@ int pbx_profile_percentiles(void *handle, int f_src, const double *h_f, int w_sr
 // and errors as pbx_profile_select followed by pbx_profile_binned_equaln;
 // the distinct sums of the requested statistics (<= AS_MAXM) are
 // accumulated inside the assignment pass (more: separate moment passes).
-int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mass, int64_t n,
-                              int on_device, int use_sphere, const double *sphere,
-                              const int64_t *fam, int nfam, int ndim, int64_t nbins, int has_min,
-                              double bin_min, int has_max, double bin_max, int build_csr,
-                              int n_stats, const int *f_src, const int *w_src,
-                              const uint32_t *cols, int64_t *n_kept, double *h_edges,
-                              int64_t *n_edges, int64_t *h_counts, int64_t *n_valid,
-                              double *h_moments) {
+//
+// comm (pbx_profile_radial_equaln_comm): this rank's particles of a profile
+// sharded over the communicator's ranks.  The same kernels
+// with four device all-reduces between them and one extra host read-back:
+// the selection's key-range slots (max) -> global window geometry; the
+// level-0 digit histogram (sum) -> every rank resolves the same digits and
+// groups; each rank gathers its keys of the chosen digits into its own
+// slice of the GLOBAL group segments (dist_rank_offsets) and a sum
+// all-reduce of the zeroed segment array all-gathers them -> every rank
+// finishes the same edges; the packed counts and per-bin sums (sum).  The
+// ctl read-back after the resolve sizes the segment array on the host.
+static int radial_equaln_entry(void *comm, void *handle, const double *pos, const double *mass,
+                               int64_t n, int on_device, int use_sphere, const double *sphere,
+                               const int64_t *fam, int nfam, int ndim, int64_t nbins, int has_min,
+                               double bin_min, int has_max, double bin_max, int build_csr,
+                               int n_stats, const int *f_src, const int *w_src,
+                               const uint32_t *cols, int64_t *n_kept, double *h_edges,
+                               int64_t *n_edges, int64_t *h_counts, int64_t *n_valid,
+                               double *h_moments, int64_t *h_counts_local) {
   return guard([&] {
     Profile &P = as_profile(handle);
+    const bool dist = comm != nullptr;
+    const CommRanks cr = dist ? comm_ranks(comm) : CommRanks{1, 0};
     if (nbins < 1) fail(PBX_ERR_VALUE, "nbins must be >= 1");
     if (nbins + 1 > MS_MAXQ) fail(PBX_ERR_VALUE, "the fused path supports nbins <= %d", MS_MAXQ - 1);
     if (n_stats < 0 || n_stats > 16) fail(PBX_ERR_VALUE, "at most 16 statistics");
@@ -4291,13 +4324,17 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     // small selections: the whole step as one persistent launch (radial_mono)
     double *hp = nullptr;
     int nsum = 0;
-    if (lazy && mono_enabled())
+    int64_t n_global = 0;  // dist: kept particles over all ranks
+    if (lazy && mono_enabled() && !dist)
       hp = radial_mono_run(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
                            nbins, ka, kb, empty_bounds, fs, &nsum);
     if (!hp) {  // the multi-kernel path
       ++P.n_multi;
       const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
                                         nfam, ndim, lazy, 0, 0, /*tiled=*/true);
+      if (dist)  // global key range: every min / max slot pair (~min, max) max-reduced
+        comm_allreduce(comm, (uint64_t *)P.selst.p + nt + 1, (uint64_t *)P.selst.p + nt + 1,
+                       2 * MM_SLOTS, 2, 2, st);
       const int64_t n_sel = nt ? P.sel_span : 0;  // tiled particles (the families' span)
       const bool tiled = P.x_tiled;  // x by tile (large inputs): tile offsets from fused_hist0
       uint64_t *stat = (uint64_t *)P.selst.p;
@@ -4315,11 +4352,20 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       const bool agath = tiled && lazy && n_sel && !agather_off();
       uint32_t *bcnt = agath ? (uint32_t *)P.fblk.get(sizeof(uint32_t) * 3 * (size_t)g0) : nullptr;
       const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
-                           (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0};
+                           (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0, (int)dist};
       hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
                          rows);
       hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
                          (const uint32_t *)rows, g0, H);
+      int64_t *gsc = nullptr;  // dist: [global kept count][ctl copy]
+      uint32_t *lc_all = nullptr;
+      if (dist) {
+        gsc = (int64_t *)P.dscal.get(sizeof(int64_t) * 2 + sizeof(FusedCtl));
+        lc_all = (uint32_t *)P.dlc.get(sizeof(uint32_t) * (size_t)cr.nranks * MS_MAXQ);
+        PBX_HIP(hipMemsetAsync(lc_all, 0, sizeof(uint32_t) * (size_t)cr.nranks * MS_MAXQ, st));
+        comm_allreduce(comm, &ctl->n, gsc, 1, 1, 0, st);
+        comm_allreduce(comm, H, H, MS0_DIG, 3, 0, st);
+      }
       MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
       uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)g0) * (MS_MAXQ + 1));
       uint32_t *goff = gdig + (MS_MAXQ + 1), *gq = goff + (MS_MAXQ + 1);
@@ -4328,8 +4374,28 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                          goff, gq);
       hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
                          (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff,
-                         bcnt);
-      uint64_t *seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)(n_sel ? n_sel : 1));
+                         bcnt, dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr);
+      int64_t seg_total = 0;  // dist: keys in all ranks' group segments
+      if (dist) {
+        comm_allreduce(comm, lc_all, lc_all, (int64_t)cr.nranks * MS_MAXQ, 3, 0, st);
+        hipLaunchKernelGGL(dist_rank_offsets, dim3(nq), dim3(TPB), 0, st, (const FusedCtl *)ctl,
+                           (const uint32_t *)lc_all, cr.rank, g0, boff);
+        PBX_HIP(hipGetLastError());
+        // the one extra read-back: the global segment length (and kept count)
+        FusedCtl *hc = (FusedCtl *)P.pin.get(sizeof(FusedCtl) + 16);
+        int64_t *hn = (int64_t *)(hc + 1);
+        PBX_HIP(hipMemcpyAsync(hc, ctl, sizeof(FusedCtl), hipMemcpyDeviceToHost, st));
+        PBX_HIP(hipMemcpyAsync(hn, gsc, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        PBX_HIP(hipStreamSynchronize(st));
+        n_global = *hn;
+        seg_total = (hc->err & 2) ? 0 : hc->total;
+        if (n_global >= (int64_t)1 << 32)  // (every rank sees the same count: all fail here)
+          fail(PBX_ERR_VALUE, "distributed equaln over %lld particles: the u32 digit "
+               "histograms hold at most 2**32 - 1", (long long)n_global);
+      }
+      uint64_t *seg = (uint64_t *)P.fseg.get(
+          sizeof(uint64_t) * (size_t)std::max<int64_t>(1, std::max<int64_t>(n_sel, seg_total)));
+      if (seg_total) PBX_HIP(hipMemsetAsync(seg, 0, sizeof(uint64_t) * (size_t)seg_total, st));
       double *de = (double *)P.edges.get(sizeof(double) * (size_t)nq);
       uint32_t *bins = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)(n_sel ? n_sel : 1));
       P.bins_in8 = agath;
@@ -4370,6 +4436,8 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
                            (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff,
                            seg, tiled ? (const uint64_t *)stat : nullptr, nt);
       }
+      if (dist)  // every rank's group keys, each in its own slice: the all-gather
+        comm_allreduce(comm, seg, seg, seg_total, 2, 0, st);
       hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
                          (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
                          (const uint64_t *)seg, de);
@@ -4493,16 +4561,26 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
         }
       }
       // the results packed on the device, one copy, one sync
-      nsum = maccs ? fs.nm * (int)nb : 0;
+      // (dist: every rank packs the fused sums' columns, zeros without
+      // particles, so the all-reduced regions have the same length)
+      nsum = (maccs || (dist && fs.nm)) ? fs.nm * (int)nb : 0;
+      if (!maccs) ablocks = 0;
       const int ntot = NC + nq + (int)nb + nsum;
-      double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)ntot);
+      const int nloc = dist ? (int)nb : 0;  // dist: this rank's counts after the global ones
+      double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)(ntot + nloc));
       const int nhead = (int)ceil_div(NC + nq + (int)nb, TPB);
       hipLaunchKernelGGL(fused_pack, dim3(nhead + nsum), dim3(TPB), 0, st, (const FusedCtl *)ctl,
                          (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
                          (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead,
                          (const double *)maccs2, maccs2 ? (int64_t)g0 : 0);
-      hp = (double *)P.pin.get(sizeof(double) * (size_t)ntot);
-      PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * ntot, hipMemcpyDeviceToHost, st));
+      if (dist) {
+        PBX_HIP(hipMemcpyAsync(dpk + ntot, dpk + NC + nq, sizeof(double) * nb,
+                               hipMemcpyDeviceToDevice, st));
+        comm_allreduce(comm, dpk + NC + nq, dpk + NC + nq, nb, 2, 0, st);   // counts (u64)
+        comm_allreduce(comm, dpk + NC + nq + nb, dpk + NC + nq + nb, nsum, 0, 0, st);  // sums
+      }
+      hp = (double *)P.pin.get(sizeof(double) * (size_t)(ntot + nloc));
+      PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * (ntot + nloc), hipMemcpyDeviceToHost, st));
       PBX_HIP(hipStreamSynchronize(st));
     }
     const FusedCtl *hc = (const FusedCtl *)hp;
@@ -4514,9 +4592,11 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     P.mm[0] = c.kmin;
     P.mm[1] = c.kmax;
     select_commit(P, c.n);
+    if (dist) P.mm_valid = false;  // the pack's key range is the global one
     *n_kept = c.n;
-    if (c.n == 0) fail(PBX_ERR_VALUE, "Cannot create bins: input array is empty");
+    if ((dist ? n_global : c.n) == 0) fail(PBX_ERR_VALUE, "Cannot create bins: input array is empty");
     const int64_t m = c.m;
+    int64_t sv_local = 0;  // dist: this rank's particles in bins
     if ((c.err & 2) || m == 0) fail(PBX_ERR_VALUE, "index 0 is out of bounds for axis 0 with size 0");
     std::memcpy(h_edges, he, sizeof(double) * nq);
     if (m < 2) {  // the reference's degenerate [s0, s0]: one bin, stepwise
@@ -4528,7 +4608,17 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       for (int k = 0; k < n_stats; ++k)
         moments_device(P, st, f_src[k], nullptr, P.field, w_src[k], nullptr, P.weight, cols[k],
                        accs + k * NMOM);
-      PBX_HIP(hipMemcpyAsync(h_counts, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      if (dist) {
+        PBX_HIP(hipMemcpyAsync(&sv_local, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        PBX_HIP(hipStreamSynchronize(st));
+        int64_t *gc = (int64_t *)P.dscal.get(sizeof(int64_t) * 2 + sizeof(FusedCtl));
+        PBX_HIP(hipMemcpyAsync(gc, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        comm_allreduce(comm, gc, gc, 1, 1, 0, st);
+        comm_allreduce(comm, accs, accs, (int64_t)n_stats * NMOM, 0, 0, st);
+        PBX_HIP(hipMemcpyAsync(h_counts, gc, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      } else {
+        PBX_HIP(hipMemcpyAsync(h_counts, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      }
       if (n_stats)
         PBX_HIP(hipMemcpyAsync(h_moments, accs, sizeof(double) * n_stats * NMOM,
                                hipMemcpyDeviceToHost, st));
@@ -4538,6 +4628,11 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
       P.nb = nb;
       P.csr_ready = build_csr != 0;
       std::memcpy(h_counts, hcn, sizeof(int64_t) * nb);
+      if (dist) {  // this rank's counts follow the packed (global) results
+        const int64_t *hl = (const int64_t *)(hp + NC + nq + nb + nsum);
+        for (int64_t b2 = 0; b2 < nb; ++b2) sv_local += hl[b2];
+        if (h_counts_local) std::memcpy(h_counts_local, hl, sizeof(int64_t) * nb);
+      }
       if (fs.nm) {  // expand the monomial sums into [stat][bin][column]
         for (int k = 0; k < n_stats; ++k)
           for (int64_t b2 = 0; b2 < nb; ++b2)
@@ -4549,6 +4644,7 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
         for (int k = 0; k < n_stats; ++k)
           moments_device(P, st, f_src[k], nullptr, P.field, w_src[k], nullptr, P.weight, cols[k],
                          accs + k * len);
+        if (dist) comm_allreduce(comm, accs, accs, (int64_t)n_stats * len, 0, 0, st);
         PBX_HIP(hipMemcpyAsync(h_moments, accs, sizeof(double) * n_stats * len,
                                hipMemcpyDeviceToHost, st));
         PBX_HIP(hipStreamSynchronize(st));
@@ -4558,9 +4654,42 @@ int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mas
     const int64_t nbo = *n_edges - 1;
     int64_t sv = 0;
     for (int64_t k = 0; k < nbo; ++k) sv += h_counts[k];
+    if (dist) {
+      sv = sv_local;
+      if (h_counts_local && nbo == 1 && m < 2) h_counts_local[0] = sv_local;
+    }
     P.n_valid = sv;
     *n_valid = sv;
   });
+}
+
+int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mass, int64_t n,
+                              int on_device, int use_sphere, const double *sphere,
+                              const int64_t *fam, int nfam, int ndim, int64_t nbins, int has_min,
+                              double bin_min, int has_max, double bin_max, int build_csr,
+                              int n_stats, const int *f_src, const int *w_src,
+                              const uint32_t *cols, int64_t *n_kept, double *h_edges,
+                              int64_t *n_edges, int64_t *h_counts, int64_t *n_valid,
+                              double *h_moments) {
+  return radial_equaln_entry(nullptr, handle, pos, mass, n, on_device, use_sphere, sphere, fam, nfam,
+                             ndim, nbins, has_min, bin_min, has_max, bin_max, build_csr, n_stats,
+                             f_src, w_src, cols, n_kept, h_edges, n_edges, h_counts, n_valid,
+                             h_moments, nullptr);
+}
+
+int pbx_profile_radial_equaln_comm(void *comm, void *handle, const double *pos, const double *mass,
+                                   int64_t n, int on_device, int use_sphere, const double *sphere,
+                                   const int64_t *fam, int nfam, int ndim, int64_t nbins,
+                                   int has_min, double bin_min, int has_max, double bin_max,
+                                   int build_csr, int n_stats, const int *f_src, const int *w_src,
+                                   const uint32_t *cols, int64_t *n_kept, double *h_edges,
+                                   int64_t *n_edges, int64_t *h_counts, int64_t *h_counts_local,
+                                   int64_t *n_valid, double *h_moments) {
+  if (!comm) return guard([&] { fail(PBX_ERR_VALUE, "null communicator"); });
+  return radial_equaln_entry(comm, handle, pos, mass, n, on_device, use_sphere, sphere, fam, nfam,
+                             ndim, nbins, has_min, bin_min, has_max, bin_max, build_csr, n_stats,
+                             f_src, w_src, cols, n_kept, h_edges, n_edges, h_counts, n_valid,
+                             h_moments, h_counts_local);
 }
 
 }  // extern "C"

@@ -126,6 +126,12 @@ _SIGNATURES: dict[str, tuple] = {
                                           c_double, c_int, c_double, c_int, c_int, c_void_p,
                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_void_p]),
+    "pbx_profile_radial_equaln_comm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                               c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                                               c_int64, c_int, c_double, c_int, c_double, c_int,
+                                               c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p]),
     "pbx_profile_binned_equaln": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double,
                                           c_int, c_int, POINTER(c_int), POINTER(c_int),
                                           POINTER(c_uint32), _dp, POINTER(c_int64), _i64p,

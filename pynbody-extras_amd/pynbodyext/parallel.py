@@ -416,6 +416,19 @@ class ShardedProfile:
         self.world = comm.nranks if comm is not None else 1
         self.rank = comm.rank if comm is not None else 0
 
+    def radial_equaln(self, pos, mass=None, **kw):
+        """The whole equaln radial profile of the sharded particles in one
+        call per rank (DeviceBins.radial_equaln with the communicator:
+        selection, global edges, assignment, CSR, global counts and sums with
+        device all-reduces between the kernels).  Returns (global edges,
+        global counts, global per-statistic sums); this rank's counts and CSR
+        stay in ``self.dev``."""
+        from .profiles._device import DeviceBins
+
+        _, edges, counts, mom = DeviceBins.radial_equaln(pos, mass, into=self.dev, comm=self.comm,
+                                                         **kw)
+        return edges, counts, mom
+
     def edges_equaln(self, nbins: int, bin_min=None, bin_max=None) -> np.ndarray:
         if self.comm is None:
             return self.dev.edges_equaln(nbins, bin_min, bin_max)

@@ -128,10 +128,15 @@ class DeviceBins:
     def radial_equaln(cls, pos, mass=None, *, nbins: int, sphere=None, families=None,
                       ndim: int = 3, bin_min=None, bin_max=None, stats=(), csr=True,
                       on_device: bool = False, n: int | None = None,
-                      into: "DeviceBins | None" = None):
+                      into: "DeviceBins | None" = None, comm=None):
         """select() followed by binned_equaln() with ONE host round trip
         (pbx_profile_radial_equaln).  Returns (handle, edges, counts, moments)
         with the same values and errors as the two calls.
+
+        ``comm`` (a parallel.Communicator): this rank's share of a profile
+        sharded over the ranks (pbx_profile_radial_equaln_comm) — global
+        edges, counts and sums, device all-reduces between the kernels; the
+        handle keeps this rank's selection, counts (``.counts``) and CSR.
 
         With ``on_device=True`` the selection is lazy: the weights of the kept
         particles are read from the caller's ``mass`` device array by the
@@ -140,8 +145,9 @@ class DeviceBins:
         array must stay alive and unchanged until that call or the next
         selection on this handle (pbx.h, pbx_profile_radial_equaln).  Host
         arrays are staged into the handle and carry no such contract."""
-        if not on_device and (np.asarray(pos).dtype == np.float32 or
-                              (mass is not None and np.asarray(mass).dtype == np.float32)):
+        if comm is None and not on_device and (
+                np.asarray(pos).dtype == np.float32 or
+                (mass is not None and np.asarray(mass).dtype == np.float32)):
             # float32 snapshots: r in float32 arithmetic exactly as select()
             # computes it (the one-sync kernels read float64 only), then the
             # same binning pass — identical to select() + binned_equaln()
@@ -160,7 +166,8 @@ class DeviceBins:
         if on_device:
             key = (pos, mass, None if sphere is None else (tuple(sphere[0]), float(sphere[1])),
                    None if families is None else tuple(map(tuple, families)), ndim, n,
-                   tuple(map(tuple, stats)), nbins, bin_min, bin_max, bool(csr))
+                   tuple(map(tuple, stats)), nbins, bin_min, bin_max, bool(csr),
+                   None if comm is None else comm.handle.value)
         cached = getattr(d, "_req", None)
         if key is not None and cached is not None and cached[0] == key:
             args, keep, fs, ws, cs, head, refs, outs = cached[1]
@@ -176,14 +183,22 @@ class DeviceBins:
             e_buf, c_buf = np.empty(nq), np.zeros(nbins, dtype=np.int64)
             m_buf = np.zeros((max(k, 1), nbins, NMOM))
             kept, ne, nv = refs
-            outs = (e_buf, c_buf, m_buf, (byref(kept), nat.dptr(e_buf), byref(ne), _i64(c_buf),
-                                          byref(nv), nat.dptr(m_buf)))
+            if comm is None:
+                outs = (e_buf, c_buf, m_buf, (byref(kept), nat.dptr(e_buf), byref(ne), _i64(c_buf),
+                                              byref(nv), nat.dptr(m_buf)), None)
+            else:
+                cl_buf = np.zeros(nbins, dtype=np.int64)
+                outs = (e_buf, c_buf, m_buf, (byref(kept), nat.dptr(e_buf), byref(ne), _i64(c_buf),
+                                              _i64(cl_buf), byref(nv), nat.dptr(m_buf)), cl_buf)
             if key is not None:
                 d._req = (key, (args, keep, fs, ws, cs, head, refs, outs))
         kept, ne, nv = refs
-        edges, counts, mom, optrs = outs
+        edges, counts, mom, optrs, local = outs
         try:
-            nat.call("pbx_profile_radial_equaln", d._h, *args, *head, *optrs)
+            if comm is None:
+                nat.call("pbx_profile_radial_equaln", d._h, *args, *head, *optrs)
+            else:
+                nat.call("pbx_profile_radial_equaln_comm", comm.handle, d._h, *args, *head, *optrs)
         except ValueError as e:
             if str(e).startswith("index 0 is out of bounds"):
                 raise IndexError(str(e)) from None
@@ -198,8 +213,9 @@ class DeviceBins:
         if nb != nbins:  # degenerate: one bin, compact layout [k][1][7]
             mom = mom.reshape(-1)[: max(k, 1) * NMOM].reshape(max(k, 1), 1, NMOM)
             counts = counts[:1]
+            local = local[:1] if local is not None else None
         counts = counts.copy()  # (the staging arrays are reused by the next call)
-        d.counts = counts
+        d.counts = counts if local is None else local.copy()  # this rank's (CSR lengths)
         return d, edges[: ne.value].copy(), counts, [mom[i].copy() for i in range(k)]
 
     def path_stats(self) -> dict:

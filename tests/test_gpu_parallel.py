@@ -212,3 +212,68 @@ def test_sharded_profile_world1_matches_single(gpu):
         a.close()
         b.close()
         comm.destroy()
+
+
+@pytest.mark.parametrize("case", ["small", "tiled", "family", "clip", "nan", "single", "many_stats",
+                                  "wide", "nothing_kept", "empty_window"])
+def test_radial_equaln_comm_world1_matches_single(gpu, case):
+    """pbx_profile_radial_equaln_comm through a 1-rank RCCL communicator (the
+    distributed pipeline: key-range / digit-histogram / group-key / result
+    all-reduces between the kernels, the segment sized from the mid-call
+    read-back) = the single-device pbx_profile_radial_equaln: edges, counts,
+    CSR bit-identical, sums to rounding, same errors; local counts = global."""
+    from pynbodyext.parallel import ShardedProfile
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X, DeviceBins
+
+    rng = np.random.default_rng(41)
+    n = 4_400_000 if case == "tiled" else 300_000
+    pos = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    kw = dict(nbins=128, sphere=None, families=None, bin_min=None, bin_max=None,
+              stats=[(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)])
+    if case == "family":
+        kw.update(sphere=((0.3, 0.0, -0.1), 6.0), families=[(1_000, 120_000), (150_000, 290_000)])
+    elif case == "clip":
+        kw.update(bin_min=0.5, bin_max=6.0)
+    elif case == "nan":
+        pos[::61] = np.nan
+    elif case == "single":
+        kw.update(bin_min=1.0, bin_max=1.0)
+        pos[9] = [1.0, 0.0, 0.0]
+    elif case == "many_stats":
+        kw.update(nbins=64, stats=[(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11),
+                                   (SRC_X, SRC_NONE, 0x7f), (SRC_W, SRC_W, 0x7f),
+                                   (SRC_X, SRC_W, 0x7f), (SRC_W, SRC_NONE, 0x18)])
+    elif case == "wide":
+        kw.update(nbins=300)
+    elif case == "nothing_kept":
+        kw.update(sphere=((1e6, 0.0, 0.0), 1.0))
+    elif case == "empty_window":
+        kw.update(bin_min=1e9, bin_max=2e9)
+    comm = Communicator(1, 0, Communicator.unique_id())
+    a, b = DeviceBins(), DeviceBins()
+    try:
+        sp = ShardedProfile(comm, a, offset=0)
+        if case in ("nothing_kept", "empty_window"):
+            exc = IndexError if case == "empty_window" else ValueError
+            with pytest.raises(exc) as e1:
+                sp.radial_equaln(pos, mass, **kw)
+            with pytest.raises(exc) as e2:
+                DeviceBins.radial_equaln(pos, mass, into=b, **kw)
+            assert str(e1.value) == str(e2.value)
+            return
+        for _ in range(2):  # the second call reuses the handle's buffers
+            e1, c1, m1 = sp.radial_equaln(pos, mass, **kw)
+            _, e2, c2, m2 = DeviceBins.radial_equaln(pos, mass, into=b, **kw)
+            assert np.array_equal(e1, e2, equal_nan=True)
+            assert np.array_equal(c1, c2) and np.array_equal(a.counts, c2)
+            assert a.n == b.n and a.n_valid == b.n_valid
+            for u, v in zip(m1, m2):
+                np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300)
+            p1, o1 = a.csr()
+            p2, o2 = b.csr()
+            assert np.array_equal(p1, p2) and np.array_equal(o1, o2)
+    finally:
+        a.close()
+        b.close()
+        comm.destroy()
