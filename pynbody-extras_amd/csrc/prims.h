@@ -40,6 +40,26 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+// In-launch hand-off loads / stores (relaxed agent-scope atomics: global
+// load / store ... sc1): a word stored sc1 by its producer — whose wave
+// drains vmcnt(0) before it signals — and loaded sc1 by its consumer needs
+// no release / acquire fence (a fence writes back the whole XCD L2).  Used
+// by radial_mono's grid barriers and the octree payload up-sweep.
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1d(const double *p) {
+  return __builtin_bit_cast(double, ld_sc1((const uint64_t *)p));
+}
+__device__ __forceinline__ void st_sc1d(double *p, double v) {
+  st_sc1((uint64_t *)p, __builtin_bit_cast(uint64_t, v));
+}
+
 // number of set bits of m in lanes below this lane
 __device__ __forceinline__ uint32_t rank_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),

@@ -2036,20 +2036,7 @@ constexpr size_t BAR_WORDS = (size_t)BAR_LINE * 11;
 // agent-scope release writes back the whole XCD L2 (~2-6 us per wave that
 // issues it): with one per wave per phase the first version spent ~40 us
 // per phase in fences.
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void st_sc1(T *p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1d(const double *p) {
-  return __builtin_bit_cast(double, ld_sc1((const uint64_t *)p));
-}
-__device__ __forceinline__ void st_sc1d(double *p, double v) {
-  st_sc1((uint64_t *)p, __builtin_bit_cast(uint64_t, v));
-}
+// (ld_sc1 / st_sc1 / ld_sc1d / st_sc1d: prims.h)
 
 // Grid barrier of a co-resident grid, XCD-hierarchical: a block arrives on
 // the counter of its group (block % 8, the dispatcher's XCD round robin:
