@@ -25,8 +25,7 @@ d_pos, d_mass = nat.DeviceArray.from_host(pos), nat.DeviceArray.from_host(mass)
 d_pot, d_acc = nat.DeviceArray(8 * n), nat.DeviceArray(24 * n)
 tree = Octree._from_device(d_pos.ptr, n, d_mass.ptr, 8, 3)
 want = nat.WANT_POT | nat.WANT_ACC
-for label, first, count in [("full", 0, n), ("range3of8", 1553737, 501626), ("full", 0, n),
-                            ("range3of8", 1553737, 501626)]:
+for label, first, count in [("full", 0, n), ("full", 0, n)]:
     if os.path.exists(trace):
         os.remove(trace)
     tree._compute_range_device(0.5, want, first, count, 1, d_pot.ptr, d_acc.ptr, None)
@@ -45,6 +44,11 @@ for label, first, count in [("full", 0, n), ("range3of8", 1553737, 501626), ("fu
            "last_start_us": float(s.max()),
            "t90_us": float(ends[int(0.9 * len(ends))]), "t99_us": float(ends[int(0.99 * len(ends))]),
            "steps_mean": float(st.mean()), "steps_max": int(st.max()),
-           "corr_dur_steps": float(np.corrcoef(d, st.astype(float))[0, 1])}
+           "corr_dur_steps": float(np.corrcoef(d, st.astype(float))[0, 1]),
+           "mean_concurrency": float(d.sum() / span),
+           "starts_per_us_mid": float(np.sum((s > 0.25 * span) & (s < 0.75 * span)) / (0.5 * span))}
+    # concurrency over time (waves running at 20 sample points)
+    ts = np.linspace(0, span, 21)[1:-1]
+    out["concurrency_samples"] = [int(np.sum((s <= x) & (e > x))) for x in ts]
     print(json.dumps(out), flush=True)
 tree.close()
