@@ -374,6 +374,12 @@ int pbx_profile_radial_equaln_comm(void *comm, void *handle, const double *pos, 
  * multi-kernel path (a silent ~2x slowdown if non-zero), calls that took
  * the multi-kernel path}. */
 int pbx_profile_path_stats(void *handle, int64_t *out);
+/* Telemetry of the tiled (>= 1024 selection tiles) multi-kernel calls of
+ * pbx_profile_radial_equaln on this handle (no reference counterpart):
+ * out[2] = {tiled calls, of those the calls whose level-0 digit histogram
+ * was counted by the selection kernel with the previous tiled call's digit
+ * geometry (every window key inside it), so x was not read a second time}. */
+int pbx_profile_level0_stats(void *handle, int64_t *out);
 /* Per-bin percentiles of the last assignment — replaces the per-bin loop of
  * ProfileArray._compute for Percentile / Median / Abs_pXX
  * (proarray.py:272-334 + :689-722): h_out[bin*nq + k] = np.interp(q[k],

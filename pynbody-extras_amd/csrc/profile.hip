@@ -240,7 +240,11 @@ __global__ void __launch_bounds__(BT)
   __syncthreads();
   uint32_t run = s_excl;
   for (int ww = 0; ww < w; ++ww) run += wcnt[ww];
-  if (LAZY && p.tiled) xo += (int64_t)tile * TILE;  // the tile's own slots
+  // tiled: x in particle-slot layout, the kept particle of slot j of tile t
+  // at xo[t * TILE + j] (no in-tile compaction: the readers' addresses do
+  // not wait for the keep words)
+  const bool slots = LAZY && p.tiled;
+  if (slots) xo += (int64_t)tile * TILE + (int64_t)w * (TILE / NW);
 #pragma unroll
   for (int k = 0; k < SI; ++k) {
     bool keep = (keepbits >> k) & 1u;
@@ -255,7 +259,7 @@ __global__ void __launch_bounds__(BT)
     if (keep) {
 #endif
       int64_t i = wbase + k * 64 + lane;
-      uint32_t pos_out = run + rank_below(b);
+      uint32_t pos_out = slots ? (uint32_t)(k * 64) + lane : run + rank_below(b);
       xo[pos_out] = xv[k];
       if (!LAZY) {
         if (wo) wo[pos_out] = mv[k];
@@ -332,15 +336,26 @@ __device__ uint32_t tile_scan_block(const uint64_t *__restrict__ status, uint32_
   return carry;
 }
 
-// a tiled selection's x compacted (for the consumers that read x by
-// selection index)
+// a tiled selection's per-slot values (x, or assign_gather's byte bins)
+// compacted to selection order (for the consumers that index by selection
+// index): slot 64 j + lane of tile t -> wpre[j] + its rank in word j
+template <typename T, typename U>
 __global__ void __launch_bounds__(TPB)
-    tile_compact(const double *__restrict__ xt, const uint32_t *__restrict__ toff, uint32_t nt,
-                 int64_t n, double *__restrict__ xc) {
+    tile_compact(const T *__restrict__ vt, const uint64_t *__restrict__ kw,
+                 const uint32_t *__restrict__ toff, U *__restrict__ vc) {
+  __shared__ uint64_t wrd[64];
+  __shared__ uint32_t wpre[64];
   const uint32_t t = blockIdx.x;
-  const uint32_t o = toff[t];
-  const uint32_t c = (uint32_t)((t + 1 < nt ? (int64_t)toff[t + 1] : n) - o);
-  for (uint32_t j = threadIdx.x; j < c; j += TPB) xc[o + j] = xt[(int64_t)t * TILE + j];
+  sel_tile_words(kw, toff, t, wrd, wpre);
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+#pragma unroll 4
+  for (int k = 0; k < 16; ++k) {
+    const int j = w * 16 + k;
+    const uint64_t word = wrd[j];
+    if ((word >> lane) & 1ull) vc[wpre[j] + rank_below(word)] = (U)vt[(int64_t)t * TILE + 64 * j + lane];
+  }
 }
 
 // weights and original indices of a lazy selection, materialised on demand
@@ -493,6 +508,37 @@ __global__ void __launch_bounds__(TPB)
   uint32_t s = 0;
   for (int r = blockIdx.y; r < nrows; r += gridDim.y) s += rows[(int64_t)r * MS0_DIG + d];
   if (s) atomicAdd(&H[d], s);
+}
+
+// the same over select_tiles' rows (two u16 counts per word) when the call
+// kept the hinted geometry (ctl->hint), else over fused_hist0's u32 rows.
+// Thread = one word (two digits); blockIdx.y takes every gridDim.y-th row.
+__global__ void __launch_bounds__(TPB)
+    msel_reduce0h(const uint32_t *__restrict__ rows, int nrows, const uint32_t *__restrict__ rows16,
+                  int nrows16, const int32_t *__restrict__ hint, uint32_t *__restrict__ H) {
+  const int q = blockIdx.x * TPB + threadIdx.x;  // word q: digits 2q, 2q + 1
+  uint32_t a = 0, b = 0;
+  if (*hint) {
+    constexpr int U = 8;  // rows in flight per thread
+    for (int r0 = blockIdx.y * U; r0 < nrows16; r0 += gridDim.y * U) {
+      uint32_t v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u] = r0 + u < nrows16 ? rows16[(int64_t)(r0 + u) * (MS0_DIG / 2) + q] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        a += v[u] & 0xffffu;
+        b += v[u] >> 16;
+      }
+    }
+  } else {
+    for (int r = blockIdx.y; r < nrows; r += gridDim.y) {
+      a += rows[(int64_t)r * MS0_DIG + 2 * q];
+      b += rows[(int64_t)r * MS0_DIG + 2 * q + 1];
+    }
+  }
+  if (a) atomicAdd(&H[2 * q], a);
+  if (b) atomicAdd(&H[2 * q + 1], b);
 }
 
 // levels >= 1: keys whose prefix is an active group add to that group's
@@ -739,7 +785,23 @@ struct FusedCtl {
   int32_t ng;      // chosen level-0 buckets (groups)
   int64_t total;   // keys gathered into the group segments
   uint64_t kmin, kmax;
+  int32_t hint;    // 1: the level-0 geometry (lo, s0, w0) is the previous call's, its
+                   // histogram was built by select_tiles (no re-read of x)
+  int32_t pad_;
 };
+
+// Level-0 digit geometry of a handle's previous tiled call (select_tiles
+// counts this call's keys with it while they are still in registers; the
+// call keeps it iff every window key fell inside it).  Two slots per
+// handle, by call parity: a call reads one and writes the other.
+struct SelHint {
+  uint64_t lo;
+  int32_t s, w;
+  int32_t valid, pad;
+};
+// select_tiles blocks per assign_gather block (tile sub-ranges): 3 x 255
+// blocks of 8 waves at <= 80 VGPRs (6 waves per SIMD) are all resident at once
+constexpr int SH_K = 3;
 
 
 // The step's control record from the selection's status words: kept count
@@ -757,33 +819,28 @@ struct FusedSetup {
   uint32_t *zero;  // words block 0 zeroes for later kernels (fused_boff's per-block counts)
   int nzero;
   int dist;  // one rank of several: the key range (mm slots) is global, no keys here is no error
+  const uint64_t *kw;  // tiled: the selection's keep words (slot i holds a key iff its bit is set)
+  const SelHint *hint;   // tiled, one rank: the geometry select_tiles counted with (or null)
+  const uint32_t *hflag; // select_tiles: a window key fell outside the hint (or null)
+  SelHint *hint_out;     // fused_hist0 block 0: this call's own geometry, for the next call
+  const uint32_t *btot;  // tiled: select_tiles' block totals (SH_K (gridDim - 1) blocks)
 };
 
 // Element range of fused_hist0 / fused_gather: the kept x [0, n), or with
-// a tiled selection the tiles' slots [0, nt * TILE) of which slot j of
-// tile t holds a key iff j < its count.  One block step covers EL_STEP
-// slots = two whole tiles, so the two counts are wave-uniform.
+// a tiled selection the tiles' particle slots [0, nt * TILE), slot i holding
+// a key iff bit i % 64 of keep word i / 64 is set.  One block step covers
+// EL_STEP slots = two whole tiles.
 constexpr int EL_U = 4;  // 16-byte loads per lane per step (two keys each)
 constexpr int64_t EL_STEP = (int64_t)MS0_TPB * 2 * EL_U;
 static_assert(EL_STEP == 2 * TILE, "a step is two tiles");
 struct ElRange {
-  const uint64_t *stat;  // tiled: the select's status words (count in the low bits)
+  const uint64_t *kw;  // tiled: the selection's keep words
   uint32_t nt;
   int64_t n;    // kept keys
   int64_t lim;  // slots
-  __device__ uint32_t count(int64_t t) const {
-    return t < (int64_t)nt ? (uint32_t)(stat[t] & kStVal) : 0u;
-  }
 };
-__device__ __forceinline__ ElRange el_range(const uint64_t *stat, uint32_t nt, int64_t n) {
-  return stat ? ElRange{stat, nt, n, (int64_t)nt * TILE} : ElRange{nullptr, 0u, n, n};
-}
-// key slot i of the step starting at i0 holds a key
-__device__ __forceinline__ bool el_valid(const ElRange &r, int64_t i0, int64_t i, uint32_t c0,
-                                         uint32_t c1) {
-  if (!r.stat) return i < r.n;
-  const int64_t j = i - i0;
-  return (j < TILE) ? j < (int64_t)c0 : (j - TILE) < (int64_t)c1;
+__device__ __forceinline__ ElRange el_range(const uint64_t *kw, uint32_t nt, int64_t n) {
+  return kw ? ElRange{kw, nt, n, (int64_t)nt * TILE} : ElRange{nullptr, 0u, n, n};
 }
 
 __device__ FusedCtl fused_ctl(const FusedSetup &f) {
@@ -819,6 +876,219 @@ __device__ FusedCtl fused_ctl(const FusedSetup &f) {
   return c;
 }
 
+// fused_ctl, then the hinted geometry when select_tiles counted every
+// window key with it (the digits of any base <= the window's lowest key and
+// any width covering its highest key rank the keys the same: same edges)
+__device__ FusedCtl fused_ctl_eff(const FusedSetup &f) {
+  FusedCtl c = fused_ctl(f);
+  if (f.hint && !f.dist && !(c.err & 2)) {
+    const SelHint h = *f.hint;
+    if (h.valid && !*f.hflag) {
+      c.lo = h.lo;
+      c.s0 = h.s;
+      c.w0 = h.w;
+      c.hint = 1;
+    }
+  }
+  return c;
+}
+
+// Tiled lazy selection (large inputs), persistent: block j takes the
+// j % SH_K-th part of the tile range assign_gather block 1 + j / SH_K walks
+// (tile_range); each of its 8 waves streams its 512-particle slice of every
+// tile with no block barrier in the loop: mask + x (8 particles per lane,
+// all loads in flight), x stored in particle-slot layout, the keep words,
+// each word's prefix INSIDE ITS WAVE SLICE (kpre) and the slice's count
+// (wcnt[t][w]).  At the end one barrier: the block's tiles' offsets
+// relative to the block (toff; fused_hist0 adds the block's base from the
+// block totals btot), the key range.
+// With a valid hint (the previous tiled call's level-0 geometry) the block
+// also counts every window key's level-0 digit in LDS (two u16 counts per
+// word: at most SH_TMAX tiles = 61440 keys per block) while x is still in
+// registers, and stores its row — fused_hist0 then need not read x again; a
+// window key outside the hint's range sets *hflag and the call falls back.
+constexpr int SH_BT = 512;
+constexpr int SH_NW = SH_BT / 64;  // wave slices per tile
+constexpr uint32_t SH_TMAX = 15;   // tiles per block for the u16 digit counts
+constexpr uint32_t SH_MAXT = 64;   // tiles per block for the block-local offsets (LDS)
+// FAM: several family slices (membership tested per particle); else every
+// particle of the span [base, n) is a member (no family, or one slice: the
+// span is that slice) and the 16 slice bounds stay out of the registers.
+template <bool FAM>
+__global__ void __launch_bounds__(SH_BT)
+    select_tiles(const double *__restrict__ pos, int64_t n, SelectParams p, uint32_t nt,
+                 uint32_t G0, double *__restrict__ xo, uint64_t *__restrict__ kw,
+                 uint16_t *__restrict__ kpre, uint32_t *__restrict__ wcnt,
+                 uint32_t *__restrict__ toff, uint32_t *__restrict__ btot,
+                 unsigned long long *__restrict__ minmax, const SelHint *__restrict__ hint,
+                 uint64_t ka, uint64_t kb, uint32_t *__restrict__ rows16,
+                 uint32_t *__restrict__ hflag) {
+  constexpr int SI = TILE / SH_BT;
+  __shared__ uint32_t lh[MS0_DIG / 2];
+  __shared__ uint32_t tcnt[SH_MAXT][SH_NW];
+  __shared__ unsigned long long wmin[SH_NW], wmax[SH_NW];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane = lane_id();
+  // this block's tiles: part j % SH_K of assign block 1 + j / SH_K's range
+  const uint32_t ab = blockIdx.x / SH_K, sub = blockIdx.x % SH_K;
+  const uint32_t ta0 = (uint32_t)((uint64_t)nt * ab / (G0 - 1));
+  const uint32_t tb0 = (uint32_t)((uint64_t)nt * (ab + 1) / (G0 - 1));
+  const uint32_t ta = ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * sub / SH_K);
+  const uint32_t tb = ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * (sub + 1) / SH_K);
+  SelHint h{};
+  if (hint) h = *hint;
+  const bool hv = h.valid && rows16 && tb - ta <= SH_TMAX;
+  const uint64_t hlo = h.lo;
+  const int hsh = h.s;
+  // highest key the hint's digits cover: lo + 2^(s + w) - 1 (saturating)
+  const int hb = h.s + h.w;
+  const uint64_t hspan = hb >= 64 ? ~0ull : ((1ull << hb) - 1);
+  const uint64_t hhi = hlo + hspan < hlo ? ~0ull : hlo + hspan;
+  if (hv) {
+    for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) lh[i] = 0;
+    __syncthreads();
+  }
+  unsigned long long kmin = ~0ull, kmax = 0ull;
+  bool oob = false;
+  for (uint32_t tile0 = ta; tile0 < tb; ++tile0) {
+#ifdef PBX_DIAG_SEL_ILV  // timing diagnostic only: tiles interleaved over the blocks (wrong offsets)
+    uint32_t tile = blockIdx.x + (tile0 - ta) * gridDim.x;
+    tile = tile < nt ? tile : nt - 1;
+#else
+    const uint32_t tile = tile0;
+#endif
+    const int64_t wbase = p.base + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW);
+    double px[SI], py[SI], pz[SI], xv[SI];
+    uint32_t inbits = 0;
+#pragma unroll
+    for (int k = 0; k < SI; ++k) {
+      const int64_t i = wbase + k * 64 + lane;
+      const bool in = (i < n) && (!FAM || in_family(i, p));
+      inbits |= (uint32_t)in << k;
+      const double *q = pos + 3 * (in ? i : 0);
+      px[k] = q[0];
+      py[k] = q[1];
+      pz[k] = q[2];
+    }
+    double *xt = xo + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW);
+    const int64_t wj = (int64_t)tile * (TILE / 64) + w * SI;
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < SI; ++k) {
+      xv[k] = 0.0;
+      const bool keep = ((inbits >> k) & 1u) && select_xyz(px[k], py[k], pz[k], p, xv[k]);
+      const uint64_t bal = __ballot(keep);
+      if (lane == 0) {
+        kw[wj + k] = bal;
+        kpre[wj + k] = (uint16_t)run;  // kept particles before the word in this wave's slice
+      }
+      run += (uint32_t)__popcll(bal);
+      if (keep) {
+        xt[k * 64 + lane] = xv[k];
+        const uint64_t kk = dkey(xv[k]);
+        kmin = kk < kmin ? kk : kmin;
+        kmax = kk > kmax ? kk : kmax;
+        if (hv && kk >= ka && kk <= kb) {
+          if (kk >= hlo && kk <= hhi) {
+            const uint32_t d = (uint32_t)((kk - hlo) >> hsh);
+            atomicAdd(&lh[d >> 1], 1u << (16 * (d & 1)));
+          } else {
+            oob = true;
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      wcnt[(int64_t)tile * SH_NW + w] = run;
+      if (tile0 - ta < SH_MAXT) tcnt[tile0 - ta][w] = run;
+    }
+  }
+  // the block's key range: one atomic pair per block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(kmin, o, 64);
+    const unsigned long long b = __shfl_xor(kmax, o, 64);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if (lane == 0) {
+    wmin[w] = kmin;
+    wmax[w] = kmax;
+  }
+  const uint64_t anyoob = __ballot(oob);
+  if (anyoob && lane == 0) atomicOr(hflag, 1u);
+  __syncthreads();
+  if (w == 0) {
+    // block-local exclusive tile offsets (lane = tile, 64 at a time) and the block total
+    uint32_t carry = 0;
+    for (uint32_t t0 = ta; t0 < tb; t0 += 64) {
+      const uint32_t t = t0 + lane;
+      uint32_t c = 0;
+      if (t < tb) {
+        if (t - ta < SH_MAXT) {
+#pragma unroll
+          for (int ww = 0; ww < SH_NW; ++ww) c += tcnt[t - ta][ww];
+        } else {
+#pragma unroll
+          for (int ww = 0; ww < SH_NW; ++ww) c += wcnt[(int64_t)t * SH_NW + ww];
+        }
+      }
+      uint32_t x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+      }
+      if (t < tb) toff[t] = carry + x - c;
+      carry += __shfl(x, 63, 64);
+    }
+    if (lane == 0) {
+      btot[blockIdx.x] = carry;
+      unsigned long long a = ~0ull, b = 0ull;
+      for (int ww = 0; ww < SH_NW; ++ww) {
+        a = wmin[ww] < a ? wmin[ww] : a;
+        b = wmax[ww] > b ? wmax[ww] : b;
+      }
+      unsigned long long *mmq = minmax + 2 * (blockIdx.x % MM_SLOTS);
+      if (a != ~0ull) atomicMax(&mmq[0], ~a);
+      if (b != 0ull) atomicMax(&mmq[1], b);
+    }
+  }
+  if (hv) {  // this block's row (coalesced words)
+    uint32_t *row = rows16 + (int64_t)blockIdx.x * (MS0_DIG / 2);
+    for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) row[i] = lh[i];
+  } else if (hint && h.valid && threadIdx.x == 0) {
+    atomicOr(hflag, 1u);  // too many tiles for u16 counts: fall back (not below 2^28 particles)
+  }
+}
+
+// fused_hist0 blocks >= 1 (tiled): the global tile offsets, select_tiles'
+// block-local ones plus each select block's base (the sum of the block
+// totals before it); block 0: the kept count
+__device__ void tile_offsets_fix(const uint32_t *__restrict__ btot, uint32_t nt, uint32_t *toff,
+                                 uint32_t *red) {
+  const uint32_t G0 = gridDim.x;
+  if (blockIdx.x == 0 || G0 < 2) return;
+  const uint32_t ab = blockIdx.x - 1;  // select blocks ab SH_K .. + SH_K - 1
+  const uint32_t j0 = ab * SH_K;
+  uint32_t v = 0;
+  for (uint32_t j = threadIdx.x; j < j0; j += blockDim.x) v += btot[j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int q = 0; q < (int)(blockDim.x >> 6); ++q) base += red[q];
+  const uint32_t ta0 = (uint32_t)((uint64_t)nt * ab / (G0 - 1));
+  const uint32_t tb0 = (uint32_t)((uint64_t)nt * (ab + 1) / (G0 - 1));
+  for (uint32_t sb = 0; sb < (uint32_t)SH_K; ++sb) {
+    const uint32_t ta = ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * sb / SH_K);
+    const uint32_t tb = ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * (sb + 1) / SH_K);
+    for (uint32_t t = ta + threadIdx.x; t < tb; t += blockDim.x) toff[t] += base;
+    base += btot[j0 + sb];
+  }
+}
+
 // every key slot of this block (grid-stride by EL_STEP): f(x value, valid).
 // (Issuing the next step's loads before this step's keys are processed made
 // fused_gather slower at 64M, 71 -> 91 us: kept single-step.)
@@ -841,42 +1111,47 @@ template <class F>
 __device__ __forceinline__ void el_for_each(const double *__restrict__ x, const ElRange &er,
                                             int64_t lim, F &&f) {
   constexpr int U = EL_U;
-  if (er.stat) {
+  if (er.kw) {
     uint32_t ta, tb;
     tile_range(er.nt, ta, tb);
     if (lim == 0 || ta >= tb) return;
-    // unconditional 16-B loads (a lone last tile re-reads itself for its
-    // missing partner: no branch around a load), the next step's in flight
-    // while this one is processed (ping-pong, no register copies)
-    auto ld = [&](uint32_t t, double *v) {
+    // unconditional 16-B loads of slot pairs with their keep words (a lone
+    // last tile re-reads itself for its missing partner: no branch around a
+    // load), the next step's in flight while this one is processed
+    // (ping-pong, no register copies)
+    auto ld = [&](uint32_t t, double *v, uint64_t *kv) {
       const int64_t i0 = (int64_t)t * TILE;
       const int64_t end = (int64_t)(t + 1 < tb ? t + 2 : t + 1) * TILE;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + 2 * (u * MS0_TPB + threadIdx.x);
-        const double2 q = *(const double2 *)(x + (i < end ? i : i - TILE));
+        const int64_t ii = i < end ? i : i - TILE;
+        const double2 q = *(const double2 *)(x + ii);
         v[2 * u] = q.x;
         v[2 * u + 1] = q.y;
+        kv[u] = er.kw[ii >> 6];
       }
     };
-    auto use = [&](uint32_t t, const double *v) {
-      const int64_t i0 = (int64_t)t * TILE;
-      const uint32_t c0 = er.count(t);
-      const uint32_t c1 = t + 1 < tb ? er.count(t + 1) : 0u;
+    auto use = [&](uint32_t t, const double *v, const uint64_t *kv) {
+      const bool two = t + 1 < tb;
 #pragma unroll
       for (int u = 0; u < 2 * U; ++u) {
-        const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
-        f(v[u], el_valid(er, i0, i, c0, c1));
+        const int64_t j = 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
+        f(v[u], (j < TILE || two) && ((kv[u >> 1] >> (j & 63)) & 1ull));
       }
     };
     double va[2 * U], vb[2 * U];
-    ld(ta, va);
+    uint64_t ka[U], kb[U];
+    // unconditional loads (past the range: the first tile again), so the
+    // same loads are in flight on every path and the vmcnt waits stay exact
+    auto cl = [&](uint32_t t) { return t < tb ? t : ta; };
+    ld(ta, va, ka);
     for (uint32_t t = ta; t < tb; t += 4) {
-      if (t + 2 < tb) ld(t + 2, vb);
-      use(t, va);
+      ld(cl(t + 2), vb, kb);
+      use(t, va, ka);
       if (t + 2 >= tb) break;
-      if (t + 4 < tb) ld(t + 4, va);
-      use(t + 2, vb);
+      ld(cl(t + 4), va, ka);
+      use(t + 2, vb, kb);
     }
     return;
   }
@@ -884,12 +1159,10 @@ __device__ __forceinline__ void el_for_each(const double *__restrict__ x, const 
     double v[2 * U];
 #pragma unroll
     for (int u = 0; u < U; ++u) load_pair(x, i0 + 2 * (u * MS0_TPB + threadIdx.x), lim, v + 2 * u);
-    const uint32_t c0 = er.stat ? er.count(i0 / TILE) : 0u;
-    const uint32_t c1 = er.stat ? er.count(i0 / TILE + 1) : 0u;
 #pragma unroll
     for (int u = 0; u < 2 * U; ++u) {
       const int64_t i = i0 + 2 * ((u >> 1) * MS0_TPB + threadIdx.x) + (u & 1);
-      f(v[u], el_valid(er, i0, i, c0, c1));
+      f(v[u], i < er.n);
     }
   }
 }
@@ -903,12 +1176,39 @@ __global__ void __launch_bounds__(MS0_TPB)
                 uint32_t *__restrict__ rows) {
   __shared__ uint32_t lh[MS0_DIG];
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
-  const FusedCtl ctl = fused_ctl(fsu);
+  const FusedCtl ctl = fused_ctl_eff(fsu);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && fsu.hint_out) {
+    // this call's window key range widened by 1/64 of its span on each side
+    // (a similar next call still fits), as a level-0 geometry for the next call
+    const FusedCtl nat = fused_ctl(fsu);
+    SelHint h{};
+    if (!(nat.err & 2)) {
+      const uint64_t hi = fsu.kb < nat.kmax ? fsu.kb : nat.kmax;
+      const uint64_t m = (hi - nat.lo) >> 6;
+      const uint64_t lo2 = nat.lo >= m ? nat.lo - m : 0ull;
+      const uint64_t hi2 = hi + m < hi ? ~0ull : hi + m;
+      const uint64_t span = hi2 - lo2;
+      const int B = span ? 64 - __builtin_clzll(span) : 1;
+      h.w = B < MS0_BITS ? B : MS0_BITS;
+      h.s = B - h.w;
+      h.lo = lo2;
+      h.valid = 1;
+    }
+    *fsu.hint_out = h;
+  }
+  __shared__ uint32_t red[MS0_TPB / 64];
   if (blockIdx.x == 0) {  // the step's shared state: control record, zeroed counts / H
-    if (fsu.tiled) {  // tiled selection: tile offsets and the kept count (no keys: lo > hi above)
-      __shared__ uint32_t wsum[MS0_TPB / 64];
-      const uint32_t total = tile_scan_block(fsu.stat, fsu.nt, fsu.toff, wsum);
+    if (fsu.tiled) {  // tiled selection: the kept count = the sum of select_tiles' block totals
+      const uint32_t G1 = SH_K * (gridDim.x - 1);
+      uint32_t v = 0;
+      for (uint32_t j = threadIdx.x; j < G1; j += MS0_TPB) v += fsu.btot[j];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+      __syncthreads();
       if (threadIdx.x == 0) {
+        uint32_t total = 0;
+        for (int q = 0; q < MS0_TPB / 64; ++q) total += red[q];
         FusedCtl c = ctl;
         c.n = total;
         *ctl_out = c;
@@ -920,9 +1220,11 @@ __global__ void __launch_bounds__(MS0_TPB)
     for (int k = threadIdx.x; k < MS0_DIG; k += MS0_TPB) H[k] = 0;   // for msel_reduce0
     for (int k = threadIdx.x; k < fsu.nzero; k += MS0_TPB) fsu.zero[k] = 0;
   }
+  if (fsu.tiled) tile_offsets_fix(fsu.btot, fsu.nt, fsu.toff, red);  // (blocks >= 1)
+  if (ctl.hint) return;  // select_tiles counted the keys (msel_reduce0 sums its rows)
   __syncthreads();
   const uint64_t ka = fsu.ka, kb = fsu.kb;
-  const ElRange er = el_range(fsu.tiled ? fsu.stat : nullptr, fsu.nt, (ctl.err & 2) ? 0 : ctl.n);
+  const ElRange er = el_range(fsu.tiled ? fsu.kw : nullptr, fsu.nt, (ctl.err & 2) ? 0 : ctl.n);
   const int64_t lim = (ctl.err & 2) ? 0 : er.lim;
   const uint64_t base = ctl.lo;
   const int s = ctl.s0;
@@ -1060,12 +1362,21 @@ __global__ void __launch_bounds__(TPB)
     fused_boff(const uint32_t *__restrict__ rows, int g0, const FusedCtl *__restrict__ ctl,
                const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ goff,
                uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
-               uint32_t *__restrict__ lc) {
+               uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16) {
   __shared__ uint32_t wsum[NWAVE];
   const int g = blockIdx.x;
   if ((ctl->err & 2) || g >= ctl->ng) return;
   const int b = threadIdx.x;  // g0 <= TPB
-  const uint32_t c = b < g0 ? rows[(int64_t)b * MS0_DIG + gdig[g]] : 0u;
+  uint32_t c = 0;
+  if (ctl->hint) {  // select_tiles blocks (b - 1) SH_K .. + SH_K - 1 cover block b's tiles
+    const uint32_t d = gdig[g];
+    if (b >= 1 && b < g0)
+      for (int j = 0; j < SH_K; ++j)
+        c += (rows16[(int64_t)((b - 1) * SH_K + j) * (MS0_DIG / 2) + (d >> 1)] >> (16 * (d & 1))) &
+             0xffffu;
+  } else if (b < g0) {
+    c = rows[(int64_t)b * MS0_DIG + gdig[g]];
+  }
   uint32_t tot;
   const uint32_t ex = block_excl_scan(c, wsum, &tot);
   if (b < g0) boff[(int64_t)b * MS_MAXQ + g] = goff[g] + ex;
@@ -1097,7 +1408,7 @@ __global__ void __launch_bounds__(MS0_TPB)
     fused_gather(const double *__restrict__ x, uint64_t ka, uint64_t kb,
                  const FusedCtl *__restrict__ ctl, const uint32_t *__restrict__ gdig,
                  const uint32_t *__restrict__ boff, uint64_t *__restrict__ seg,
-                 const uint64_t *__restrict__ tstat, uint32_t nt) {
+                 const uint64_t *__restrict__ tkw, uint32_t nt) {
   __shared__ uint16_t gidx[MS0_DIG];
   __shared__ uint32_t slot[MS_MAXQ];
   if (ctl->err & 2) return;
@@ -1112,7 +1423,7 @@ __global__ void __launch_bounds__(MS0_TPB)
     slot[i] = boff[(int64_t)blockIdx.x * MS_MAXQ + i];
   }
   __syncthreads();
-  const ElRange er = el_range(tstat, nt, n);
+  const ElRange er = el_range(tkw, nt, n);
   const int64_t lim = er.lim;
   el_for_each(x, er, lim, [&](double xv, bool ok) {
     const uint64_t key = dkey(xv);
@@ -1416,7 +1727,9 @@ __global__ void __launch_bounds__(BT)
       if (i < n) bins[i] = b[k];
     }
     if (MOM) {
-      for (int q = 0; q < fs.nm; ++q) {  // uniform
+#pragma unroll
+      for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+        if (q >= fs.nm) break;
         const int col = fs.col[q], fq = fs.f[q], wq = fs.w[q];
         double *aq = acc + (int64_t)q * nb;
 #pragma unroll
@@ -1541,8 +1854,9 @@ __global__ void __launch_bounds__(BT)
       if (lane >= (uint32_t)o) incl += y;
     }
     const uint32_t pre = toff[t] + incl - cw;
-    // x of a tiled selection sits in the tile's own slots
-    const double *xt = xtiled ? x + ((int64_t)t * TILE - (int64_t)toff[t]) : x;
+    // x of a tiled selection sits in the tile's particle slots
+    const double *xt = xtiled ? x + (int64_t)t * TILE : x;
+    const int64_t dflt = xtiled ? 0 : (int64_t)toff[t];
     const int64_t pbase = base + (int64_t)t * TILE + lane;
     uint32_t *hrow = th[t - t0];
     double nv[CH], nw[CH];
@@ -1557,8 +1871,8 @@ __global__ void __launch_bounds__(BT)
         const bool kp = (wj >> lane) & 1ull;
         keep |= (uint32_t)kp << kk;
         pos[kk] = pj + rank_below(wj);
-        v[kk] = xt[kp ? pos[kk] : toff[t]];  // unconditional loads (see assign_gather)
-        const double mv = (wneed ? mass : xt)[(kp && wneed) ? pbase + 64 * j : (wneed ? base : toff[t])];
+        v[kk] = xtiled ? xt[64 * j + lane] : xt[kp ? pos[kk] : dflt];  // unconditional loads
+        const double mv = (wneed ? mass : xt)[(kp && wneed) ? pbase + 64 * j : (wneed ? base : dflt)];
         wv[kk] = wneed ? mv : 1.0;
       }
     };
@@ -1597,7 +1911,9 @@ __global__ void __launch_bounds__(BT)
 #else
       if (MOM) {
 #endif
-        for (int q = 0; q < fs.nm; ++q) {  // uniform
+#pragma unroll
+        for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+          if (q >= fs.nm) break;
           const int col = fs.col[q], fq = fs.f[q], wq = fs.w[q];
           double *aq = acc + (int64_t)q * nb;
 #pragma unroll
@@ -1647,7 +1963,7 @@ constexpr int AG_TR = 64;
 #endif
 constexpr int AG_W = PBX_AG_W;                // keep words of a tile per wave
 constexpr int AG_TPS = AG_W * (MS0_TPB / 64) / 64;  // tiles per step (the block's waves)
-struct AgRec {  // a deferred key: key - window base, weight, compacted position, tile
+struct AgRec {  // a deferred key: key - window base, weight, particle slot, tile
   uint64_t off;
   double w;
   uint32_t pos, t;
@@ -1674,11 +1990,10 @@ __device__ __forceinline__ uint32_t block_prefix(const uint32_t *__restrict__ v,
 
 template <bool MOM>
 __global__ void __launch_bounds__(MS0_TPB)
-    assign_gather(const double *__restrict__ x, const uint64_t *__restrict__ kw,
-                  const uint16_t *__restrict__ kpre, const uint32_t *__restrict__ toff,
-                  int64_t base, uint32_t nt,
-                  const double *__restrict__ mass, const FusedCtl *__restrict__ ctl, uint64_t ka,
-                  uint64_t kb, const MsRank *__restrict__ R, int nq,
+    assign_gather(const double *__restrict__ x, const uint64_t *__restrict__ kw, int64_t base,
+                  int64_t span, uint32_t nt, const double *__restrict__ mass,
+                  const FusedCtl *__restrict__ ctl, uint64_t ka, uint64_t kb,
+                  const MsRank *__restrict__ R, int nq,
                   const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ boff, int nb,
                   uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
                   double *__restrict__ slab, GatherOut go) {
@@ -1730,82 +2045,127 @@ __global__ void __launch_bounds__(MS0_TPB)
   const int wl = w % (64 / AG_W), sub = w / (64 / AG_W);
   const uint32_t lane = lane_id();
   const bool wneed = mass != nullptr;
-  // one tile's share of a wave: loads issued (issue) one tile before they
-  // are binned (bin), ping-pong buffers so no register copy waits on them
+  // one tile's share of a wave: x, masses and keep words by particle slot,
+  // so no load address waits for anything; three buffers, loads issued two
+  // tiles ahead.  No branch around a load (a missing mass array reads x,
+  // and the weight is 1), so the in-order vmcnt waits stay exact.
   struct Part {
     double v[AG_W], m[AG_W];
-    uint32_t pos[AG_W];
-    uint32_t keep;
+    uint64_t k[AG_W];
   };
-  // a wave's AG_W keep words of tile t and their in-tile prefixes come in as
-  // scalar loads (lgkmcnt): the vector-load queue (vmcnt, in order) holds
-  // only x / mass, so tile t + 1's stay in flight while tile t is binned
+  const double *mp = wneed ? mass + base : x;
+  // the keep words as VECTOR loads (every lane the same address: one line):
+  // a scalar load would be waited for with lgkmcnt(0) — SMEM returns out of
+  // order — at the first LDS read after it, i.e. every tile's lookups would
+  // wait for the keep words of the tiles in flight
+  const uint32_t vz = vgpr_zero();
   auto issue = [&](uint32_t t, Part &P) {
-    const int64_t j0 = (int64_t)t * 64 + wl * AG_W;
-    const uint32_t to = toff[t];
-    const double *xt = x + ((int64_t)t * TILE - (int64_t)to);  // x of tile t by position
-    const int64_t pb = base + (int64_t)t * TILE + lane;
-    // every load unconditional (a lane without a particle reads the tile's
-    // first slot / the span's first mass): no branch around a load
-    const double *mp = wneed ? mass : xt + to;
-    P.keep = 0;
+#ifdef PBX_DIAG_AG_ILV  // timing diagnostic only: tiles interleaved over the blocks
+    {
+      const uint32_t G = gridDim.x - 1, b = blockIdx.x - 1;
+      const uint32_t t2 = b + (t - ta) * G;
+      t = t2 < nt ? t2 : nt - 1;
+    }
+#endif
+    const int64_t s0 = (int64_t)t * TILE + 64 * (wl * AG_W);
 #pragma unroll
     for (int kk = 0; kk < AG_W; ++kk) {
-      const int j = wl * AG_W + kk;
-      const uint64_t wj = kw[j0 + kk];
-      const uint32_t pj = to + kpre[j0 + kk];
-      const bool kp = (wj >> lane) & 1ull;
-      P.keep |= (uint32_t)kp << kk;
-      P.pos[kk] = pj + rank_below(wj);
-      P.v[kk] = xt[kp ? P.pos[kk] : to];
-      const double mv = mp[(kp && wneed) ? pb + 64 * j : (wneed ? base : 0)];
-      P.m[kk] = wneed ? mv : 1.0;
+      const int64_t sl = s0 + 64 * kk + lane;
+      P.v[kk] = x[sl];
+      P.m[kk] = mp[wneed ? (sl < span ? sl : span - 1) : sl];
+      P.k[kk] = kw[(s0 >> 6) + kk + vz];
     }
   };
+  constexpr uint32_t SKIP = 0xffffu, DEFER = 0xfffeu;
   auto bin = [&](uint32_t t, uint32_t tl, const Part &P) {
+#ifdef PBX_DIAG_AG_LOADONLY  // timing diagnostic only: loads consumed, nothing binned
+    {
+      double z = 0.0;
+      uint64_t kz = 0;
+      for (int kk = 0; kk < AG_W; ++kk) {
+        z += P.v[kk] * P.m[kk];
+        kz ^= P.k[kk];
+      }
+      if (z == 1234.5 && kz == 7) acc[0] = z;
+      return;
+    }
+#endif
+    uint32_t bk[AG_W];
+    double wv[AG_W];
+    uint64_t anydef = 0;
 #pragma unroll
     for (int kk = 0; kk < AG_W; ++kk) {
-      if (!((P.keep >> kk) & 1u)) continue;
-      const double xv = P.v[kk];
-      const uint64_t key = dkey(xv);
-      uint32_t b = (uint32_t)nb;
-      bool defer = false;
-      if (win && key >= ka && key <= kb) {  // fused_hist0's window
-        const uint32_t d = (uint32_t)((key - lo) >> s);
-        const uint32_t e = dtab[d];
-        if (e & 0x8000u) {
-          const uint32_t g = e & 0x7fffu;
-          go.seg[atomicAdd(&sslot[g], 1u)] = key - lo;
-          defer = true;  // NaN too: its bin is below the first NaN edge, if any (bin_of)
-          go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{key - lo, P.m[kk], P.pos[kk], t};
-        } else {
-          b = e;  // (NaN in a digit without edges: no NaN edge, dropped like the table says)
-        }
+      const bool kp = (P.k[kk] >> lane) & 1ull;
+      const uint64_t key = dkey(P.v[kk]);
+      const bool inw = win && key >= ka && key <= kb;  // fused_hist0's window
+      const uint32_t e = dtab[inw ? (uint32_t)((key - lo) >> s) : 0u];
+      // (NaN in a digit without edges: no NaN edge, dropped like the table says;
+      // NaN in a group's digit is deferred: its bin is below the first NaN edge)
+      const bool def = kp && inw && (e & 0x8000u);
+      bk[kk] = !kp ? SKIP : def ? DEFER : inw ? e : (uint32_t)nb;
+      wv[kk] = wneed ? P.m[kk] : 1.0;
+      anydef |= __ballot(def);
+    }
+    const uint32_t sbase = t * (uint32_t)TILE + 64u * (uint32_t)(wl * AG_W) + lane;
+#ifndef PBX_DIAG_AG_NOBIN  // (timing diagnostic: no byte stores / tile counts)
+#pragma unroll
+    for (int kk = 0; kk < AG_W; ++kk)
+      if (bk[kk] <= (uint32_t)nb) {
+        bins[sbase + 64u * kk] = (uint8_t)bk[kk];
+        atomicAdd(&th[tl * nrs + bk[kk]], 1u);
       }
-      if (defer) continue;
-      bins[P.pos[kk]] = (uint8_t)b;
-      atomicAdd(&th[tl * nrs + b], 1u);
-      if (MOM && b < (uint32_t)nb)
-        for (int q = 0; q < fs.nm; ++q) {  // uniform
-          const double f = fs.f[q] == 0 ? xv : P.m[kk];
-          const double ww = fs.w[q] == 0 ? xv : P.m[kk];
-          atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
+#endif
+#ifdef PBX_DIAG_AG_NOSUM  // (timing diagnostic: no per-bin sums)
+    if (false) {
+#else
+    if (MOM) {
+#endif
+#pragma unroll
+      for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+        if (q >= fs.nm) break;
+        double *aq = acc + q * nb;
+#pragma unroll
+        for (int kk = 0; kk < AG_W; ++kk)
+          if (bk[kk] < (uint32_t)nb) {
+            const double f = fs.f[q] == 0 ? P.v[kk] : wv[kk];
+            const double ww = fs.w[q] == 0 ? P.v[kk] : wv[kk];
+            atomicAdd(&aq[bk[kk]], monomial(fs.col[q], f, ww));
+          }
+      }
+    }
+    if (anydef) {  // rare (edge-holding digits): the group segment + the block's deferred list
+#pragma unroll
+      for (int kk = 0; kk < AG_W; ++kk)
+        if (bk[kk] == DEFER) {
+          const uint64_t off = dkey(P.v[kk]) - lo;
+          const uint32_t g = dtab[(uint32_t)(off >> s)] & 0x7fffu;
+          go.seg[atomicAdd(&sslot[g], 1u)] = off;
+          go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{off, wv[kk], sbase + 64u * kk, t};
         }
     }
   };
   for (uint32_t r0 = ta; r0 < tb; r0 += AG_TR) {
     const uint32_t r1 = min(tb, r0 + (uint32_t)AG_TR);
-    Part A, B;
+    Part A, B, C;
     constexpr uint32_t S1 = AG_TPS;
     const uint32_t t0 = r0 + sub;
-    if (t0 < r1) issue(t0, A);
-    for (uint32_t t = t0; t < r1; t += 2 * S1) {
-      // the next tile's loads go out before this one is binned
-      if (t + S1 < r1) issue(t + S1, B);
+    // every issue unconditional (a tile past the range re-reads the last
+    // one): the same loads are in flight on every path, so the compiler's
+    // vmcnt waits stay exact (a conditional issue made it wait for all)
+    auto cl = [&](uint32_t t) { return t < r1 ? t : r1 - 1; };
+    if (t0 < r1) {
+      issue(t0, A);
+      issue(cl(t0 + S1), B);
+    }
+    for (uint32_t t = t0; t < r1; t += 3 * S1) {
+      issue(cl(t + 2 * S1), C);
       bin(t, t - r0, A);
       if (t + S1 >= r1) break;
-      if (t + 2 * S1 < r1) issue(t + 2 * S1, A);
+      issue(cl(t + 3 * S1), A);
       bin(t + S1, t + S1 - r0, B);
+      if (t + 2 * S1 >= r1) break;
+      issue(cl(t + 4 * S1), B);
+      bin(t + 2 * S1, t + 2 * S1 - r0, C);
     }
     __syncthreads();
     const int nrt = (int)(r1 - r0);
@@ -1882,7 +2242,9 @@ __global__ void __launch_bounds__(MS0_TPB)
         else atomicAdd(&tile_hist[(int64_t)b * nt + r[u].t], 1u);
       }
       if (MOM && ok && b < (uint32_t)nb)
-        for (int q = 0; q < fs.nm; ++q) {
+#pragma unroll
+        for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+          if (q >= fs.nm) break;
           const double f = fs.f[q] == 0 ? v : r[u].w;
           const double ww = fs.w[q] == 0 ? v : r[u].w;
           atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
@@ -1984,6 +2346,121 @@ __global__ void __launch_bounds__(TPB)
       sv[q] = (uint16_t)(w * 1024 + k * 64 + lane);
     }
   }
+  __syncthreads();
+  for (int j = threadIdx.x; j < (int)tn; j += TPB) {
+    const uint32_t dgt = sk[j];
+    perm[gofs[dgt] + ((uint32_t)j - dstart[dgt])] = (int32_t)(o + sv[j]);
+  }
+}
+
+// Stable CSR scatter over a tiled selection's particle slots (assign_gather
+// bytes): csr_sel's scheme with element e = slot (wave, iteration, lane) =
+// particle order, valid iff its keep bit is set (keep words loaded up front
+// into SGPRs: every load address is known at launch), value = the selection
+// index toff[t] + kpre + rank in the word.  Each element's wave-local rank
+// is taken right after its peer leader's returning LDS atomic.
+// STAGE: the tile is sorted by bin in LDS and written out run by run
+// (coalesced); else every element is stored at its CSR position directly
+// (a (bin, tile) run is one block's, so L2 merges its lines; no 12 KB of LDS).
+// ORD: the wave-local ranks straight from the returning LDS atomics (lane-
+// ordered, lds_atomics_lane_ordered); else peer masks (8 ballots each)
+template <bool STAGE, bool ORD>
+__global__ void __launch_bounds__(TPB)
+    csr_slots(const uint32_t *__restrict__ toff, const uint64_t *__restrict__ kw,
+              const uint16_t *__restrict__ kpre, const uint32_t *__restrict__ wcnt,
+              const uint8_t *__restrict__ bins, const uint32_t *__restrict__ offs,
+              uint32_t ntiles, int32_t *__restrict__ perm, uint32_t nrows) {
+  __shared__ uint32_t run[NWAVE][RADIX + 1];  // (+ a spare word: ORD's dropped lanes)
+  __shared__ uint32_t dstart[RADIX];
+  __shared__ uint32_t gofs[RADIX];
+  __shared__ uint32_t wsum[NWAVE];
+  __shared__ uint8_t sk[STAGE ? TILE : 1];
+  __shared__ uint16_t sv[STAGE ? TILE : 1];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // keep words: scalar loads
+  const uint32_t lane = lane_id();
+  const uint32_t t = blockIdx.x;
+  const int d0 = threadIdx.x;  // TPB == RADIX
+  const uint32_t dr = (uint32_t)d0 < nrows ? (uint32_t)d0 : nrows - 1;  // no branch around the load
+  const uint32_t go0 = offs[(int64_t)dr * ntiles + t];
+  const uint32_t go = (uint32_t)d0 < nrows ? go0 : 0u;
+  const uint8_t *bt = bins + (int64_t)t * TILE + w * 1024 + lane;
+  const uint64_t *kwt = kw + (int64_t)t * 64 + w * 16;
+  const uint16_t *kpt = kpre + (int64_t)t * 64 + w * 16;
+  const uint32_t o = toff[t];
+  // kpre counts inside select_tiles' 512-particle wave slices: this wave's
+  // 16 words are slices 2w, 2w + 1
+  static_assert(SH_NW == 2 * NWAVE, "two select slices per CSR wave");
+  const uint32_t *wct = wcnt + (int64_t)t * SH_NW;
+  uint32_t sbase0 = 0, tn = 0;
+#pragma unroll
+  for (int q = 0; q < SH_NW; ++q) {
+    const uint32_t c = wct[q];
+    sbase0 += q < 2 * w ? c : 0u;
+    tn += c;
+  }
+  const uint32_t sbase1 = sbase0 + wct[2 * w];
+  uint64_t wds[16];  // the wave's keep words, loaded before any store
+  uint32_t key[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t v = kwt[k];
+    wds[k] = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+    key[k] = bt[k * 64];  // unconditional: every slot exists
+  }
+  for (int d = threadIdx.x; d < NWAVE * (RADIX + 1); d += TPB) (&run[0][0])[d] = 0;
+  __syncthreads();
+  uint32_t lp[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t wd = wds[k];
+    const bool ok = (wd >> lane) & 1ull;
+    const uint32_t dgt = key[k] & 255u;
+    if (ORD) {  // dropped lanes count on a spare word (every lane issues: no branch)
+      lp[k] = atomicAdd(&run[w][ok ? dgt : RADIX], 1u);
+    } else {
+      uint64_t m = peers8(dgt, wd);
+      m = ok ? m : 0ull;
+      const uint32_t ret =
+          (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
+      const int leader = m ? __builtin_ctzll(m) : (int)lane;
+      lp[k] = (uint32_t)__shfl((int)ret, leader, 64) + rank_below(m);
+    }
+  }
+  __syncthreads();
+  {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) tot += run[ww][d0];
+    const uint32_t st = block_excl_scan(tot, wsum, nullptr);
+    dstart[d0] = st;
+    gofs[d0] = go;
+    // STAGE: tile-local sorted position; else the CSR position itself
+    uint32_t a = STAGE ? st : go;
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) {
+      const uint32_t c = run[ww][d0];
+      run[ww][d0] = a;
+      a += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t wd = wds[k];
+    if ((wd >> lane) & 1ull) {
+      const uint32_t dgt = key[k] & 255u;
+      const uint32_t q = run[w][dgt] + lp[k];
+      const uint32_t v = (k < 8 ? sbase0 : sbase1) + (uint32_t)kpt[k] + rank_below(wd);
+      if (STAGE) {
+        sk[q] = (uint8_t)dgt;
+        sv[q] = (uint16_t)v;
+      } else {
+        perm[q] = (int32_t)(o + v);
+      }
+    }
+  }
+  if (!STAGE) return;
   __syncthreads();
   for (int j = threadIdx.x; j < (int)tn; j += TPB) {
     const uint32_t dgt = sk[j];
@@ -2489,7 +2966,9 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       bk[k] = kp ? bin_of(xv[k], e_lds, nb) : (uint32_t)nb + 1;
       if (kp) a.bins[pos[k]] = bk[k];
     }
-    for (int q = 0; q < nm; ++q) {  // uniform
+#pragma unroll
+    for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: the fields are kernel-argument scalars
+      if (q >= nm) break;
       const int col = a.fs.col[q], fq = a.fs.f[q], wq = a.fs.w[q];
       double *aq = acc + q * nb;
 #pragma unroll
@@ -2948,6 +3427,10 @@ struct Profile {
   bool bins_in8 = false;  // the last assignment's bins are bytes in bins8 (ensure_bins32)
   // lazy selection (select_launch): keep words, tile offsets, staged masses
   Buf kw, toff, mstage, xc, kpre;
+  // tiled radial calls: level-0 geometry hints (two SelHint slots, by call
+  // parity) and select_tiles' digit rows
+  Buf shint, srows, swc, sbt;  // + select_tiles' per-(tile, wave) counts and block totals
+  uint64_t n_tiled = 0;
   bool lazy = false, w_ready = false, idx_ready = false;
   bool x_tiled = false;  // x holds a tiled selection (tile t at x[t * TILE ..]): ensure_x
   int64_t sel_base = 0, sel_span = 0;
@@ -2963,22 +3446,22 @@ struct Profile {
   // path counters (pbx_profile_path_stats): one-launch calls, of them
   // discarded (re-run by the multi-kernel path), multi-kernel calls
   int64_t n_mono = 0, n_mono_discard = 0, n_multi = 0;
+  // tiled multi-kernel calls, of them with the level-0 histogram from
+  // select_tiles (the hinted geometry held: no re-read of x)
+  int64_t n_tiled_calls = 0, n_hinted = 0;
 };
 
 static void ensure_x(Profile &P, hipStream_t st);
 
-__global__ void widen_bins(const uint8_t *__restrict__ b8, int64_t n, uint32_t *__restrict__ b) {
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB)
-    b[i] = b8[i];
-}
-
-// bins as uint32 for the consumers that read them (assign_gather leaves bytes)
+// bins as uint32 by selection index for the consumers that read them
+// (assign_gather leaves bytes by particle slot)
 static void ensure_bins32(Profile &P, hipStream_t st) {
   if (!P.bins_in8) return;
-  if (P.n > 0) {
+  if (P.n > 0 && P.sel_nt) {
     uint32_t *b = (uint32_t *)P.bins.get(sizeof(uint32_t) * (size_t)P.n);
-    const unsigned grid = (unsigned)std::min<int64_t>(4096, (P.n + TPB - 1) / TPB);
-    hipLaunchKernelGGL(widen_bins, dim3(grid), dim3(TPB), 0, st, (const uint8_t *)P.bins8.p, P.n, b);
+    hipLaunchKernelGGL((tile_compact<uint8_t, uint32_t>), dim3(P.sel_nt), dim3(TPB), 0, st,
+                       (const uint8_t *)P.bins8.p, (const uint64_t *)P.kw.p,
+                       (const uint32_t *)P.toff.p, b);
     PBX_HIP(hipGetLastError());
   }
   P.bins_in8 = false;
@@ -3339,10 +3822,21 @@ static SelPrep select_prep(Profile &P, hipStream_t st, const void *pos, const vo
   return r;
 }
 
+// grid of the fused level-0 kernels (fused_hist0, assign_gather, ...) over n_sel particles
+static int fused_grid(int64_t n_sel) {
+  return (int)std::min<int64_t>(256, std::max<int64_t>(1, n_sel / (MS0_TPB * 16)));
+}
+
+struct TileHist {  // select_tiles' hinted level-0 histogram (null hint: none)
+  const SelHint *hint = nullptr;
+  uint64_t ka = 0, kb = ~0ull;
+};
+
 static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
                               int64_t n, int on_device, int use_sphere, const double *sphere,
                               const int64_t *fam, int nfam, int ndim, bool lazy = false,
-                              int pos_f32 = 0, int mass_f32 = 0, bool tiled = false) {
+                              int pos_f32 = 0, int mass_f32 = 0, bool tiled = false,
+                              const TileHist *th = nullptr) {
   const SelPrep r = select_prep(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
                                 lazy, pos_f32, mass_f32, tiled);
   const SelectParams &sp = r.sp;
@@ -3350,8 +3844,8 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
   const int64_t hi = r.hi, span = r.span;
   const void *d_pos = r.d_pos, *d_mass = r.d_mass;
   // per-tile look-back status words + ticket / watchdog (selection scratch)
-  // [stat nt][ctrl: ticket, watchdog][MM_SLOTS x (~min key, max key)]: one zero fill
-  const size_t nst = (size_t)nt + 1 + 2 * MM_SLOTS;
+  // [stat nt][ctrl: ticket, watchdog][MM_SLOTS x (~min key, max key)][hint flag]: one zero fill
+  const size_t nst = (size_t)nt + 1 + 2 * MM_SLOTS + 1;
   uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * nst);
   uint32_t *ctrl = (uint32_t *)(stat + nt);
   double *xo = r.xo;
@@ -3385,7 +3879,20 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
         const char *v = std::getenv("PBX_SEL_BT");
         return !(v && std::strcmp(v, "256") == 0);
       }();
-      if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
+      if (lazy && P.x_tiled) {  // persistent tiles (+ the hinted level-0 histogram)
+        const int G0 = fused_grid(span);
+        const unsigned G1 = (unsigned)(SH_K * (G0 - 1));
+        uint32_t *rows16 = nullptr;
+        if (th && th->hint)
+          rows16 = (uint32_t *)P.srows.get(sizeof(uint32_t) * (size_t)G1 * (MS0_DIG / 2));
+        uint32_t *wc = (uint32_t *)P.swc.get(sizeof(uint32_t) * (size_t)nt * SH_NW);
+        uint32_t *bt = (uint32_t *)P.sbt.get(sizeof(uint32_t) * (size_t)G1);
+        hipLaunchKernelGGL(sp.nfam > 1 ? select_tiles<true> : select_tiles<false>, dim3(G1),
+                           dim3(SH_BT), 0, st, (const double *)d_pos, hi,
+                           sp, nt, (uint32_t)G0, xo, kw, r.kpre, wc, toff, bt, mm,
+                           th ? th->hint : nullptr, th ? th->ka : 0ull, th ? th->kb : ~0ull, rows16,
+                           (uint32_t *)(mm + 2 * MM_SLOTS));
+      } else if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
       else if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
       else if (sel512) go(select_onepass<512, false, double>, 512, 0.0);
       else go(select_onepass<TPB, false, double>, TPB, 0.0);
@@ -3422,8 +3929,9 @@ static void ensure_x(Profile &P, hipStream_t st) {
   if (!P.x_tiled) return;
   double *xc = (double *)P.xc.get(sizeof(double) * (size_t)std::max<int64_t>(P.n, 1));
   if (P.sel_nt && P.n)
-    hipLaunchKernelGGL(tile_compact, dim3(P.sel_nt), dim3(TPB), 0, st, (const double *)P.x.p,
-                       (const uint32_t *)P.toff.p, P.sel_nt, P.n, xc);
+    hipLaunchKernelGGL((tile_compact<double, double>), dim3(P.sel_nt), dim3(TPB), 0, st,
+                       (const double *)P.x.p, (const uint64_t *)P.kw.p, (const uint32_t *)P.toff.p,
+                       xc);
   PBX_HIP(hipGetLastError());
   std::swap(P.x, P.xc);
   P.x_tiled = false;
@@ -3755,12 +4263,22 @@ int pbx_profile_destroy(void *handle) {
                   &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst, &p->accs,
                   &p->pk0, &p->pk1, &p->pv0, &p->pv1, &p->pbk, &p->pcdf, &p->poff, &p->pq, &p->pout,
                   &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack, &p->frec, &p->fblk,
-                  &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->mono, &p->bar,
+                  &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->shint, &p->srows,
+                  &p->swc, &p->sbt, &p->mono, &p->bar,
                   &p->mono_trace, &p->dscal, &p->dlc};
     for (Buf *b : all) b->release();
     p->pin.release();
     p->mpin.release();
     delete p;
+  });
+}
+
+int pbx_profile_level0_stats(void *handle, int64_t *out) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (!out) fail(PBX_ERR_VALUE, "null output");
+    out[0] = P.n_tiled_calls;
+    out[1] = P.n_hinted;
   });
 }
 
@@ -4310,6 +4828,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
     static_assert(sizeof(FusedCtl) % sizeof(double) == 0, "FusedCtl packs as doubles");
     // small selections: the whole step as one persistent launch (radial_mono)
     double *hp = nullptr;
+    bool tiled_call = false;  // the multi-kernel path over a tiled selection
     int nsum = 0;
     int64_t n_global = 0;  // dist: kept particles over all ranks
     if (lazy && mono_enabled() && !dist)
@@ -4317,8 +4836,30 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                            nbins, ka, kb, empty_bounds, fs, &nsum);
     if (!hp) {  // the multi-kernel path
       ++P.n_multi;
+      // one rank, lazy: the level-0 histogram of a tiled selection is built by
+      // select_tiles with the previous tiled call's geometry (slot n_tiled & 1;
+      // fused_hist0 writes this call's into the other slot)
+      SelHint *hints = nullptr;
+      static const bool hint_env = [] {  // A/B: PBX_SEL_HINT=0 always re-reads x for level 0
+        const char *v = std::getenv("PBX_SEL_HINT");
+        return !(v && v[0] == '0');
+      }();
+      if (!dist && lazy && hint_env) {
+        if (!P.shint.p) {
+          P.shint.get(2 * sizeof(SelHint));
+          PBX_HIP(hipMemsetAsync(P.shint.p, 0, 2 * sizeof(SelHint), st));
+        }
+        hints = (SelHint *)P.shint.p;
+      }
+      TileHist thist;
+      thist.hint = hints ? hints + (P.n_tiled & 1) : nullptr;
+      thist.ka = ka;
+      thist.kb = empty_bounds ? 0ull : kb;
       const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
-                                        nfam, ndim, lazy, 0, 0, /*tiled=*/true);
+                                        nfam, ndim, lazy, 0, 0, /*tiled=*/true, &thist);
+      const bool hinted = hints && P.x_tiled;
+      tiled_call = P.x_tiled;
+      if (hinted) ++P.n_tiled;  // (the next tiled call reads the slot this one writes)
       if (dist)  // global key range: every min / max slot pair (~min, max) max-reduced
         comm_allreduce(comm, (uint64_t *)P.selst.p + nt + 1, (uint64_t *)P.selst.p + nt + 1,
                        2 * MM_SLOTS, 2, 2, st);
@@ -4332,18 +4873,23 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       const double *x = (const double *)P.x.p;
       // level 0 (rows -> H), resolve + groups, per-block offsets, gather,
       // per-group finish -> edges
-      const int g0 = (int)std::min<int64_t>(256, std::max<int64_t>(1, n_sel / (MS0_TPB * 16)));
+      const int g0 = fused_grid(n_sel);
       uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
       // tiled selections: assignment fused with the gather (assign_gather),
       // the deferred keys binned block by block by fix_deferred
       const bool agath = tiled && lazy && n_sel && !agather_off();
       uint32_t *bcnt = agath ? (uint32_t *)P.fblk.get(sizeof(uint32_t) * 3 * (size_t)g0) : nullptr;
+      const uint32_t *hflag = (const uint32_t *)(stat + nt + 1 + 2 * MM_SLOTS);
       const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
-                           (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0, (int)dist};
+                           (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0, (int)dist,
+                           (const uint64_t *)P.kw.p,
+                           hinted ? hints + ((P.n_tiled - 1) & 1) : nullptr, hflag,
+                           hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p};
       hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
                          rows);
-      hipLaunchKernelGGL(msel_reduce0, dim3(MS0_DIG / TPB, 8), dim3(TPB), 0, st,
-                         (const uint32_t *)rows, g0, H);
+      hipLaunchKernelGGL(msel_reduce0h, dim3(MS0_DIG / 2 / TPB, 32), dim3(TPB), 0, st,
+                         (const uint32_t *)rows, g0, (const uint32_t *)P.srows.p,
+                         hinted ? SH_K * (g0 - 1) : 0, (const int32_t *)&ctl->hint, H);
       int64_t *gsc = nullptr;  // dist: [global kept count][ctl copy]
       uint32_t *lc_all = nullptr;
       if (dist) {
@@ -4361,7 +4907,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                          goff, gq);
       hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
                          (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff,
-                         bcnt, dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr);
+                         bcnt, dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr,
+                         (const uint32_t *)P.srows.p);
       int64_t seg_total = 0;  // dist: keys in all ranks' group segments
       if (dist) {
         comm_allreduce(comm, lc_all, lc_all, (int64_t)cr.nranks * MS_MAXQ, 3, 0, st);
@@ -4397,15 +4944,14 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         const int nr = (int)nb + 1;
         const int64_t macc = (int64_t)fs.nm * nb;
         th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * nr);
-        bins8 = (uint8_t *)P.bins8.get((size_t)n_sel);
+        bins8 = (uint8_t *)P.bins8.get((size_t)nt * TILE);  // by particle slot
         double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)(2 * g0) * macc) : nullptr;
         go = GatherOut{seg, (AgRec *)P.frec.get(sizeof(AgRec) * (size_t)n_sel), bcnt, bcnt + g0,
                        bcnt + 2 * g0};
         const size_t lds = sizeof(double) * (size_t)macc + sizeof(uint32_t) * (size_t)(nr | 1) * AG_TR;
         auto ag = [&](auto kern) {
           hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, x, (const uint64_t *)P.kw.p,
-                             (const uint16_t *)P.kpre.p, (const uint32_t *)P.toff.p, P.sel_base,
-                             nt, P.sel_mass,
+                             P.sel_base, P.sel_span, nt, P.sel_mass,
                              (const FusedCtl *)ctl, ka, kb, (const MsRank *)R, nq,
                              (const uint32_t *)gdig, (const uint32_t *)boff, (int)nb, bins8, th,
                              fs, slab, go);
@@ -4421,7 +4967,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       } else {
         hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
                            (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)boff,
-                           seg, tiled ? (const uint64_t *)stat : nullptr, nt);
+                           seg, tiled ? (const uint64_t *)P.kw.p : nullptr, nt);
       }
       if (dist)  // every rank's group keys, each in its own slice: the all-gather
         comm_allreduce(comm, seg, seg, seg_total, 2, 0, st);
@@ -4446,9 +4992,17 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         cnt_offs = th;
         if (build_csr) {
           int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
-          hipLaunchKernelGGL(csr_sel<uint8_t>, dim3(nt), dim3(TPB), 0, st,
-                             (const uint32_t *)P.toff.p, n_dev, (const uint8_t *)bins8,
-                             (const uint32_t *)th, nt, perm, nr);
+          static const bool stage = [] {  // A/B: PBX_CSR_DIRECT=1 stores without LDS staging
+            const char *v = std::getenv("PBX_CSR_DIRECT");
+            return !(v && v[0] == '1');
+          }();
+          const bool ord = lds_atomics_lane_ordered(d.id, st);
+          auto cs = stage ? (ord ? csr_slots<true, true> : csr_slots<true, false>)
+                          : (ord ? csr_slots<false, true> : csr_slots<false, false>);
+          hipLaunchKernelGGL(cs, dim3(nt), dim3(TPB), 0, st,
+                             (const uint32_t *)P.toff.p, (const uint64_t *)P.kw.p,
+                             (const uint16_t *)P.kpre.p, (const uint32_t *)P.swc.p,
+                             (const uint8_t *)bins8, (const uint32_t *)th, nt, perm, nr);
           PBX_HIP(hipGetLastError());
         }
       } else if (n_sel && lazy) {
@@ -4576,6 +5130,10 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
     const double *hmo = (const double *)(hcn + nb);
     const FusedCtl c = *hc;
     if (c.err & 1) fail(PBX_ERR_RUNTIME, "selection look-back did not complete");
+    if (tiled_call) {
+      ++P.n_tiled_calls;
+      if (c.hint) ++P.n_hinted;
+    }
     P.mm[0] = c.kmin;
     P.mm[1] = c.kmax;
     select_commit(P, c.n);

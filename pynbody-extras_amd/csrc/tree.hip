@@ -542,7 +542,7 @@ __device__ __forceinline__ void p2m_add(double (&M)[ncoef(P)], double m, double 
 //   M[l,m,n] += sum_{i<=l, j<=m, k<=n} C[i,j,k] (-t)^(l-i,m-j,n-k) / (l-i)!(m-j)!(n-k)!
 template <int P>
 __device__ __forceinline__ void m2m_add(double (&M)[ncoef(P)], const double *__restrict__ C,
-                                        double tx, double ty, double tz) {
+                                        int64_t cs, double tx, double ty, double tz) {
   double ex[P + 1], ey[P + 1], ez[P + 1];
   ex[0] = ey[0] = ez[0] = 1.0;
   static_for<P>([&](auto ac) {
@@ -552,7 +552,7 @@ __device__ __forceinline__ void m2m_add(double (&M)[ncoef(P)], const double *__r
     ez[a] = ez[a - 1] * (-tz) * (1.0 / a);
   });
   double c[ncoef(P)];
-  static_for<ncoef(P)>([&](auto sc) { c[decltype(sc)::value] = C[decltype(sc)::value]; });
+  static_for<ncoef(P)>([&](auto sc) { c[decltype(sc)::value] = C[decltype(sc)::value * cs]; });
   static_for<ncoef(P)>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     constexpr int l = kSlots[s].l, m = kSlots[s].m, n = kSlots[s].n;
@@ -619,7 +619,7 @@ struct PayloadView {
   const double *soft;  // sorted softenings or null
   double4 *com;        // com xyz + mass
   double *hmax;        // or null
-  double *mom;         // ncoef(P) per node (P >= 2) or null
+  double *mom;         // ncoef(P) per node (P >= 2) or null; coefficient q of node k at q * nn + k
   // the node's walk record, written here too (DFS preorder pre[k])
   const int32_t *pre, *size;
   const double4 *ncen;
@@ -627,14 +627,28 @@ struct PayloadView {
   double *walk;
 };
 
-// one level of the bottom-up payload pass (tree.rs:866-1067)
+// one level of the bottom-up payload pass (tree.rs:866-1067).
+// Layout for coalesced stores: the moments are coefficient-major (q * nn +
+// k: a wave's consecutive nodes store consecutive words), and the walk
+// records (DFS preorder, scattered over the array: 64 lanes x 24 words
+// would touch 64 lines per store) go through LDS and leave record by
+// record, consecutive lanes on consecutive words of one record.
+constexpr int PL_TPB = 256;
+template <int P> __host__ __device__ constexpr bool rec_via_lds() { return rec_stride<P>() <= 24; }
 template <int P>
-__global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, int32_t b) {
-  int32_t k = a + (int32_t)(blockIdx.x * TPB + threadIdx.x);
-  if (k >= b) return;
+__global__ void __launch_bounds__(PL_TPB) payload_level(PayloadView v, int32_t a, int32_t b) {
+  constexpr int RS = rec_stride<P>();
+  constexpr int RSP = RS + 1;  // LDS row stride (odd: lanes on distinct banks)
+  __shared__ double rs[rec_via_lds<P>() ? (PL_TPB / 64) * 64 * RSP : 1];
+  __shared__ int32_t rpk[rec_via_lds<P>() ? PL_TPB : 1];
+  const int32_t k = a + (int32_t)(blockIdx.x * PL_TPB + threadIdx.x);
+  const bool live = k < b;
+  const int64_t nn = v.nn;
   double mass = 0.0, cx = 0.0, cy = 0.0, cz = 0.0, hm = 0.0;
-  const int32_t nc = v.nchild[k];
-  if (nc == 0) {
+  double M[P >= 2 ? ncoef(P) : 1];
+  static_for<(P >= 2 ? ncoef(P) : 1)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
+  const int32_t nc = live ? v.nchild[k] : 0;
+  if (live && nc == 0) {
     const int32_t s = v.nstart[k], c = v.ncount[k];
     // leaves of up to PL particles: every record in flight at once, then the
     // same ordered sums as the general loop (identical results)
@@ -673,25 +687,23 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
     }
     if (v.hmax)
       for (int32_t j = s; j < s + c; ++j) hm = __builtin_fmax(hm, __builtin_fmax(v.soft[j], 0.0));
-    if (P >= 2 && mass != 0.0) {
-      double M[ncoef(P)];
-      static_for<ncoef(P)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
-      if (small) {
+    if constexpr (P >= 2) {
+      if (mass != 0.0) {
+        if (small) {
 #pragma unroll
-        for (int q = 0; q < PL; ++q) {
-          if (q >= c) break;
-          p2m_add<P>(M, rr[q].w, rr[q].x - cx, rr[q].y - cy, rr[q].z - cz);
-        }
-      } else {
-        for (int32_t j = s; j < s + c; ++j) {
-          const double4 r = v.rec[j];
-          p2m_add<P>(M, r.w, r.x - cx, r.y - cy, r.z - cz);
+          for (int q = 0; q < PL; ++q) {
+            if (q >= c) break;
+            p2m_add<P>(M, rr[q].w, rr[q].x - cx, rr[q].y - cy, rr[q].z - cz);
+          }
+        } else {
+          for (int32_t j = s; j < s + c; ++j) {
+            const double4 r = v.rec[j];
+            p2m_add<P>(M, r.w, r.x - cx, r.y - cy, r.z - cz);
+          }
         }
       }
-      static_for<ncoef(P)>(
-          [&](auto qc) { v.mom[(int64_t)k * ncoef(P) + decltype(qc)::value] = M[decltype(qc)::value]; });
     }
-  } else {
+  } else if (live) {
     const int32_t f = v.nfirst[k];
     double4 cq[8];  // an octree node has at most 8 children: all in flight at once
 #pragma unroll
@@ -716,33 +728,32 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
     }
     if (v.hmax)
       for (int32_t ch = f; ch < f + nc; ++ch) hm = __builtin_fmax(hm, v.hmax[ch]);
-    if (P >= 2 && mass != 0.0) {
-      double M[ncoef(P)];
-      static_for<ncoef(P)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
+    if constexpr (P >= 2) {
+      if (mass != 0.0) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (q >= nc) break;
-        const double4 c4 = cq[q];
-        if (c4.w == 0.0) continue;
-        m2m_add<P>(M, v.mom + (int64_t)(f + q) * ncoef(P), cx - c4.x, cy - c4.y, cz - c4.z);
+        for (int q = 0; q < 8; ++q) {
+          if (q >= nc) break;
+          const double4 c4 = cq[q];
+          if (c4.w == 0.0) continue;
+          m2m_add<P>(M, v.mom + (f + q), nn, cx - c4.x, cy - c4.y, cz - c4.z);
+        }
       }
-      static_for<ncoef(P)>(
-          [&](auto qc) { v.mom[(int64_t)k * ncoef(P) + decltype(qc)::value] = M[decltype(qc)::value]; });
-    } else if (P >= 2) {
-#pragma unroll
-      for (int q = 0; q < ncoef(P); ++q) v.mom[(int64_t)k * ncoef(P) + q] = 0.0;
     }
   }
-  if (P >= 2 && nc == 0 && mass == 0.0) {
-#pragma unroll
-    for (int q = 0; q < ncoef(P); ++q) v.mom[(int64_t)k * ncoef(P) + q] = 0.0;
+  if (live) {
+    if constexpr (P >= 2)  // coefficient-major: coalesced over the wave's nodes
+      static_for<ncoef(P)>([&](auto qc) {
+        v.mom[(int64_t)decltype(qc)::value * nn + k] = M[decltype(qc)::value];
+      });
+    v.com[k] = make_double4(cx, cy, cz, mass);
+    if (v.hmax) v.hmax[k] = hm;
   }
-  v.com[k] = make_double4(cx, cy, cz, mass);
-  if (v.hmax) v.hmax[k] = hm;
-  {  // the walk record (was pack_walk / pack_coef / pack_moments)
+  // the walk record (was pack_walk / pack_coef / pack_moments)
+  double r[RS];
+  int32_t pk = 0;
+  if (live) {
 #pragma clang fp contract(off)
-    const int32_t pk = v.pre[k];
-    double *r = v.walk + (int64_t)pk * rec_stride<P>();
+    pk = v.pre[k];
     r[0] = cx;
     r[1] = cy;
     r[2] = cz;
@@ -754,23 +765,36 @@ __global__ void __launch_bounds__(TPB) payload_level(PayloadView v, int32_t a, i
     // (the same threading as tree.rs:736-776, renumbered)
     const int64_t after = (int64_t)pk + v.size[k];
     const bool leaf = nc == 0;
-    int32_t *ir = (int32_t *)(r + 6);
-    ir[0] = after < v.nn ? (int32_t)after : -1;
+    int32_t ir[4];
+    ir[0] = after < nn ? (int32_t)after : -1;
     ir[1] = leaf ? -1 : pk + 1;
     ir[2] = leaf ? v.nstart[k] : 0;
     ir[3] = leaf ? v.ncount[k] : 0;
-    if constexpr (P >= 2) {
-      const double *Mk = v.mom + (int64_t)k * ncoef(P);  // just written by this thread
-      if constexpr (P == 2 || P == 3) {
-        double Mc[ncoef(P)];
+    r[6] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[0] | ((uint64_t)(uint32_t)ir[1] << 32));
+    r[7] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[2] | ((uint64_t)(uint32_t)ir[3] << 32));
+    if constexpr (P == 2 || P == 3) {
+      detraced_coef<P>(M, r + 8);
+    } else if constexpr (P >= 4) {
 #pragma unroll
-        for (int q = 0; q < ncoef(P); ++q) Mc[q] = Mk[q];
-        detraced_coef<P>(Mc, r + 8);
-      } else {
-#pragma unroll
-        for (int q = 0; q < ncoef(P); ++q) r[8 + q] = Mk[q];
-      }
+      for (int q = 0; q < ncoef(P); ++q) r[8 + q] = M[q];
     }
+  }
+  if constexpr (rec_via_lds<P>()) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double *wr = rs + w * 64 * RSP;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) wr[lane * RSP + j] = r[j];
+    rpk[threadIdx.x] = live ? pk : -1;
+    __syncthreads();
+    // record i of this wave, word j: lanes on consecutive words
+    for (int idx = lane; idx < 64 * RS; idx += 64) {
+      const int i = idx / RS, j = idx - i * RS;
+      const int32_t pi = rpk[w * 64 + i];
+      if (pi >= 0) v.walk[(int64_t)pi * RS + j] = wr[i * RSP + j];
+    }
+  } else if (live) {
+#pragma unroll
+    for (int j = 0; j < RS; ++j) v.walk[(int64_t)pk * RS + j] = r[j];
   }
 }
 
@@ -1944,7 +1968,9 @@ template <int P>
 static void run_payload(Octree &T, hipStream_t st, PayloadView v) {
   for (int L = (int)T.lvl.size() - 2; L >= 0; --L) {
     const int32_t a = T.lvl[L], b = T.lvl[L + 1];
-    if (b > a) hipLaunchKernelGGL(payload_level<P>, dim3(nblk(b - a)), dim3(TPB), 0, st, v, a, b);
+    if (b > a)
+      hipLaunchKernelGGL(payload_level<P>, dim3((unsigned)((b - a + PL_TPB - 1) / PL_TPB)),
+                         dim3(PL_TPB), 0, st, v, a, b);
   }
   PBX_HIP(hipGetLastError());
 }
@@ -2241,20 +2267,39 @@ __global__ void __launch_bounds__(TPB)
 }
 
 // out = [counts nb (u64)][moments nb x 7]: column j summed over the rows in
-// a fixed order (thread j, rows 0, 1, ...)
-__global__ void radial_moments_reduce(const double *__restrict__ slab,
-                                      const uint32_t *__restrict__ cslab, int rows, int nb,
-                                      double *__restrict__ out) {
-  const int j = blockIdx.x * TPB + threadIdx.x;
+// a fixed order: RR_G row groups (group g: rows g, g + RR_G, ...) summed
+// by one thread each, coalesced over RR_C columns, then the group partials
+// in group order (LDS).  (One thread per column over all rows took 130 us
+// at 4M: ~2k dependent rows per thread.)
+constexpr int RR_C = 32, RR_G = 32;
+__global__ void __launch_bounds__(RR_C * RR_G)
+    radial_moments_reduce(const double *__restrict__ slab, const uint32_t *__restrict__ cslab,
+                          int rows, int nb, double *__restrict__ out) {
+  __shared__ double ps[RR_G][RR_C + 1];
+  __shared__ unsigned long long pc[RR_G][RR_C + 1];
+  const int c = threadIdx.x % RR_C, g = threadIdx.x / RR_C;
+  const int j = blockIdx.x * RR_C + c;
+  double sum = 0.0;
+  unsigned long long cnt = 0;
   if (j < nb) {
-    unsigned long long c = 0;
-    for (int r = 0; r < rows; ++r) c += cslab[(int64_t)r * nb + j];
-    out[j] = __builtin_bit_cast(double, c);
+    for (int r = g; r < rows; r += RR_G) cnt += cslab[(int64_t)r * nb + j];
   } else if (j < 8 * nb) {
     const int k = j - nb;
-    double s = 0.0;
-    for (int r = 0; r < rows; ++r) s += slab[(int64_t)r * 7 * nb + k];
-    out[j] = s;
+    for (int r = g; r < rows; r += RR_G) sum += slab[(int64_t)r * 7 * nb + k];
+  }
+  ps[g][c] = sum;
+  pc[g][c] = cnt;
+  __syncthreads();
+  if (g == 0 && j < 8 * nb) {
+    if (j < nb) {
+      unsigned long long t = 0;
+      for (int q = 0; q < RR_G; ++q) t += pc[q][c];
+      out[j] = __builtin_bit_cast(double, t);
+    } else {
+      double t = 0.0;
+      for (int q = 0; q < RR_G; ++q) t += ps[q][c];
+      out[j] = t;
+    }
   }
 }
 
@@ -2493,7 +2538,8 @@ int pbx_octree_radial_moments(pbx_octree *t, int64_t first, int64_t count, const
     const size_t lds = (e_lds ? eb : 0) + lds_acc;  // <= 61,440 B at RM_MAXB
     hipLaunchKernelGGL(radial_moments_kernel, dim3(rows), dim3(TPB), lds, st, T.rec.as<double4>(),
                        d_f, first, count, (const double *)de, nb, slab, cslab, e_lds);
-    hipLaunchKernelGGL(radial_moments_reduce, dim3(nblk(8 * (int64_t)nb)), dim3(TPB), 0, st,
+    hipLaunchKernelGGL(radial_moments_reduce, dim3((unsigned)((8 * (int64_t)nb + RR_C - 1) / RR_C)),
+                       dim3(RR_C * RR_G), 0, st,
                        (const double *)slab, (const uint32_t *)cslab, rows, nb, out);
     PBX_HIP(hipGetLastError());
     PBX_HIP(hipMemcpyAsync(hp, out, ob, hipMemcpyDeviceToHost, st));
@@ -2586,9 +2632,17 @@ int pbx_octree_export(pbx_octree *t, double *center, double *com, double *hmax, 
     }
     std::vector<int32_t> pm(n);
     if (perm) dl(pm.data(), T.perm.p, 4 * n);
-    if (moments && T.has_bh && T.moment_order() >= 2)
-      dl(moments, T.mom.p, 8 * (size_t)nn * ncoef(T.moment_order()));
+    std::vector<double> momq;  // coefficient-major on the device
+    if (moments && T.has_bh && T.moment_order() >= 2) {
+      momq.resize((size_t)nn * ncoef(T.moment_order()));
+      dl(momq.data(), T.mom.p, 8 * momq.size());
+    }
     PBX_HIP(hipStreamSynchronize(st));
+    if (!momq.empty()) {
+      const int nq = ncoef(T.moment_order());
+      for (int64_t i = 0; i < nn; ++i)
+        for (int q = 0; q < nq; ++q) moments[i * nq + q] = momq[(size_t)q * nn + i];
+    }
     for (int64_t i = 0; i < nn; ++i) {
       if (links) {
         links[3 * i] = c[i] ? a[i] : -1;

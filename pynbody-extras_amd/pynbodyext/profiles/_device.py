@@ -226,6 +226,15 @@ class DeviceBins:
         nat.call("pbx_profile_path_stats", self._h, _i64(out))
         return {"mono": int(out[0]), "mono_discarded": int(out[1]), "multi": int(out[2])}
 
+    def level0_stats(self) -> dict:
+        """Tiled multi-kernel radial_equaln calls on this handle, and of them
+        those whose level-0 digit histogram the selection kernel counted with
+        the previous tiled call's geometry (no second read of x;
+        pbx_profile_level0_stats)."""
+        out = np.zeros(2, dtype=np.int64)
+        nat.call("pbx_profile_level0_stats", self._h, _i64(out))
+        return {"tiled": int(out[0]), "hinted": int(out[1])}
+
     def selection(self, idx=True, x=True, w=True):
         """(original indices int64, x, weights) of the fused selection."""
         oi = np.empty(self.n, dtype=np.int64) if idx else None

@@ -650,10 +650,83 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
                     assert np.array_equal(a2.percentiles([10, 50, 90]), b.percentiles([10, 50, 90]))
                 finally:
                     a2.close()
+            if n > 1_000_000:
+                # the same call again on the handle: select_tiles counts the
+                # level-0 histogram with this call's digit geometry (no second
+                # read of x) — same edges, counts, CSR; sums to float-add order
+                st0 = a.level0_stats()
+                assert st0 == {"tiled": 1, "hinted": 0}, st0
+                _, e3, c3, m3 = DeviceBins.radial_equaln(pos, mass, nbins=nb, sphere=sphere,
+                                                         families=fams, bin_min=lo, bin_max=hi,
+                                                         stats=stats, into=a)
+                assert a.level0_stats() == {"tiled": 2, "hinted": 1}, a.level0_stats()
+                assert np.array_equal(e3, e1, equal_nan=True) and np.array_equal(c3, c1)
+                for u, v in zip(m3, m1):
+                    np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300)
+                p4, o4 = a.csr()
+                assert np.array_equal(p4, p1) and np.array_equal(o4, o1)
         finally:
             a.close()
     finally:
         b.close()
+
+
+def test_radial_equaln_tiled_level0_hint_transitions(gpu):
+    """Tiled calls on one handle (>= 1024 selection tiles): a call whose
+    window keys all fall inside the previous tiled call's level-0 digit range
+    takes the histogram select_tiles counted with it (no second read of x);
+    a call with a key outside it (a wider or shifted radius range, a NaN, a
+    clipped window) falls back to the re-read — either way edges, counts and
+    CSR equal the oracle's (bins.py:720-746, :346-395) and the sums agree to
+    1e-12."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(33)
+    n = 4_400_000
+    base = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    nanpos = base.copy()
+    nanpos[::997] = np.nan
+    # (positions, bin_min, bin_max, level-0 histogram from the selection?
+    # None: either — the digits are valid both ways, only coarser or finer)
+    calls = [(base, None, None, False),          # first tiled call: no geometry yet
+             (base, None, None, True),           # the same keys
+             (base * 0.999, None, None, True),   # within the range's 1/64 margins
+             (base * 1e6, None, None, False),    # 20 octaves above it
+             (base * 1e6, None, None, True),
+             (base * 1e-6, None, None, False),   # far below it
+             (nanpos * 1e-6, None, None, False), # NaN keys (the largest key) escape it
+             (nanpos * 1e-6, None, None, True),  # (NaN-wide digits: coarse, still exact)
+             (base, 1.0, 4.0, None),             # a window inside the NaN-wide range
+             (base, 1.0, 4.0, True),
+             (base, 2.0, None, None)]            # a window open above
+    h = DeviceBins()
+    try:
+        hinted = 0
+        for k, (pos, lo, hi, want_hint) in enumerate(calls):
+            _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h,
+                                                  bin_min=lo, bin_max=hi)
+            st = h.level0_stats()
+            got_hint = st["hinted"] - hinted
+            hinted = st["hinted"]
+            assert st["tiled"] == k + 1, (k, st)
+            if want_hint is not None:
+                assert got_hint == int(want_hint), (k, st)
+            ref = _oracle_radial(pos, mass, None, None, 128, lo, hi)
+            assert np.array_equal(e, ref["edges"], equal_nan=True), k
+            assert np.array_equal(c, ref["counts"]), k
+            p, o = h.csr()
+            assert np.array_equal(o, ref["offsets"]) and np.array_equal(p, ref["perm"]), k
+            ne = c > 0
+            for (f, w, cols), got in zip(stats, m):
+                for col in range(7):
+                    if (cols >> col) & 1 and not (w == -1 and col in (0, 1, 2, 5)):
+                        want = _oracle_col(ref, f, w, col)
+                        np.testing.assert_allclose(got[ne, col], want[ne], rtol=1e-12,
+                                                   atol=1e-12 * np.nanmax(np.abs(want[ne])))
+    finally:
+        h.close()
 
 
 def test_radial_equaln_one_launch_reused_handle_and_size_boundary(gpu):
