@@ -10,7 +10,6 @@
 #pragma once
 
 #include <algorithm>
-#include <mutex>
 
 #include "pbx_common.h"
 
@@ -127,43 +126,6 @@ __device__ __forceinline__ uint32_t bin_of(double v, E e, int nb) {
   }
   return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
 }
-
-// Same-address lanes of ONE returning LDS atomic get their old values in
-// ascending lane order on gfx950 (measured: tools/probe_ldsorder.hip, 1.5e9
-// lane results over 1..511 addresses and 4 strides, no exception), so
-// `atomicAdd(&count[digit], 1)` alone gives every lane its stable rank among
-// the wave's earlier elements of its digit — no peer-mask ballots.  Not an
-// ISA guarantee: lds_order_probe re-checks it once per device at first use
-// (lds_atomics_lane_ordered) and the kernels that rely on it fall back to
-// peers8 ranks if it ever fails.
-namespace {
-__global__ void __launch_bounds__(256) lds_order_probe(unsigned long long *bad) {
-  __shared__ uint32_t cnt[4][1024];
-  const int w = threadIdx.x >> 6;
-  const uint32_t lane = lane_id();
-  uint32_t x = 2654435761u * (blockIdx.x * 256 + threadIdx.x + 1);
-  unsigned long long nb = 0;
-  for (int it = 0; it < 48; ++it) {
-    const uint32_t K = 1u + (uint32_t)((it * 37) % 256);  // addresses d * stride < 1024
-    const uint32_t stride = 1u + (uint32_t)(it & 3);
-    for (int i = lane; i < 1024; i += 64) cnt[w][i] = 0;
-    __builtin_amdgcn_s_waitcnt(0);  // the zeros land before the atomics (a store may trail them)
-    x ^= x << 13;
-    x ^= x >> 17;
-    x ^= x << 5;
-    const uint32_t d = (x >> 8) % K;
-    const uint32_t r = atomicAdd(&cnt[w][d * stride], 1u);
-    uint64_t m = ~0ull;
-#pragma unroll
-    for (int b = 0; b < 9; ++b) {
-      const uint64_t bal = __ballot((d >> b) & 1u);
-      m &= ((d >> b) & 1u) ? bal : ~bal;
-    }
-    nb += (r != rank_below(m)) ? 1ull : 0ull;
-  }
-  if (nb) atomicAdd(bad, nb);
-}
-}  // namespace
 
 // exclusive scan of one u32 per thread over the block
 __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t *lds_wave, uint32_t *total) {
@@ -359,14 +321,12 @@ enum ValMode { VAL_NONE = 0, VAL_IOTA = 1, VAL_ARRAY = 2 };
 // and then written out run by run: consecutive threads store consecutive
 // addresses of one digit's output run (a direct scatter would store 64
 // lanes into up to 64 different runs).  kout may be null (values only).
-// ORD: wave-local ranks from the lane-ordered returning LDS atomics
-// (lds_atomics_lane_ordered), else from peer masks
-template <typename K, int VM, bool ORD>
+template <typename K, int VM>
 __global__ void __launch_bounds__(TPB)
     radix_scatter(const K *__restrict__ kin, const int32_t *__restrict__ vin, int64_t n, int shift,
                   const uint32_t *__restrict__ offs, uint32_t ntiles, K *__restrict__ kout,
                   int32_t *__restrict__ vout, const int64_t *__restrict__ n_dev) {
-  __shared__ uint32_t run[NWAVE][RADIX + 1];  // (+ a spare word: ORD's lanes past n)
+  __shared__ uint32_t run[NWAVE][RADIX];
   if (n_dev) n = *n_dev;  // device-resident length (<= the n the grid was sized for)
   __shared__ uint32_t dstart[RADIX];  // tile-local start of each digit
   __shared__ uint32_t gofs[RADIX];    // global start of each digit's run of this tile
@@ -375,7 +335,7 @@ __global__ void __launch_bounds__(TPB)
   __shared__ int32_t sv[VM == VAL_NONE ? 1 : TILE];
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
-  for (int d = threadIdx.x; d < NWAVE * (RADIX + 1); d += TPB) (&run[0][0])[d] = 0;
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
   __syncthreads();
   const int64_t tbase = (int64_t)blockIdx.x * TILE;
   const int64_t wbase = tbase + (int64_t)w * (TILE / NWAVE);
@@ -394,31 +354,22 @@ __global__ void __launch_bounds__(TPB)
   // atomic; a wave's LDS operations execute in issue order, so the 16
   // atomics go out back to back and each returns the count of that digit
   // in the wave's earlier items (no round trip per k).
-  if (ORD) {
+  uint32_t ret[IPT];
+  uint64_t pm[IPT];
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int64_t i = wbase + k * 64 + lane;
-      const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
-      lp[k] = atomicAdd(&run[w][i < n ? d : RADIX], 1u);
-    }
-  } else {
-    uint32_t ret[IPT];
-    uint64_t pm[IPT];
+  for (int k = 0; k < IPT; ++k) {
+    const int64_t i = wbase + k * 64 + lane;
+    const bool ok = i < n;
+    const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
+    const uint64_t m = peers8(d, __ballot(ok));
+    pm[k] = ok ? m : 0ull;
+    ret[k] = (ok && rank_below(m) == 0) ? atomicAdd(&run[w][d], (uint32_t)__popcll(m)) : 0u;
+  }
 #pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int64_t i = wbase + k * 64 + lane;
-      const bool ok = i < n;
-      const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
-      const uint64_t m = peers8(d, __ballot(ok));
-      pm[k] = ok ? m : 0ull;
-      ret[k] = (ok && rank_below(m) == 0) ? atomicAdd(&run[w][d], (uint32_t)__popcll(m)) : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < IPT; ++k) {
-      const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
-      const uint32_t before = (uint32_t)__shfl((int)ret[k], leader, 64);
-      lp[k] = before + rank_below(pm[k]);
-    }
+  for (int k = 0; k < IPT; ++k) {
+    const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
+    const uint32_t before = (uint32_t)__shfl((int)ret[k], leader, 64);
+    lp[k] = before + rank_below(pm[k]);
   }
   __syncthreads();
   // tile-local digit starts, per-wave starts inside them, global run starts
@@ -516,29 +467,6 @@ struct HostBuf {
 
 static inline uint32_t ntiles_of(int64_t n) { return (uint32_t)((n + TILE - 1) / TILE); }
 
-// lds_order_probe on the current device, once per device per process
-// (~1k blocks, well under a millisecond); false (peers8 ranks) on any failure
-static inline bool lds_atomics_lane_ordered(int dev, hipStream_t st) {
-  static std::mutex mu;
-  static int state[64] = {};  // 0 unknown, 1 ordered, 2 not
-  std::lock_guard<std::mutex> lk(mu);
-  if (dev < 0 || dev >= 64) return false;
-  if (state[dev] == 0) {
-    unsigned long long *d = nullptr, h = 1;
-    bool ok = hipMalloc(&d, sizeof(h)) == hipSuccess;
-    ok = ok && hipMemsetAsync(d, 0, sizeof(h), st) == hipSuccess;
-    if (ok) {
-      hipLaunchKernelGGL(lds_order_probe, dim3(1024), dim3(256), 0, st, d);
-      ok = hipGetLastError() == hipSuccess &&
-           hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, st) == hipSuccess &&
-           hipStreamSynchronize(st) == hipSuccess;
-    }
-    if (d) (void)hipFree(d);
-    state[dev] = (ok && h == 0) ? 1 : 2;
-  }
-  return state[dev] == 1;
-}
-
 // Exclusive scan of len u32 in place, any length: one launch (scan_onepass).
 // `ws` holds [ticket counter, watchdog][status word per tile]; its host-side
 // epoch tags this call's status words.
@@ -572,19 +500,15 @@ static void radix_pass(Buf &hist_buf, Buf &tsum, hipStream_t st, const K *kin, c
   if (!prehist)
     hipLaunchKernelGGL(radix_hist<K>, dim3(nt), dim3(TPB), 0, st, kin, n, shift, hist, nt, n_dev);
   scan_u32(tsum, st, hist, (int64_t)nt * RADIX);
-  int dev = -1;
-  (void)hipGetDevice(&dev);
-  const bool ord = lds_atomics_lane_ordered(dev, st);
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nt), dim3(TPB), 0, st, kin, vin, n, shift, hist, nt, kout, vout,
-                       n_dev);
-  };
   if (vm == VAL_NONE)
-    go(ord ? radix_scatter<K, VAL_NONE, true> : radix_scatter<K, VAL_NONE, false>);
+    hipLaunchKernelGGL((radix_scatter<K, VAL_NONE>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout, n_dev);
   else if (vm == VAL_IOTA)
-    go(ord ? radix_scatter<K, VAL_IOTA, true> : radix_scatter<K, VAL_IOTA, false>);
+    hipLaunchKernelGGL((radix_scatter<K, VAL_IOTA>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout, n_dev);
   else
-    go(ord ? radix_scatter<K, VAL_ARRAY, true> : radix_scatter<K, VAL_ARRAY, false>);
+    hipLaunchKernelGGL((radix_scatter<K, VAL_ARRAY>), dim3(nt), dim3(TPB), 0, st, kin, vin, n,
+                       shift, hist, nt, kout, vout, n_dev);
   PBX_HIP(hipGetLastError());
 }
 

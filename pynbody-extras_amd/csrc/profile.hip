@@ -2362,15 +2362,13 @@ __global__ void __launch_bounds__(TPB)
 // STAGE: the tile is sorted by bin in LDS and written out run by run
 // (coalesced); else every element is stored at its CSR position directly
 // (a (bin, tile) run is one block's, so L2 merges its lines; no 12 KB of LDS).
-// ORD: the wave-local ranks straight from the returning LDS atomics (lane-
-// ordered, lds_atomics_lane_ordered); else peer masks (8 ballots each)
-template <bool STAGE, bool ORD>
+template <bool STAGE>
 __global__ void __launch_bounds__(TPB)
     csr_slots(const uint32_t *__restrict__ toff, const uint64_t *__restrict__ kw,
               const uint16_t *__restrict__ kpre, const uint32_t *__restrict__ wcnt,
               const uint8_t *__restrict__ bins, const uint32_t *__restrict__ offs,
               uint32_t ntiles, int32_t *__restrict__ perm, uint32_t nrows) {
-  __shared__ uint32_t run[NWAVE][RADIX + 1];  // (+ a spare word: ORD's dropped lanes)
+  __shared__ uint32_t run[NWAVE][RADIX];
   __shared__ uint32_t dstart[RADIX];
   __shared__ uint32_t gofs[RADIX];
   __shared__ uint32_t wsum[NWAVE];
@@ -2408,7 +2406,7 @@ __global__ void __launch_bounds__(TPB)
              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
     key[k] = bt[k * 64];  // unconditional: every slot exists
   }
-  for (int d = threadIdx.x; d < NWAVE * (RADIX + 1); d += TPB) (&run[0][0])[d] = 0;
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
   __syncthreads();
   uint32_t lp[16];
 #pragma unroll
@@ -2416,16 +2414,12 @@ __global__ void __launch_bounds__(TPB)
     const uint64_t wd = wds[k];
     const bool ok = (wd >> lane) & 1ull;
     const uint32_t dgt = key[k] & 255u;
-    if (ORD) {  // dropped lanes count on a spare word (every lane issues: no branch)
-      lp[k] = atomicAdd(&run[w][ok ? dgt : RADIX], 1u);
-    } else {
-      uint64_t m = peers8(dgt, wd);
-      m = ok ? m : 0ull;
-      const uint32_t ret =
-          (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
-      const int leader = m ? __builtin_ctzll(m) : (int)lane;
-      lp[k] = (uint32_t)__shfl((int)ret, leader, 64) + rank_below(m);
-    }
+    uint64_t m = peers8(dgt, wd);
+    m = ok ? m : 0ull;
+    const uint32_t ret =
+        (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
+    const int leader = m ? __builtin_ctzll(m) : (int)lane;
+    lp[k] = (uint32_t)__shfl((int)ret, leader, 64) + rank_below(m);
   }
   __syncthreads();
   {
@@ -4996,10 +4990,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
             const char *v = std::getenv("PBX_CSR_DIRECT");
             return !(v && v[0] == '1');
           }();
-          const bool ord = lds_atomics_lane_ordered(d.id, st);
-          auto cs = stage ? (ord ? csr_slots<true, true> : csr_slots<true, false>)
-                          : (ord ? csr_slots<false, true> : csr_slots<false, false>);
-          hipLaunchKernelGGL(cs, dim3(nt), dim3(TPB), 0, st,
+          hipLaunchKernelGGL(stage ? csr_slots<true> : csr_slots<false>, dim3(nt), dim3(TPB), 0, st,
                              (const uint32_t *)P.toff.p, (const uint64_t *)P.kw.p,
                              (const uint16_t *)P.kpre.p, (const uint32_t *)P.swc.p,
                              (const uint8_t *)bins8, (const uint32_t *)th, nt, perm, nr);
