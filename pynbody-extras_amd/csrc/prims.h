@@ -76,15 +76,20 @@ __device__ __forceinline__ uint32_t rank_below(uint64_t m) {
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// lanes (of `valid`) whose 8-bit digit equals this lane's
+// lanes (of `valid`) whose 8-bit digit equals this lane's: per bit, the
+// lane's bit as 0 / -1 (one v_bfe_i32), the ballot of it, and the two mask
+// halves ANDed with XNOR(ballot, bit) — 6 VALU per bit (the select form
+// `bit ? bal : ~bal` compiled to ~15)
 __device__ __forceinline__ uint64_t peers8(uint32_t d, uint64_t valid) {
-  uint64_t m = valid;
+  uint32_t lo = (uint32_t)valid, hi = (uint32_t)(valid >> 32);
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    uint64_t bal = __ballot((d >> b) & 1u);
-    m &= ((d >> b) & 1u) ? bal : ~bal;
+    const uint32_t sp = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);  // 0 or 0xffffffff
+    const uint64_t bal = __ballot(sp != 0u);
+    lo &= ~((uint32_t)bal ^ sp);
+    hi &= ~((uint32_t)(bal >> 32) ^ sp);
   }
-  return m;
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then

@@ -50,6 +50,7 @@ struct SelectParams {
   int64_t base;  // first particle of the tiles (the families' span; 0 without families)
   int mass_f32;  // masses are float (else double)
   int tiled;     // lazy + tiled: x of tile t at xo[t * TILE ..], no look-back
+  int sphere_origin;  // the Sphere is centred at (0, 0, 0) (and ndim == 3): its test IS r^2 < R^2
   double cx, cy, cz, r2max;
   int64_t fam_lo[MAX_FAM];
   int64_t fam_hi[MAX_FAM];
@@ -73,6 +74,16 @@ __device__ __forceinline__ bool in_family(int64_t i, const SelectParams &p) {
 template <typename T>
 __device__ __forceinline__ bool select_xyz(T px, T py, T pz, const SelectParams &p, double &x) {
 #pragma clang fp contract(off)
+  if constexpr (std::is_same<T, double>::value) {
+    // a Sphere at the origin: dx = x - 0.0 is x exactly (NaN and -0.0
+    // included), so ((dx*dx + dy*dy) + dz*dz) is r^2 itself — one sum of
+    // squares for both the test and r
+    if (p.sphere_origin) {
+      const double r2 = (px * px + py * py) + pz * pz;
+      x = __builtin_sqrt(r2);
+      return r2 < p.r2max;
+    }
+  }
   bool keep = true;
   if (p.use_sphere) {
     double dx = (double)px - p.cx, dy = (double)py - p.cy, dz = (double)pz - p.cz;
@@ -950,33 +961,39 @@ __global__ void __launch_bounds__(SH_BT)
   }
   unsigned long long kmin = ~0ull, kmax = 0ull;
   bool oob = false;
-  for (uint32_t tile0 = ta; tile0 < tb; ++tile0) {
-#ifdef PBX_DIAG_SEL_ILV  // timing diagnostic only: tiles interleaved over the blocks (wrong offsets)
-    uint32_t tile = blockIdx.x + (tile0 - ta) * gridDim.x;
-    tile = tile < nt ? tile : nt - 1;
-#else
-    const uint32_t tile = tile0;
-#endif
-    const int64_t wbase = p.base + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW);
-    double px[SI], py[SI], pz[SI], xv[SI];
-    uint32_t inbits = 0;
+  // a wave's slice of a tile in two halves of SH_HALF particles per lane,
+  // software-pipelined: the next half's positions are loaded while this
+  // half is selected (ping-pong registers; every load unconditional — past
+  // the range the last tile again — so the vmcnt waits stay exact).  (All
+  // blocks start together: without the overlap each wave's loads and math
+  // alternated in lockstep with its neighbours', 283 us at 64M.)
+  constexpr int SH_HALF = SI / 2;
+  struct Half {
+    double x[SH_HALF], y[SH_HALF], z[SH_HALF];
+    uint32_t in;
+  };
+  auto ld = [&](uint32_t tile, int h, Half &H) {
+    const int64_t wbase = p.base + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW) + h * SH_HALF * 64;
+    H.in = 0;
 #pragma unroll
-    for (int k = 0; k < SI; ++k) {
+    for (int k = 0; k < SH_HALF; ++k) {
       const int64_t i = wbase + k * 64 + lane;
       const bool in = (i < n) && (!FAM || in_family(i, p));
-      inbits |= (uint32_t)in << k;
+      H.in |= (uint32_t)in << k;
       const double *q = pos + 3 * (in ? i : 0);
-      px[k] = q[0];
-      py[k] = q[1];
-      pz[k] = q[2];
+      H.x[k] = q[0];
+      H.y[k] = q[1];
+      H.z[k] = q[2];
     }
-    double *xt = xo + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW);
-    const int64_t wj = (int64_t)tile * (TILE / 64) + w * SI;
-    uint32_t run = 0;
+  };
+  uint32_t run = 0;
+  auto sel = [&](uint32_t tile, int h, const Half &H) {
+    double *xt = xo + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW) + h * SH_HALF * 64;
+    const int64_t wj = (int64_t)tile * (TILE / 64) + w * SI + h * SH_HALF;
 #pragma unroll
-    for (int k = 0; k < SI; ++k) {
-      xv[k] = 0.0;
-      const bool keep = ((inbits >> k) & 1u) && select_xyz(px[k], py[k], pz[k], p, xv[k]);
+    for (int k = 0; k < SH_HALF; ++k) {
+      double xv = 0.0;
+      const bool keep = ((H.in >> k) & 1u) && select_xyz(H.x[k], H.y[k], H.z[k], p, xv);
       const uint64_t bal = __ballot(keep);
       if (lane == 0) {
         kw[wj + k] = bal;
@@ -984,8 +1001,8 @@ __global__ void __launch_bounds__(SH_BT)
       }
       run += (uint32_t)__popcll(bal);
       if (keep) {
-        xt[k * 64 + lane] = xv[k];
-        const uint64_t kk = dkey(xv[k]);
+        xt[k * 64 + lane] = xv;
+        const uint64_t kk = dkey(xv);
         kmin = kk < kmin ? kk : kmin;
         kmax = kk > kmax ? kk : kmax;
         if (hv && kk >= ka && kk <= kb) {
@@ -998,9 +1015,18 @@ __global__ void __launch_bounds__(SH_BT)
         }
       }
     }
+  };
+  Half A, B;
+  if (ta < tb) ld(ta, 0, A);
+  for (uint32_t tile = ta; tile < tb; ++tile) {
+    ld(tile, 1, B);
+    run = 0;
+    sel(tile, 0, A);
+    ld(tile + 1 < tb ? tile + 1 : tile, 0, A);
+    sel(tile, 1, B);
     if (lane == 0) {
       wcnt[(int64_t)tile * SH_NW + w] = run;
-      if (tile0 - ta < SH_MAXT) tcnt[tile0 - ta][w] = run;
+      if (tile - ta < SH_MAXT) tcnt[tile - ta][w] = run;
     }
   }
   // the block's key range: one atomic pair per block
@@ -3755,6 +3781,8 @@ static SelPrep select_prep(Profile &P, hipStream_t st, const void *pos, const vo
     sp.cy = sphere[1];
     sp.cz = sphere[2];
     sp.r2max = sphere[3];
+    // (+0.0 or -0.0 centre: x - c == x for every x)
+    sp.sphere_origin = ndim == 3 && sphere[0] == 0.0 && sphere[1] == 0.0 && sphere[2] == 0.0;
   }
   int64_t lo = 0, hi = n;  // the span holding every family member
   if (nfam > 0) {

@@ -968,7 +968,7 @@ __global__ void __launch_bounds__(WALK_TPB)
     walk_kernel(WalkParams wp) {
   constexpr int RS = rec_stride<P>();
   constexpr int NCH = (P == 2 || P == 3) ? RS / 8 : 1;  // chunks loaded eagerly
-  const unsigned long long t_start = wp.trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  const unsigned long long t_start = wp.trace ? (unsigned long long)wall_clock64() : 0ull;  // (100 MHz)
   const unsigned lb = wp.xcd_chunk ? xcd_chunk_swizzle(blockIdx.x, wp.xcd_chunk) : blockIdx.x;
   const int64_t t = (int64_t)lb * blockDim.x + threadIdx.x;
   const bool lane0 = (threadIdx.x & 63) == 0;
@@ -1139,7 +1139,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   if (wp.trace && lane0) {
     const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     wp.trace[3 * wv] = t_start;
-    wp.trace[3 * wv + 1] = __builtin_amdgcn_s_memrealtime();
+    wp.trace[3 * wv + 1] = (unsigned long long)wall_clock64();
     wp.trace[3 * wv + 2] = (unsigned long long)steps;
   }
   if (!valid) return;

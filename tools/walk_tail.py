@@ -25,7 +25,7 @@ d_pos, d_mass = nat.DeviceArray.from_host(pos), nat.DeviceArray.from_host(mass)
 d_pot, d_acc = nat.DeviceArray(8 * n), nat.DeviceArray(24 * n)
 tree = Octree._from_device(d_pos.ptr, n, d_mass.ptr, 8, 3)
 want = nat.WANT_POT | nat.WANT_ACC
-for label, first, count in [("full", 0, n), ("full", 0, n)]:
+for label, first, count in [("full", 0, n), ("full", 0, n), ("range", 0, n // 8), ("range", 3 * n // 8, n // 8)]:
     if os.path.exists(trace):
         os.remove(trace)
     tree._compute_range_device(0.5, want, first, count, 1, d_pot.ptr, d_acc.ptr, None)
