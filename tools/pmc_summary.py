@@ -74,7 +74,7 @@ def main():
         # one profile step of the PMC run = the dispatches of its selection
         # kernel (one per step); shared radix/scan kernels of the tree build
         # are excluded from the per-step sum
-        sel = [r for r in prof if "select_onepass" in r["kernel"]]
+        sel = [r for r in prof if "select_onepass" in r["kernel"] or "select_tiles" in r["kernel"]]
         steps = sel[0]["dispatches"] if sel else None
         own = [r for r in prof if "pbx::prof::" in r["kernel"] or "unsigned int, 1>" in r["kernel"]
                or "scan_onepass" in r["kernel"]]
