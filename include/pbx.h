@@ -218,6 +218,12 @@ int pbx_octree_leaf_particles(pbx_octree *tree, int64_t first, int64_t count, do
 int pbx_octree_radial_moments(pbx_octree *tree, int64_t first, int64_t count, const double *d_f,
                               const double *h_edges, int64_t nbins, int64_t *h_counts,
                               double *h_moments);
+/* The same into DEVICE memory, no sync: d_out = nbins int64 counts followed
+ * by nbins x 7 doubles (row-major), e.g. for an in-place all-reduce of the
+ * ranks' partial profiles before one read-back. */
+int pbx_octree_radial_moments_device(pbx_octree *tree, int64_t first, int64_t count,
+                                     const double *d_f, const double *h_edges, int64_t nbins,
+                                     void *d_out);
 /* Multi-GPU load balance without an extra walk (the reference has one
  * process; its rayon pool splits targets dynamically, tree.rs:1443-1556):
  * cost_to_orig scatters per-target costs held in leaf order (n int32, e.g.
@@ -228,6 +234,11 @@ int pbx_octree_radial_moments(pbx_octree *tree, int64_t first, int64_t count, co
  * pynbodyext.parallel.balanced_ranges.  Device pointers; balance syncs. */
 int pbx_octree_cost_to_orig(pbx_octree *tree, const int32_t *d_cost_leaf, int32_t *d_cost_orig);
 int pbx_octree_balance(pbx_octree *tree, const int32_t *d_cost_orig, int world, int64_t *cuts);
+/* What d_cost of compute_range holds: kind 0 (default) the target's accepted
+ * nodes + leaf pairs; kind 1 its wave's work (the wave's node steps + its
+ * 4-record leaf rounds, the same for the 64 targets of one wave), which is
+ * what a walk's time follows — ShardedTree balances on it. */
+int pbx_octree_set_cost_kind(pbx_octree *tree, int kind);
 /* out[13] = {n, nodes, levels, has_mass_payload, has_hmax,
  *            accepted node interactions and leaf pairs of the last walk,
  *            path words, wave steps and active-lane steps of the last walk

@@ -851,7 +851,8 @@ struct WalkParams {
   int64_t m;                // number of targets
   int64_t first;            // self mode: targets are leaf-order particles first .. first+m-1
   int compact;              // self mode: 1 -> outputs at t (leaf order), 0 -> original index
-  int32_t *cost;            // optional per-target interaction count (nodes + leaf pairs)
+  int32_t *cost;            // optional per-target cost (cost_kind)
+  int cost_kind;            // 0: interactions (nodes + leaf pairs); 1: the wave's work
   double theta2;
   double sep;               // multipole_min_separation_factor (kernel.rs:20-37)
   int kernel;
@@ -1000,6 +1001,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
   uint32_t steps = 0;          // the wave moves strictly forward in DFS order
+  uint32_t leaf_rounds = 0;    // 4-record leaf rounds (cost_kind 1)
   // One path through the body, no `continue`: every exit of a divergent
   // region merges into the same accumulator registers, and p takes one
   // select at the bottom (a body with three early exits to the latch made
@@ -1117,6 +1119,7 @@ __global__ void __launch_bounds__(WALK_TPB)
     if (live && first < 0) {  // leaf: direct sum in ascending index order
       const int32_t s = chunk_i(c[0], 14), e = s + chunk_i(c[0], 15);
       ++leaf_steps;
+      leaf_rounds += (uint32_t)(e - s + 3) >> 2;
       leaf_active += na;
       n_pp += (unsigned long long)na * (unsigned long long)(e - s);
       if (act) {
@@ -1144,7 +1147,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   }
   if (!valid) return;
   const int64_t o = (self_mode && !wp.compact) ? (int64_t)wp.perm[wp.first + t] : t;
-  if (wp.cost) wp.cost[t] = cost;
+  if (wp.cost) wp.cost[t] = wp.cost_kind ? (int32_t)(steps + leaf_rounds) : cost;
   if (WANT & PBX_WANT_POT) wp.pot[o] = ph;
   if (WANT & PBX_WANT_ACC) {
     wp.acc[3 * o] = ax;
@@ -1574,6 +1577,7 @@ struct Octree {
   Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
   Buf bal;                   // cost-balanced ranges: chunk sums + cuts
+  int cost_kind = 0;                   // d_cost contents (WalkParams::cost_kind)
   Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
   Buf rec0;                  // {x, y, z, m} in original order (path_keys)
   bool rec0_valid = false;   // rec0 holds the current masses
@@ -2110,6 +2114,7 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   }
   wp.max_steps = T.nn + 16;
   wp.fault = (unsigned int *)(ctr + 2);
+  wp.cost_kind = T.cost_kind;
   // softened leaves need softenings; the guard needs h_max; at query points
   // there is no target softening (tree.rs:1516,1547)
   const bool soft = T.has_hmax || T.soft_set;
@@ -2505,47 +2510,70 @@ int pbx_octree_leaf_particles(pbx_octree *t, int64_t first, int64_t count, doubl
   });
 }
 
+// select + assign + moments of a leaf-order range, fused: the device result
+// [nbins int64 counts | nbins x 7 doubles] in the device's staging slot
+static const double *radial_moments_run(Octree &T, int64_t first, int64_t count, const double *d_f,
+                                        const double *h_edges, int64_t nbins, Device &dev) {
+  if (first < 0 || count < 0 || first + count > T.n) fail(PBX_ERR_VALUE, "range outside the tree");
+  if (!T.has_bh) fail(PBX_ERR_VALUE, "mass payload not built; call build_mass() first");
+  if (nbins < 1 || nbins > RM_MAXB) fail(PBX_ERR_VALUE, "nbins must be in [1, %d]", RM_MAXB);
+  for (int64_t k = 0; k < nbins; ++k)
+    if (!(h_edges[k] <= h_edges[k + 1]))
+      fail(PBX_ERR_VALUE, "bin edges must be increasing");
+  hipStream_t st = dev.stream;
+  const int nb = (int)nbins;
+  const int rows = (int)std::max<int64_t>(1, std::min<int64_t>(512, (count + RM_CHUNK - 1) / RM_CHUNK));
+  const size_t eb = sizeof(double) * (size_t)(nb + 1);
+  const size_t sb = sizeof(double) * 7 * (size_t)nb * rows, cb = sizeof(uint32_t) * (size_t)nb * rows;
+  const size_t ob = sizeof(double) * 8 * (size_t)nb;
+  char *w = (char *)dev.slot(kSlotProf7).ensure(eb + sb + cb + ob + 64);
+  double *de = (double *)w;
+  double *slab = (double *)(w + ((eb + 15) & ~(size_t)15));
+  uint32_t *cslab = (uint32_t *)((char *)slab + sb);
+  double *out = (double *)(((uintptr_t)((char *)cslab + cb) + 15) & ~(uintptr_t)15);
+  PBX_HIP(hipMemcpyAsync(de, h_edges, eb, hipMemcpyHostToDevice, st));
+  const size_t lds_acc = sizeof(double) * 7 * nb + sizeof(uint32_t) * nb;
+  const int e_lds = eb + lds_acc <= 65536 ? 1 : 0;
+  const size_t lds = (e_lds ? eb : 0) + lds_acc;  // <= 61,440 B at RM_MAXB
+  hipLaunchKernelGGL(radial_moments_kernel, dim3(rows), dim3(TPB), lds, st, T.rec.as<double4>(),
+                     d_f, first, count, (const double *)de, nb, slab, cslab, e_lds);
+  hipLaunchKernelGGL(radial_moments_reduce, dim3((unsigned)((8 * (int64_t)nb + RR_C - 1) / RR_C)),
+                     dim3(RR_C * RR_G), 0, st,
+                     (const double *)slab, (const uint32_t *)cslab, rows, nb, out);
+  PBX_HIP(hipGetLastError());
+  return out;
+}
+
 int pbx_octree_radial_moments(pbx_octree *t, int64_t first, int64_t count, const double *d_f,
                               const double *h_edges, int64_t nbins, int64_t *h_counts,
                               double *h_moments) {
   return guard([&] {
     Octree &T = as_tree(t);
-    if (first < 0 || count < 0 || first + count > T.n) fail(PBX_ERR_VALUE, "range outside the tree");
-    if (!T.has_bh) fail(PBX_ERR_VALUE, "mass payload not built; call build_mass() first");
-    if (nbins < 1 || nbins > RM_MAXB) fail(PBX_ERR_VALUE, "nbins must be in [1, %d]", RM_MAXB);
-    for (int64_t k = 0; k < nbins; ++k)
-      if (!(h_edges[k] <= h_edges[k + 1]))
-        fail(PBX_ERR_VALUE, "bin edges must be increasing");
     Device &dev = current_device();
     std::lock_guard<std::mutex> lk(dev.mu);
-    hipStream_t st = dev.stream;
     ScopedTimer tm("octree.radial_moments");
-    const int nb = (int)nbins;
-    const int rows = (int)std::max<int64_t>(1, std::min<int64_t>(512, (count + RM_CHUNK - 1) / RM_CHUNK));
-    const size_t eb = sizeof(double) * (size_t)(nb + 1);
-    const size_t sb = sizeof(double) * 7 * (size_t)nb * rows, cb = sizeof(uint32_t) * (size_t)nb * rows;
-    const size_t ob = sizeof(double) * 8 * (size_t)nb;
-    char *w = (char *)dev.slot(kSlotProf7).ensure(eb + sb + cb + ob + 64);
-    double *de = (double *)w;
-    double *slab = (double *)(w + ((eb + 15) & ~(size_t)15));
-    uint32_t *cslab = (uint32_t *)((char *)slab + sb);
-    double *out = (double *)(((uintptr_t)((char *)cslab + cb) + 15) & ~(uintptr_t)15);
-    prim::HostBuf &hb = T.rm_pin;
-    double *hp = (double *)hb.get(ob);
-    PBX_HIP(hipMemcpyAsync(de, h_edges, eb, hipMemcpyHostToDevice, st));
-    const size_t lds_acc = sizeof(double) * 7 * nb + sizeof(uint32_t) * nb;
-    const int e_lds = eb + lds_acc <= 65536 ? 1 : 0;
-    const size_t lds = (e_lds ? eb : 0) + lds_acc;  // <= 61,440 B at RM_MAXB
-    hipLaunchKernelGGL(radial_moments_kernel, dim3(rows), dim3(TPB), lds, st, T.rec.as<double4>(),
-                       d_f, first, count, (const double *)de, nb, slab, cslab, e_lds);
-    hipLaunchKernelGGL(radial_moments_reduce, dim3((unsigned)((8 * (int64_t)nb + RR_C - 1) / RR_C)),
-                       dim3(RR_C * RR_G), 0, st,
-                       (const double *)slab, (const uint32_t *)cslab, rows, nb, out);
-    PBX_HIP(hipGetLastError());
-    PBX_HIP(hipMemcpyAsync(hp, out, ob, hipMemcpyDeviceToHost, st));
-    PBX_HIP(hipStreamSynchronize(st));
-    std::memcpy(h_counts, hp, sizeof(int64_t) * nb);
-    std::memcpy(h_moments, hp + nb, sizeof(double) * 7 * nb);
+    const double *out = radial_moments_run(T, first, count, d_f, h_edges, nbins, dev);
+    const size_t ob = sizeof(double) * 8 * (size_t)nbins;
+    double *hp = (double *)T.rm_pin.get(ob);
+    PBX_HIP(hipMemcpyAsync(hp, out, ob, hipMemcpyDeviceToHost, dev.stream));
+    PBX_HIP(hipStreamSynchronize(dev.stream));
+    std::memcpy(h_counts, hp, sizeof(int64_t) * nbins);
+    std::memcpy(h_moments, hp + nbins, sizeof(double) * 7 * nbins);
+  });
+}
+
+int pbx_octree_radial_moments_device(pbx_octree *t, int64_t first, int64_t count,
+                                     const double *d_f, const double *h_edges, int64_t nbins,
+                                     void *d_out) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (!d_out) fail(PBX_ERR_VALUE, "null output");
+    Device &dev = current_device();
+    std::lock_guard<std::mutex> lk(dev.mu);
+    ScopedTimer tm("octree.radial_moments");
+    const double *out = radial_moments_run(T, first, count, d_f, h_edges, nbins, dev);
+    PBX_HIP(hipMemcpyAsync(d_out, out, sizeof(double) * 8 * (size_t)nbins,
+                           hipMemcpyDeviceToDevice, dev.stream));
   });
 }
 
@@ -2559,6 +2587,14 @@ int pbx_octree_cost_to_orig(pbx_octree *t, const int32_t *d_cost_leaf, int32_t *
       hipLaunchKernelGGL(cost_to_orig, dim3(nblk(T.n)), dim3(TPB), 0, dev.stream, d_cost_leaf,
                          T.perm.as<int32_t>(), T.n, d_cost_orig);
     PBX_HIP(hipGetLastError());
+  });
+}
+
+int pbx_octree_set_cost_kind(pbx_octree *t, int kind) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (kind != 0 && kind != 1) fail(PBX_ERR_VALUE, "cost kind must be 0 or 1");
+    T.cost_kind = kind;
   });
 }
 

@@ -306,9 +306,20 @@ class Octree:
                  nat.dptr(edges), nb, counts.ctypes.data_as(nat._i64p), nat.dptr(mom))
         return counts, mom
 
+    def _radial_moments_into(self, first: int, count: int, d_f, edges, d_out) -> None:
+        """_radial_moments_device into device memory (no sync): d_out holds
+        nbins int64 counts, then nbins x 7 doubles."""
+        edges = np.ascontiguousarray(edges, dtype=np.float64)
+        nat.call("pbx_octree_radial_moments_device", self._h, int(first), int(count), d_f,
+                 nat.dptr(edges), len(edges) - 1, d_out)
+
     def _cost_to_orig_device(self, d_cost_leaf, d_cost_orig) -> None:
         """Per-target costs in this build's leaf order -> original order."""
         nat.call("pbx_octree_cost_to_orig", self._h, d_cost_leaf, d_cost_orig)
+
+    def _set_cost_kind(self, kind: int) -> None:
+        """compute_range's d_cost: 0 interactions per target, 1 the wave's work."""
+        nat.call("pbx_octree_set_cost_kind", self._h, int(kind))
 
     def _balance_device(self, d_cost_orig, world: int) -> list[tuple[int, int]]:
         """[(first, count)] per rank: contiguous leaf-order ranges of equal

@@ -98,8 +98,11 @@ _SIGNATURES: dict[str, tuple] = {
                                           c_void_p]),
     "pbx_octree_radial_moments": (c_int, [c_void_p, c_int64, c_int64, c_void_p, _dp, c_int64,
                                           _i64p, _dp]),
+    "pbx_octree_radial_moments_device": (c_int, [c_void_p, c_int64, c_int64, c_void_p, _dp,
+                                                 c_int64, c_void_p]),
     "pbx_octree_cost_to_orig": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pbx_octree_balance": (c_int, [c_void_p, c_void_p, c_int, _i64p]),
+    "pbx_octree_set_cost_kind": (c_int, [c_void_p, c_int]),
     "pbx_octree_info": (c_int, [c_void_p, _i64p]),
     "pbx_octree_export": (c_int, [c_void_p, _dp, _dp, _dp, _i64p, _i64p, _i64p, _dp]),
     "pbx_profile_create": (c_int, [POINTER(c_void_p)]),

@@ -274,9 +274,10 @@ class ShardedTree:
       changed snapshot / leaf order still maps); before any walk, equal
       target counts.  Device-side (two small kernels, one (world+1)-int
       read-back) — no extra walk;
-    * ``walk()``    — this rank's targets, writing their costs; the costs are
-      all-gathered (RCCL, 4 bytes per particle) and moved to original order
-      for the next step's balance;
+    * ``walk()``    — this rank's targets, writing their costs (the work of
+      each target's wave: node steps + 4-record leaf rounds, what the walk's
+      time follows); the costs are all-gathered (RCCL, 4 bytes per particle)
+      and moved to original order for the next step;
     * ``profile()`` — per-bin partial moments of this rank's targets, one
       RCCL all-reduce of nbins x 7 doubles.
 
@@ -301,6 +302,7 @@ class ShardedTree:
         self.d_cost_orig = nat.DeviceArray(4 * max(cap, 1))  # original order, carried
         self.have_costs = False
         self.info = None
+        self.d_prof = None  # [counts | moments] of the profile all-reduce
 
     def build(self):
         from ._engine import Octree
@@ -308,6 +310,7 @@ class ShardedTree:
         if self.tree is None:
             self.tree = Octree._from_device(self.d_pos.ptr, self.n, self.d_mass.ptr, self.leaf,
                                             self.order)
+            self.tree._set_cost_kind(1)
         else:  # next step / snapshot: same handle, HBM buffers reused
             self.tree._rebuild_device(self.d_pos.ptr, self.n, self.d_mass.ptr)
 
@@ -353,13 +356,24 @@ class ShardedTree:
         (pbx_octree_radial_moments); the summed bin counts are left in
         ``dev_bins.counts`` when a DeviceBins is given."""
         first, count = self.ranges[self.rank] if self.ranges else (0, self.n)
-        counts, mom = self.tree._radial_moments_device(first, count, self.d_pot.ptr, edges)
-        if self.comm is not None and self.world > 1:
-            # one all-reduce of [moments | counts] through the communicator's
-            # persistent staging (no allocation per step)
-            flat = self.comm.allreduce_host(np.concatenate([mom.ravel(), counts.astype(np.float64)]))
-            mom = flat[:mom.size].reshape(mom.shape)
-            counts = np.rint(flat[mom.size:]).astype(np.int64)
+        if self.comm is not None:
+            # the partial profile stays on the device: [counts | moments]
+            # all-reduced in place (RCCL), one read-back
+            nb = len(edges) - 1
+            if self.d_prof is None or self.d_prof.nbytes < 64 * nb:
+                if self.d_prof is not None:
+                    self.d_prof.free()
+                self.d_prof = nat.DeviceArray(64 * nb)
+            self.tree._radial_moments_into(first, count, self.d_pot.ptr, edges, self.d_prof.ptr)
+            self.comm.allreduce(self.d_prof.ptr, self.d_prof.ptr, nb, DT_I64)
+            self.comm.allreduce(self.d_prof.offset(8 * nb), self.d_prof.offset(8 * nb), 7 * nb,
+                                DT_F64)
+            flat = np.empty(8 * nb)
+            self.d_prof.download(flat)
+            counts = flat[:nb].view(np.int64).copy()
+            mom = flat[nb:].reshape(nb, 7)
+        else:
+            counts, mom = self.tree._radial_moments_device(first, count, self.d_pot.ptr, edges)
         if dev_bins is not None:
             dev_bins.counts = counts
             dev_bins.nbins = len(counts)
@@ -375,8 +389,10 @@ class ShardedTree:
         if self.tree is not None:
             self.tree.close()
             self.tree = None
-        for a in (self.d_pot, self.d_acc, self.d_cost, self.d_cost_orig):
-            a.free()
+        for a in (self.d_pot, self.d_acc, self.d_cost, self.d_cost_orig, self.d_prof):
+            if a is not None:
+                a.free()
+        self.d_prof = None
 
 
 def distributed_equaln(dev, comm, nbins: int, bin_min=None, bin_max=None) -> np.ndarray:

@@ -101,6 +101,7 @@ def test_config5_tree_4m_fast_with_potential_profile(gpu):
             mom = solver.step(prof, edges)  # build, balance, walk, profile
             counts = prof.counts.copy()
             d_cost = nat.DeviceArray(4 * n)
+            solver.tree._set_cost_kind(0)  # interaction counts (ShardedTree: wave work)
             solver.tree._compute_range_device(theta, nat.WANT_POT | nat.WANT_ACC, 0, n, 1,
                                               solver.d_pot.ptr, solver.d_acc.ptr, d_cost.ptr)
         info = solver.tree.info()
@@ -191,8 +192,44 @@ class _EmulatedComm:
     def allreduce_sum_f64(self, *a):
         pass
 
+    def allreduce(self, *a):  # in place on the device: this rank's partials
+        pass
+
     def allreduce_host(self, a, op=0):  # this rank's partials (the test sums them)
         return np.array(a, copy=True)
+
+
+def test_sharded_tree_rccl_world1_matches_single(gpu):
+    """ShardedTree through a 1-rank RCCL communicator: the profile's partial
+    [counts | moments] all-reduced in place on the device, then read back
+    once, equals the communicator-free solve, step after step."""
+    from pynbodyext.parallel import Communicator, ShardedTree
+    from pynbodyext.profiles._device import DeviceBins
+
+    n, theta = 200_000, 0.5
+    pos, mass = plummer(n, seed=23)
+    d_pos, d_mass = nat.DeviceArray.from_host(pos), nat.DeviceArray.from_host(mass)
+    edges = np.logspace(np.log10(0.01), np.log10(50.0), 129)
+    comm = Communicator(1, 0, Communicator.unique_id())
+    single = ShardedTree(None, n, d_pos, d_mass, 8, 3, theta)
+    ranked = ShardedTree(comm, n, d_pos, d_mass, 8, 3, theta)
+    b0, b1 = DeviceBins(), DeviceBins()
+    try:
+        mom0 = single.step(b0, edges)
+        pot0 = single.d_pot.download(np.empty(n))
+        for _ in range(2):
+            mom1 = ranked.step(b1, edges)
+            assert np.array_equal(b1.counts, b0.counts)
+            assert np.array_equal(ranked.d_pot.download(np.empty(n)), pot0)
+            np.testing.assert_allclose(mom1, mom0, rtol=1e-12, atol=1e-300)
+    finally:
+        for t in (single, ranked):
+            t.close()
+        for b in (b0, b1):
+            b.close()
+        comm.destroy()
+        d_pos.free()
+        d_mass.free()
 
 
 def test_sharded_tree_emulated_ranks_match_single(gpu):

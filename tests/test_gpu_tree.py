@@ -377,6 +377,42 @@ def test_range_walk_shards_equal_full(gpu):
         dev._compute_range_device(0.5, nat.WANT_POT, n - 5, 10, 1, d_pot.ptr, None, None)
 
 
+def test_range_walk_wave_costs(gpu):
+    """ShardedTree's cost kind 1 writes every target its wave's work (node
+    steps + 4-record leaf rounds, equal over the 64 targets of a wave,
+    summing to at least the wave-step counters); outputs do not change."""
+    from pynbodyext import _native as nat
+
+    n = 64 * 4688
+    pos, mass = plummer(n, seed=101)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    want = nat.WANT_POT | nat.WANT_ACC
+    d_pot, d_acc = nat.DeviceArray(8 * n), nat.DeviceArray(24 * n)
+    d_cost = nat.DeviceArray(4 * n)
+
+    def walk(first, count, cost=None):
+        dev._compute_range_device(0.5, want, first, count, 1, d_pot.ptr, d_acc.ptr, cost)
+        p, a = np.empty(count), np.empty((count, 3))
+        d_pot.download(p)
+        d_acc.download(a)
+        return p, a
+
+    p0, a0 = walk(0, n)
+    with pytest.raises(ValueError, match="cost kind"):
+        dev._set_cost_kind(2)
+    dev._set_cost_kind(1)
+    p1, a1 = walk(0, n, d_cost.ptr)
+    assert np.array_equal(p1, p0) and np.array_equal(a1, a0)
+    info = dev.info()
+    cost = d_cost.download(np.empty(n, dtype=np.int32)).reshape(-1, 64)
+    assert (cost == cost[:, :1]).all()  # one value per wave
+    wave = cost[:, 0].astype(np.int64)
+    assert wave.min() > 0
+    assert info["wave_steps"] + info["leaf_wave_steps"] <= wave.sum()
+    for a in (d_pot, d_acc, d_cost):
+        a.free()
+
+
 @pytest.mark.parametrize("nbins", [963, 964, 1024])
 def test_radial_moments_max_bins(gpu, nbins):
     """pbx_octree_radial_moments at the largest bin counts: up to 963 bins the

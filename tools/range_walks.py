@@ -3,8 +3,10 @@
 costs, split into `world` cost-balanced leaf-order ranges exactly as
 ShardedTree does (pbx_octree_balance over the previous walk's costs), and
 each range is walked alone (compact outputs) and timed with HIP events on
-the library stream.  An 8-rank step is bounded by build + max(range walk)
-+ profile (+ the cost all-gather / all-reduce, not timed here).
+the library stream.  Cases: ranges balanced on interaction counts (cost
+kind 0), on wave work (kind 1, ShardedTree's), and equal target counts.
+An 8-rank step is bounded by build + max(range walk) + profile (+ the cost
+all-gather / all-reduce, not timed here).
 usage: python tools/range_walks.py [n] [world] [reps]"""
 import json
 import sys
@@ -45,25 +47,31 @@ def timed(fn):
 
 tree = Octree._from_device(d_pos.ptr, n, d_mass.ptr, 8, 3)
 build_ms = timed(lambda: tree._rebuild_device(d_pos.ptr, n, d_mass.ptr))
-full_ms = timed(lambda: tree._compute_range_device(0.5, want, 0, n, 1, d_pot.ptr, d_acc.ptr,
-                                                   d_cost.ptr))
-tree._cost_to_orig_device(d_cost.ptr, d_cost_orig.ptr)
-cost = np.empty(n, dtype=np.int32)
-d_cost.download(cost)
-out = {"n": n, "world": world, "build_ms": build_ms, "full_walk_ms": full_ms}
-bal = tree._balance_device(d_cost_orig.ptr, world)
-for label, ranges in [("cost_balanced", bal),
-                      ("equal_count", [((n * r) // world, (n * (r + 1)) // world - (n * r) // world)
-                                       for r in range(world)])]:
-    walks, csum = [], []
+out = {"n": n, "world": world, "build_ms": build_ms}
+costs = {}
+for kind, label in ((0, "interactions"), (1, "wave_work")):
+    tree._set_cost_kind(kind)
+    ms = timed(lambda: tree._compute_range_device(0.5, want, 0, n, 1, d_pot.ptr, d_acc.ptr,
+                                                  d_cost.ptr))
+    out["full_walk_ms" if kind == 0 else "full_walk_ms_k1"] = ms
+    c = nat.DeviceArray(4 * n)
+    tree._cost_to_orig_device(d_cost.ptr, c.ptr)
+    costs[label] = c
+full_ms = out["full_walk_ms"]
+cases = [("cost_balanced", "interactions"), ("wave_balanced", "wave_work"),
+         ("equal_count", None)]
+for label, ckey in cases:
+    if ckey is None:
+        ranges = [((n * r) // world, (n * (r + 1)) // world - (n * r) // world) for r in range(world)]
+    else:
+        ranges = tree._balance_device(costs[ckey].ptr, world)
+    walks = []
     for first, count in ranges:
         walks.append(timed(lambda f=first, c=count: tree._compute_range_device(
             0.5, want, f, c, 1, d_pot.ptr, d_acc.ptr, None)))
-        csum.append(int(cost[first:first + count].astype(np.int64).sum()))
     mx, mean = max(walks), float(np.mean(walks))
     out[label] = {"ranges": ranges, "walk_ms": walks, "max_ms": mx, "mean_ms": mean,
                   "max_over_mean": mx / mean, "sum_ms": float(np.sum(walks)),
-                  "cost_sums": csum,
                   "bound_speedup_vs_full": (build_ms + full_ms) / (build_ms + mx)}
 print(json.dumps(out), flush=True)
 tree.close()
