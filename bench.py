@@ -635,7 +635,10 @@ def main():
         # every rank: with N > 1 (or PBX_BENCH_FORCE_DIST=1) the sharded
         # profile with global edges (distributed radix select over RCCL)
         sizes = [int(s) for s in args.profile_sizes.split(",") if s]
-        sweep = bench_profile(sizes, steps=max(3, args.steps), warmup=1,
+        # a 1M call is ~0.1 ms: the median of K calls at the bench's default
+        # K = 5 moves by +-10 % from run to run, so the profile leg times
+        # max(K, 200) calls per size (0.15 s at 64M)
+        sweep = bench_profile(sizes, steps=max(200, args.steps), warmup=max(5, args.warmup),
                               cpu=not args.no_cpu_baseline and rank == 0 and world == 1,
                               dist=dist if dist.comm is not None else None)
     dist.close()

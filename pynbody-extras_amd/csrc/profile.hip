@@ -2607,13 +2607,19 @@ struct MonoArgs {
 // End of a block's part of the call: the block whose completion brings the
 // (monotonic) counter to its target writes the pack's tag.  A call in which
 // a block gave up at a barrier never reaches the target: no tag, and the
-// host discards the call.
+// host discards the call.  The host may read the pack as soon as it sees
+// the tag (radial_mono_run spins on it): every block's pack stores are
+// released at system scope before its count, the tag after the last count.
 __device__ void mono_done(const MonoArgs &a, int tagpos) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's pack stores have landed
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint64_t old = __hip_atomic_fetch_add(a.bar + BAR_LINE * 10, 1ull, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == a.done_target) a.pack[tagpos] = __builtin_bit_cast(double, a.gen0);
+    __threadfence_system();
+    const uint64_t old = __hip_atomic_fetch_add(a.bar + BAR_LINE * 10, 1ull, __ATOMIC_ACQ_REL,
+                                                __HIP_MEMORY_SCOPE_SYSTEM);
+    if (old + 1 == a.done_target)
+      __hip_atomic_store((uint64_t *)(a.pack + tagpos), a.gen0, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -4222,7 +4228,27 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   P.bar_gen += 5;
   P.bar_done += nt;
   ++P.n_mono;
-  PBX_HIP(hipStreamSynchronize(st));
+  // completion: the tag in mapped host memory, polled (a stream sync wakes
+  // the host several microseconds after the kernel ends); the stream is
+  // queried now and then, so a discarded call (no tag) ends the wait too
+  static const bool spin = [] {
+    const char *v = std::getenv("PBX_MONO_SPIN");
+    return !(v && v[0] == '0');
+  }();
+  if (spin) {
+    volatile uint64_t *tag = (volatile uint64_t *)(hp + ntot);
+    for (uint32_t k = 1; *tag == ~0ull; ++k) {
+      if ((k & 1023u) == 0) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) PBX_HIP(q);
+      }
+      __builtin_ia32_pause();
+    }
+    if (*tag != a.gen0) PBX_HIP(hipStreamSynchronize(st));
+  } else {
+    PBX_HIP(hipStreamSynchronize(st));
+  }
   if (__builtin_bit_cast(uint64_t, ((volatile double *)hp)[ntot]) != a.gen0) {
     P.bar_n = 0;  // discarded: zero the barrier words before the next call
     ++P.n_mono_discard;

@@ -202,6 +202,39 @@ def call(name: str, *args) -> None:
     check(getattr(load(), name)(*args))
 
 
+_raw_lib = None
+_CArg = type(ctypes.byref(ctypes.c_int()))
+
+
+class Prepared:
+    """A native call whose arguments do not change between calls, converted
+    to ctypes objects once: a repeated 26-argument call otherwise spends
+    ~4 us per call in ctypes' per-argument conversions (measured on the
+    1M-particle profile step, whose whole host share is ~30 us)."""
+
+    __slots__ = ("fn", "args")
+
+    def __init__(self, name: str, *args):
+        global _raw_lib
+        lib = load()
+        if _raw_lib is None:  # a second handle: its functions carry no argtypes
+            _raw_lib = ctypes.CDLL(lib._name, mode=ctypes.RTLD_GLOBAL)
+        self.fn = getattr(_raw_lib, name)
+        self.fn.restype = c_int
+        conv = []
+        for t, v in zip(_SIGNATURES[name][1], args, strict=True):
+            if isinstance(v, (ctypes._SimpleCData, ctypes._Pointer, ctypes.Array, _CArg)):
+                conv.append(v)
+            elif v is None:
+                conv.append(t())
+            else:
+                conv.append(t(v))
+        self.args = tuple(conv)
+
+    def __call__(self) -> None:
+        check(self.fn(*self.args))
+
+
 def dptr(a: np.ndarray | None):
     """double* of a C-contiguous float64 array (or NULL)."""
     if a is None:

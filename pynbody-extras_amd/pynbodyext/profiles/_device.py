@@ -164,13 +164,15 @@ class DeviceBins:
         # returned arrays are fresh copies every call.
         key = None
         if on_device:
-            key = (pos, mass, None if sphere is None else (tuple(sphere[0]), float(sphere[1])),
+            key = (d._h.value if d._h is not None else None, pos, mass,
+                   None if sphere is None else (tuple(sphere[0]), float(sphere[1])),
                    None if families is None else tuple(map(tuple, families)), ndim, n,
                    tuple(map(tuple, stats)), nbins, bin_min, bin_max, bool(csr),
                    None if comm is None else comm.handle.value)
         cached = getattr(d, "_req", None)
+        prep = None
         if key is not None and cached is not None and cached[0] == key:
-            args, keep, fs, ws, cs, head, refs, outs = cached[1]
+            args, keep, fs, ws, cs, head, refs, outs, prep = cached[1]
         else:
             args, keep = cls._select_args(pos, mass, sphere, families, ndim, on_device, n)
             fs = (c_int * max(k, 1))(*[int(s[0]) for s in stats])
@@ -190,12 +192,19 @@ class DeviceBins:
                 cl_buf = np.zeros(nbins, dtype=np.int64)
                 outs = (e_buf, c_buf, m_buf, (byref(kept), nat.dptr(e_buf), byref(ne), _i64(c_buf),
                                               _i64(cl_buf), byref(nv), nat.dptr(m_buf)), cl_buf)
-            if key is not None:
-                d._req = (key, (args, keep, fs, ws, cs, head, refs, outs))
+            if key is not None:  # the whole argument list, converted once
+                optrs_ = outs[3]
+                prep = nat.Prepared("pbx_profile_radial_equaln", d._h, *args, *head, *optrs_) \
+                    if comm is None else \
+                    nat.Prepared("pbx_profile_radial_equaln_comm", comm.handle, d._h, *args, *head,
+                                 *optrs_)
+                d._req = (key, (args, keep, fs, ws, cs, head, refs, outs, prep))
         kept, ne, nv = refs
         edges, counts, mom, optrs, local = outs
         try:
-            if comm is None:
+            if prep is not None:
+                prep()
+            elif comm is None:
                 nat.call("pbx_profile_radial_equaln", d._h, *args, *head, *optrs)
             else:
                 nat.call("pbx_profile_radial_equaln_comm", comm.handle, d._h, *args, *head, *optrs)
