@@ -233,35 +233,45 @@ __device__ __forceinline__ double dist2_fma(double dx, double dy, double dz) {
 
 // ------------------------------------------------------------------ build
 // bounding box: ordered keys of min x,y,z and max x,y,z (NaN ignored like
-// the `<` / `>` updates of tree.rs:631-640)
+// the `<` / `>` updates of tree.rs:631-640).  The positions are read as one
+// flat array of 3n doubles, lane-contiguous, four loads in flight per
+// thread; the grid holds a multiple of 3 threads, so every element a thread
+// sees lies on the same axis (its index mod 3).
 __global__ void __launch_bounds__(TPB) bbox_kernel(const double *__restrict__ pos, int64_t n,
                                                    unsigned long long *__restrict__ out) {
   __shared__ unsigned long long red[6][NWAVE];
-  unsigned long long mn[3] = {~0ull, ~0ull, ~0ull}, mx[3] = {0ull, 0ull, 0ull};
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+  const int64_t T = (int64_t)gridDim.x * TPB;  // a multiple of 3
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x, m = 3 * n;
+  unsigned long long mn = ~0ull, mx = 0ull;
+  auto take = [&](double v) {
+    if (v != v) return;
+    const unsigned long long k = dkey(v);
+    mn = k < mn ? k : mn;
+    mx = k > mx ? k : mx;
+  };
+  int64_t j = t;
+  for (; j + 3 * T < m; j += 4 * T) {
+    double v[4];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      double v = pos[3 * i + d];
-      if (v != v) continue;
-      unsigned long long k = dkey(v);
-      mn[d] = k < mn[d] ? k : mn[d];
-      mx[d] = k > mx[d] ? k : mx[d];
-    }
+    for (int u = 0; u < 4; ++u) v[u] = pos[j + u * T];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) take(v[u]);
   }
+  for (; j < m; j += T) take(pos[j]);
+  const int ax = (int)(t % 3);
+  const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
+    unsigned long long lo = ax == d ? mn : ~0ull, hi = ax == d ? mx : 0ull;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
-      unsigned long long a = __shfl_xor(mn[d], o, 64), b = __shfl_xor(mx[d], o, 64);
-      mn[d] = a < mn[d] ? a : mn[d];
-      mx[d] = b > mx[d] ? b : mx[d];
+      const unsigned long long a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
     }
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    for (int d = 0; d < 3; ++d) {
-      red[d][w] = mn[d];
-      red[3 + d][w] = mx[d];
+    if ((threadIdx.x & 63) == 0) {
+      red[d][w] = lo;
+      red[3 + d][w] = hi;
     }
   }
   __syncthreads();
@@ -1317,12 +1327,13 @@ __global__ void __launch_bounds__(TPB)
                  const int32_t *__restrict__ b2p, const int32_t *__restrict__ p2b, int64_t nn,
                  double4 root, BuildView v, int32_t *__restrict__ size) {
 #pragma clang fp contract(off)
-  // threads walk the nodes in preorder (their start / level loads coalesce,
-  // neighbouring threads scan neighbouring paths); outputs go to the
-  // breadth-first slot
-  const int32_t pre = (int32_t)((int64_t)blockIdx.x * TPB + threadIdx.x);
-  if (pre >= nn) return;
-  const int64_t k = p2b[pre];
+  // threads take the nodes in breadth-first order, so the six per-node
+  // outputs are coalesced stores (in preorder they were scattered 4-byte
+  // writes, a cache line each); a level's nodes are in preorder order, so
+  // their start / level / path reads stay close together
+  const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k >= nn) return;
+  const int32_t pre = b2p[k];
   const int64_t i = start[pre];
   const int d = (int)level[pre];
   const int f = fd[i];
@@ -1870,8 +1881,9 @@ static void build_structure(Octree &T, hipStream_t st) {
     unsigned long long h[6] = {~0ull, ~0ull, ~0ull, 0ull, 0ull, 0ull};
     PBX_HIP(hipMemcpyAsync(bb, h, 48, hipMemcpyHostToDevice, st));
     if (n > 0)
-      hipLaunchKernelGGL(bbox_kernel, dim3(std::min<unsigned>(1024, nblk(n))), dim3(TPB), 0, st,
-                         T.pos.as<double>(), n, bb);
+      hipLaunchKernelGGL(bbox_kernel,  // 3k blocks (TPB = 256): 3 | threads
+                         dim3(3 * std::min<unsigned>(256, (nblk(3 * n) + 2) / 3)), dim3(TPB), 0,
+                         st, T.pos.as<double>(), n, bb);
     PBX_HIP(hipMemcpyAsync(h, bb, 48, hipMemcpyDeviceToHost, st));
     PBX_HIP(hipStreamSynchronize(st));
     for (int d = 0; d < 3; ++d) {
