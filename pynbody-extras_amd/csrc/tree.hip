@@ -1006,8 +1006,11 @@ __global__ void __launch_bounds__(WALK_TPB)
   double ph = 0.0, ax = 0.0, ay = 0.0, az = 0.0;
   int32_t cost = 0;  // this lane's accepted nodes + leaf pairs
   // wave-uniform counters (ballot popcounts, kept in SGPRs)
-  unsigned long long n_node = 0, n_pp = 0, n_active = 0;
-  unsigned long long leaf_steps = 0, leaf_active = 0, open_steps = 0;
+  // (32-bit: a wave's counts stay below 2^32 — at most 64 lanes x 2^31
+  // pairs would not, so n_pp is added to 64 bits per leaf; one scalar add
+  // per counter instead of an add / add-with-carry pair)
+  uint32_t n_node = 0, n_active = 0, leaf_steps = 0, leaf_active = 0, open_steps = 0;
+  unsigned long long n_pp = 0;
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
   uint32_t steps = 0;          // the wave moves strictly forward in DFS order
@@ -1123,7 +1126,7 @@ __global__ void __launch_bounds__(WALK_TPB)
     }
     const unsigned no = (unsigned)__popcll(__ballot(open));
     n_node += na - no;  // active lanes accept or open
-    open_steps += (no + 63u) >> 6;  // no in [0, 64]: integer, stays scalar
+    open_steps += no ? 1u : 0u;
     nw = no ? first : next;
     }
     if (live && first < 0) {  // leaf: direct sum in ascending index order
@@ -1166,13 +1169,13 @@ __global__ void __launch_bounds__(WALK_TPB)
   }
   if (wp.counters) {
     if (lane0) {
-      atomicAdd(&wp.counters[0], n_node);
+      atomicAdd(&wp.counters[0], (unsigned long long)n_node);
       atomicAdd(&wp.counters[1], n_pp);
       atomicAdd(&wp.counters[3], (unsigned long long)steps);
-      atomicAdd(&wp.counters[4], n_active);
-      atomicAdd(&wp.counters[5], leaf_steps);
-      atomicAdd(&wp.counters[6], leaf_active);
-      atomicAdd(&wp.counters[7], open_steps);
+      atomicAdd(&wp.counters[4], (unsigned long long)n_active);
+      atomicAdd(&wp.counters[5], (unsigned long long)leaf_steps);
+      atomicAdd(&wp.counters[6], (unsigned long long)leaf_active);
+      atomicAdd(&wp.counters[7], (unsigned long long)open_steps);
     }
   }
 }
