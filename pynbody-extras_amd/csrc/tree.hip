@@ -637,175 +637,251 @@ struct PayloadView {
   double *walk;
 };
 
-// one level of the bottom-up payload pass (tree.rs:866-1067).
-// Layout for coalesced stores: the moments are coefficient-major (q * nn +
-// k: a wave's consecutive nodes store consecutive words), and the walk
-// records (DFS preorder, scattered over the array: 64 lanes x 24 words
-// would touch 64 lines per store) go through LDS and leave record by
-// record, consecutive lanes on consecutive words of one record.
+// Bottom-up payload pass (tree.rs:866-1067) in two parts:
+//  * payload_leaves: every leaf at once (leaves depend on nothing; 85 % of
+//    the nodes at 4M) — mass / COM over its records in index order, h_max,
+//    P2M at the COM, one lane per leaf;
+//  * payload_internal, one launch per level, bottom up: EIGHT lanes per
+//    internal node, lane q on child q.  Every lane sums the children's mass
+//    and COM in octant order exactly as the reference (contraction off:
+//    bit-identical), then lane q shifts child q's moments to the node's COM
+//    (M2M) and the eight shifted moments are added by a fixed butterfly.
+//    One lane per node made each node ~11 dependent memory round trips
+//    (links, child COMs, then each child's 20 moments in turn) at 2 waves
+//    per SIMD: the levels were latency-bound (SQ counters,
+//    profiles/r3/payload_split_rejected/); with a lane per child the
+//    children's moments arrive in one round trip and a level has 8x the
+//    waves to hide it.
+// Moments are coefficient-major (q * nn + k) and the walk records (DFS
+// preorder) leave in record-contiguous pieces.
 constexpr int PL_TPB = 256;
-template <int P> __host__ __device__ constexpr bool rec_via_lds() { return rec_stride<P>() <= 24; }
+
+// the node's walk record: [cx cy cz mass | size2 hmax | next first |
+// leaf_start count] and the evaluation coefficients
 template <int P>
-__global__ void __launch_bounds__(PL_TPB) payload_level(PayloadView v, int32_t a, int32_t b) {
+__device__ __forceinline__ void walk_record(const PayloadView &v, int32_t k, int32_t pk, int32_t nc,
+                                            double cx, double cy, double cz, double mass, double hm,
+                                            const double *M, double *r) {
+#pragma clang fp contract(off)
+  r[0] = cx;
+  r[1] = cy;
+  r[2] = cz;
+  r[3] = mass;
+  const double sz = v.ncen[k].w * 2.0;  // tree.rs:794-798
+  r[4] = sz * sz;
+  r[5] = v.hmax ? hm : 0.0;
+  // DFS preorder ids: first child = k + 1, next_branch = k + subtree size
+  // (the same threading as tree.rs:736-776, renumbered)
+  const int64_t after = (int64_t)pk + v.size[k];
+  const bool leaf = nc == 0;
+  int32_t ir[4];
+  ir[0] = after < v.nn ? (int32_t)after : -1;
+  ir[1] = leaf ? -1 : pk + 1;
+  ir[2] = leaf ? v.nstart[k] : 0;
+  ir[3] = leaf ? v.ncount[k] : 0;
+  r[6] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[0] | ((uint64_t)(uint32_t)ir[1] << 32));
+  r[7] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[2] | ((uint64_t)(uint32_t)ir[3] << 32));
+  if constexpr (P == 2 || P == 3) {
+    detraced_coef<P>(M, r + 8);
+  } else if constexpr (P >= 4) {
+#pragma unroll
+    for (int q = 0; q < ncoef(P); ++q) r[8 + q] = M[q];
+  }
+}
+
+template <int P>
+__global__ void __launch_bounds__(PL_TPB) payload_leaves(PayloadView v) {
   constexpr int RS = rec_stride<P>();
-  constexpr int RSP = RS + 1;  // LDS row stride (odd: lanes on distinct banks)
-  __shared__ double rs[rec_via_lds<P>() ? (PL_TPB / 64) * 64 * RSP : 1];
-  __shared__ int32_t rpk[rec_via_lds<P>() ? PL_TPB : 1];
-  const int32_t k = a + (int32_t)(blockIdx.x * PL_TPB + threadIdx.x);
-  const bool live = k < b;
-  const int64_t nn = v.nn;
+  constexpr int HW = (RS + 1) / 2;  // record words per transposition half
+  constexpr int HP = HW + 1;        // LDS row stride (odd)
+  __shared__ double rs[(PL_TPB / 64) * 64 * HP];
+  const int64_t k64 = (int64_t)blockIdx.x * PL_TPB + threadIdx.x;
+  const bool in = k64 < v.nn;
+  const int32_t k = in ? (int32_t)k64 : 0;
+  // the node's fields all at once (no branch between their loads)
+  const int32_t nch = in ? v.nchild[k] : 1;
+  const int32_t s0 = v.nstart[k], c0 = v.ncount[k], pk0 = v.pre[k];
+  const bool live = in && nch == 0;
+  const int32_t s = s0, c = live ? c0 : 0, pk = live ? pk0 : -1;
   double mass = 0.0, cx = 0.0, cy = 0.0, cz = 0.0, hm = 0.0;
-  double M[P >= 2 ? ncoef(P) : 1];
-  static_for<(P >= 2 ? ncoef(P) : 1)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
-  const int32_t nc = live ? v.nchild[k] : 0;
-  if (live && nc == 0) {
-    const int32_t s = v.nstart[k], c = v.ncount[k];
-    // leaves of up to PL particles: every record in flight at once, then the
-    // same ordered sums as the general loop (identical results)
-    constexpr int PL = 8;
-    double4 rr[PL];
-    const bool small = c <= PL;
+  constexpr int PL = 8;  // leaves of up to PL records: all of them in flight at once
+  double4 rr[PL];
+  const bool small = c <= PL;
+  if (small) {
+#pragma unroll
+    for (int q = 0; q < PL; ++q) rr[q] = v.rec[q < c ? s + q : s];
+  }
+  {
+#pragma clang fp contract(off)
     if (small) {
 #pragma unroll
-      for (int q = 0; q < PL; ++q) rr[q] = v.rec[q < c ? s + q : s];
+      for (int q = 0; q < PL; ++q) {
+        if (q >= c) break;
+        mass += rr[q].w;
+        cx += rr[q].x * rr[q].w;
+        cy += rr[q].y * rr[q].w;
+        cz += rr[q].z * rr[q].w;
+      }
+    } else {
+      for (int32_t j = s; j < s + c; ++j) {
+        const double4 r = v.rec[j];
+        mass += r.w;
+        cx += r.x * r.w;
+        cy += r.y * r.w;
+        cz += r.z * r.w;
+      }
     }
-    {
-#pragma clang fp contract(off)
+    if (mass > 0.0) {
+      cx /= mass;
+      cy /= mass;
+      cz /= mass;
+    }
+  }
+  if (v.hmax)
+    for (int32_t j = s; j < s + c; ++j) hm = __builtin_fmax(hm, __builtin_fmax(v.soft[j], 0.0));
+  double M[P >= 2 ? ncoef(P) : 1];
+  static_for<(P >= 2 ? ncoef(P) : 1)>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
+  if constexpr (P >= 2) {
+    if (mass != 0.0) {
       if (small) {
 #pragma unroll
         for (int q = 0; q < PL; ++q) {
           if (q >= c) break;
-          mass += rr[q].w;
-          cx += rr[q].x * rr[q].w;
-          cy += rr[q].y * rr[q].w;
-          cz += rr[q].z * rr[q].w;
+          p2m_add<P>(M, rr[q].w, rr[q].x - cx, rr[q].y - cy, rr[q].z - cz);
         }
       } else {
         for (int32_t j = s; j < s + c; ++j) {
           const double4 r = v.rec[j];
-          mass += r.w;
-          cx += r.x * r.w;
-          cy += r.y * r.w;
-          cz += r.z * r.w;
-        }
-      }
-      if (mass > 0.0) {
-        cx /= mass;
-        cy /= mass;
-        cz /= mass;
-      }
-    }
-    if (v.hmax)
-      for (int32_t j = s; j < s + c; ++j) hm = __builtin_fmax(hm, __builtin_fmax(v.soft[j], 0.0));
-    if constexpr (P >= 2) {
-      if (mass != 0.0) {
-        if (small) {
-#pragma unroll
-          for (int q = 0; q < PL; ++q) {
-            if (q >= c) break;
-            p2m_add<P>(M, rr[q].w, rr[q].x - cx, rr[q].y - cy, rr[q].z - cz);
-          }
-        } else {
-          for (int32_t j = s; j < s + c; ++j) {
-            const double4 r = v.rec[j];
-            p2m_add<P>(M, r.w, r.x - cx, r.y - cy, r.z - cz);
-          }
+          p2m_add<P>(M, r.w, r.x - cx, r.y - cy, r.z - cz);
         }
       }
     }
-  } else if (live) {
-    const int32_t f = v.nfirst[k];
-    double4 cq[8];  // an octree node has at most 8 children: all in flight at once
-#pragma unroll
-    for (int q = 0; q < 8; ++q) cq[q] = v.com[q < nc ? f + q : f];
-    {
-#pragma clang fp contract(off)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (q >= nc) break;
-        const double4 c4 = cq[q];
-        if (c4.w == 0.0) continue;
-        mass += c4.w;
-        cx += c4.x * c4.w;
-        cy += c4.y * c4.w;
-        cz += c4.z * c4.w;
-      }
-      if (mass > 0.0) {
-        cx /= mass;
-        cy /= mass;
-        cz /= mass;
-      }
-    }
-    if (v.hmax)
-      for (int32_t ch = f; ch < f + nc; ++ch) hm = __builtin_fmax(hm, v.hmax[ch]);
-    if constexpr (P >= 2) {
-      if (mass != 0.0) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          if (q >= nc) break;
-          const double4 c4 = cq[q];
-          if (c4.w == 0.0) continue;
-          m2m_add<P>(M, v.mom + (f + q), nn, cx - c4.x, cy - c4.y, cz - c4.z);
-        }
-      }
-    }
+    if (live)
+      static_for<ncoef(P)>([&](auto qc) {
+        v.mom[(int64_t)decltype(qc)::value * v.nn + k] = M[decltype(qc)::value];
+      });
   }
   if (live) {
-    if constexpr (P >= 2)  // coefficient-major: coalesced over the wave's nodes
-      static_for<ncoef(P)>([&](auto qc) {
-        v.mom[(int64_t)decltype(qc)::value * nn + k] = M[decltype(qc)::value];
-      });
     v.com[k] = make_double4(cx, cy, cz, mass);
     if (v.hmax) v.hmax[k] = hm;
   }
-  // the walk record (was pack_walk / pack_coef / pack_moments)
-  double r[RS];
-  int32_t pk = 0;
-  if (live) {
+  double r[2 * HW];
+  r[2 * HW - 1] = 0.0;
+  if (live) walk_record<P>(v, k, pk, 0, cx, cy, cz, mass, hm, M, r);
+  // the records leave through this wave's LDS rows, half a record at a
+  // time: consecutive lanes store consecutive words of one record (no block
+  // barrier: a wave's LDS operations complete in order)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double *wr = rs + w * 64 * HP;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int j = 0; j < HW; ++j) wr[lane * HP + j] = r[h * HW + j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int idx = lane; idx < 64 * HW; idx += 64) {
+      const int i = idx / HW, j = idx - i * HW;
+      const int32_t pi = __shfl(pk, i, 64);
+      if (pi >= 0 && h * HW + j < RS) v.walk[(int64_t)pi * RS + h * HW + j] = wr[i * HP + j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// the internal nodes, breadth-first (so level by level): flag, scan, list
+__global__ void internal_flags(const int32_t *__restrict__ nchild, int64_t nn,
+                               uint32_t *__restrict__ flag) {
+  const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k <= nn) flag[k] = (k < nn && nchild[k] > 0) ? 1u : 0u;
+}
+__global__ void internal_list(const int32_t *__restrict__ nchild, const uint32_t *__restrict__ scan,
+                              int64_t nn, int32_t *__restrict__ list) {
+  const int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (k < nn && nchild[k] > 0) list[scan[k]] = (int32_t)k;
+}
+
+constexpr int PI_G = 8;  // lanes per internal node: one per child slot
+template <int P>
+__global__ void __launch_bounds__(PL_TPB)
+    payload_internal(PayloadView v, const int32_t *__restrict__ ilist,
+                     const uint32_t *__restrict__ iscan, int32_t a, int32_t b, int64_t lo_h,
+                     int64_t hi_h) {
+  constexpr int RS = rec_stride<P>();
+  constexpr int NM = P >= 2 ? ncoef(P) : 1;
+  // the level's run of the internal list: from the host when the build
+  // counted it (lo_h >= 0), else from the scan
+  const uint32_t lo = lo_h >= 0 ? (uint32_t)lo_h : iscan[a];
+  const uint32_t hi = lo_h >= 0 ? (uint32_t)hi_h : iscan[b];
+  const uint32_t g0 = lo + blockIdx.x * (PL_TPB / PI_G);
+  if (g0 >= hi) return;  // (uniform: the grid is an upper bound)
+  const int q = (int)(threadIdx.x & (PI_G - 1));
+  const uint32_t g = g0 + threadIdx.x / PI_G;
+  const bool live = g < hi;
+  const int32_t k = live ? ilist[g] : 0;
+  const int32_t nc = live ? v.nchild[k] : 0, f = live ? v.nfirst[k] : 0;
+  const int32_t pk = live ? v.pre[k] : 0;
+  const int64_t nn = v.nn;
+  // mass / COM over the children in octant order, on every lane alike
+  double4 cq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cq[j] = v.com[j < nc ? f + j : f];
+  double mass = 0.0, cx = 0.0, cy = 0.0, cz = 0.0, hm = 0.0;
+  {
 #pragma clang fp contract(off)
-    pk = v.pre[k];
-    r[0] = cx;
-    r[1] = cy;
-    r[2] = cz;
-    r[3] = mass;
-    const double sz = v.ncen[k].w * 2.0;  // tree.rs:794-798
-    r[4] = sz * sz;
-    r[5] = v.hmax ? hm : 0.0;
-    // DFS preorder ids: first child = k + 1, next_branch = k + subtree size
-    // (the same threading as tree.rs:736-776, renumbered)
-    const int64_t after = (int64_t)pk + v.size[k];
-    const bool leaf = nc == 0;
-    int32_t ir[4];
-    ir[0] = after < nn ? (int32_t)after : -1;
-    ir[1] = leaf ? -1 : pk + 1;
-    ir[2] = leaf ? v.nstart[k] : 0;
-    ir[3] = leaf ? v.ncount[k] : 0;
-    r[6] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[0] | ((uint64_t)(uint32_t)ir[1] << 32));
-    r[7] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[2] | ((uint64_t)(uint32_t)ir[3] << 32));
-    if constexpr (P == 2 || P == 3) {
-      detraced_coef<P>(M, r + 8);
-    } else if constexpr (P >= 4) {
 #pragma unroll
-      for (int q = 0; q < ncoef(P); ++q) r[8 + q] = M[q];
+    for (int j = 0; j < 8; ++j) {
+      if (j >= nc) break;
+      const double4 c4 = cq[j];
+      if (c4.w == 0.0) continue;
+      mass += c4.w;
+      cx += c4.x * c4.w;
+      cy += c4.y * c4.w;
+      cz += c4.z * c4.w;
+    }
+    if (mass > 0.0) {
+      cx /= mass;
+      cy /= mass;
+      cz /= mass;
     }
   }
-  if constexpr (rec_via_lds<P>()) {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double *wr = rs + w * 64 * RSP;
+  if (v.hmax) {  // the children's h_max (lane q: child q), max over the group
+    hm = q < nc ? v.hmax[f + q] : 0.0;
 #pragma unroll
-    for (int j = 0; j < RS; ++j) wr[lane * RSP + j] = r[j];
-    rpk[threadIdx.x] = live ? pk : -1;
-    __syncthreads();
-    // record i of this wave, word j: lanes on consecutive words
-    for (int idx = lane; idx < 64 * RS; idx += 64) {
-      const int i = idx / RS, j = idx - i * RS;
-      const int32_t pi = rpk[w * 64 + i];
-      if (pi >= 0) v.walk[(int64_t)pi * RS + j] = wr[i * RSP + j];
-    }
-  } else if (live) {
-#pragma unroll
-    for (int j = 0; j < RS; ++j) v.walk[(int64_t)pk * RS + j] = r[j];
+    for (int o = 1; o < PI_G; o <<= 1) hm = __builtin_fmax(hm, __shfl_xor(hm, o, 64));
   }
+  double M[NM];
+  static_for<NM>([&](auto qc) { M[decltype(qc)::value] = 0.0; });
+  if constexpr (P >= 2) {
+    // child q's moments shifted to this node's COM
+    const double4 mine = v.com[q < nc ? f + q : f];  // (a load: a select chain over cq spills)
+    if (live && q < nc && mass != 0.0 && mine.w != 0.0)
+      m2m_add<P>(M, v.mom + (f + q), nn, cx - mine.x, cy - mine.y, cz - mine.z);
+    // the eight children's shifts, added by a fixed butterfly
+#pragma unroll
+    for (int o = 1; o < PI_G; o <<= 1)
+      static_for<NM>([&](auto qc) {
+        constexpr int t = decltype(qc)::value;
+        M[t] += __shfl_xor(M[t], o, 64);
+      });
+  }
+  if (!live) return;
+  if constexpr (P >= 2)
+    static_for<NM>([&](auto qc) {
+      constexpr int t = decltype(qc)::value;
+      if (t % PI_G == q) v.mom[(int64_t)t * nn + k] = M[t];
+    });
+  if (q == 0) {
+    v.com[k] = make_double4(cx, cy, cz, mass);
+    if (v.hmax) v.hmax[k] = hm;
+  }
+  double r[RS];
+  walk_record<P>(v, k, pk, nc, cx, cy, cz, mass, hm, M, r);
+#pragma unroll
+  for (int j = 0; j < RS; ++j)
+    if (j % PI_G == q) v.walk[(int64_t)pk * RS + j] = r[j];
 }
 
 // Detraced evaluation coefficients (orders 2 and 3).  With raw moments
@@ -1254,9 +1330,9 @@ __global__ void __launch_bounds__(TPB)
     bp_depth(const uint8_t *__restrict__ eq, const uint8_t *__restrict__ win, int64_t n, int D,
              int64_t cap, uint8_t *__restrict__ fd, uint8_t *__restrict__ lv,
              uint32_t *__restrict__ cnt, unsigned int *__restrict__ flag) {
-  __shared__ unsigned int h[BP_MAX_LEVEL + 1];
+  __shared__ unsigned int h[BP_MAX_LEVEL + 1], hin[BP_MAX_LEVEL + 1];
   __shared__ uint8_t sw[TPB + 64];  // the windows [i - cap, i] of the chunk, cap <= 64
-  for (int d = threadIdx.x; d <= BP_MAX_LEVEL; d += TPB) h[d] = 0u;
+  for (int d = threadIdx.x; d <= BP_MAX_LEVEL; d += TPB) h[d] = hin[d] = 0u;
   bool over = false;
   for (int64_t base = (int64_t)blockIdx.x * TPB; base < n; base += (int64_t)gridDim.x * TPB) {
     __syncthreads();  // the previous chunk's windows are read
@@ -1282,7 +1358,8 @@ __global__ void __launch_bounds__(TPB)
       lv[i] = (uint8_t)L;
       cnt[i] = (uint32_t)(L >= f ? L - f + 1 : 0);
     }
-    // nodes per level: one ballot per level and wave
+    // nodes per level and of them internal ones (all but the deepest node
+    // starting at i): ballots per level and wave
     int dmax = ok ? L : -1;
     for (int o = 32; o > 0; o >>= 1) {
       const int y = __shfl_xor(dmax, o, 64);
@@ -1290,14 +1367,18 @@ __global__ void __launch_bounds__(TPB)
     }
     for (int d = 0; d <= dmax; ++d) {
       const uint32_t c = (uint32_t)__popcll(__ballot(ok && f <= d && d <= L));
+      const uint32_t ci = (uint32_t)__popcll(__ballot(ok && f <= d && d < L));
       if ((threadIdx.x & 63) == 0 && c) atomicAdd(&h[d], c);
+      if ((threadIdx.x & 63) == 0 && ci) atomicAdd(&hin[d], ci);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) cnt[n] = 0u;  // scan sentinel: S[n] = nodes
   if (__ballot(over) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
   __syncthreads();
-  for (int d = threadIdx.x; d <= BP_MAX_LEVEL; d += TPB)
+  for (int d = threadIdx.x; d <= BP_MAX_LEVEL; d += TPB) {
     if (h[d]) atomicAdd(&flag[1 + d], h[d]);
+    if (hin[d]) atomicAdd(&flag[2 + BP_MAX_LEVEL + d], hin[d]);
+  }
 }
 
 // every node in preorder: its level and start
@@ -1584,6 +1665,7 @@ struct Octree {
   double root[4] = {0, 0, 0, 0};
   int64_t nn = 0, cap = 0;
   std::vector<int32_t> lvl;  // first node id of every level (+ end)
+  std::vector<int32_t> lvl_int;  // internal nodes per level (parallel build; else empty)
   Buf pos, mass, soft;       // original order (device copies)
   Buf perm, rec, soft_s;     // leaf order
   Buf trace;                 // PBX_WALK_TRACE diagnostic
@@ -1591,6 +1673,7 @@ struct Octree {
   Buf com, hmax, mom, coef, walk;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
   Buf bal;                   // cost-balanced ranges: chunk sums + cuts
+  Buf iscan, ilist, iws;     // payload: internal-node flags / scan, list, scan state
   int cost_kind = 0;                   // d_cost contents (WalkParams::cost_kind)
   Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
   Buf rec0;                  // {x, y, z, m} in original order (path_keys)
@@ -1600,7 +1683,7 @@ struct Octree {
     Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
                    &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &keys, &ktmp0,
                    &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
-                   &counters, &trace, &bal, &bp_fl, &bp_eq, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
+                   &counters, &trace, &bal, &iscan, &ilist, &iws, &bp_fl, &bp_eq, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
                    &bp_p2b};
     for (Buf *b : bufs) b->release();
     rm_pin.release();
@@ -1727,7 +1810,8 @@ static bool split_parallel(Octree &T, hipStream_t st, int sorted_levels) {
   uint8_t *fd = (uint8_t *)T.bp_fl.get(2 * (size_t)n + 16);
   uint8_t *lv = fd + n;
   uint32_t *S = (uint32_t *)T.bp_s.get(4 * (size_t)(n + 1));
-  const size_t nctl = 2 + BP_MAX_LEVEL + 1;
+  // [undecidable flag][nodes per level][internal nodes per level][nodes]
+  const size_t nctl = 3 + 2 * (size_t)BP_MAX_LEVEL + 1;
   unsigned int *ctl = (unsigned int *)T.bp_ctl.get(4 * nctl);
   PBX_HIP(hipMemsetAsync(ctl, 0, 4 * nctl, st));
   uint8_t *eq = (uint8_t *)T.bp_eq.get(2 * (size_t)n + 16), *win = eq + n;
@@ -1745,10 +1829,12 @@ static bool split_parallel(Octree &T, hipStream_t st, int sorted_levels) {
   const int64_t nn = h[nctl - 1];
   // levels: nodes per level -> breadth-first id ranges
   T.lvl.assign(1, 0);
+  T.lvl_int.clear();
   int64_t tot = 0;
   for (int d = 0; d <= BP_MAX_LEVEL && tot < nn; ++d) {
     tot += h[1 + d];
     T.lvl.push_back((int32_t)tot);
+    T.lvl_int.push_back((int32_t)h[2 + BP_MAX_LEVEL + d]);
   }
   if (tot != nn || nn < 1) fail(PBX_ERR_RUNTIME, "parallel octree build: %lld nodes by level, %lld in all",
                                 (long long)tot, (long long)nn);
@@ -1816,6 +1902,7 @@ static bool split_levels(Octree &T, hipStream_t st) {
   int64_t F = read_u32(sm, st);
   T.nn = 1;
   T.lvl.assign({0, 1});
+  T.lvl_int.clear();
   int d = 0;
   while (F > 0) {
     if (d >= LPW * T.nwords) return false;
@@ -1919,6 +2006,7 @@ static void build_structure(Octree &T, hipStream_t st) {
     PBX_HIP(hipStreamSynchronize(st));
     T.nn = 1;
     T.lvl.assign({0, 1});
+    T.lvl_int.clear();
     T.rec.get(64);
     preorder(T, st);
     return;
@@ -1985,11 +2073,31 @@ static void pack_particles(Octree &T, hipStream_t st) {
 
 template <int P>
 static void run_payload(Octree &T, hipStream_t st, PayloadView v) {
-  for (int L = (int)T.lvl.size() - 2; L >= 0; --L) {
+  const int64_t nn = T.nn;
+  if (nn <= 0) return;
+  hipLaunchKernelGGL(payload_leaves<P>, dim3((unsigned)((nn + PL_TPB - 1) / PL_TPB)), dim3(PL_TPB),
+                     0, st, v);
+  // the internal nodes as one breadth-first list (flag, scan, scatter)
+  uint32_t *iscan = (uint32_t *)T.iscan.get(sizeof(uint32_t) * (size_t)(nn + 1));
+  int32_t *ilist = (int32_t *)T.ilist.get(sizeof(int32_t) * (size_t)nn);
+  hipLaunchKernelGGL(internal_flags, dim3(nblk(nn + 1)), dim3(TPB), 0, st, v.nchild, nn, iscan);
+  prim::scan_u32(T.iws, st, iscan, nn + 1);
+  hipLaunchKernelGGL(internal_list, dim3(nblk(nn)), dim3(TPB), 0, st, v.nchild, iscan, nn, ilist);
+  const int nl = (int)T.lvl.size() - 1;
+  const bool counted = (int64_t)T.lvl_int.size() == nl;
+  std::vector<int64_t> ibase(nl + 1, 0);  // first list slot of each level (counted builds)
+  for (int L = 0; counted && L < nl; ++L) ibase[L + 1] = ibase[L] + T.lvl_int[L];
+  for (int L = nl - 2; L >= 0; --L) {
     const int32_t a = T.lvl[L], b = T.lvl[L + 1];
-    if (b > a)
-      hipLaunchKernelGGL(payload_level<P>, dim3((unsigned)((b - a + PL_TPB - 1) / PL_TPB)),
-                         dim3(PL_TPB), 0, st, v, a, b);
+    // internal nodes of level L: counted by the parallel build, else at
+    // most its nodes and at most the next level's
+    const int64_t ub = counted ? T.lvl_int[L]
+                       : std::min<int64_t>(b - a, T.lvl[L + 2] - T.lvl[L + 1]);
+    if (ub > 0)
+      hipLaunchKernelGGL(payload_internal<P>,
+                         dim3((unsigned)((ub * PI_G + PL_TPB - 1) / PL_TPB)), dim3(PL_TPB), 0, st,
+                         v, (const int32_t *)ilist, (const uint32_t *)iscan, a, b,
+                         counted ? ibase[L] : (int64_t)-1, counted ? ibase[L + 1] : (int64_t)-1);
   }
   PBX_HIP(hipGetLastError());
 }
