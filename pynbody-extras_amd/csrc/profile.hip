@@ -1201,7 +1201,6 @@ __global__ void __launch_bounds__(MS0_TPB)
                 unsigned long long *__restrict__ counts, int nb, uint32_t *__restrict__ H,
                 uint32_t *__restrict__ rows) {
   __shared__ uint32_t lh[MS0_DIG];
-  for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
   const FusedCtl ctl = fused_ctl_eff(fsu);
   if (blockIdx.x == 0 && threadIdx.x == 0 && fsu.hint_out) {
     // this call's window key range widened by 1/64 of its span on each side
@@ -1248,6 +1247,7 @@ __global__ void __launch_bounds__(MS0_TPB)
   }
   if (fsu.tiled) tile_offsets_fix(fsu.btot, fsu.nt, fsu.toff, red);  // (blocks >= 1)
   if (ctl.hint) return;  // select_tiles counted the keys (msel_reduce0 sums its rows)
+  for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
   __syncthreads();
   const uint64_t ka = fsu.ka, kb = fsu.kb;
   const ElRange er = el_range(fsu.tiled ? fsu.kw : nullptr, fsu.nt, (ctl.err & 2) ? 0 : ctl.n);
