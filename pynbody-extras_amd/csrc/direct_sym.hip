@@ -18,7 +18,8 @@
 // consecutive I-blocks and walks a range of J-chunks; for each J-chunk a wave
 // evaluates the 256 x 256 pairs with its targets in registers while the
 // chunk's sources — and their accumulators — rotate one lane per step around
-// the wave (ds_bpermute, LDS crossbar, no VALU): after 64 steps every source
+// the wave (ds_bpermute on the LDS crossbar; sx, sy by DPP wave_rol:1 on the
+// VALU, see PBX_SYM_DPP_MASK): after 64 steps every source
 // met every target, so neither side needs a cross-lane reduction.  Chunk
 // j > block b: both sides accumulate; j == b: target side only (each
 // ordered pair exactly once, self pair masked); j < b: skipped (done by the
@@ -56,6 +57,26 @@ __device__ __forceinline__ double rot(double v, int addr) {
   const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(b >> 32));
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
 }
+
+// the same rotation on the VALU: DPP wave_rol:1 (lane l takes lane l + 1's
+// value, lane 63 lane 0's), no LDS operation / lgkmcnt slot
+__device__ __forceinline__ double rot_dpp(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x134, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x134, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
+}
+// Which of a slot's eight rotated values go through DPP (bits: sx sy sz sm
+// sp sa sb sc) instead of the LDS crossbar.  A slot's 16 ds_bpermute per
+// step exceed the 15 LDS operations a wave may have in flight (lgkmcnt):
+// the waves waited on LDS 22 % of their cycles (SQ_WAIT_INST_LDS).  Moving
+// some rotations to the VALU (v_mov_b32_dpp wave_rol:1) trades VALU issue
+// for LDS slots; same-box A/B at 1M (`profiles/r3/sym_dpp_ab/`): all LDS
+// 375.9 / 377.2 ms, accumulators on DPP 369.4, the four source values
+// 360.0 / 360.2, sx and sy 358.2 / 358.5, everything on DPP ~400.
+#ifndef PBX_SYM_DPP_MASK
+#define PBX_SYM_DPP_MASK 0x03
+#endif
 
 // One J-chunk for one wave.  SYMM: both sides; else the diagonal chunk
 // (target side only, self pair masked at rotation 0).
@@ -115,16 +136,19 @@ __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t j
       }
       // pass this slot on as soon as its pairs are done: the LDS-crossbar
       // round trip overlaps the next slot's arithmetic
-      sx[ks] = rot(sx[ks], addr);
-      sy[ks] = rot(sy[ks], addr);
-      sz[ks] = rot(sz[ks], addr);
-      sm[ks] = rot(sm[ks], addr);
+      auto rt = [&](double x, int bit) {
+        return ((PBX_SYM_DPP_MASK >> bit) & 1) ? rot_dpp(x) : rot(x, addr);
+      };
+      sx[ks] = rt(sx[ks], 0);
+      sy[ks] = rt(sy[ks], 1);
+      sz[ks] = rt(sz[ks], 2);
+      sm[ks] = rt(sm[ks], 3);
       if (SYMM) {
-        if (WANT & PBX_WANT_POT) sp[ks] = rot(sp[ks], addr);
+        if (WANT & PBX_WANT_POT) sp[ks] = rt(sp[ks], 4);
         if (WANT & PBX_WANT_ACC) {
-          sa[ks] = rot(sa[ks], addr);
-          sb[ks] = rot(sb[ks], addr);
-          sc[ks] = rot(sc[ks], addr);
+          sa[ks] = rt(sa[ks], 5);
+          sb[ks] = rt(sb[ks], 6);
+          sc[ks] = rt(sc[ks], 7);
         }
       }
     }
