@@ -18,8 +18,9 @@
 // consecutive I-blocks and walks a range of J-chunks; for each J-chunk a wave
 // evaluates the 256 x 256 pairs with its targets in registers while the
 // chunk's sources — and their accumulators — rotate one lane per step around
-// the wave (ds_bpermute on the LDS crossbar; sx, sy by DPP wave_rol:1 on the
-// VALU, see PBX_SYM_DPP_MASK): after 64 steps every source
+// the wave (sources and the potential / x-force partials by DPP wave_rol:1
+// on the VALU, the y / z partials by ds_bpermute on the LDS crossbar, see
+// PBX_SYM_DPP_MASK): after 64 steps every source
 // met every target, so neither side needs a cross-lane reduction.  Chunk
 // j > block b: both sides accumulate; j == b: target side only (each
 // ordered pair exactly once, self pair masked); j < b: skipped (done by the
@@ -62,8 +63,12 @@ __device__ __forceinline__ double rot(double v, int addr) {
 // value, lane 63 lane 0's), no LDS operation / lgkmcnt slot
 __device__ __forceinline__ double rot_dpp(double v) {
   const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x134, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x134, 0xF, 0xF, false);
+  // (old = the source itself: every lane receives a value, and the
+  // rotated word may then reuse the source's register — no v_mov of 0 and
+  // no copy back into the loop-carried register)
+  const int l0 = (int)(uint32_t)b, h0 = (int)(uint32_t)(b >> 32);
+  const int lo = __builtin_amdgcn_update_dpp(l0, l0, 0x134, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(h0, h0, 0x134, 0xF, 0xF, false);
   return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo);
 }
 // Which of a slot's eight rotated values go through DPP (bits: sx sy sz sm
@@ -71,11 +76,13 @@ __device__ __forceinline__ double rot_dpp(double v) {
 // step exceed the 15 LDS operations a wave may have in flight (lgkmcnt):
 // the waves waited on LDS 22 % of their cycles (SQ_WAIT_INST_LDS).  Moving
 // some rotations to the VALU (v_mov_b32_dpp wave_rol:1) trades VALU issue
-// for LDS slots; same-box A/B at 1M (`profiles/r3/sym_dpp_ab/`): all LDS
-// 375.9 / 377.2 ms, accumulators on DPP 369.4, the four source values
-// 360.0 / 360.2, sx and sy 358.2 / 358.5, everything on DPP ~400.
+// for LDS slots.  Same-box A/B at 1M (`profiles/r3/sym_dpp_ab/`): all LDS
+// 376-377 ms; with the DPP result written in place (old = source) sx, sy
+// 348, the four source values 339, those and sp, sa 333-343 (the best on
+// two boxes), everything 334; before in-place DPP every rotated word cost
+// a v_mov of 0 and a copy back (sx, sy: 358 ms).
 #ifndef PBX_SYM_DPP_MASK
-#define PBX_SYM_DPP_MASK 0x03
+#define PBX_SYM_DPP_MASK 0x3F
 #endif
 
 // One J-chunk for one wave.  SYMM: both sides; else the diagonal chunk
