@@ -679,6 +679,14 @@ __device__ __forceinline__ void walk_record(const PayloadView &v, int32_t k, int
   ir[1] = leaf ? -1 : pk + 1;
   ir[2] = leaf ? v.nstart[k] : 0;
   ir[3] = leaf ? v.ncount[k] : 0;
+  // an empty node (mass 0, tree.rs:1087-1090: skipped) walks as a leaf of no
+  // records: no descent, no pairs, the same next — one sign test in the
+  // walk decides leaf / internal
+  if (mass == 0.0) {
+    ir[1] = -1;
+    ir[2] = 0;
+    ir[3] = 0;
+  }
   r[6] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[0] | ((uint64_t)(uint32_t)ir[1] << 32));
   r[7] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[2] | ((uint64_t)(uint32_t)ir[3] << 32));
   if constexpr (P == 2 || P == 3) {
@@ -1110,12 +1118,11 @@ __global__ void __launch_bounds__(WALK_TPB)
     n_active += na;  // SIMD efficiency counter
     bool open = false;
     int32_t nw = next;
-    // tree.rs:1087-1090: empty nodes are skipped (mass != 0.0 on the bits,
-    // so the test stays on the scalar unit: SALU has no f64 compare)
-    const bool live = ((c[0][7] & 0x7fffffffu) | c[0][6]) != 0u;
-    // two independent uniform ifs, not an if / else chain (the chain made a
+    // tree.rs:1087-1090: empty nodes are skipped — their records say "leaf
+    // of no records" (walk_record), so the sign of `first` alone decides.
+    // Two independent uniform ifs, not an if / else chain (the chain made a
     // flow block through which the internal path's values were copied)
-    if (live && first >= 0) {
+    if (first >= 0) {
     {  // the test runs on every lane (some lane is always active at w, so an
        // `if (act)` would never skip it; as a branch it doubled the phis)
       const double dx = chunk_d(c[0], 0) - tx, dy = chunk_d(c[0], 1) - ty,
@@ -1205,7 +1212,7 @@ __global__ void __launch_bounds__(WALK_TPB)
     open_steps += no ? 1u : 0u;
     nw = no ? first : next;
     }
-    if (live && first < 0) {  // leaf: direct sum in ascending index order
+    if (first < 0) {  // leaf: direct sum in ascending index order
       const int32_t s = chunk_i(c[0], 14), e = s + chunk_i(c[0], 15);
       ++leaf_steps;
       leaf_rounds += (uint32_t)(e - s + 3) >> 2;

@@ -116,6 +116,22 @@ def test_plummer_orders(gpu, order):
     check_walk(dev, ref, 0.5, len(pos))
 
 
+def test_zero_mass_subtrees(gpu):
+    """Empty nodes (mass 0) are skipped (tree.rs:1087-1090): a region of
+    zero-mass particles (whole empty subtrees) and scattered zero masses —
+    the oracle's structure, opening decisions and values."""
+    pos, mass = plummer(20_000, seed=77)
+    mass = mass.copy()
+    mass[pos[:, 0] > 0.3] = 0.0
+    mass[::7] = 0.0
+    dev = _engine.Octree(pos, mass, 8, 3)
+    ref = ot.RefOctree(pos, mass, 8, 3)
+    check_structure(dev, ref, 3)
+    check_walk(dev, ref, 0.5, len(pos))
+    q = plummer(2000, seed=78)[0] * 1.2
+    assert rel_pot(dev.potentials_at_points(q, 0.5), ref.potentials_at_points(q, 0.5)) < TIGHT
+
+
 @pytest.mark.parametrize("leaf", [1, 3, 32, 100])
 def test_leaf_capacities(gpu, leaf):
     pos = uniform(6000, leaf)
