@@ -1106,6 +1106,12 @@ __global__ void __launch_bounds__(WALK_TPB)
   // phi registers: ~20 v_mov_b64 per wave step, as many VALU issues as the
   // opening test itself).
   const uint32_t max_steps = (uint32_t)wp.max_steps;
+  // theta^2 in a VGPR pair: left a kernel argument, it was reloaded from the
+  // kernarg segment every step (a scalar load and its wait; SGPRs are full)
+  const uint64_t th2b = __builtin_bit_cast(uint64_t, wp.theta2);
+  const double theta2 = __builtin_bit_cast(
+      double, ((uint64_t)((uint32_t)(th2b >> 32) | vgpr_zero()) << 32) |
+                  (uint64_t)((uint32_t)th2b | vgpr_zero()));
   while (w >= 0 && steps < max_steps) {  // corrupted links: stop instead of hanging
     ++steps;
     w = __builtin_amdgcn_readfirstlane(w);  // uniform: keep it (and the address math) scalar
@@ -1137,7 +1143,7 @@ __global__ void __launch_bounds__(WALK_TPB)
           soft_ok = dist2 > ch * ch;
         }
       }
-      const bool accept = act && soft_ok && chunk_d(c[0], 4) < wp.theta2 * dist2;
+      const bool accept = act && soft_ok && chunk_d(c[0], 4) < theta2 * dist2;
       open = act && !accept;
       cost += accept ? 1 : 0;
       if (accept) {
