@@ -1057,7 +1057,9 @@ __device__ __forceinline__ void leaf_sum(const WalkParams &wp, int32_t s, int32_
 // 8 the 64-VGPR budget spilled to scratch inside the accept path and parked
 // ~30 SGPRs in VGPR lanes — 110 v_readlane; at 7: 88 SGPRs, 65 VGPRs, no
 // scratch, 20 v_readlane, walk 44.5 -> 44.2 ms same-box A/B).
-template <int P, int WANT, bool SOFT, bool RAW>
+// LCOST: per-lane interaction counts are wanted (cost kind 0 with a cost
+// array); otherwise their per-step VALU updates are compiled out
+template <int P, int WANT, bool SOFT, bool RAW, bool LCOST = true>
 __global__ void __launch_bounds__(WALK_TPB)
     __attribute__((amdgpu_waves_per_eu((P <= 3 && !SOFT) ? 7 : 1, 7)))
     walk_kernel(WalkParams wp) {
@@ -1145,7 +1147,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       }
       const bool accept = act && soft_ok && chunk_d(c[0], 4) < theta2 * dist2;
       open = act && !accept;
-      cost += accept ? 1 : 0;
+      if (LCOST) cost += accept ? 1 : 0;
       if (accept) {
         if constexpr (P == 0) {  // monopole without multipoles (tree.rs:1126-1129, 1284-1291)
           const double y = rsq_walk<RAW>(dist2 + kR2Tiny);
@@ -1225,7 +1227,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       leaf_active += na;
       n_pp += (unsigned long long)na * (unsigned long long)(e - s);
       if (act) {
-        cost += e - s;
+        if (LCOST) cost += e - s;
 #ifndef PBX_DIAG_SKIP_LEAF  // timing diagnostic: leaves visited, pairs not evaluated
         // only a target's own leaf needs the self-pair mask (an int compare
         // and four selects per pair): every other leaf takes the plain loop
@@ -2192,14 +2194,19 @@ static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
     grid = (grid + round - 1) / round * round;
   }
   const bool raw = !precise_mode();
+  const bool lcost = wp.cost && !wp.cost_kind;  // per-lane counts wanted
   if (soft && raw)
     hipLaunchKernelGGL((walk_kernel<P, WANT, true, true>), dim3(grid), dim3(tpb), 0, st, wp);
   else if (soft)
     hipLaunchKernelGGL((walk_kernel<P, WANT, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
+  else if (raw && lcost)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, true>), dim3(grid), dim3(tpb), 0, st, wp);
   else if (raw)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true>), dim3(grid), dim3(tpb), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
+  else if (lcost)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, true>), dim3(grid), dim3(tpb), 0, st, wp);
   else
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false>), dim3(grid), dim3(tpb), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false>), dim3(grid), dim3(tpb), 0, st, wp);
 }
 
 template <int P>
