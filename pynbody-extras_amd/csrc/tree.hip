@@ -635,6 +635,7 @@ struct PayloadView {
   const double4 *ncen;
   int64_t nn;
   double *walk;
+  const uint8_t *leaf_dfs;  // per DFS id: no children (walk-record flags), or null
 };
 
 // Bottom-up payload pass (tree.rs:866-1067) in two parts:
@@ -656,8 +657,25 @@ struct PayloadView {
 // preorder) leave in record-contiguous pieces.
 constexpr int PL_TPB = 256;
 
+// Walk-record flags: bits of the record's leaf-count word (dword 15) saying
+// whether the node the wave steps to next — `next`, or `first` when some
+// lane opens — is a leaf.  A leaf step reads only the record's first
+// 64-byte chunk, so the walk then issues one scalar load for it instead of
+// the record's NCH.  The flags come from the structure (no children), known
+// before any payload: an empty internal node (walked as a leaf) is simply
+// not flagged and loads its whole record.
+constexpr uint32_t WF_NEXT_LEAF = 1u << 30, WF_FIRST_LEAF = 1u << 29;
+constexpr uint32_t WF_COUNT = WF_FIRST_LEAF - 1u;
+
+// leaf_dfs[pre[k]] = node k has no children
+__global__ void leaf_dfs_kernel(const int32_t *__restrict__ nchild, const int32_t *__restrict__ pre,
+                                int64_t nn, uint8_t *__restrict__ leaf_dfs) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nn) leaf_dfs[pre[k]] = nchild[k] == 0 ? 1 : 0;
+}
+
 // the node's walk record: [cx cy cz mass | size2 hmax | next first |
-// leaf_start count] and the evaluation coefficients
+// leaf_start count + flags] and the evaluation coefficients
 template <int P>
 __device__ __forceinline__ void walk_record(const PayloadView &v, int32_t k, int32_t pk, int32_t nc,
                                             double cx, double cy, double cz, double mass, double hm,
@@ -686,6 +704,10 @@ __device__ __forceinline__ void walk_record(const PayloadView &v, int32_t k, int
     ir[1] = -1;
     ir[2] = 0;
     ir[3] = 0;
+  }
+  if (v.leaf_dfs) {
+    if (ir[0] >= 0 && v.leaf_dfs[ir[0]]) ir[3] |= (int32_t)WF_NEXT_LEAF;
+    if (ir[1] >= 0 && v.leaf_dfs[ir[1]]) ir[3] |= (int32_t)WF_FIRST_LEAF;
   }
   r[6] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[0] | ((uint64_t)(uint32_t)ir[1] << 32));
   r[7] = __builtin_bit_cast(double, (uint64_t)(uint32_t)ir[2] | ((uint64_t)(uint32_t)ir[3] << 32));
@@ -994,6 +1016,35 @@ __device__ __forceinline__ void load_chunks(const double *ptr, u32x16 (&c)[NCH])
   }
 }
 
+// load_chunks for a walk step: the chunks past the first only when the
+// node is not known to be a leaf (leaf = 1).  One asm block with its own
+// branch, so the chunk registers are the same on both paths (as two C++
+// paths the chunks became phis of undefined values: ~200 SGPR spills)
+template <int NCH>
+__device__ __forceinline__ void load_chunks_node(const double *ptr, u32x16 (&c)[NCH], uint32_t leaf) {
+  if constexpr (NCH == 1) {
+    load_chunks<1>(ptr, c);
+  } else {
+    const uint64_t a = (uint64_t)ptr;
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const double *base = (const double *)(((uint64_t)hi << 32) | (uint64_t)lo);
+    const uint32_t lf = (uint32_t)__builtin_amdgcn_readfirstlane((int)leaf);
+    if constexpr (NCH == 2) {
+      asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_bitcmp1_b32 %3, 0\n\t"
+                   "s_cbranch_scc1 1f\n\ts_load_dwordx16 %1, %2, 0x40\n1:\n\t"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=&s"(c[0]), "=&s"(c[1]) : "s"(base), "s"(lf) : "memory", "scc");
+    } else {
+      static_assert(NCH == 3, "node records are 1-3 chunks");
+      asm volatile("s_load_dwordx16 %0, %3, 0x0\n\ts_bitcmp1_b32 %4, 0\n\t"
+                   "s_cbranch_scc1 1f\n\ts_load_dwordx16 %1, %3, 0x40\n\t"
+                   "s_load_dwordx16 %2, %3, 0x80\n1:\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&s"(c[0]), "=&s"(c[1]), "=&s"(c[2]) : "s"(base), "s"(lf) : "memory", "scc");
+    }
+  }
+}
+
 // one source pair of a leaf (tree.rs:98-417), self pair neutralised
 template <int WANT, bool SOFT, bool RAW>
 __device__ __forceinline__ void leaf_pair(const WalkParams &wp, double sx, double sy, double sz,
@@ -1099,6 +1150,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   unsigned long long n_pp = 0;
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
+  uint32_t wleaf = 0;          // w is a leaf (record flags; the root: unknown)
   uint32_t steps = 0;          // the wave moves strictly forward in DFS order
   uint32_t leaf_rounds = 0;    // 4-record leaf rounds (cost_kind 1)
   // One path through the body, no `continue`: every exit of a divergent
@@ -1118,9 +1170,11 @@ __global__ void __launch_bounds__(WALK_TPB)
     ++steps;
     w = __builtin_amdgcn_readfirstlane(w);  // uniform: keep it (and the address math) scalar
     u32x16 c[NCH];
-    load_chunks<NCH>(wp.walk + (int64_t)w * RS, c);
+    load_chunks_node<NCH>(wp.walk + (int64_t)w * RS, c, wleaf);
     const double mass = chunk_d(c[0], 3);
     const int32_t next = chunk_i(c[0], 12), first = chunk_i(c[0], 13);
+    const uint32_t wflags = (uint32_t)chunk_i(c[0], 15);
+    uint32_t nleaf = wflags & WF_NEXT_LEAF;
     const bool act = (p == w);
     const unsigned na = (unsigned)__popcll(__ballot(act));
     n_active += na;  // SIMD efficiency counter
@@ -1219,9 +1273,10 @@ __global__ void __launch_bounds__(WALK_TPB)
     n_node += na - no;  // active lanes accept or open
     open_steps += no ? 1u : 0u;
     nw = no ? first : next;
+    nleaf = no ? (wflags & WF_FIRST_LEAF) : nleaf;
     }
     if (first < 0) {  // leaf: direct sum in ascending index order
-      const int32_t s = chunk_i(c[0], 14), e = s + chunk_i(c[0], 15);
+      const int32_t s = chunk_i(c[0], 14), e = s + (int32_t)(wflags & WF_COUNT);
       ++leaf_steps;
       leaf_rounds += (uint32_t)(e - s + 3) >> 2;
       leaf_active += na;
@@ -1241,6 +1296,7 @@ __global__ void __launch_bounds__(WALK_TPB)
     }
     p = act ? (open ? first : next) : p;
     w = nw;
+    wleaf = nleaf ? 1u : 0u;
   }
   if (w >= 0 && lane0) atomicOr(wp.fault, 1u);
   if (wp.trace && lane0) {
@@ -1685,7 +1741,7 @@ struct Octree {
   Buf perm, rec, soft_s;     // leaf order
   Buf trace;                 // PBX_WALK_TRACE diagnostic
   Buf nstart, ncount, nfirst, nnext, nchild, ncen, pre, size;
-  Buf com, hmax, mom, coef, walk;
+  Buf com, hmax, mom, coef, walk, leaf_dfs;
   Buf keys, ktmp0, ktmp1, vtmp, hist, tsum, front0, front1, lb, cnt, flags, small, counters;
   Buf bal;                   // cost-balanced ranges: chunk sums + cuts
   Buf iscan, ilist, iws;     // payload: internal-node flags / scan, list, scan state
@@ -1696,7 +1752,7 @@ struct Octree {
   prim::HostBuf rm_pin;      // radial_moments readback staging
   ~Octree() {
     Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
-                   &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &keys, &ktmp0,
+                   &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &leaf_dfs, &keys, &ktmp0,
                    &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
                    &counters, &trace, &bal, &iscan, &ilist, &iws, &bp_fl, &bp_eq, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
                    &bp_p2b};
@@ -2138,6 +2194,14 @@ static void build_payload(Octree &T, hipStream_t st) {
   v.ncen = T.ncen.as<double4>();
   v.nn = T.nn;
   auto walk_buf = [&](int stride) { return (double *)T.walk.get(8 * (size_t)T.nn * stride); };
+  // walk-record leaf flags share the count word: counts stay below WF_FIRST_LEAF
+  v.leaf_dfs = nullptr;
+  if (T.nn > 0 && T.n < (int64_t)WF_FIRST_LEAF) {
+    uint8_t *ld = (uint8_t *)T.leaf_dfs.get((size_t)T.nn);
+    hipLaunchKernelGGL(leaf_dfs_kernel, dim3((unsigned)((T.nn + 255) / 256)), dim3(256), 0, st,
+                       (const int32_t *)v.nchild, v.pre, (int64_t)T.nn, ld);
+    v.leaf_dfs = ld;
+  }
   switch (P) {
     case 0:
     case 1:
