@@ -1150,7 +1150,6 @@ __global__ void __launch_bounds__(WALK_TPB)
   unsigned long long n_pp = 0;
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
-  uint32_t wleaf = 0;          // w is a leaf (record flags; the root: unknown)
   uint32_t steps = 0;          // the wave moves strictly forward in DFS order
   uint32_t leaf_rounds = 0;    // 4-record leaf rounds (cost_kind 1)
   // One path through the body, no `continue`: every exit of a divergent
@@ -1169,6 +1168,9 @@ __global__ void __launch_bounds__(WALK_TPB)
   while (w >= 0 && steps < max_steps) {  // corrupted links: stop instead of hanging
     ++steps;
     w = __builtin_amdgcn_readfirstlane(w);  // uniform: keep it (and the address math) scalar
+    // bit 30 of w: the node is a leaf (walk-record flags; set only below)
+    const uint32_t wleaf = ((uint32_t)w >> 30) & 1u;
+    w &= 0x3fffffff;
     u32x16 c[NCH];
     load_chunks_node<NCH>(wp.walk + (int64_t)w * RS, c, wleaf);
     const double mass = chunk_d(c[0], 3);
@@ -1295,8 +1297,8 @@ __global__ void __launch_bounds__(WALK_TPB)
       }
     }
     p = act ? (open ? first : next) : p;
-    w = nw;
-    wleaf = nleaf ? 1u : 0u;
+    // (nleaf is set only for a real node: nw >= 0)
+    w = nw | (nleaf ? 0x40000000 : 0);
   }
   if (w >= 0 && lane0) atomicOr(wp.fault, 1u);
   if (wp.trace && lane0) {
@@ -2196,7 +2198,7 @@ static void build_payload(Octree &T, hipStream_t st) {
   auto walk_buf = [&](int stride) { return (double *)T.walk.get(8 * (size_t)T.nn * stride); };
   // walk-record leaf flags share the count word: counts stay below WF_FIRST_LEAF
   v.leaf_dfs = nullptr;
-  if (T.nn > 0 && T.n < (int64_t)WF_FIRST_LEAF) {
+  if (T.nn > 0 && T.n < (int64_t)WF_FIRST_LEAF && T.nn < (int64_t)WF_NEXT_LEAF) {
     uint8_t *ld = (uint8_t *)T.leaf_dfs.get((size_t)T.nn);
     hipLaunchKernelGGL(leaf_dfs_kernel, dim3((unsigned)((T.nn + 255) / 256)), dim3(256), 0, st,
                        (const int32_t *)v.nchild, v.pre, (int64_t)T.nn, ld);
