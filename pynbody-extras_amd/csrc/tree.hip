@@ -2235,7 +2235,7 @@ static void build_payload(Octree &T, hipStream_t st) {
 static unsigned walk_xcd_chunk() {
   static const unsigned c = [] {
     const char *v = std::getenv("PBX_WALK_XCD_CHUNK");
-    return v ? (unsigned)std::strtoul(v, nullptr, 10) : 64u;
+    return v ? (unsigned)std::strtoul(v, nullptr, 10) : 128u;
   }();
   return c;
 }
