@@ -435,6 +435,28 @@ int pbx_comm_allreduce_host(void *comm, void *h_buf, int64_t count, int dtype, i
 int pbx_comm_barrier(void *comm);
 int pbx_comm_max_f64(void *comm, double value, double *out);
 
+/* A communicator whose collectives go through a caller-supplied HOST
+ * transport instead of RCCL (no reference counterpart).  Every collective
+ * of the library — the pbx_comm_* calls above and the all-reduces inside
+ * pbx_profile_radial_equaln_comm — stages its device bytes through pinned
+ * host memory (D2H, stream sync), calls `fn`, and copies the result back.
+ * fn(ctx, kind, h_buf, count, dtype, op, counts, displs) returns 0 on
+ * success:
+ *   kind PBX_COLL_ALLREDUCE: reduce `count` elements of `dtype` (codes as
+ *     pbx_comm_allreduce) with `op` over the ranks, in place in h_buf;
+ *   kind PBX_COLL_ALLGATHERV: h_buf holds the whole byte buffer with this
+ *     rank's segment [displs[rank], +counts[rank]) in place; fill in the
+ *     others (count = nranks).
+ * While fn runs, a library call that issued the collective has released
+ * the device lock, so the ranks of one process may be threads sharing one
+ * device (the one-GPU multi-rank tests) — or processes on a host transport
+ * (MPI, shared memory) where RCCL is unavailable. */
+#define PBX_COLL_ALLREDUCE 0
+#define PBX_COLL_ALLGATHERV 1
+typedef int (*pbx_host_collective_fn)(void *ctx, int kind, void *h_buf, int64_t count, int dtype,
+                                      int op, const int64_t *counts, const int64_t *displs);
+int pbx_comm_init_host(void **comm, int nranks, int rank, pbx_host_collective_fn fn, void *ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,7 +9,10 @@
 // All collectives run on the library stream of the calling thread's device.
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <climits>
 #include <cstring>
+#include <vector>
 
 #include "pbx_common.h"
 
@@ -24,6 +27,9 @@ namespace pbx {
 
 struct Comm {
   ncclComm_t nccl = nullptr;
+  // host transport (pbx_comm_init_host) instead of RCCL
+  pbx_host_collective_fn host = nullptr;
+  void *host_ctx = nullptr;
   int nranks = 0;
   int rank = 0;
   int device = -1;
@@ -38,20 +44,81 @@ static size_t dtype_size(int dtype) { return dtype == 3 ? 4 : 8; }
 static const ncclDataType_t kTypes[] = {ncclFloat64, ncclInt64, ncclUint64, ncclUint32};
 static const ncclRedOp_t kOps[] = {ncclSum, ncclMin, ncclMax};
 
-CommRanks comm_ranks(void *comm) {
+static Comm *as_comm(void *comm) {
   Comm *c = (Comm *)comm;
   if (!c) fail(PBX_ERR_VALUE, "null communicator");
-  if (current_device().id != c->device)
-    fail(PBX_ERR_VALUE, "communicator belongs to device %d", c->device);
+  return c;
+}
+
+static Device &comm_device(Comm *c) {
+  Device &d = current_device();
+  if (d.id != c->device) fail(PBX_ERR_VALUE, "communicator belongs to device %d", c->device);
+  return d;
+}
+
+static void check_codes(int dtype, int op) {
+  if (dtype < 0 || dtype > 3) fail(PBX_ERR_VALUE, "bad dtype %d", dtype);
+  if (op < 0 || op > 2) fail(PBX_ERR_VALUE, "bad reduction op %d", op);
+}
+
+// The communicator's pinned host staging, grown on demand (with its HBM twin
+// for pbx_comm_allreduce_host).
+static void *host_stage(Comm *c, size_t bytes) {
+  if (bytes > c->stage_bytes) {
+    if (c->dstage) (void)hipFree(c->dstage);
+    if (c->hstage) (void)hipHostFree(c->hstage);
+    c->dstage = c->hstage = nullptr;
+    c->stage_bytes = 0;
+    const size_t want = bytes < 65536 ? 65536 : bytes;
+    PBX_HIP(hipMalloc(&c->dstage, want));
+    PBX_HIP(hipHostMalloc(&c->hstage, want, hipHostMallocDefault));
+    c->stage_bytes = want;
+  }
+  return c->hstage;
+}
+
+// Call the host transport.  `locked`: the caller holds d.mu (a library
+// pipeline issuing a collective between its kernels); it is released while
+// the transport waits for the other ranks, which may be threads of this
+// process driving the same device.
+static void host_call(Comm *c, Device &d, bool locked, int kind, void *h, int64_t count, int dtype,
+                      int op, const int64_t *counts, const int64_t *displs) {
+  if (locked) d.mu.unlock();
+  const int r = c->host(c->host_ctx, kind, h, count, dtype, op, counts, displs);
+  if (locked) d.mu.lock();
+  if (r != 0) fail(PBX_ERR_RUNTIME, "host collective (kind %d, rank %d of %d) failed: %d", kind,
+                   c->rank, c->nranks, r);
+}
+
+// Device all-reduce through the host transport: D2H, transport, H2D, each
+// step drained (the staging is reused by the next collective).
+static void host_allreduce_dev(Comm *c, Device &d, bool locked, const void *send, void *recv,
+                               int64_t count, int dtype, int op) {
+  const size_t bytes = dtype_size(dtype) * (size_t)count;
+  void *h = host_stage(c, bytes);
+  PBX_HIP(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, d.stream));
+  PBX_HIP(hipStreamSynchronize(d.stream));
+  host_call(c, d, locked, PBX_COLL_ALLREDUCE, h, count, dtype, op, nullptr, nullptr);
+  PBX_HIP(hipMemcpyAsync(recv, h, bytes, hipMemcpyHostToDevice, d.stream));
+  PBX_HIP(hipStreamSynchronize(d.stream));
+}
+
+CommRanks comm_ranks(void *comm) {
+  Comm *c = as_comm(comm);
+  comm_device(c);
   return CommRanks{c->nranks, c->rank};
 }
 
+// (called by library pipelines that hold the device lock)
 void comm_allreduce(void *comm, const void *send, void *recv, int64_t count, int dtype, int op,
                     hipStream_t st) {
-  Comm *c = (Comm *)comm;
-  if (dtype < 0 || dtype > 3) fail(PBX_ERR_VALUE, "bad dtype %d", dtype);
-  if (op < 0 || op > 2) fail(PBX_ERR_VALUE, "bad reduction op %d", op);
+  Comm *c = as_comm(comm);
+  check_codes(dtype, op);
   if (count <= 0) return;
+  if (c->host) {
+    host_allreduce_dev(c, comm_device(c), true, send, recv, count, dtype, op);
+    return;
+  }
   PBX_NCCL(ncclAllReduce(send, recv, (size_t)count, kTypes[dtype], kOps[op], c->nccl, st));
 }
 
@@ -93,6 +160,22 @@ int pbx_comm_init(void **comm, int nranks, int rank, const unsigned char *uid) {
   });
 }
 
+int pbx_comm_init_host(void **comm, int nranks, int rank, pbx_host_collective_fn fn, void *ctx) {
+  return guard([&] {
+    if (nranks < 1 || rank < 0 || rank >= nranks)
+      fail(PBX_ERR_VALUE, "bad rank %d / nranks %d", rank, nranks);
+    if (!fn) fail(PBX_ERR_VALUE, "null host collective");
+    Device &d = current_device();
+    Comm *c = new Comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = d.id;
+    c->host = fn;
+    c->host_ctx = ctx;
+    *comm = c;
+  });
+}
+
 int pbx_comm_destroy(void *comm) {
   return guard([&] {
     Comm *c = (Comm *)comm;
@@ -109,11 +192,28 @@ int pbx_comm_destroy(void *comm) {
 // already in place.  Afterwards every rank holds all segments.
 int pbx_comm_allgatherv(void *comm, void *d_buf, const int64_t *counts, const int64_t *displs) {
   return guard([&] {
-    Comm *c = (Comm *)comm;
-    if (!c) fail(PBX_ERR_VALUE, "null communicator");
-    Device &d = current_device();
-    if (d.id != c->device) fail(PBX_ERR_VALUE, "communicator belongs to device %d", c->device);
+    Comm *c = as_comm(comm);
+    Device &d = comm_device(c);
     char *base = (char *)d_buf;
+    if (c->host) {  // the whole span through host staging
+      int64_t lo = INT64_MAX, hi = 0;
+      for (int r = 0; r < c->nranks; ++r) {
+        if (counts[r] < 0 || displs[r] < 0) fail(PBX_ERR_VALUE, "negative segment");
+        if (counts[r] == 0) continue;
+        lo = std::min(lo, displs[r]);
+        hi = std::max(hi, displs[r] + counts[r]);
+      }
+      if (hi == 0) return;
+      std::vector<int64_t> dl(displs, displs + c->nranks);
+      for (auto &v : dl) v -= lo;
+      char *h = (char *)host_stage(c, (size_t)(hi - lo));
+      PBX_HIP(hipMemcpyAsync(h, base + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, d.stream));
+      PBX_HIP(hipStreamSynchronize(d.stream));
+      host_call(c, d, false, PBX_COLL_ALLGATHERV, h, c->nranks, 0, 0, counts, dl.data());
+      PBX_HIP(hipMemcpyAsync(base + lo, h, (size_t)(hi - lo), hipMemcpyHostToDevice, d.stream));
+      PBX_HIP(hipStreamSynchronize(d.stream));
+      return;
+    }
     PBX_NCCL(ncclGroupStart());
     for (int r = 0; r < c->nranks; ++r) {
       if (counts[r] <= 0) continue;
@@ -124,22 +224,75 @@ int pbx_comm_allgatherv(void *comm, void *d_buf, const int64_t *counts, const in
   });
 }
 
+// Generic all-reduce on the library stream.  dtype: 0 f64, 1 i64, 2 u64,
+// 3 u32; op: 0 sum, 1 min, 2 max (e.g. the u32 digit histograms and the u64
+// key range of the distributed equaln).
+static void allreduce_dev(void *comm, const void *d_send, void *d_recv, int64_t count, int dtype,
+                          int op) {
+  Comm *c = as_comm(comm);
+  check_codes(dtype, op);
+  if (count < 0) fail(PBX_ERR_VALUE, "negative count");
+  Device &d = comm_device(c);
+  if (c->host) {
+    if (count) host_allreduce_dev(c, d, false, d_send, d_recv, count, dtype, op);
+    return;
+  }
+  PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, kTypes[dtype], kOps[op], c->nccl, d.stream));
+}
+
+int pbx_comm_allreduce(void *comm, const void *d_send, void *d_recv, int64_t count, int dtype,
+                       int op) {
+  return guard([&] { allreduce_dev(comm, d_send, d_recv, count, dtype, op); });
+}
+
 int pbx_comm_allreduce_f64(void *comm, const double *d_send, double *d_recv, int64_t count) {
-  return guard([&] {
-    Comm *c = (Comm *)comm;
-    if (!c) fail(PBX_ERR_VALUE, "null communicator");
-    Device &d = current_device();
-    PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, ncclFloat64, ncclSum, c->nccl, d.stream));
-  });
+  return guard([&] { allreduce_dev(comm, d_send, d_recv, count, 0, 0); });
+}
+
+int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv, int64_t count) {
+  return guard([&] { allreduce_dev(comm, d_send, d_recv, count, 1, 0); });
+}
+
+// All-reduce of a small host array in place (dtype / op as above): one H2D,
+// the collective and one D2H on the library stream through the
+// communicator's persistent staging, one stream sync (host transport: the
+// transport on the caller's array).
+static void allreduce_host(Comm *c, void *h_buf, int64_t count, int dtype, int op) {
+  check_codes(dtype, op);
+  if (count < 0) fail(PBX_ERR_VALUE, "negative count");
+  Device &d = comm_device(c);
+  const size_t bytes = dtype_size(dtype) * (size_t)count;
+  if (bytes == 0) return;
+  if (c->host) {
+    host_call(c, d, false, PBX_COLL_ALLREDUCE, h_buf, count, dtype, op, nullptr, nullptr);
+    return;
+  }
+  host_stage(c, bytes);
+  std::memcpy(c->hstage, h_buf, bytes);
+  PBX_HIP(hipMemcpyAsync(c->dstage, c->hstage, bytes, hipMemcpyHostToDevice, d.stream));
+  PBX_NCCL(ncclAllReduce(c->dstage, c->dstage, (size_t)count, kTypes[dtype], kOps[op], c->nccl,
+                         d.stream));
+  PBX_HIP(hipMemcpyAsync(c->hstage, c->dstage, bytes, hipMemcpyDeviceToHost, d.stream));
+  PBX_HIP(hipStreamSynchronize(d.stream));
+  std::memcpy(h_buf, c->hstage, bytes);
+}
+
+int pbx_comm_allreduce_host(void *comm, void *h_buf, int64_t count, int dtype, int op) {
+  return guard([&] { allreduce_host(as_comm(comm), h_buf, count, dtype, op); });
 }
 
 // Control-plane helpers on the data-plane communicator: a device barrier
 // (1-element all-reduce + stream sync) and max-over-ranks of a host scalar.
 int pbx_comm_barrier(void *comm) {
   return guard([&] {
-    Comm *c = (Comm *)comm;
-    if (!c) fail(PBX_ERR_VALUE, "null communicator");
-    Device &d = current_device();
+    Comm *c = as_comm(comm);
+    Device &d = comm_device(c);
+    if (c->host) {
+      PBX_HIP(hipStreamSynchronize(d.stream));
+      int64_t one = 1;
+      allreduce_host(c, &one, 1, 1, 0);
+      return;
+    }
     int64_t *buf = (int64_t *)d.slot(kSlotComm).ensure(64);
     PBX_NCCL(ncclAllReduce(buf, buf, 1, ncclInt64, ncclSum, c->nccl, d.stream));
     PBX_HIP(hipStreamSynchronize(d.stream));
@@ -148,77 +301,19 @@ int pbx_comm_barrier(void *comm) {
 
 int pbx_comm_max_f64(void *comm, double value, double *out) {
   return guard([&] {
-    Comm *c = (Comm *)comm;
-    if (!c) fail(PBX_ERR_VALUE, "null communicator");
-    Device &d = current_device();
+    Comm *c = as_comm(comm);
+    Device &d = comm_device(c);
+    if (c->host) {
+      double v = value;
+      allreduce_host(c, &v, 1, 0, 2);
+      *out = v;
+      return;
+    }
     double *buf = (double *)d.slot(kSlotComm).ensure(64);
     PBX_HIP(hipMemcpyAsync(buf, &value, sizeof(double), hipMemcpyHostToDevice, d.stream));
     PBX_NCCL(ncclAllReduce(buf, buf, 1, ncclFloat64, ncclMax, c->nccl, d.stream));
     PBX_HIP(hipMemcpyAsync(out, buf, sizeof(double), hipMemcpyDeviceToHost, d.stream));
     PBX_HIP(hipStreamSynchronize(d.stream));
-  });
-}
-
-int pbx_comm_allreduce_i64(void *comm, const int64_t *d_send, int64_t *d_recv, int64_t count) {
-  return guard([&] {
-    Comm *c = (Comm *)comm;
-    if (!c) fail(PBX_ERR_VALUE, "null communicator");
-    Device &d = current_device();
-    PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, ncclInt64, ncclSum, c->nccl, d.stream));
-  });
-}
-
-// Generic all-reduce on the library stream.  dtype: 0 f64, 1 i64, 2 u64,
-// 3 u32; op: 0 sum, 1 min, 2 max (e.g. the u32 digit histograms and the u64
-// key range of the distributed equaln).
-int pbx_comm_allreduce(void *comm, const void *d_send, void *d_recv, int64_t count, int dtype,
-                       int op) {
-  return guard([&] {
-    Comm *c = (Comm *)comm;
-    if (!c) fail(PBX_ERR_VALUE, "null communicator");
-    static const ncclDataType_t types[] = {ncclFloat64, ncclInt64, ncclUint64, ncclUint32};
-    static const ncclRedOp_t ops[] = {ncclSum, ncclMin, ncclMax};
-    if (dtype < 0 || dtype > 3) fail(PBX_ERR_VALUE, "bad dtype %d", dtype);
-    if (op < 0 || op > 2) fail(PBX_ERR_VALUE, "bad reduction op %d", op);
-    Device &d = current_device();
-    PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, types[dtype], ops[op], c->nccl,
-                           d.stream));
-  });
-}
-
-// All-reduce of a small host array in place (dtype / op as above): one H2D,
-// the collective and one D2H on the library stream through the
-// communicator's persistent staging, one stream sync.
-int pbx_comm_allreduce_host(void *comm, void *h_buf, int64_t count, int dtype, int op) {
-  return guard([&] {
-    Comm *c = (Comm *)comm;
-    if (!c) fail(PBX_ERR_VALUE, "null communicator");
-    static const ncclDataType_t types[] = {ncclFloat64, ncclInt64, ncclUint64, ncclUint32};
-    static const ncclRedOp_t ops[] = {ncclSum, ncclMin, ncclMax};
-    if (dtype < 0 || dtype > 3) fail(PBX_ERR_VALUE, "bad dtype %d", dtype);
-    if (op < 0 || op > 2) fail(PBX_ERR_VALUE, "bad reduction op %d", op);
-    if (count < 0) fail(PBX_ERR_VALUE, "negative count");
-    Device &d = current_device();
-    if (d.id != c->device) fail(PBX_ERR_VALUE, "communicator belongs to device %d", c->device);
-    const size_t bytes = dtype_size(dtype) * (size_t)count;
-    if (bytes == 0) return;
-    if (bytes > c->stage_bytes) {
-      if (c->dstage) (void)hipFree(c->dstage);
-      if (c->hstage) (void)hipHostFree(c->hstage);
-      c->dstage = c->hstage = nullptr;
-      c->stage_bytes = 0;
-      const size_t want = bytes < 65536 ? 65536 : bytes;
-      PBX_HIP(hipMalloc(&c->dstage, want));
-      PBX_HIP(hipHostMalloc(&c->hstage, want, hipHostMallocDefault));
-      c->stage_bytes = want;
-    }
-    std::memcpy(c->hstage, h_buf, bytes);
-    PBX_HIP(hipMemcpyAsync(c->dstage, c->hstage, bytes, hipMemcpyHostToDevice, d.stream));
-    PBX_NCCL(ncclAllReduce(c->dstage, c->dstage, (size_t)count, types[dtype], ops[op], c->nccl,
-                           d.stream));
-    PBX_HIP(hipMemcpyAsync(c->hstage, c->dstage, bytes, hipMemcpyDeviceToHost, d.stream));
-    PBX_HIP(hipStreamSynchronize(d.stream));
-    std::memcpy(h_buf, c->hstage, bytes);
   });
 }
 

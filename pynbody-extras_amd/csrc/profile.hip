@@ -1425,6 +1425,14 @@ __global__ void __launch_bounds__(TPB)
   for (int b = threadIdx.x; b < g0; b += TPB) boff[(int64_t)b * MS_MAXQ + g] += before;
 }
 
+// Distributed: this rank's {kept count, look-back failure} for one i64 sum
+// all-reduce, so a selection that failed on ANY rank fails on every rank at
+// the same point (before the later collectives), not just on its own.
+__global__ void dist_status(const FusedCtl *__restrict__ ctl, int64_t *__restrict__ out) {
+  out[0] = ctl->n;
+  out[1] = ctl->err & 1;
+}
+
 // keys of the chosen level-0 buckets -> their group's segment (key - base).
 // Same grid and element order as fused_hist0, so block b owns exactly the
 // slots fused_boff gave it; inside the block an LDS counter per group hands
@@ -4941,10 +4949,12 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       int64_t *gsc = nullptr;  // dist: [global kept count][ctl copy]
       uint32_t *lc_all = nullptr;
       if (dist) {
-        gsc = (int64_t *)P.dscal.get(sizeof(int64_t) * 2 + sizeof(FusedCtl));
+        gsc = (int64_t *)P.dscal.get(sizeof(int64_t) * 4 + sizeof(FusedCtl));
         lc_all = (uint32_t *)P.dlc.get(sizeof(uint32_t) * (size_t)cr.nranks * MS_MAXQ);
         PBX_HIP(hipMemsetAsync(lc_all, 0, sizeof(uint32_t) * (size_t)cr.nranks * MS_MAXQ, st));
-        comm_allreduce(comm, &ctl->n, gsc, 1, 1, 0, st);
+        // [global kept count, ranks whose look-back failed]
+        hipLaunchKernelGGL(dist_status, dim3(1), dim3(1), 0, st, (const FusedCtl *)ctl, gsc + 2);
+        comm_allreduce(comm, gsc + 2, gsc, 2, 1, 0, st);
         comm_allreduce(comm, H, H, MS0_DIG, 3, 0, st);
       }
       MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
@@ -4967,9 +4977,12 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         FusedCtl *hc = (FusedCtl *)P.pin.get(sizeof(FusedCtl) + 16);
         int64_t *hn = (int64_t *)(hc + 1);
         PBX_HIP(hipMemcpyAsync(hc, ctl, sizeof(FusedCtl), hipMemcpyDeviceToHost, st));
-        PBX_HIP(hipMemcpyAsync(hn, gsc, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        PBX_HIP(hipMemcpyAsync(hn, gsc, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
         PBX_HIP(hipStreamSynchronize(st));
-        n_global = *hn;
+        n_global = hn[0];
+        if (hn[1])  // (every rank sees the same sum: all fail here, no rank left in a collective)
+          fail(PBX_ERR_RUNTIME, "selection look-back did not complete (%lld of %d ranks)",
+               (long long)hn[1], cr.nranks);
         seg_total = (hc->err & 2) ? 0 : hc->total;
         if (n_global >= (int64_t)1 << 32)  // (every rank sees the same count: all fail here)
           fail(PBX_ERR_VALUE, "distributed equaln over %lld particles: the u32 digit "
@@ -5201,7 +5214,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       if (dist) {
         PBX_HIP(hipMemcpyAsync(&sv_local, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
         PBX_HIP(hipStreamSynchronize(st));
-        int64_t *gc = (int64_t *)P.dscal.get(sizeof(int64_t) * 2 + sizeof(FusedCtl));
+        int64_t *gc = (int64_t *)P.dscal.get(sizeof(int64_t) * 4 + sizeof(FusedCtl));
         PBX_HIP(hipMemcpyAsync(gc, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
         comm_allreduce(comm, gc, gc, 1, 1, 0, st);
         comm_allreduce(comm, accs, accs, (int64_t)n_stats * NMOM, 0, 0, st);

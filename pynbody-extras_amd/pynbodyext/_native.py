@@ -37,6 +37,12 @@ _lib: ctypes.CDLL | None = None
 _dp = POINTER(c_double)
 _i64p = POINTER(c_int64)
 
+# pbx_host_collective_fn (include/pbx.h, pbx_comm_init_host)
+HOST_COLLECTIVE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
+                                      _i64p, _i64p)
+COLL_ALLREDUCE = 0
+COLL_ALLGATHERV = 1
+
 
 class NativeLibraryMissing(ImportError):
     """libpbx.so has not been built (run ``__graft_entry__.build()``)."""
@@ -158,6 +164,7 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_profile_msel_edges": (c_int, [c_void_p, _dp, POINTER(c_int64)]),
     "pbx_comm_barrier": (c_int, [c_void_p]),
     "pbx_comm_max_f64": (c_int, [c_void_p, c_double, POINTER(c_double)]),
+    "pbx_comm_init_host": (c_int, [POINTER(c_void_p), c_int, c_int, HOST_COLLECTIVE_FN, c_void_p]),
 }
 
 

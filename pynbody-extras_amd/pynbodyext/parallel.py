@@ -111,6 +111,143 @@ class Communicator:
         self.handle = c_void_p()
 
 
+_NP_DTYPES = (np.float64, np.int64, np.uint64, np.uint32)  # pbx_comm_allreduce dtype codes
+
+
+class HostCommunicator(Communicator):
+    """A communicator whose collectives run over a HOST transport instead of
+    RCCL (pbx_comm_init_host): the library stages every collective's device
+    bytes through pinned memory and calls ``transport``, an object with
+
+    * ``allreduce(a: np.ndarray, op: int)`` — reduce ``a`` over the ranks in
+      place (OP_SUM / OP_MIN / OP_MAX);
+    * ``allgatherv(buf: np.ndarray[uint8], counts, displs)`` — fill in the
+      other ranks' byte segments of ``buf`` (this rank's is in place).
+
+    Every library path that takes a communicator (ShardedDirect, ShardedTree,
+    ShardedProfile, the one-call distributed profile) runs over it unchanged;
+    :class:`ThreadLoopback` is the transport for several ranks as threads of
+    one process on one GPU."""
+
+    def __init__(self, nranks: int, rank: int, transport):
+        self.nranks, self.rank = int(nranks), int(rank)
+        self.transport = transport
+
+        def fn(_ctx, kind, buf, count, dtype, op, counts, displs):
+            try:
+                if kind == nat.COLL_ALLREDUCE:
+                    dt = np.dtype(_NP_DTYPES[dtype])
+                    a = np.ctypeslib.as_array(
+                        (ctypes.c_uint8 * (int(count) * dt.itemsize)).from_address(buf)).view(dt)
+                    transport.allreduce(a, int(op))
+                elif kind == nat.COLL_ALLGATHERV:
+                    c = [int(counts[r]) for r in range(self.nranks)]
+                    d = [int(displs[r]) for r in range(self.nranks)]
+                    size = max((d[r] + c[r] for r in range(self.nranks) if c[r]), default=0)
+                    b = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(buf))
+                    transport.allgatherv(b, c, d)
+                else:
+                    return 2
+                return 0
+            except BaseException as e:  # noqa: BLE001 - reported as a status to C
+                self.error = e
+                abort = getattr(transport, "abort", None)
+                if abort is not None:
+                    abort()
+                return 1
+
+        self.error = None
+        self._fn = nat.HOST_COLLECTIVE_FN(fn)  # kept alive as long as the handle
+        h = c_void_p()
+        nat.call("pbx_comm_init_host", ctypes.byref(h), self.nranks, self.rank, self._fn, None)
+        self.handle = h
+
+
+class ThreadLoopback:
+    """Host transport for ``world`` ranks that are threads of ONE process
+    sharing one device: what a multi-GPU job does, on one GPU (the library
+    releases its device lock while a rank waits in a collective).  Sums are
+    taken in rank order; a rank that fails aborts the group so no rank waits
+    forever.  ``run(fn)`` calls ``fn(comm)`` on one thread per rank and
+    returns the per-rank results (re-raising the first failure)."""
+
+    def __init__(self, world: int, timeout: float = 120.0):
+        import threading
+
+        self.world = int(world)
+        self._barrier = threading.Barrier(self.world, timeout=timeout)
+        self._slots = [None] * self.world
+        self._rank = threading.local()
+
+    def abort(self) -> None:
+        self._barrier.abort()
+
+    def _exchange(self, item):
+        self._slots[self._rank.value] = item
+        self._barrier.wait()
+        return list(self._slots)
+
+    def allreduce(self, a: np.ndarray, op: int) -> None:
+        parts = self._exchange(a.copy())
+        if len({(p.shape, p.dtype.str) for p in parts}) > 1:
+            raise RuntimeError("all-reduce of different sizes / types across ranks: "
+                               f"{[(p.shape, p.dtype.str) for p in parts]}")
+        if op == OP_SUM:
+            acc = parts[0].copy()
+            for p in parts[1:]:
+                acc += p  # rank order (u32: wraps like the RCCL sum)
+        elif op == OP_MIN:
+            acc = np.minimum.reduce(parts)
+        else:
+            acc = np.maximum.reduce(parts)
+        self._barrier.wait()  # every rank read the slots before any overwrites them
+        a[...] = acc
+
+    def allgatherv(self, buf: np.ndarray, counts, displs) -> None:
+        r = self._rank.value
+        mine = buf[displs[r]:displs[r] + counts[r]].copy()
+        parts = self._exchange((list(counts), list(displs), mine))
+        if any(p[0] != parts[0][0] or p[1] != parts[0][1] for p in parts):
+            raise RuntimeError("all-gather-v with different segment tables across ranks")
+        self._barrier.wait()
+        for q, (_, _, seg) in enumerate(parts):
+            if q != r and counts[q]:
+                buf[displs[q]:displs[q] + counts[q]] = seg
+
+    def run(self, fn):
+        """fn(comm) on one thread per rank; returns [result of rank r]."""
+        import threading
+
+        out = [None] * self.world
+        errs = [None] * self.world
+
+        def body(r):
+            self._rank.value = r
+            comm = None
+            try:
+                comm = HostCommunicator(self.world, r, self)
+                out[r] = fn(comm)
+            except BaseException as e:  # noqa: BLE001
+                errs[r] = (comm.error if comm is not None else None) or e
+                self.abort()
+            finally:
+                if comm is not None:
+                    comm.destroy()
+
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(self.world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for e in errs:
+            if e is not None and not isinstance(e, threading.BrokenBarrierError):
+                raise e
+        for e in errs:
+            if e is not None:
+                raise e
+        return out
+
+
 class FileRendezvous:
     """Out-of-band exchange of the RCCL unique id between the ranks of ONE
     node, through a file in a local directory.

@@ -1,11 +1,13 @@
 """N>1 host logic on CPU: world_size-2 gloo processes.
 
-Covers the multi-GPU bookkeeping of pynbodyext.parallel (balanced
-contiguous shards, all-gather-v of the 32-byte source records with uneven
-shards, self-skip offsets of the sharded solve) and the bench control plane
-(barrier, max over ranks).  The device all-gather itself is RCCL on the GPU
-box; here the same record layout is gathered with gloo and each rank's
-targets are solved by the oracle, then compared with the unsharded oracle.
+Runs the host logic of pynbodyext.parallel.ShardedDirect / ShardedTree
+unchanged in 2 gloo processes: balanced contiguous shards, the all-gather-v
+of the 32-byte source records with uneven shards, self-skip offsets, the
+weight-split symmetric triangle + accumulator all-reduce, cost-balanced
+tree ranges with the cost all-gather, the profile all-reduce.  The device
+layer is replaced by oracle stand-ins and the collectives by gloo
+(tests/_mock_device.py); the real kernels over real collectives at world
+2-4 are tests/test_gpu_multirank.py (ranks as threads on one GPU).
 """
 import os
 import socket
@@ -39,42 +41,42 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, q):
-    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd")]
+def _worker(rank, world, port, n, symmetric, q):
+    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd"), str(ROOT / "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
 
-    from oracle import gravity as og
-    from pynbodyext.parallel import all_shards, shard_bounds
+    import _mock_device as md
+    from pynbodyext import parallel
     from pynbodyext.synthetic import plummer
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        parallel.nat = md.make_nat()      # device layer -> numpy / oracle stand-ins
+        comm = md.GlooHostComm(dist, torch)
         pos, mass = plummer(n, seed=77)
-        lo, hi = shard_bounds(n, world, rank)
-        # pack the local shard exactly like pbx_pack_sources: {x, y, z, m}
-        rec_local = np.concatenate([pos[lo:hi], mass[lo:hi, None]], axis=1)
-        shards = all_shards(n, world)
-        maxn = max(h - l for l, h in shards)
-        buf = torch.zeros((maxn, 4), dtype=torch.float64)
-        buf[: hi - lo] = torch.from_numpy(rec_local)
-        parts = [torch.zeros_like(buf) for _ in range(world)]
-        dist.all_gather(parts, buf)
-        rec = np.concatenate([parts[r][: h - l].numpy() for r, (l, h) in enumerate(shards)])
+        lo, hi = parallel.shard_bounds(n, world, rank)
+        # ShardedDirect's own host logic: shards, record all-gather-v, the
+        # weight-balanced unit ranges + accumulator all-reduce, finish
+        s = parallel.ShardedDirect(comm, n, pos[lo:hi], mass[lo:hi], symmetric=symmetric)
+        s.step()
+        rec = md.view(s.d_rec.ptr, 32 * n, np.float64).reshape(n, 4)
         assert np.array_equal(rec[:, :3], pos) and np.array_equal(rec[:, 3], mass)
-        # this rank's targets against all sources, self-skip at global index lo + t
-        pot, acc = og.direct_subset(np.ascontiguousarray(rec[:, :3]), np.ascontiguousarray(rec[:, 3]),
-                                    np.arange(lo, hi))
+        pot, acc = s.results()
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.barrier()
-        q.put((rank, lo, hi, pot, acc, float(t.item())))
+        q.put((rank, lo, hi, pot, acc, float(t.item()), s.units if symmetric else None))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_direct_world2_matches_unsharded():
+@pytest.mark.parametrize("symmetric", [False, True])
+def test_sharded_direct_world2_matches_unsharded(symmetric):
+    """ShardedDirect (pynbodyext.parallel) over 2 gloo ranks with uneven
+    shards: its host logic unchanged, the device calls replaced by the oracle
+    (tests/_mock_device.py), the collectives by gloo = the unsharded oracle."""
     import multiprocessing as mp
 
     from oracle import gravity as og
@@ -84,7 +86,8 @@ def test_sharded_direct_world2_matches_unsharded():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, symmetric, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -94,10 +97,18 @@ def test_sharded_direct_world2_matches_unsharded():
     pos, mass = plummer(n, seed=77)
     pot_ref = og.direct_potentials(pos, mass)
     acc_ref = og.direct_accelerations(pos, mass)
-    for rank, lo, hi, pot, acc, tmax in res:
+    res.sort(key=lambda r: r[0])
+    if symmetric:  # the two ranks' unit ranges tile the triangle
+        assert res[0][6][0] == 0 and res[0][6][1] == res[1][6][0]
+        assert res[1][6][1] == (n + 63) // 64
+    for rank, lo, hi, pot, acc, tmax, _ in res:
         assert tmax == float(world)
-        np.testing.assert_array_equal(pot, pot_ref[lo:hi])
-        np.testing.assert_array_equal(acc, acc_ref[lo:hi])
+        if symmetric:  # every unordered pair once, summed in another order
+            np.testing.assert_allclose(pot, pot_ref[lo:hi], rtol=1e-12)
+            np.testing.assert_allclose(acc, acc_ref[lo:hi], rtol=1e-9, atol=1e-12)
+        else:
+            np.testing.assert_array_equal(pot, pot_ref[lo:hi])
+            np.testing.assert_array_equal(acc, acc_ref[lo:hi])
 
 
 def _rdzv_worker(rank, world, d, q):
@@ -142,44 +153,45 @@ def test_balanced_ranges():
 
 
 def _tree_worker(rank, world, port, n, q):
-    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd")]
+    sys.path[:0] = [str(ROOT), str(ROOT / "pynbody-extras_amd"), str(ROOT / "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
 
-    from oracle import tree as ot
-    from pynbodyext.parallel import balanced_ranges
+    import _mock_device as md
+    from pynbodyext import _engine, parallel
     from pynbodyext.synthetic import plummer
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        parallel.nat = md.make_nat()
+        _engine.Octree = md.MockOctree        # the oracle tree behind the Octree surface
+        comm = md.GlooHostComm(dist, torch)
         pos, mass = plummer(n, seed=91)
-        ref = ot.RefOctree(pos, mass, 8, 3)       # every rank builds the tree
-        e = ref.export()
-        order = e["perm"]                          # leaf order -> original index
-        # costs of a first walk, then this rank's balanced leaf-order range
-        _, _, nn, npp = ref.compute_subset(order, 0.5)
-        first, count = balanced_ranges(nn + npp, world)[rank]
-        idx = order[first:first + count]
-        pot, _, _, _ = ref.compute_subset(idx, 0.5)
-        r = np.sqrt((pos[idx] ** 2).sum(1))
+        d_pos, d_mass = md.DeviceArray.from_host(pos), md.DeviceArray.from_host(mass)
         edges = np.logspace(np.log10(0.01), np.log10(50.0), 33)
-        b = np.searchsorted(edges, r, side="left") - 1
-        ok = (b >= 0) & (b < 32)
-        part = np.zeros((32, 2))
-        np.add.at(part[:, 0], b[ok], mass[idx][ok])
-        np.add.at(part[:, 1], b[ok], mass[idx][ok] * pot[ok])
-        t = torch.from_numpy(part)
-        dist.all_reduce(t)                         # RCCL all-reduce on the GPU box
-        q.put((rank, first, count, t.numpy().copy()))
+        s = parallel.ShardedTree(comm, n, d_pos, d_mass, 8, 3, 0.5)
+        steps = []
+        for _ in range(2):  # step 2 balances on step 1's all-gathered costs
+            mom = s.step(None, edges)
+            first, count = s.ranges[rank]
+            pot = md.view(s.d_pot.ptr, 8 * count, np.float64).copy()
+            steps.append((list(s.ranges), s.tree.perm[first:first + count].copy(), pot, mom))
+        q.put((rank, steps))
     finally:
         dist.destroy_process_group()
 
 
 def test_sharded_tree_world2_profile_matches_unsharded():
+    """ShardedTree (pynbodyext.parallel) over 2 gloo ranks, two steps: its
+    host logic unchanged (ranges, cost all-gather-v -> original order ->
+    balance, profile all-reduce), the tree = oracle/tree_ref.c behind the
+    Octree surface (tests/_mock_device.py).  Every target's potential equals
+    the unsharded oracle walk's, the all-reduced profile the unsharded one."""
     import multiprocessing as mp
 
     from oracle import tree as ot
+    from pynbodyext.parallel import all_shards
     from pynbodyext.synthetic import plummer
 
     n, world = 3000, 2
@@ -189,23 +201,30 @@ def test_sharded_tree_world2_profile_matches_unsharded():
     procs = [ctx.Process(target=_tree_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = dict(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
-    assert res[0][1] == 0 and res[0][2] + res[1][2] == n and res[1][1] == res[0][2]
     pos, mass = plummer(n, seed=91)
-    pot = ot.RefOctree(pos, mass, 8, 3).compute_potentials(0.5)
-    r = np.sqrt((pos ** 2).sum(1))
+    pot_ref = ot.RefOctree(pos, mass, 8, 3).compute_potentials(0.5)
+    r = np.sqrt((pos[:, 0] * pos[:, 0] + pos[:, 1] * pos[:, 1]) + pos[:, 2] * pos[:, 2])
     edges = np.logspace(np.log10(0.01), np.log10(50.0), 33)
     b = np.searchsorted(edges, r, side="left") - 1
     ok = (b >= 0) & (b < 32)
     full = np.zeros((32, 2))
     np.add.at(full[:, 0], b[ok], mass[ok])
-    np.add.at(full[:, 1], b[ok], mass[ok] * pot[ok])
-    for _, _, _, part in res:
-        np.testing.assert_allclose(part, full, rtol=1e-12, atol=1e-15)
+    np.add.at(full[:, 1], b[ok], mass[ok] * pot_ref[ok])
+    for step in range(2):
+        ranges = res[0][step][0]
+        assert res[1][step][0] == ranges
+        assert ranges[0][0] == 0 and sum(c for _, c in ranges) == n
+        pot = np.full(n, np.nan)
+        for rank in range(world):
+            _, idx, p, mom = res[rank][step]
+            pot[idx] = p
+            np.testing.assert_allclose(mom[:, :2], full, rtol=1e-12, atol=1e-15)
+        np.testing.assert_array_equal(pot, pot_ref)
+    assert res[0][1][0] != [(lo, hi - lo) for lo, hi in all_shards(n, world)]
 
 
 def _equaln_worker(rank, world, port, q):
