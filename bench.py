@@ -54,9 +54,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the radial-profile leg (config 3)")
-    ap.add_argument("--profile-sizes", default="1000000,16000000,64000000",
+    ap.add_argument("--profile-sizes", default="1000000,16000000,64000000,256000000",
                     help="comma-separated particle counts of the profile size sweep")
     ap.add_argument("--no-tree", action="store_true", help="skip the Barnes-Hut leg (config 5)")
+    ap.add_argument("--no-api", action="store_true",
+                    help="skip the API-level (host arrays, H2D/D2H inclusive) direct-sum timing")
     ap.add_argument("--tree-n", type=int, default=4_000_000)
     return ap.parse_args()
 
@@ -294,6 +296,27 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                "stream_ms": td * 1e3}
         if dist is None:
             row["path"] = dev.path_stats()  # one-launch / discarded / multi-kernel calls
+            lv = dev.level0_stats()
+            if lv["tiled"]:
+                # the steps above reuse the previous call's level-0 digit
+                # geometry (same snapshot every call); a first call or a new
+                # snapshot re-reads x for its level-0 histogram: time that too
+                row["level0_hinted_calls"] = lv
+                dev.set_level0_hint(False)
+                ct, cd = [], []
+                for _ in range(max(20, steps // 10)):
+                    t0 = time.perf_counter()
+                    e0.record()
+                    step()
+                    e1.record()
+                    nat.synchronize()
+                    ct.append(time.perf_counter() - t0)
+                    cd.append(e0.elapsed_ms(e1))
+                dev.set_level0_hint(True)
+                row["cold_ms"] = float(np.median(ct)) * 1e3
+                row["cold_stream_ms"] = float(np.median(cd))
+                row["cold_note"] = ("level-0 geometry hint off (pbx_profile_set_level0_hint 0): "
+                                    "every call re-reads x, as a first call / new snapshot does")
         out.append(row)
         if cpu and world == 1:
             from oracle import profile_ref as pr
@@ -455,7 +478,8 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
                      "unit": "TFLOP/s", "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
                      "traffic": pmc_traffic("tree")[0], "kernel": "walk_kernel<order 3, pot+acc>",
                      "flop_per_node": TREE_FLOP_NODE, "flop_per_leaf_pair": TREE_FLOP_PP,
-                     "kernel_ms": walk_ms},
+                     "kernel_ms": walk_ms, "mode": "precise" if nat.get_precise() else "fast",
+                     "traffic_source": pmc_traffic("tree")[1]},
         "profile_check": {"bins_nonempty": int(np.sum(mom[:, 0] > 0)),
                           "phi_innermost_bin": float(phi_profile[mom[:, 0] > 0][0]),
                           "phi_outermost_bin": float(phi_profile[mom[:, 0] > 0][-1])},
@@ -486,13 +510,42 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
     return out
 
 
+def bench_api(pos, mass, reps: int = 2) -> dict:
+    """API-level direct sum (BASELINE.md §3 GPU timing rules: "API time
+    includes H2D/D2H"): the reference's host-array entry points
+    pynbodyext._rust.direct_potentials_py / direct_accelerations_py
+    (gravity.rs:448-512, :585-644) on the same 1M particles — upload,
+    kernel, download and host-side checks inside the timed call."""
+    from pynbodyext import _rust
+
+    n = len(pos)
+    _rust.direct_potentials_py(pos, mass)      # warm: device workspace allocated
+    _rust.direct_accelerations_py(pos, mass)
+    tp, ta = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _rust.direct_potentials_py(pos, mass)
+        tp.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        _rust.direct_accelerations_py(pos, mass)
+        ta.append(time.perf_counter() - t0)
+    p, a = float(np.median(tp)), float(np.median(ta))
+    pairs = float(n) * float(n - 1)
+    return {"n": n, "potentials_ms": p * 1e3, "accelerations_ms": a * 1e3,
+            "potentials_pairs_per_s": pairs / p, "accelerations_pairs_per_s": pairs / a,
+            "note": "host numpy arrays in and out (PCIe-inclusive), one call per quantity as the "
+                    "reference API has; the bench's value is the device-resident fused solve"}
+
+
 def pmc_profile_step_bytes(n: int):
-    """HBM bytes of one 64M profile step from the committed PMC summary."""
+    """HBM bytes of one n-particle profile step from the committed PMC
+    summary (profiles/pmc_profile_latest.json, collected at its "n")."""
     f = ROOT / "profiles" / "pmc_profile_latest.json"
-    if n != 64_000_000 or not f.exists():
+    if not f.exists():
         return None
     try:
-        return json.loads(f.read_text()).get("hbm_bytes_per_step")
+        d = json.loads(f.read_text())
+        return d.get("hbm_bytes_per_step") if int(d.get("n", 64_000_000)) == n else None
     except Exception:
         return None
 
@@ -641,6 +694,9 @@ def main():
         sweep = bench_profile(sizes, steps=max(200, args.steps), warmup=max(5, args.warmup),
                               cpu=not args.no_cpu_baseline and rank == 0 and world == 1,
                               dist=dist if dist.comm is not None else None)
+    api = None
+    if world == 1 and not args.no_api:
+        api = bench_api(pos, mass)
     dist.close()
     if rank != 0:
         return
@@ -680,16 +736,31 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_src,
             "kernel": "sym_kernel<pot+acc> (each unordered pair once)" if solver.symmetric else "direct_kernel<Newtonian, pot+acc, self-skip>",
+            "mode": "precise" if nat.get_precise() else "fast",
+            "mode_note": "fast: v_rsq_f64 unrefined (~5e-8 per pair, <= 1e-7 vs the oracle); "
+                         "precise: + one Newton step (pbx_set_precise)",
             "flop_per_pair": FLOP_PER_PAIR,
             "kernel_ms": kern_avg_ms,
             "frac_is": "algorithmic: 22 flop per ORDERED pair delivered (SURVEY.md §8d)",
             **executed_issue(solver.symmetric, pairs_launch, kern_avg_ms),
         },
         "cpu_baseline": cpu,
+        "api_level": api,
     }
     if sweep is not None:
         head = sweep[0]
         big = max(sweep, key=lambda r: r["hbm_gbs_algorithmic_per_gpu"])
+        # counter-based: the PMC run's HBM bytes per step over this run's stream time
+        counter = None
+        for r in sweep:
+            b = pmc_profile_step_bytes(r["n_per_gpu"])
+            if b:
+                gbs = b / (r["stream_ms"] * 1e-3) / 1e9
+                counter = {"n_per_gpu": r["n_per_gpu"], "hbm_bytes_per_step": b,
+                           "achieved_gbs": gbs, "frac_of_spec": gbs / HBM_PEAK_GBS,
+                           "frac_of_measured_copy_6290": gbs / 6290.0,
+                           "source": "profiles/pmc_profile_latest.json (2 x FETCH_SIZE + "
+                                     "WRITE_SIZE of every profile kernel) / this run's stream_ms"}
         out["profile"] = {
             "metric": "particles/sec (RadialProfileBuilder equaln 128, Sphere&FamilyFilter, "
                       "weight=mass)",
@@ -710,6 +781,12 @@ def main():
                          "traffic": pmc_profile_step_bytes(big["n_per_gpu"]),
                          "traffic_note": "HBM bytes per 64M step (all profile kernels, PMC "
                                          "run committed in profiles/pmc_profile_latest.json)"},
+            "counter_roofline": counter,
+            "cold_handle": {"n_per_gpu": big["n_per_gpu"], "stream_ms": big.get("cold_stream_ms"),
+                            "ms": big.get("cold_ms"), "warm_stream_ms": big["stream_ms"],
+                            "frac_cold": (big["n_per_gpu"] * PROFILE_BYTES_PER_PARTICLE /
+                                          (big["cold_stream_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                            if big.get("cold_stream_ms") else None},
             "parity_at_roofline_point": big.get("parity_vs_oracle"),
             "one_launch_discards": (head.get("path") or {}).get("mono_discarded"),
             "sweep": sweep,

@@ -391,6 +391,11 @@ int pbx_profile_path_stats(void *handle, int64_t *out);
  * was counted by the selection kernel with the previous tiled call's digit
  * geometry (every window key inside it), so x was not read a second time}. */
 int pbx_profile_level0_stats(void *handle, int64_t *out);
+/* enabled = 0: this handle's tiled calls never use the previous call's
+ * level-0 digit geometry (every call re-reads x for its level-0 histogram:
+ * the cost of a first call / a new snapshot); 1 (default): use it when it
+ * holds.  Results are identical either way. */
+int pbx_profile_set_level0_hint(void *handle, int enabled);
 /* Per-bin percentiles of the last assignment — replaces the per-bin loop of
  * ProfileArray._compute for Percentile / Median / Abs_pXX
  * (proarray.py:272-334 + :689-722): h_out[bin*nq + k] = np.interp(q[k],

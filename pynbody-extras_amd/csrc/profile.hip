@@ -1084,7 +1084,11 @@ __global__ void __launch_bounds__(SH_BT)
     uint32_t *row = rows16 + (int64_t)blockIdx.x * (MS0_DIG / 2);
     for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) row[i] = lh[i];
   } else if (hint && h.valid && threadIdx.x == 0) {
-    atomicOr(hflag, 1u);  // too many tiles for u16 counts: fall back (not below 2^28 particles)
+    // more than SH_TMAX tiles for this block's u16 counts: fall back to the
+    // re-read.  With SH_K * 255 = 765 select blocks that is a family span
+    // above 765 * 15 * 4096 ~ 47M particles (the 64M bench point's dm span is
+    // 38.4M; its 256M point re-reads x every call)
+    atomicOr(hflag, 1u);
   }
 }
 
@@ -3483,6 +3487,7 @@ struct Profile {
   // tiled multi-kernel calls, of them with the level-0 histogram from
   // select_tiles (the hinted geometry held: no re-read of x)
   int64_t n_tiled_calls = 0, n_hinted = 0;
+  bool hint_off = false;  // pbx_profile_set_level0_hint(handle, 0): every tiled call re-reads x
 };
 
 static void ensure_x(Profile &P, hipStream_t st);
@@ -4338,6 +4343,13 @@ int pbx_profile_level0_stats(void *handle, int64_t *out) {
   });
 }
 
+int pbx_profile_set_level0_hint(void *handle, int enabled) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    P.hint_off = enabled == 0;
+  });
+}
+
 int pbx_profile_path_stats(void *handle, int64_t *out) {
   return guard([&] {
     Profile &P = as_profile(handle);
@@ -4900,7 +4912,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         const char *v = std::getenv("PBX_SEL_HINT");
         return !(v && v[0] == '0');
       }();
-      if (!dist && lazy && hint_env) {
+      if (!dist && lazy && hint_env && !P.hint_off) {
         if (!P.shint.p) {
           P.shint.get(2 * sizeof(SelHint));
           PBX_HIP(hipMemsetAsync(P.shint.p, 0, 2 * sizeof(SelHint), st));

@@ -244,6 +244,13 @@ class DeviceBins:
         nat.call("pbx_profile_level0_stats", self._h, _i64(out))
         return {"tiled": int(out[0]), "hinted": int(out[1])}
 
+    def set_level0_hint(self, enabled: bool) -> None:
+        """False: every tiled radial_equaln call on this handle re-reads x for
+        its level-0 histogram (what a first call or a new snapshot costs);
+        True (default): reuse the previous call's digit geometry when it
+        holds.  Same results either way (pbx_profile_set_level0_hint)."""
+        nat.call("pbx_profile_set_level0_hint", self._h, 1 if enabled else 0)
+
     def selection(self, idx=True, x=True, w=True):
         """(original indices int64, x, weights) of the fused selection."""
         oi = np.empty(self.n, dtype=np.int64) if idx else None

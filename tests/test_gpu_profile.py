@@ -207,12 +207,13 @@ def test_fused_builder_matches_oracle_config3(gpu):
 @pytest.mark.parametrize("n", [8_000_000, 32_000_000])
 def test_fused_config3_large_input_path(gpu, n):
     """Config 3 on the tiled path (>= 1024 selection tiles of the dm span:
-    1,172 tiles at 8M, 4,688 at 32M): the 512-thread lazy selection
-    (select_onepass<512>), fused_hist0 over tile ranges, assign_gather with
-    byte bins and the deferred edge-digit keys (fix_deferred), csr_sel and
-    the counts from the scanned [bin][tile] table — edges, counts and CSR
-    bit-exact against the oracle, sums to 1e-12 (the 1M case above runs
-    the one-launch radial_mono)."""
+    1,172 tiles at 8M, 4,688 at 32M): the persistent tiled selection
+    (select_tiles, x and byte bins in particle-slot layout), fused_hist0
+    fixing the tile offsets (or re-reading x for the level-0 histogram),
+    assign_gather with byte bins and the deferred edge-digit keys
+    (fix_deferred), the [bin][tile] scan, csr_slots and the counts from the
+    scanned table — edges, counts and CSR bit-exact against the oracle, sums
+    to 1e-12 (the 1M case above runs the one-launch radial_mono)."""
     sim = plummer_snapshot(n, seed=1004)
     prof = RadialProfileBuilder(ndim=3, weight="mass", bins_type="equaln", nbins=128).filter(
         Sphere(10.0) & FamilyFilter("dm"))(sim)
@@ -725,6 +726,32 @@ def test_radial_equaln_tiled_level0_hint_transitions(gpu):
                         want = _oracle_col(ref, f, w, col)
                         np.testing.assert_allclose(got[ne, col], want[ne], rtol=1e-12,
                                                    atol=1e-12 * np.nanmax(np.abs(want[ne])))
+    finally:
+        h.close()
+
+
+def test_radial_equaln_level0_hint_switch(gpu):
+    """set_level0_hint(False) (the bench's cold-handle timing): repeated
+    tiled calls on one handle re-read x every time — no call hinted — and
+    return what the hinted calls return (edges, counts, CSR identical)."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W
+
+    rng = np.random.default_rng(35)
+    pos = rng.normal(scale=3.0, size=(4_300_000, 3))
+    mass = rng.uniform(0.5, 1.5, len(pos))
+    stats = [(SRC_W, SRC_NONE, 1 << 3)]
+    h = DeviceBins()
+    try:
+        out = []
+        for enabled in (True, True, False, False, True):
+            h.set_level0_hint(enabled)
+            _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h)
+            out.append((e, c, m[0], *h.csr(), h.level0_stats()["hinted"]))
+        assert [o[5] for o in out] == [0, 1, 1, 1, 2]
+        for o in out[1:]:
+            assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+            assert np.array_equal(o[3], out[0][3]) and np.array_equal(o[4], out[0][4])
+            np.testing.assert_allclose(o[2], out[0][2], rtol=1e-12, atol=1e-300)
     finally:
         h.close()
 
