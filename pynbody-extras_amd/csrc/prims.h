@@ -92,6 +92,41 @@ __device__ __forceinline__ uint64_t peers8(uint32_t d, uint64_t valid) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Stable wave-local ranks from LDS instead of ballots (peers8 costs ~85 VALU
+// per item and made the CSR / radix scatters VALU-bound): for item k every
+// valid lane ORs its lane bit into its digit's 64-bit word of this wave's
+// pmask row (ds_or_b64: OR commutes, the lanes' order inside the instruction
+// does not matter), reads the word back (= its peers), reads the digit's
+// running count run[d], and the group writes count + popcount back and
+// clears the word.  One wave's LDS instructions execute in issue order, so
+// each read sees all of item k's ORs and none of item k + 1's.  Relaxed
+// wavefront-scope atomics keep the accesses as ds_ instructions in program
+// order (volatile ones became FLAT accesses, not ordered against ds_or).
+// lp[k] = the item's rank among the wave's earlier items of its digit;
+// run[d] ends as the wave's count of digit d.  pmask (RADIX words) must be
+// zero on entry and is zero on exit.
+template <int IPT>
+__device__ __forceinline__ void wave_ranks_lds(const uint32_t (&dig)[IPT], const bool (&ok)[IPT],
+                                               uint32_t *run, uint64_t *pmask,
+                                               uint32_t (&lp)[IPT]) {
+  const uint64_t lbit = 1ull << lane_id();
+#pragma unroll
+  for (int k = 0; k < IPT; ++k) {
+    uint32_t l = 0;
+    if (ok[k]) {
+      const uint32_t d = dig[k];
+      __hip_atomic_fetch_or(&pmask[d], lbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint64_t m = __hip_atomic_load(&pmask[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint32_t base = __hip_atomic_load(&run[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __hip_atomic_store(&run[d], base + (uint32_t)__popcll(m), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __hip_atomic_store(&pmask[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      l = base + rank_below(m);
+    }
+    lp[k] = l;
+  }
+}
+
 // bin = searchsorted(edges, x, 'left') - 1, x == e[0] -> 0, then
 // x == e[nb] -> nb-1, invalid (out of range) -> nb (bins.py:368-379).
 // Branchless lower bound over the nb+1 edges: the trip count depends on nb
@@ -336,11 +371,16 @@ __global__ void __launch_bounds__(TPB)
   __shared__ uint32_t dstart[RADIX];  // tile-local start of each digit
   __shared__ uint32_t gofs[RADIX];    // global start of each digit's run of this tile
   __shared__ uint32_t wsum[NWAVE];
-  __shared__ K sk[TILE];
+  __shared__ __attribute__((aligned(16))) K sk[TILE];
   __shared__ int32_t sv[VM == VAL_NONE ? 1 : TILE];
+  static_assert(sizeof(K) * TILE >= sizeof(uint64_t) * NWAVE * RADIX, "pmask fits in sk");
+  uint64_t *pmask = (uint64_t *)sk;  // phase 1 only: [NWAVE][RADIX] peer words
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
-  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) {
+    (&run[0][0])[d] = 0;
+    pmask[d] = 0ull;
+  }
   __syncthreads();
   const int64_t tbase = (int64_t)blockIdx.x * TILE;
   const int64_t wbase = tbase + (int64_t)w * (TILE / NWAVE);
@@ -359,22 +399,15 @@ __global__ void __launch_bounds__(TPB)
   // atomic; a wave's LDS operations execute in issue order, so the 16
   // atomics go out back to back and each returns the count of that digit
   // in the wave's earlier items (no round trip per k).
-  uint32_t ret[IPT];
-  uint64_t pm[IPT];
+  {
+    uint32_t dg[IPT];
+    bool okk[IPT];
 #pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int64_t i = wbase + k * 64 + lane;
-    const bool ok = i < n;
-    const uint32_t d = (uint32_t)(key[k] >> shift) & 255u;
-    const uint64_t m = peers8(d, __ballot(ok));
-    pm[k] = ok ? m : 0ull;
-    ret[k] = (ok && rank_below(m) == 0) ? atomicAdd(&run[w][d], (uint32_t)__popcll(m)) : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < IPT; ++k) {
-    const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
-    const uint32_t before = (uint32_t)__shfl((int)ret[k], leader, 64);
-    lp[k] = before + rank_below(pm[k]);
+    for (int k = 0; k < IPT; ++k) {
+      okk[k] = wbase + k * 64 + lane < n;
+      dg[k] = (uint32_t)(key[k] >> shift) & 255u;
+    }
+    wave_ranks_lds<IPT>(dg, okk, &run[w][0], pmask + w * RADIX, lp);
   }
   __syncthreads();
   // tile-local digit starts, per-wave starts inside them, global run starts

@@ -2323,7 +2323,8 @@ __global__ void __launch_bounds__(TPB)
   __shared__ uint32_t gofs[RADIX];
   __shared__ uint32_t wsum[NWAVE];
   __shared__ uint8_t sk[TILE];
-  __shared__ uint16_t sv[TILE];
+  __shared__ __attribute__((aligned(16))) uint16_t sv[TILE];  // (first: the ranks' peer words)
+  uint64_t *pmask = (uint64_t *)sv;
   const int w = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const uint32_t t = blockIdx.x;
@@ -2331,7 +2332,10 @@ __global__ void __launch_bounds__(TPB)
   const uint32_t tn = (t + 1 < ntiles ? toff[t + 1] : (uint32_t)*n_dev) - o;
   const int d0 = threadIdx.x;  // TPB == RADIX
   const uint32_t go = (uint32_t)d0 < nrows ? offs[(int64_t)d0 * ntiles + t] : 0u;
-  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) {
+    (&run[0][0])[d] = 0;
+    pmask[d] = 0ull;
+  }
   uint32_t key[16];
   uint64_t okm[16];
 #pragma unroll
@@ -2342,21 +2346,16 @@ __global__ void __launch_bounds__(TPB)
     key[k] = (uint32_t)bins[o + (ok ? e : 0u)];  // unconditional (o: this tile's or the next's first)
   }
   __syncthreads();
-  uint32_t ret[16], lp[16];
-  uint64_t pm[16];
+  uint32_t lp[16];
+  {
+    uint32_t dg[16];
+    bool okk[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const bool ok = (okm[k] >> lane) & 1ull;
-    const uint32_t dgt = key[k] & 255u;
-    const uint64_t m = peers8(dgt, okm[k]);
-    pm[k] = ok ? m : 0ull;
-    ret[k] = (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
-    const uint32_t before = (uint32_t)__shfl((int)ret[k], leader, 64);
-    lp[k] = before + rank_below(pm[k]);
+    for (int k = 0; k < 16; ++k) {
+      okk[k] = (okm[k] >> lane) & 1ull;
+      dg[k] = key[k] & 255u;
+    }
+    wave_ranks_lds<16>(dg, okk, &run[w][0], pmask + w * RADIX, lp);
   }
   __syncthreads();
   {
@@ -2400,21 +2399,31 @@ __global__ void __launch_bounds__(TPB)
 // STAGE: the tile is sorted by bin in LDS and written out run by run
 // (coalesced); else every element is stored at its CSR position directly
 // (a (bin, tile) run is one block's, so L2 merges its lines; no 12 KB of LDS).
-template <bool STAGE>
+// LDSM: the wave-local stable ranks from LDS (prims.h wave_ranks_lds) instead
+// of ballots: ~12 VALU + 5 LDS instructions per 64 slots instead of peers8's
+// ~85 VALU, which made csr_slots VALU-bound (SQ_ACTIVE_INST_VALU = 94 of its
+// 107 us at 64M, profiles/r4/pmc_r4b; 105.5 -> 90.6 us same box).
+template <bool STAGE, bool LDSM>
 __global__ void __launch_bounds__(TPB)
     csr_slots(const uint32_t *__restrict__ toff, const uint64_t *__restrict__ kw,
               const uint16_t *__restrict__ kpre, const uint32_t *__restrict__ wcnt,
               const uint8_t *__restrict__ bins, const uint32_t *__restrict__ offs,
-              uint32_t ntiles, int32_t *__restrict__ perm, uint32_t nrows) {
+              uint32_t ntiles, int32_t *__restrict__ perm, uint32_t nrows, int xcd) {
   __shared__ uint32_t run[NWAVE][RADIX];
   __shared__ uint32_t dstart[RADIX];
   __shared__ uint32_t gofs[RADIX];
   __shared__ uint32_t wsum[NWAVE];
   __shared__ uint8_t sk[STAGE ? TILE : 1];
-  __shared__ uint16_t sv[STAGE ? TILE : 1];
+  // sv, and during the ranking the [NWAVE][RADIX] peer words (8 KB either way)
+  __shared__ __attribute__((aligned(16))) uint16_t sv[TILE];
+  static_assert(sizeof(uint16_t) * TILE == sizeof(uint64_t) * NWAVE * RADIX, "pmask aliases sv");
+  uint64_t *pmask = (uint64_t *)sv;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // keep words: scalar loads
   const uint32_t lane = lane_id();
-  const uint32_t t = blockIdx.x;
+  // xcd: each XCD takes one contiguous run of tiles (xcd_swizzle), so a
+  // (bin, tile) run's output lines shared with the next tile's run, and the
+  // [bin][tile] offset words 16 tiles share, stay in one L2 (speed only)
+  const uint32_t t = xcd ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
   const int d0 = threadIdx.x;  // TPB == RADIX
   const uint32_t dr = (uint32_t)d0 < nrows ? (uint32_t)d0 : nrows - 1;  // no branch around the load
   const uint32_t go0 = offs[(int64_t)dr * ntiles + t];
@@ -2444,20 +2453,34 @@ __global__ void __launch_bounds__(TPB)
              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
     key[k] = bt[k * 64];  // unconditional: every slot exists
   }
-  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) (&run[0][0])[d] = 0;
+  for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) {
+    (&run[0][0])[d] = 0;
+    if (LDSM) pmask[d] = 0ull;
+  }
   __syncthreads();
   uint32_t lp[16];
+  if (LDSM) {
+    uint32_t dg[16];
+    bool okk[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint64_t wd = wds[k];
-    const bool ok = (wd >> lane) & 1ull;
-    const uint32_t dgt = key[k] & 255u;
-    uint64_t m = peers8(dgt, wd);
-    m = ok ? m : 0ull;
-    const uint32_t ret =
-        (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
-    const int leader = m ? __builtin_ctzll(m) : (int)lane;
-    lp[k] = (uint32_t)__shfl((int)ret, leader, 64) + rank_below(m);
+    for (int k = 0; k < 16; ++k) {
+      okk[k] = (wds[k] >> lane) & 1ull;
+      dg[k] = key[k] & 255u;
+    }
+    wave_ranks_lds<16>(dg, okk, &run[w][0], pmask + w * RADIX, lp);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t wd = wds[k];
+      const bool ok = (wd >> lane) & 1ull;
+      const uint32_t dgt = key[k] & 255u;
+      uint64_t m = peers8(dgt, wd);
+      m = ok ? m : 0ull;
+      const uint32_t ret =
+          (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
+      const int leader = m ? __builtin_ctzll(m) : (int)lane;
+      lp[k] = (uint32_t)__shfl((int)ret, leader, 64) + rank_below(m);
+    }
   }
   __syncthreads();
   {
@@ -2991,13 +3014,18 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   double *acc = (double *)((char *)L1 + sizeof(uint32_t) * MONO_NW * RADIX);
   const int nm = a.fs.nm, macc = nm * nb;
   for (int i = tid; i < nq; i += MONO_BT) e_lds[i] = ld_sc1d(&a.edges[i]);
-  for (int i = tid; i < MONO_NW * RADIX; i += MONO_BT) runs[i] = 0;
+  // the ranks' peer words (prims.h wave_ranks_lds) in L0: free between the
+  // finish (phase 4) and the CSR offsets (phase 6)
+  uint64_t *pmask = (uint64_t *)L0;
+  static_assert(sizeof(uint32_t) * MS0_DIG >= sizeof(uint64_t) * MONO_NW * RADIX, "pmask in L0");
+  for (int i = tid; i < MONO_NW * RADIX; i += MONO_BT) {
+    runs[i] = 0;
+    pmask[i] = 0ull;
+  }
   for (int i = tid; i < macc; i += MONO_BT) acc[i] = 0.0;
   __syncthreads();
   uint32_t bk[MONO_SI], lp[MONO_SI];
   {
-    uint32_t ret[MONO_SI];
-    uint64_t pm[MONO_SI];
 #pragma unroll
     for (int k = 0; k < MONO_SI; ++k) {
       const bool kp = (keepbits >> k) & 1u;
@@ -3017,20 +3045,15 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
         atomicAdd(&aq[bk[k]], monomial(col, f, ww));
       }
     }
-#pragma unroll
-    for (int k = 0; k < MONO_SI; ++k) {  // element order (wave, k, lane) = particle order
-      const bool kp = (keepbits >> k) & 1u;
-      const uint32_t dgt = bk[k] & 255u;
-      const uint64_t m = peers8(dgt, bal[k]);
-      pm[k] = kp ? m : 0ull;
-      ret[k] = (kp && rank_below(m) == 0) ? atomicAdd(&runs[w * RADIX + dgt], (uint32_t)__popcll(m))
-                                          : 0u;
-    }
+    // element order (wave, k, lane) = particle order
+    uint32_t dg[MONO_SI];
+    bool okk[MONO_SI];
 #pragma unroll
     for (int k = 0; k < MONO_SI; ++k) {
-      const int leader = pm[k] ? __builtin_ctzll(pm[k]) : (int)lane;
-      lp[k] = (uint32_t)__shfl((int)ret[k], leader, 64) + rank_below(pm[k]);
+      okk[k] = (keepbits >> k) & 1u;
+      dg[k] = bk[k] & 255u;
     }
+    wave_ranks_lds<MONO_SI>(dg, okk, runs + w * RADIX, pmask + w * RADIX, lp);
   }
   __syncthreads();
   if (tid < RADIX) {  // the tile's count of bin d; runs -> offsets over the waves
@@ -5069,10 +5092,20 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
             const char *v = std::getenv("PBX_CSR_DIRECT");
             return !(v && v[0] == '1');
           }();
-          hipLaunchKernelGGL(stage ? csr_slots<true> : csr_slots<false>, dim3(nt), dim3(TPB), 0, st,
+          static const bool peers_env = [] {  // A/B: PBX_CSR_PEERS=1 ranks with peers8 ballots
+            const char *v = std::getenv("PBX_CSR_PEERS");
+            return v && v[0] == '1';
+          }();
+          auto csrk = stage ? (peers_env ? csr_slots<true, false> : csr_slots<true, true>)
+                            : (peers_env ? csr_slots<false, false> : csr_slots<false, true>);
+          static const int xcd_env = [] {  // A/B: PBX_CSR_XCD=0 keeps launch order
+            const char *v = std::getenv("PBX_CSR_XCD");
+            return (v && v[0] == '0') ? 0 : 1;
+          }();
+          hipLaunchKernelGGL(csrk, dim3(nt), dim3(TPB), 0, st,
                              (const uint32_t *)P.toff.p, (const uint64_t *)P.kw.p,
                              (const uint16_t *)P.kpre.p, (const uint32_t *)P.swc.p,
-                             (const uint8_t *)bins8, (const uint32_t *)th, nt, perm, nr);
+                             (const uint8_t *)bins8, (const uint32_t *)th, nt, perm, nr, xcd_env);
           PBX_HIP(hipGetLastError());
         }
       } else if (n_sel && lazy) {

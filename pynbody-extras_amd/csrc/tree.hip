@@ -2137,6 +2137,9 @@ static void pack_particles(Octree &T, hipStream_t st) {
       hipLaunchKernelGGL(interleave_records, dim3(nblk(n)), dim3(TPB), 0, st, T.pos.as<double>(),
                          T.user_mass ? T.mass.as<double>() : (const double *)nullptr, n, rec0);
     T.rec0_valid = true;
+    // (one record per thread: a 4-records-per-thread variant with all
+    // gathers in flight measured the same, 98.6 vs 100.6 us at 4M — the
+    // random 32-byte reads are line-bound, not latency-bound)
     hipLaunchKernelGGL(pack_records, dim3(nblk(n)), dim3(TPB), 0, st, (const double4 *)rec0,
                        T.perm.as<int32_t>(), n, rec);
     if (T.soft_set) gather_softenings(T, st);
