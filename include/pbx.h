@@ -239,6 +239,16 @@ int pbx_octree_balance(pbx_octree *tree, const int32_t *d_cost_orig, int world, 
  * 4-record leaf rounds, the same for the 64 targets of one wave), which is
  * what a walk's time follows — ShardedTree balances on it. */
 int pbx_octree_set_cost_kind(pbx_octree *tree, int kind);
+/* Wave split for range walks (speed only, every target's result unchanged):
+ * d_cost_orig = device array of n per-particle costs in ORIGINAL particle
+ * order from an earlier walk (cost kind 1: the wave's work, e.g. after
+ * pbx_octree_cost_to_orig — what ShardedTree all-gathers).  Every later
+ * self-mode walk (64-thread walk blocks) splits the 64-target groups whose
+ * cost is >= permille/1000 of the largest into two 32-target waves,
+ * dispatched first (at most 1/8 of the groups): a range walk ends with its
+ * longest wave, and a smaller wave walks a shorter union of its targets'
+ * walks.  NULL disables it; the array must stay valid while it is set. */
+int pbx_octree_set_wave_split(pbx_octree *tree, const int32_t *d_cost_orig, int permille);
 /* out[13] = {n, nodes, levels, has_mass_payload, has_hmax,
  *            accepted node interactions and leaf pairs of the last walk,
  *            path words, wave steps and active-lane steps of the last walk

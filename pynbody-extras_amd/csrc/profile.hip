@@ -812,7 +812,10 @@ struct SelHint {
 };
 // select_tiles blocks per assign_gather block (tile sub-ranges): 3 x 255
 // blocks of 8 waves at <= 80 VGPRs (6 waves per SIMD) are all resident at once
-constexpr int SH_K = 3;
+#ifndef PBX_SH_K
+#define PBX_SH_K 3
+#endif
+constexpr int SH_K = PBX_SH_K;
 
 
 // The step's control record from the selection's status words: kept count
@@ -922,17 +925,23 @@ constexpr int SH_BT = 512;
 constexpr int SH_NW = SH_BT / 64;  // wave slices per tile
 constexpr uint32_t SH_TMAX = 15;   // tiles per block for the u16 digit counts
 constexpr uint32_t SH_MAXT = 64;   // tiles per block for the block-local offsets (LDS)
+constexpr uint32_t SH_RSUB_MAX = 8;  // u16 count rows per block (flushed every SH_TMAX tiles)
 // FAM: several family slices (membership tested per particle); else every
 // particle of the span [base, n) is a member (no family, or one slice: the
 // span is that slice) and the 16 slice bounds stay out of the registers.
+#ifdef PBX_ST_3BUF
+#define PBX_SH_WAVES 4  // two blocks per CU
+#else
+#define PBX_SH_WAVES 1
+#endif
 template <bool FAM>
-__global__ void __launch_bounds__(SH_BT)
+__global__ void __launch_bounds__(SH_BT, PBX_SH_WAVES)
     select_tiles(const double *__restrict__ pos, int64_t n, SelectParams p, uint32_t nt,
                  uint32_t G0, double *__restrict__ xo, uint64_t *__restrict__ kw,
                  uint16_t *__restrict__ kpre, uint32_t *__restrict__ wcnt,
                  uint32_t *__restrict__ toff, uint32_t *__restrict__ btot,
                  unsigned long long *__restrict__ minmax, const SelHint *__restrict__ hint,
-                 uint64_t ka, uint64_t kb, uint32_t *__restrict__ rows16,
+                 uint64_t ka, uint64_t kb, uint32_t *__restrict__ rows16, uint32_t rsub,
                  uint32_t *__restrict__ hflag) {
   constexpr int SI = TILE / SH_BT;
   __shared__ uint32_t lh[MS0_DIG / 2];
@@ -948,7 +957,9 @@ __global__ void __launch_bounds__(SH_BT)
   const uint32_t tb = ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * (sub + 1) / SH_K);
   SelHint h{};
   if (hint) h = *hint;
-  const bool hv = h.valid && rows16 && tb - ta <= SH_TMAX;
+  // rsub rows per block: the u16 counts are flushed to the next row every
+  // SH_TMAX tiles (families above ~47M particles)
+  const bool hv = h.valid && rows16 && tb - ta <= SH_TMAX * rsub;
   const uint64_t hlo = h.lo;
   const int hsh = h.s;
   // highest key the hint's digits cover: lo + 2^(s + w) - 1 (saturating)
@@ -993,15 +1004,30 @@ __global__ void __launch_bounds__(SH_BT)
 #pragma unroll
     for (int k = 0; k < SH_HALF; ++k) {
       double xv = 0.0;
+#ifdef PBX_DIAG_ST_NOSQRT  // timing diagnostic only: x = r^2 (no sqrt)
+      xv = (H.x[k] * H.x[k] + H.y[k] * H.y[k]) + H.z[k] * H.z[k];
+      const bool keep = ((H.in >> k) & 1u) && xv < p.r2max;
+#else
       const bool keep = ((H.in >> k) & 1u) && select_xyz(H.x[k], H.y[k], H.z[k], p, xv);
+#endif
       const uint64_t bal = __ballot(keep);
-      if (lane == 0) {
+      if (lane == 0) {  // (one store per half from lane k instead: csr_slots +19 us, dropped)
         kw[wj + k] = bal;
         kpre[wj + k] = (uint16_t)run;  // kept particles before the word in this wave's slice
       }
       run += (uint32_t)__popcll(bal);
+#ifdef PBX_DIAG_ST_NOKEY  // timing diagnostic only: x stored, no key range / digit counts
+      if (keep) xt[k * 64 + lane] = xv;
+      if (false) {
+#elif defined(PBX_DIAG_ST_NOSTORE)  // timing diagnostic only: x not stored
       if (keep) {
-        xt[k * 64 + lane] = xv;
+        if (xv == 1234.5) xt[k * 64 + lane] = xv;
+#else
+      if (keep) {
+        // streaming (nt) stores: select 280 -> 274 us and assign_gather's
+        // re-read of x 202 -> 191 us at 64M (same box A/B/A/B)
+        __builtin_nontemporal_store(xv, xt + k * 64 + lane);
+#endif
         const uint64_t kk = dkey(xv);
         kmin = kk < kmin ? kk : kmin;
         kmax = kk > kmax ? kk : kmax;
@@ -1016,6 +1042,52 @@ __global__ void __launch_bounds__(SH_BT)
       }
     }
   };
+  // end of a tile: the wave's count; every SH_TMAX tiles the u16 digit rows
+  auto tile_end = [&](uint32_t tile) {
+    if (lane == 0) {
+      wcnt[(int64_t)tile * SH_NW + w] = run;
+      if (tile - ta < SH_MAXT) tcnt[tile - ta][w] = run;
+    }
+    if (hv && (tile - ta) % SH_TMAX == SH_TMAX - 1 && tile + 1 < tb) {  // (block-uniform)
+      __syncthreads();  // every wave's counts of this row's tiles are in
+      uint32_t *row = rows16 + ((int64_t)blockIdx.x * rsub + (tile - ta) / SH_TMAX) * (MS0_DIG / 2);
+      for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) {
+        row[i] = lh[i];
+        lh[i] = 0;
+      }
+      __syncthreads();
+    }
+  };
+#ifdef PBX_ST_3BUF
+  // three half buffers, two halves in flight while one is selected (twice
+  // the loads in flight per wave at the same occupancy: 2 blocks per CU)
+  const uint32_t nh = 2 * (tb - ta);
+  auto hld = [&](uint32_t k, Half &H) {  // half k of the block's range (past it: the last again)
+    const uint32_t kk = k < nh ? k : nh - 1;
+    ld(ta + kk / 2, (int)(kk & 1), H);
+  };
+  auto hsel = [&](uint32_t k, const Half &H) {
+    const uint32_t tile = ta + k / 2;
+    if ((k & 1) == 0) run = 0;
+    sel(tile, (int)(k & 1), H);
+    if (k & 1) tile_end(tile);
+  };
+  Half A, B, C;
+  if (nh) {
+    hld(0, A);
+    hld(1, B);
+  }
+  for (uint32_t k = 0; k < nh; k += 3) {
+    hld(k + 2, C);
+    hsel(k, A);
+    if (k + 1 >= nh) break;
+    hld(k + 3, A);
+    hsel(k + 1, B);
+    if (k + 2 >= nh) break;
+    hld(k + 4, B);
+    hsel(k + 2, C);
+  }
+#else
   Half A, B;
   if (ta < tb) ld(ta, 0, A);
   for (uint32_t tile = ta; tile < tb; ++tile) {
@@ -1024,11 +1096,9 @@ __global__ void __launch_bounds__(SH_BT)
     sel(tile, 0, A);
     ld(tile + 1 < tb ? tile + 1 : tile, 0, A);
     sel(tile, 1, B);
-    if (lane == 0) {
-      wcnt[(int64_t)tile * SH_NW + w] = run;
-      if (tile - ta < SH_MAXT) tcnt[tile - ta][w] = run;
-    }
+    tile_end(tile);
   }
+#endif
   // the block's key range: one atomic pair per block
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1080,14 +1150,15 @@ __global__ void __launch_bounds__(SH_BT)
       if (b != 0ull) atomicMax(&mmq[1], b);
     }
   }
-  if (hv) {  // this block's row (coalesced words)
-    uint32_t *row = rows16 + (int64_t)blockIdx.x * (MS0_DIG / 2);
-    for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) row[i] = lh[i];
+  if (hv) {  // this block's last row, and zero rows after it (coalesced words)
+    const uint32_t last = tb > ta ? (tb - ta - 1) / SH_TMAX : 0u;
+    for (uint32_t r = last; r < rsub; ++r) {
+      uint32_t *row = rows16 + ((int64_t)blockIdx.x * rsub + r) * (MS0_DIG / 2);
+      for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) row[i] = r == last ? lh[i] : 0u;
+    }
   } else if (hint && h.valid && threadIdx.x == 0) {
-    // more than SH_TMAX tiles for this block's u16 counts: fall back to the
-    // re-read.  With SH_K * 255 = 765 select blocks that is a family span
-    // above 765 * 15 * 4096 ~ 47M particles (the 64M bench point's dm span is
-    // 38.4M; its 256M point re-reads x every call)
+    // more tiles than the block's rsub rows of u16 counts hold: fall back to
+    // the re-read of x (the host sizes rsub for the span, up to SH_RSUB_MAX)
     atomicOr(hflag, 1u);
   }
 }
@@ -1392,7 +1463,7 @@ __global__ void __launch_bounds__(TPB)
     fused_boff(const uint32_t *__restrict__ rows, int g0, const FusedCtl *__restrict__ ctl,
                const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ goff,
                uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
-               uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16) {
+               uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16, uint32_t rsub) {
   __shared__ uint32_t wsum[NWAVE];
   const int g = blockIdx.x;
   if ((ctl->err & 2) || g >= ctl->ng) return;
@@ -1401,8 +1472,9 @@ __global__ void __launch_bounds__(TPB)
   if (ctl->hint) {  // select_tiles blocks (b - 1) SH_K .. + SH_K - 1 cover block b's tiles
     const uint32_t d = gdig[g];
     if (b >= 1 && b < g0)
-      for (int j = 0; j < SH_K; ++j)
-        c += (rows16[(int64_t)((b - 1) * SH_K + j) * (MS0_DIG / 2) + (d >> 1)] >> (16 * (d & 1))) &
+      for (uint32_t j = 0; j < SH_K * rsub; ++j)  // the SH_K blocks' rsub rows each
+        c += (rows16[((int64_t)(b - 1) * SH_K * rsub + j) * (MS0_DIG / 2) + (d >> 1)] >>
+              (16 * (d & 1))) &
              0xffffu;
   } else if (b < g0) {
     c = rows[(int64_t)b * MS0_DIG + gdig[g]];
@@ -1486,7 +1558,13 @@ struct FusedStats {
   int f[AS_MAXM];
   int w[AS_MAXM];
   int col[AS_MAXM];
+  int op[AS_MAXM];  // MO_* when the slot's monomial has a dedicated form, else MO_GEN
 };
+// the common monomials in their own (uniform-branch) loops: the generic
+// form selects a(f), f, ww per element (~14 VALU), these are 0-2 VALU.
+// Each is the value monomial() computes for that slot, bit for bit (the
+// products are the same products; x*1.0 is exact)
+enum : int { MO_GEN = 0, MO_W = 1, MO_X = 2, MO_XW = 3, MO_XXW = 4, MO_XX = 5, MO_WW = 6 };
 
 // monomial value of column `col` (the expression moments_kernel sums):
 // a(f) in {1, f, f*f, |f|} times b in {1, ww}; x*1.0 is exact, so this is
@@ -1496,6 +1574,33 @@ __device__ __forceinline__ double monomial(int col, double f, double ww) {
   const bool wb = (col == 0 || col == 1 || col == 2 || col == 5);
   const double a = am == 0 ? 1.0 : am == 1 ? f : am == 2 ? f * f : __builtin_fabs(f);
   return wb ? a * ww : a;
+}
+
+// aq[bk[k]] += monomial of slot (op, col, fq, wq) for the K elements whose bin
+// is < nb (LDS atomics)
+// dummy (optional): a per-lane LDS slot that takes the adds of elements
+// whose bin is >= nb, so no add is under a branch (no exec-mask jumps)
+template <int K>
+__device__ __forceinline__ void mom_add(double *aq, int op, int col, int fq, int wq,
+                                        const uint32_t *bk, const double *xv, const double *wv,
+                                        uint32_t nb, double *dummy = nullptr) {
+#define PBX_MOM_LOOP(EXPR)                                                          \
+  _Pragma("unroll") for (int k = 0; k < K; ++k) {                                   \
+    if (dummy) atomicAdd(bk[k] < nb ? &aq[bk[k]] : dummy, (EXPR));                  \
+    else if (bk[k] < nb) atomicAdd(&aq[bk[k]], (EXPR));                             \
+  }                                                                                 \
+  return;
+  switch (op) {
+    case MO_W: PBX_MOM_LOOP(wv[k])
+    case MO_X: PBX_MOM_LOOP(xv[k])
+    case MO_XW: PBX_MOM_LOOP(xv[k] * wv[k])
+    case MO_XXW: PBX_MOM_LOOP((xv[k] * xv[k]) * wv[k])
+    case MO_XX: PBX_MOM_LOOP(xv[k] * xv[k])
+    case MO_WW: PBX_MOM_LOOP(wv[k] * wv[k])
+    default:
+      PBX_MOM_LOOP(monomial(col, fq == 0 ? xv[k] : wv[k], wq == 0 ? xv[k] : wv[k]))
+  }
+#undef PBX_MOM_LOOP
 }
 
 // One block (FR_TPB threads) per group: for each of its ranks, an MSD radix
@@ -1770,17 +1875,17 @@ __global__ void __launch_bounds__(BT)
         if (q >= fs.nm) break;
         const int col = fs.col[q], fq = fs.f[q], wq = fs.w[q];
         double *aq = acc + (int64_t)q * nb;
+#ifdef PBX_DIAG_NO_MOM_ATOMICS  // timing diagnostic only: sums not accumulated
 #pragma unroll
         for (int k = 0; k < AS_IPT; ++k) {
           if (b[k] >= (uint32_t)nb) continue;
           const double f = fq == 0 ? v[k] : wv[k];
           const double ww = wq == 0 ? v[k] : wv[k];
-#ifdef PBX_DIAG_NO_MOM_ATOMICS  // timing diagnostic only: sums not accumulated
           if (monomial(col, f, ww) == 1234.5) aq[0] = 0.0;
-#else
-          atomicAdd(&aq[b[k]], monomial(col, f, ww));
-#endif
         }
+#else
+        mom_add<AS_IPT>(aq, fs.op[q], col, fq, wq, b, v, wv, (uint32_t)nb);
+#endif
       }
     }
   }
@@ -1954,13 +2059,7 @@ __global__ void __launch_bounds__(BT)
           if (q >= fs.nm) break;
           const int col = fs.col[q], fq = fs.f[q], wq = fs.w[q];
           double *aq = acc + (int64_t)q * nb;
-#pragma unroll
-          for (int kk = 0; kk < CH; ++kk) {
-            if (b[kk] >= (uint32_t)nb) continue;
-            const double f = fq == 0 ? v[kk] : wv[kk];
-            const double ww = wq == 0 ? v[kk] : wv[kk];
-            atomicAdd(&aq[b[kk]], monomial(col, f, ww));
-          }
+          mom_add<CH>(aq, fs.op[q], col, fq, wq, b, v, wv, (uint32_t)nb);
         }
       }
     }
@@ -2001,16 +2100,18 @@ constexpr int AG_TR = 64;
 #endif
 constexpr int AG_W = PBX_AG_W;                // keep words of a tile per wave
 constexpr int AG_TPS = AG_W * (MS0_TPB / 64) / 64;  // tiles per step (the block's waves)
-struct AgRec {  // a deferred key: key - window base, weight, particle slot, tile
+struct AgRec {  // a deferred key: key - window base, weight, particle slot, tile | group << 24
   uint64_t off;
   double w;
-  uint32_t pos, t;
+  uint32_t pos, tg;
 };
+constexpr uint32_t AG_TBITS = 24;  // tiles < 2^24 (profiles hold < 2^31 particles); groups < 256
 struct GatherOut {
   uint64_t *seg;          // key - window base, by segment slot
   AgRec *rec;             // deferred keys, block by block
   const uint32_t *bcnt;   // per block: keys gathered (fused_boff)
   uint32_t *rbase, *rn;   // per block: list start, deferred keys written
+  unsigned long long *rowtot;  // per bin (nb + 1 rows): kept particles, summed over blocks
 };
 
 // exclusive sum of v[0 .. k) over a block (k <= blockDim.x)
@@ -2043,6 +2144,10 @@ __global__ void __launch_bounds__(MS0_TPB)
   __shared__ uint32_t qd[RADIX];
   __shared__ uint32_t red[MS0_TPB / 64];
   __shared__ uint32_t dk;
+#ifdef PBX_AG_BF
+  __shared__ uint32_t thd[64];   // per-lane sinks of the branch-free adds
+  __shared__ double mdummy[64];
+#endif
   const int macc = MOM ? fs.nm * nb : 0;
   double *acc = (double *)smem;
   const int nr = nb + 1, nrs = nr | 1;  // th row stride odd: flush reads bank-conflict free
@@ -2109,8 +2214,9 @@ __global__ void __launch_bounds__(MS0_TPB)
 #pragma unroll
     for (int kk = 0; kk < AG_W; ++kk) {
       const int64_t sl = s0 + 64 * kk + lane;
-      P.v[kk] = x[sl];
-      P.m[kk] = mp[wneed ? (sl < span ? sl : span - 1) : sl];
+      // streaming (nt) loads, both read once: 202 -> 180 us at 64M (A/B/A/B)
+      P.v[kk] = __builtin_nontemporal_load(x + sl);
+      P.m[kk] = __builtin_nontemporal_load(mp + (wneed ? (sl < span ? sl : span - 1) : sl));
       P.k[kk] = kw[(s0 >> 6) + kk + vz];
     }
   };
@@ -2146,12 +2252,23 @@ __global__ void __launch_bounds__(MS0_TPB)
     }
     const uint32_t sbase = t * (uint32_t)TILE + 64u * (uint32_t)(wl * AG_W) + lane;
 #ifndef PBX_DIAG_AG_NOBIN  // (timing diagnostic: no byte stores / tile counts)
+#ifdef PBX_AG_BF
+    // branch-free: every slot's byte is stored (a skipped slot's 0xff is never
+    // read — csr_slots takes kept slots only — and a deferred slot's 0xfe is
+    // overwritten by fix_deferred), counts of non-bins go to a per-lane dummy
+#pragma unroll
+    for (int kk = 0; kk < AG_W; ++kk) {
+      bins[sbase + 64u * kk] = (uint8_t)bk[kk];
+      atomicAdd(bk[kk] <= (uint32_t)nb ? &th[tl * nrs + bk[kk]] : &thd[lane], 1u);
+    }
+#else
 #pragma unroll
     for (int kk = 0; kk < AG_W; ++kk)
       if (bk[kk] <= (uint32_t)nb) {
         bins[sbase + 64u * kk] = (uint8_t)bk[kk];
         atomicAdd(&th[tl * nrs + bk[kk]], 1u);
       }
+#endif
 #endif
 #ifdef PBX_DIAG_AG_NOSUM  // (timing diagnostic: no per-bin sums)
     if (false) {
@@ -2161,25 +2278,42 @@ __global__ void __launch_bounds__(MS0_TPB)
 #pragma unroll
       for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
         if (q >= fs.nm) break;
-        double *aq = acc + q * nb;
-#pragma unroll
-        for (int kk = 0; kk < AG_W; ++kk)
-          if (bk[kk] < (uint32_t)nb) {
-            const double f = fs.f[q] == 0 ? P.v[kk] : wv[kk];
-            const double ww = fs.w[q] == 0 ? P.v[kk] : wv[kk];
-            atomicAdd(&aq[bk[kk]], monomial(fs.col[q], f, ww));
-          }
+#ifdef PBX_AG_BF
+        mom_add<AG_W>(acc + q * nb, fs.op[q], fs.col[q], fs.f[q], fs.w[q], bk, P.v, wv,
+                      (uint32_t)nb, &mdummy[lane]);
+#else
+        mom_add<AG_W>(acc + q * nb, fs.op[q], fs.col[q], fs.f[q], fs.w[q], bk, P.v, wv,
+                      (uint32_t)nb);
+#endif
       }
     }
-    if (anydef) {  // rare (edge-holding digits): the group segment + the block's deferred list
+    if (anydef) {  // ~1-3 % of the keys (edge-holding digits), but some lane of almost every
+                   // call: the group segments + the block's deferred list.  One list
+                   // reservation per call for the wave (ballot ranks), the segment slots'
+                   // LDS atomics all issued before any is waited for.
+      uint64_t bal[AG_W], off[AG_W];
+      uint32_t g[AG_W], ss[AG_W], nd = 0;
 #pragma unroll
-      for (int kk = 0; kk < AG_W; ++kk)
+      for (int kk = 0; kk < AG_W; ++kk) {
+        const bool d = bk[kk] == DEFER;
+        bal[kk] = __ballot(d);
+        off[kk] = dkey(P.v[kk]) - lo;
+        g[kk] = d ? dtab[(uint32_t)(off[kk] >> s)] & 0x7fffu : 0u;
+        ss[kk] = d ? atomicAdd(&sslot[g[kk]], 1u) : 0u;
+        nd += (uint32_t)__popcll(bal[kk]);
+      }
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&dk, nd);
+      base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+#pragma unroll
+      for (int kk = 0; kk < AG_W; ++kk) {
         if (bk[kk] == DEFER) {
-          const uint64_t off = dkey(P.v[kk]) - lo;
-          const uint32_t g = dtab[(uint32_t)(off >> s)] & 0x7fffu;
-          go.seg[atomicAdd(&sslot[g], 1u)] = off;
-          go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{off, wv[kk], sbase + 64u * kk, t};
+          go.seg[ss[kk]] = off[kk];
+          go.rec[rb + base + rank_below(bal[kk])] =
+              AgRec{off[kk], wv[kk], sbase + 64u * kk, t | (g[kk] << AG_TBITS)};
         }
+        base += (uint32_t)__popcll(bal[kk]);
+      }
     }
   };
   for (uint32_t r0 = ta; r0 < tb; r0 += AG_TR) {
@@ -2211,6 +2345,12 @@ __global__ void __launch_bounds__(MS0_TPB)
       const int b = k / AG_TR, tl = k - b * AG_TR;
       if (tl < nrt) tile_hist[(int64_t)b * nt + r0 + tl] = th[tl * nrs + b];
     }
+    if (go.rowtot)  // the rows' totals (row_scan's bases): one atomic per bin and flush
+      for (int b = tid; b < nr; b += MS0_TPB) {
+        uint32_t c = 0;
+        for (int tl = 0; tl < nrt; ++tl) c += th[tl * nrs + b];
+        if (c) atomicAdd(&go.rowtot[b], (unsigned long long)c);
+      }
     __syncthreads();
     for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
     __syncthreads();
@@ -2227,78 +2367,175 @@ __global__ void __launch_bounds__(MS0_TPB)
 
 // The deferred keys' bins once fused_finish has the edges (the ~1-3 % of
 // the kept particles whose level-0 digit holds an edge): block b takes
-// assign_gather block b's list, so its byte stores and [bin][tile] count
-// atomics stay inside that block's tiles; bin_of over the edges in LDS.
+// assign_gather block b's list, so its byte stores and [bin][tile] counts
+// stay inside that block's tiles.  A key of group g lies above every edge of
+// an earlier group and below every edge of a later one, so its lower bound
+// is searched among the group's own ranks gq[g] .. gq[g + 1] only (usually
+// one or two edges, not an 8-step dependent LDS chain over all of them).
+// The [tile][bin] counts are kept in LDS for a window of the block's tiles
+// at a time (a pass over the list per window: one pass up to FD_LDSW / (nb + 1)
+// tiles, i.e. up to ~1G particles at 129 bins) — global atomics on scattered
+// (bin, tile) words ran at ~0.1 of LDS speed (256M: 203 us).
 // (A block's list mixes all groups, so a wave's keys spread over many bins:
 // plain LDS atomics; a per-distinct-bin wave reduction — dependent
 // ds_bpermute chains — took 316 us at 64M.)
 constexpr int FD_U = 4;          // keys per thread in flight
-constexpr int FD_LDSW = 16384;   // LDS words for the block's [tile][bin] counts
+constexpr int FD_LDSW = 28672;   // LDS words for the block's [tile][bin] counts (112 KB)
+
+// bin_of(v, e, nb) for a v whose lower bound lies in [qa, qb]
+__device__ __forceinline__ uint32_t bin_of_in(double v, const double *e, int nb, int qa, int qb) {
+  if (v != v) return bin_of(v, e, nb);  // rare: the first NaN edge
+  int l = qa, h = qb;  // first k in [qa, qb) with !(e[k] < v), qb if none
+  while (l < h) {
+    const int m = (l + h) >> 1;
+    if (e[m] < v) l = m + 1;
+    else h = m;
+  }
+  const int lo = l;
+  int b = lo - 1;
+  if (v == e[0]) b = 0;
+  if (v == e[nb]) b = nb - 1;
+  return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
+}
+
 template <bool MOM>
 __global__ void __launch_bounds__(MS0_TPB)
     fix_deferred(const FusedCtl *__restrict__ ctl, const AgRec *__restrict__ rec,
                  const uint32_t *__restrict__ rbase, const uint32_t *__restrict__ rn,
-                 const double *__restrict__ edges, int nb, uint8_t *__restrict__ bins,
-                 uint32_t *__restrict__ tile_hist, uint32_t nt, FusedStats fs,
-                 double *__restrict__ slab) {
+                 const double *__restrict__ edges, const uint32_t *__restrict__ gq, int nb,
+                 uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, uint32_t nt,
+                 FusedStats fs, double *__restrict__ slab, unsigned long long *__restrict__ rowtot) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t dtot[RADIX];  // per-bin totals of the block's deferred keys (rowtot)
   const int macc = MOM ? fs.nm * nb : 0;
   double *acc = (double *)smem;
   double *e = acc + macc;
-  // this block's tiles' counts [tile][bin] in LDS when they fit: global
-  // atomics execute at the memory side, one request per scattered lane
-  uint32_t *tc = (uint32_t *)(e + nb + 1);
+  uint32_t *tc = (uint32_t *)(e + nb + 1);  // [window tile][bin]
   const int tid = threadIdx.x;
   const int nrs = (nb + 1) | 1;
   uint32_t ta, tb;
   tile_range(nt, ta, tb);
-  const bool in_lds = (int64_t)(tb - ta) * nrs <= FD_LDSW;
+  const uint32_t wt = (uint32_t)(FD_LDSW / nrs);  // tiles per window
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
-  for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
-  if (in_lds)
-    for (int k = tid; k < (int)(tb - ta) * nrs; k += MS0_TPB) tc[k] = 0;
-  __syncthreads();
+  for (int k = tid; k <= nb; k += MS0_TPB) {
+    e[k] = edges[k];
+    dtot[k] = 0;
+  }
   const bool ok_all = !(ctl->err & 2);
   const int64_t r0 = rbase[blockIdx.x], cnt = ok_all ? (int64_t)rn[blockIdx.x] : 0;
   const uint64_t lo = ctl->lo;
-  for (int64_t i0 = 0; i0 < cnt; i0 += (int64_t)MS0_TPB * FD_U) {
-    AgRec r[FD_U];
+  for (uint32_t w0 = ta; w0 < tb || (w0 == ta && cnt); w0 += wt) {  // (block-uniform)
+    const uint32_t w1 = min(tb, w0 + wt);
+    for (int k = tid; k < (int)(w1 - w0) * nrs; k += MS0_TPB) tc[k] = 0;
+    __syncthreads();
+    const bool first = w0 == ta;  // bytes and sums on the first pass only
+    for (int64_t i0 = 0; i0 < cnt; i0 += (int64_t)MS0_TPB * FD_U) {
+      AgRec r[FD_U];
 #pragma unroll
-    for (int u = 0; u < FD_U; ++u) {
-      const int64_t i = i0 + u * MS0_TPB + tid;
-      r[u] = rec[r0 + (i < cnt ? i : 0)];  // unconditional loads
-    }
-#pragma unroll
-    for (int u = 0; u < FD_U; ++u) {
-      const int64_t i = i0 + u * MS0_TPB + tid;
-      const double v = dkey_inv(lo + r[u].off);
-      const bool ok = i < cnt;
-      const uint32_t b = ok ? bin_of(v, e, nb) : (uint32_t)nb;
-      if (ok) {
-        bins[r[u].pos] = (uint8_t)b;
-        if (in_lds) atomicAdd(&tc[(r[u].t - ta) * nrs + b], 1u);
-        else atomicAdd(&tile_hist[(int64_t)b * nt + r[u].t], 1u);
+      for (int u = 0; u < FD_U; ++u) {
+        const int64_t i = i0 + u * MS0_TPB + tid;
+        r[u] = rec[r0 + (i < cnt ? i : 0)];  // unconditional loads
       }
-      if (MOM && ok && b < (uint32_t)nb)
 #pragma unroll
-        for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
-          if (q >= fs.nm) break;
-          const double f = fs.f[q] == 0 ? v : r[u].w;
-          const double ww = fs.w[q] == 0 ? v : r[u].w;
-          atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
+      for (int u = 0; u < FD_U; ++u) {
+        const int64_t i = i0 + u * MS0_TPB + tid;
+        const double v = dkey_inv(lo + r[u].off);
+        const bool ok = i < cnt;
+        const uint32_t t = r[u].tg & ((1u << AG_TBITS) - 1), g = r[u].tg >> AG_TBITS;
+        const uint32_t b = ok ? bin_of_in(v, e, nb, (int)gq[g], (int)gq[g + 1]) : (uint32_t)nb;
+        if (ok) {
+          if (first) {
+            bins[r[u].pos] = (uint8_t)b;
+            if (rowtot) atomicAdd(&dtot[b], 1u);
+          }
+          if (t >= w0 && t < w1) atomicAdd(&tc[(t - w0) * nrs + b], 1u);
         }
+        if (MOM && first && ok && b < (uint32_t)nb)
+#pragma unroll
+          for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+            if (q >= fs.nm) break;
+            const double f = fs.f[q] == 0 ? v : r[u].w;
+            const double ww = fs.w[q] == 0 ? v : r[u].w;
+            atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
+          }
+      }
     }
+    __syncthreads();
+    for (int k = tid; k < (int)(w1 - w0) * (nb + 1); k += MS0_TPB) {  // the block owns these columns
+      const int b = k / (int)(w1 - w0), tl = k - b * (int)(w1 - w0);
+      const uint32_t c = tc[tl * nrs + b];
+      if (c) tile_hist[(int64_t)b * nt + w0 + tl] += c;
+    }
+    if (w1 >= tb) break;
+    __syncthreads();
   }
   __syncthreads();
-  if (in_lds)  // the block owns these columns: plain read-modify-write
-    for (int k = tid; k < (int)(tb - ta) * (nb + 1); k += MS0_TPB) {
-      const int b = k / (int)(tb - ta), tl = k - b * (int)(tb - ta);
-      const uint32_t c = tc[tl * nrs + b];
-      if (c) tile_hist[(int64_t)b * nt + ta + tl] += c;
-    }
+  if (rowtot)
+    for (int k = tid; k <= nb; k += MS0_TPB)
+      if (dtot[k]) atomicAdd(&rowtot[k], (unsigned long long)dtot[k]);
   if (MOM) {
     double *dst = slab + (int64_t)blockIdx.x * macc;
     for (int k2 = tid; k2 < macc; k2 += MS0_TPB) dst[k2] = acc[k2];
+  }
+}
+
+// The flat exclusive scan of the [bin][tile] table (row-major, nrows x ncols)
+// as nrows independent row scans: block b adds the totals of rows < b
+// (rowtot, summed by assign_gather / fix_deferred) to its row's own
+// exclusive prefix — the same words as scan_u32 over the whole table, with no
+// chain of look-backs across ~nt * nrows / 4096 tiles (11 -> ~3 us at 64M).
+constexpr int RS_TPB = 1024, RS_IPT = 16;  // a row of <= 16K tiles in one pass
+static_assert(RS_TPB >= RADIX, "one thread per row total");
+__global__ void __launch_bounds__(RS_TPB)
+    row_scan(uint32_t *__restrict__ a, uint32_t ncols, const unsigned long long *__restrict__ rowtot) {
+  __shared__ uint32_t wsum[RS_TPB / 64];
+  const int b = blockIdx.x;
+  const uint32_t lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  uint32_t *row = a + (int64_t)b * ncols;
+  // a 16-wave exclusive scan of one value per thread (+ the block total)
+  auto scan = [&](uint32_t v, uint32_t &tot) {
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t off = 0;
+    tot = 0;
+#pragma unroll
+    for (int k = 0; k < RS_TPB / 64; ++k) {
+      const uint32_t s = wsum[k];
+      off += k < wv ? s : 0u;
+      tot += s;
+    }
+    __syncthreads();
+    return off + x - v;
+  };
+  uint32_t carry;
+  {
+    uint32_t t;
+    scan((int)threadIdx.x < b ? (uint32_t)rowtot[threadIdx.x] : 0u, t);  // rows < b (nrows <= RADIX)
+    carry = t;
+  }
+  for (uint32_t c0 = 0; c0 < ncols; c0 += RS_TPB * RS_IPT) {
+    uint32_t v[RS_IPT], sum = 0;
+    const uint32_t j0 = c0 + threadIdx.x * RS_IPT;
+#pragma unroll
+    for (int k = 0; k < RS_IPT; ++k) {
+      v[k] = j0 + k < ncols ? row[j0 + k] : 0u;
+      sum += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = carry + scan(sum, tot);
+#pragma unroll
+    for (int k = 0; k < RS_IPT; ++k) {
+      if (j0 + k < ncols) row[j0 + k] = run;
+      run += v[k];
+    }
+    carry += tot;
   }
 }
 
@@ -2643,18 +2880,25 @@ struct MonoArgs {
 // (monotonic) counter to its target writes the pack's tag.  A call in which
 // a block gave up at a barrier never reaches the target: no tag, and the
 // host discards the call.  The host may read the pack as soon as it sees
-// the tag (radial_mono_run spins on it): every block's pack stores are
-// released at system scope before its count, the tag after the last count.
+// the tag (radial_mono_run spins on it).  The pack lives in coherent mapped
+// host memory (uncached on the device): a block's pack stores are performed
+// once its waves' vmcnt drains, before its agent-scope count; only the
+// block that completes the count issues the system-scope fence and the tag.
+// (A system-scope fence in EVERY block — an L2 write-back each — cost the
+// kernel 65 -> 73 us at 1M, round 3.)
 __device__ void mono_done(const MonoArgs &a, int tagpos) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's pack stores have landed
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence_system();
-    const uint64_t old = __hip_atomic_fetch_add(a.bar + BAR_LINE * 10, 1ull, __ATOMIC_ACQ_REL,
-                                                __HIP_MEMORY_SCOPE_SYSTEM);
-    if (old + 1 == a.done_target)
+    // relaxed: an acq_rel agent-scope add is an L2 write-back per block too
+    // (the pack stores are already performed: uncached memory, vmcnt drained)
+    const uint64_t old = __hip_atomic_fetch_add(a.bar + BAR_LINE * 10, 1ull, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == a.done_target) {
+      __threadfence_system();
       __hip_atomic_store((uint64_t *)(a.pack + tagpos), a.gen0, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -3035,15 +3279,8 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
 #pragma unroll
     for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: the fields are kernel-argument scalars
       if (q >= nm) break;
-      const int col = a.fs.col[q], fq = a.fs.f[q], wq = a.fs.w[q];
-      double *aq = acc + q * nb;
-#pragma unroll
-      for (int k = 0; k < MONO_SI; ++k) {
-        if (bk[k] >= (uint32_t)nb) continue;
-        const double f = fq == 0 ? xv[k] : mv[k];
-        const double ww = wq == 0 ? xv[k] : mv[k];
-        atomicAdd(&aq[bk[k]], monomial(col, f, ww));
-      }
+      mom_add<MONO_SI>(acc + q * nb, a.fs.op[q], a.fs.col[q], a.fs.f[q], a.fs.w[q], bk, xv, mv,
+                       (uint32_t)nb);
     }
     // element order (wave, k, lane) = particle order
     uint32_t dg[MONO_SI];
@@ -3496,6 +3733,7 @@ struct Profile {
   bool x_tiled = false;  // x holds a tiled selection (tile t at x[t * TILE ..]): ensure_x
   int64_t sel_base = 0, sel_span = 0;
   uint32_t sel_nt = 0;
+  uint32_t sel_rsub = 1;  // select_tiles' u16 level-0 rows per block (hinted calls)
   const double *sel_mass = nullptr;
   // one-launch radial path (radial_mono): tile records + group fill, grid
   // barrier words; barrier generation / completion count carried across calls
@@ -3946,15 +4184,21 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
       if (lazy && P.x_tiled) {  // persistent tiles (+ the hinted level-0 histogram)
         const int G0 = fused_grid(span);
         const unsigned G1 = (unsigned)(SH_K * (G0 - 1));
+        // tiles of the largest select block (tile_range of the assign block, split SH_K ways)
+        const uint64_t tab = ((uint64_t)nt + (G0 - 1) - 1) / (G0 - 1);
+        const uint64_t tsel = (tab + SH_K - 1) / SH_K + 1;
+        const uint32_t rsub = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>(SH_RSUB_MAX, (tsel + SH_TMAX - 1) / SH_TMAX));
+        P.sel_rsub = rsub;
         uint32_t *rows16 = nullptr;
         if (th && th->hint)
-          rows16 = (uint32_t *)P.srows.get(sizeof(uint32_t) * (size_t)G1 * (MS0_DIG / 2));
+          rows16 = (uint32_t *)P.srows.get(sizeof(uint32_t) * (size_t)G1 * rsub * (MS0_DIG / 2));
         uint32_t *wc = (uint32_t *)P.swc.get(sizeof(uint32_t) * (size_t)nt * SH_NW);
         uint32_t *bt = (uint32_t *)P.sbt.get(sizeof(uint32_t) * (size_t)G1);
         hipLaunchKernelGGL(sp.nfam > 1 ? select_tiles<true> : select_tiles<false>, dim3(G1),
                            dim3(SH_BT), 0, st, (const double *)d_pos, hi,
                            sp, nt, (uint32_t)G0, xo, kw, r.kpre, wc, toff, bt, mm,
-                           th ? th->hint : nullptr, th ? th->ka : 0ull, th ? th->kb : ~0ull, rows16,
+                           th ? th->hint : nullptr, th ? th->ka : 0ull, th ? th->kb : ~0ull, rows16, rsub,
                            (uint32_t *)(mm + 2 * MM_SLOTS));
       } else if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
       else if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
@@ -4911,6 +5155,9 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
           fs.f[slot] = f_src[k];
           fs.w[slot] = w_src[k];
           fs.col[slot] = c;
+          fs.op[slot] = key == 0x010u ? MO_W : key == 0x001u ? MO_X : key == 0x011u ? MO_XW
+                      : key == 0x012u ? MO_XXW : key == 0x002u ? MO_XX : key == 0x020u ? MO_WW
+                      : MO_GEN;
         }
         mono[(size_t)k * NMOM + c] = slot;
       }
@@ -4980,7 +5227,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                          rows);
       hipLaunchKernelGGL(msel_reduce0h, dim3(MS0_DIG / 2 / TPB, 32), dim3(TPB), 0, st,
                          (const uint32_t *)rows, g0, (const uint32_t *)P.srows.p,
-                         hinted ? SH_K * (g0 - 1) : 0, (const int32_t *)&ctl->hint, H);
+                         hinted ? SH_K * (g0 - 1) * (int)P.sel_rsub : 0, (const int32_t *)&ctl->hint, H);
       int64_t *gsc = nullptr;  // dist: [global kept count][ctl copy]
       uint32_t *lc_all = nullptr;
       if (dist) {
@@ -5001,7 +5248,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
                          (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff,
                          bcnt, dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr,
-                         (const uint32_t *)P.srows.p);
+                         (const uint32_t *)P.srows.p, P.sel_rsub);
       int64_t seg_total = 0;  // dist: keys in all ranks' group segments
       if (dist) {
         comm_allreduce(comm, lc_all, lc_all, (int64_t)cr.nranks * MS_MAXQ, 3, 0, st);
@@ -5043,7 +5290,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         bins8 = (uint8_t *)P.bins8.get((size_t)nt * TILE);  // by particle slot
         double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)(2 * g0) * macc) : nullptr;
         go = GatherOut{seg, (AgRec *)P.frec.get(sizeof(AgRec) * (size_t)n_sel), bcnt, bcnt + g0,
-                       bcnt + 2 * g0};
+                       bcnt + 2 * g0, cnt};
         const size_t lds = sizeof(double) * (size_t)macc + sizeof(uint32_t) * (size_t)(nr | 1) * AG_TR;
         auto ag = [&](auto kern) {
           hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, x, (const uint64_t *)P.kw.p,
@@ -5078,13 +5325,15 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         auto fd = [&](auto kern) {
           hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, (const FusedCtl *)ctl,
                              (const AgRec *)go.rec, (const uint32_t *)go.rbase,
-                             (const uint32_t *)go.rn, (const double *)de, (int)nb, bins8, th, nt,
-                             fs, maccs2);
+                             (const uint32_t *)go.rn, (const double *)de, (const uint32_t *)gq,
+                             (int)nb, bins8, th, nt, fs, maccs2, cnt);
         };
         if (fs.nm) fd(fix_deferred<true>);
         else fd(fix_deferred<false>);
         PBX_HIP(hipGetLastError());
-        scan_u32(P, st, th, (int64_t)nt * nr);
+        // the [bin][tile] table's exclusive scan, row by row (rows' totals in cnt)
+        hipLaunchKernelGGL(row_scan, dim3(nr), dim3(RS_TPB), 0, st, th, nt,
+                           (const unsigned long long *)cnt);
         cnt_offs = th;
         if (build_csr) {
           int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);

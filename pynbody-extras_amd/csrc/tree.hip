@@ -979,6 +979,9 @@ struct WalkParams {
   unsigned int *fault;           // set when a wave exceeds max_steps
   unsigned xcd_chunk;            // blocks per XCD chunk (0: launch order)
   unsigned long long *trace;     // diagnostic (PBX_WALK_TRACE): per block start, end, steps
+  const int2 *wtab;              // optional wave table (64-thread blocks): block -> {first t, count}
+  const uint32_t *wtab_n;        // its length (blocks past it exit)
+  unsigned nwt_max;              // host: the table's capacity (the grid)
 };
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
@@ -1110,17 +1113,35 @@ __device__ __forceinline__ void leaf_sum(const WalkParams &wp, int32_t s, int32_
 // scratch, 20 v_readlane, walk 44.5 -> 44.2 ms same-box A/B).
 // LCOST: per-lane interaction counts are wanted (cost kind 0 with a cost
 // array); otherwise their per-step VALU updates are compiled out
-template <int P, int WANT, bool SOFT, bool RAW, bool LCOST = true>
+// W8: 8 waves per SIMD (range walks of <= 8 x 1024 waves: every wave of the
+// grid resident at once, none waits for a slot; the register squeeze costs
+// the full walk, which keeps 7)
+template <int P, int WANT, bool SOFT, bool RAW, bool LCOST = true, bool W8 = false>
 __global__ void __launch_bounds__(WALK_TPB)
-    __attribute__((amdgpu_waves_per_eu((P <= 3 && !SOFT) ? 7 : 1, 7)))
+    __attribute__((amdgpu_waves_per_eu(W8 ? 8 : ((P <= 3 && !SOFT) ? 7 : 1), W8 ? 8 : 7)))
     walk_kernel(WalkParams wp) {
   constexpr int RS = rec_stride<P>();
   constexpr int NCH = (P == 2 || P == 3) ? RS / 8 : 1;  // chunks loaded eagerly
   const unsigned long long t_start = wp.trace ? (unsigned long long)wall_clock64() : 0ull;  // (100 MHz)
   const unsigned lb = wp.xcd_chunk ? xcd_chunk_swizzle(blockIdx.x, wp.xcd_chunk) : blockIdx.x;
-  const int64_t t = (int64_t)lb * blockDim.x + threadIdx.x;
   const bool lane0 = (threadIdx.x & 63) == 0;
-  const bool valid = t < wp.m;
+  int64_t t = (int64_t)lb * blockDim.x + threadIdx.x;
+  bool valid = t < wp.m;
+  if (wp.wtab) {  // (one wave per block) this wave's targets from the table
+    const uint32_t nwt = *wp.wtab_n;
+    if (lb >= nwt) {
+      if (wp.trace && lane0) {
+        wp.trace[3 * (int64_t)blockIdx.x] = 0;
+        wp.trace[3 * (int64_t)blockIdx.x + 1] = 0;
+        wp.trace[3 * (int64_t)blockIdx.x + 2] = 0;
+      }
+      return;
+    }
+    const int2 e = wp.wtab[lb];
+    const int ln = (int)(threadIdx.x & 63);
+    t = (int64_t)e.x + ln;
+    valid = ln < e.y;
+  }
   const bool self_mode = wp.tgt == nullptr;
   double tx = 0.0, ty = 0.0, tz = 0.0, th = 0.0;
   int32_t self32 = -1;  // this target's own record (self mode)
@@ -1327,6 +1348,87 @@ __global__ void __launch_bounds__(WALK_TPB)
       atomicAdd(&wp.counters[7], (unsigned long long)open_steps);
     }
   }
+}
+
+// Wave table of a self-mode walk of targets [first, first + m) (leaf order),
+// one 1024-thread block: group g = targets 64g .. 64g + 63, its cost c_g =
+// the larger earlier wave cost (original order, cost kind 1) of its two
+// halves' first targets.  Groups with c_g >= permille/1000 of the largest
+// (at most cap of them, and only groups of > 32 targets) become two 32-target
+// waves, listed first (their blocks dispatch first); the other groups follow
+// in order.  A wave walks the union of its targets' walks, and a 32-target
+// union takes ~0.85 of the steps of a 64-target one, so the
+// range walk's longest chains get shorter; every target's result is the
+// same whatever wave it is in (each lane sees exactly its own walk).
+__global__ void __launch_bounds__(1024)
+    wave_table_kernel(const int32_t *__restrict__ cost, const int32_t *__restrict__ perm,
+                      int64_t first, int64_t m, int permille, int2 *__restrict__ wtab,
+                      uint32_t *__restrict__ wtab_n, uint32_t cap) {
+  __shared__ int32_t red[16];
+  __shared__ uint32_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t G = (m + 63) / 64;
+  auto gcost = [&](int64_t g) {
+    const int64_t a = g * 64, b = a + 32;
+    int32_t c = cost[perm[first + a]];
+    if (b < m) c = max(c, cost[perm[first + b]]);
+    return c;
+  };
+  int32_t mx = 0;
+  for (int64_t g = tid; g < G; g += 1024) mx = max(mx, gcost(g));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) red[wv] = mx;
+  __syncthreads();
+  mx = 0;
+  for (int k = 0; k < 16; ++k) mx = max(mx, red[k]);
+  const int64_t thr = max<int64_t>(1, ((int64_t)mx * permille + 999) / 1000);
+  // heavy flag of group g (a group of > 32 targets at or above the threshold)
+  auto heavy0 = [&](int64_t g) { return g < G && g * 64 + 32 < m && gcost(g) >= thr; };
+  // pass 1: how many groups split (capped)
+  uint32_t nh = 0;
+  for (int64_t g = tid; g < G; g += 1024) nh += heavy0(g) ? 1u : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nh += __shfl_xor(nh, o, 64);
+  __syncthreads();
+  if (lane == 0) wsum[wv] = nh;
+  __syncthreads();
+  uint32_t H = 0;
+  for (int k = 0; k < 16; ++k) H += wsum[k];
+  H = min(H, cap);
+  __syncthreads();
+  // pass 2: positions (block scans of 1024 groups in order)
+  uint32_t hbase = 0;
+  for (int64_t g0 = 0; g0 < G; g0 += 1024) {
+    const int64_t g = g0 + tid;
+    const bool h0 = heavy0(g);
+    uint32_t x = h0 ? 1u : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      off += k < wv ? wsum[k] : 0u;
+      tot += wsum[k];
+    }
+    __syncthreads();
+    const uint32_t hi = hbase + off + x - (h0 ? 1u : 0u);  // heavy flags before g
+    if (g < G) {
+      const int cnt = (int)min<int64_t>(64, m - g * 64);
+      if (h0 && hi < cap) {  // split: two 32-target waves, first in the table
+        wtab[2 * hi] = make_int2((int)(g * 64), 32);
+        wtab[2 * hi + 1] = make_int2((int)(g * 64 + 32), cnt - 32);
+      } else {  // after the 2 H halves, in group order
+        wtab[2 * H + (uint32_t)(g - min(hi, cap))] = make_int2((int)(g * 64), cnt);
+      }
+    }
+    hbase += tot;
+  }
+  if (tid == 0) *wtab_n = (uint32_t)G + H;
 }
 
 __global__ void leaf_particles_kernel(const double4 *__restrict__ rec, const int32_t *__restrict__ perm,
@@ -1748,6 +1850,9 @@ struct Octree {
   Buf bal;                   // cost-balanced ranges: chunk sums + cuts
   Buf iscan, ilist, iws;     // payload: internal-node flags / scan, list, scan state
   int cost_kind = 0;                   // d_cost contents (WalkParams::cost_kind)
+  const int32_t *split_cost = nullptr;  // wave split: original-order wave costs (caller's memory)
+  int32_t split_permille = 0;
+  Buf wtab;                             // the wave table + its length
   Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
   Buf rec0;                  // {x, y, z, m} in original order (path_keys)
   bool rec0_valid = false;   // rec0 holds the current masses
@@ -2243,6 +2348,16 @@ static unsigned walk_xcd_chunk() {
   return c;
 }
 
+// small walk grids at 8 waves per SIMD (PBX_WALK_W8=0: off)
+constexpr unsigned kNumSimd = 1024;  // 256 CUs x 4
+static bool walk_w8() {
+  static const bool c = [] {
+    const char *v = std::getenv("PBX_WALK_W8");
+    return !(v && v[0] == '0');
+  }();
+  return c;
+}
+
 // threads per walk block (PBX_WALK_TPB: 64, 128 or 256)
 static unsigned walk_tpb() {
   static const unsigned c = [] {
@@ -2256,7 +2371,8 @@ static unsigned walk_tpb() {
 template <int P, int WANT>
 static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
   const unsigned tpb = walk_tpb();
-  unsigned grid = (unsigned)((wp.m + tpb - 1) / tpb);
+  unsigned grid = wp.wtab ? wp.nwt_max : (unsigned)((wp.m + tpb - 1) / tpb);
+  const unsigned waves = grid;  // (before the rounding: blocks past the work exit at once)
   wp.xcd_chunk = walk_xcd_chunk();
   if (wp.xcd_chunk) {  // whole rounds of kNumXcd chunks; the extra blocks find no targets
     const unsigned round = kNumXcd * wp.xcd_chunk;
@@ -2270,6 +2386,10 @@ static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
     hipLaunchKernelGGL((walk_kernel<P, WANT, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
   else if (raw && lcost)
     hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, true>), dim3(grid), dim3(tpb), 0, st, wp);
+  else if (raw && P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC) && tpb == 64 &&
+           waves <= 8u * kNumSimd && walk_w8())  // a range walk (config 5 at >= 8 ranks)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true>), dim3(grid), dim3(tpb), 0,
+                       st, wp);
   else if (raw)
     hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
   else if (lcost)
@@ -2314,19 +2434,38 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   wp.pot = d_pot;
   wp.acc = d_acc;
   wp.counters = ctr;
+  wp.max_steps = T.nn + 16;
+  wp.fault = (unsigned int *)(ctr + 2);
+  wp.cost_kind = T.cost_kind;
+  wp.wtab = nullptr;
+  wp.wtab_n = nullptr;
+  unsigned nwt_max = 0;  // wave table: at most this many waves
+  if (T.split_cost && d_tgt == nullptr && walk_tpb() == 64 && m > 0 && T.n > 0) {
+    // heavy 64-target groups of the earlier walk split in two, dispatched first
+    const int64_t G = (m + 63) / 64;
+    // at most 1/8 of the groups split; a grid that fits the 8-waves-per-SIMD
+    // slots (launch_walk_pw's W8) keeps fitting
+    const int64_t slots = 8 * (int64_t)kNumSimd;
+    const int64_t cap = G <= slots ? std::min<int64_t>(G / 8, slots - G) : G / 8;
+    nwt_max = (unsigned)(G + cap);
+    char *wb = (char *)T.wtab.get(sizeof(int2) * (size_t)nwt_max + 64);
+    wp.wtab = (const int2 *)(wb + 64);
+    wp.wtab_n = (const uint32_t *)wb;
+    hipLaunchKernelGGL(wave_table_kernel, dim3(1), dim3(1024), 0, st, T.split_cost,
+                       T.perm.as<int32_t>(), first, m, T.split_permille, (int2 *)(wb + 64),
+                       (uint32_t *)wb, (uint32_t)cap);
+  }
+  wp.nwt_max = nwt_max;
   wp.trace = nullptr;
   const char *trace_path = std::getenv("PBX_WALK_TRACE");  // diagnostic only
   unsigned tgrid = 0;
   if (trace_path) {
-    tgrid = (unsigned)((m + walk_tpb() - 1) / walk_tpb());
+    tgrid = nwt_max ? nwt_max : (unsigned)((m + walk_tpb() - 1) / walk_tpb());
     const unsigned c = walk_xcd_chunk();
     if (c) tgrid = (tgrid + kNumXcd * c - 1) / (kNumXcd * c) * (kNumXcd * c);
     tgrid *= walk_tpb() / 64;  // one trace record per wave
     wp.trace = (unsigned long long *)T.trace.get(24 * (size_t)tgrid);
   }
-  wp.max_steps = T.nn + 16;
-  wp.fault = (unsigned int *)(ctr + 2);
-  wp.cost_kind = T.cost_kind;
   // softened leaves need softenings; the guard needs h_max; at query points
   // there is no target softening (tree.rs:1516,1547)
   const bool soft = T.has_hmax || T.soft_set;
@@ -2799,6 +2938,16 @@ int pbx_octree_cost_to_orig(pbx_octree *t, const int32_t *d_cost_leaf, int32_t *
       hipLaunchKernelGGL(cost_to_orig, dim3(nblk(T.n)), dim3(TPB), 0, dev.stream, d_cost_leaf,
                          T.perm.as<int32_t>(), T.n, d_cost_orig);
     PBX_HIP(hipGetLastError());
+  });
+}
+
+int pbx_octree_set_wave_split(pbx_octree *t, const int32_t *d_cost_orig, int permille) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    if (d_cost_orig && (permille < 1 || permille > 1000))
+      fail(PBX_ERR_VALUE, "permille must be in [1, 1000]");
+    T.split_cost = d_cost_orig;
+    T.split_permille = permille;
   });
 }
 

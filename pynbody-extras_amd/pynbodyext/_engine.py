@@ -317,6 +317,12 @@ class Octree:
         """Per-target costs in this build's leaf order -> original order."""
         nat.call("pbx_octree_cost_to_orig", self._h, d_cost_leaf, d_cost_orig)
 
+    def _set_wave_split(self, d_cost_orig, permille: int = 750) -> None:
+        """Range walks split the 64-target groups whose earlier wave cost
+        (original order, cost kind 1) is >= permille/1000 of the largest into
+        two 32-target waves dispatched first (speed only); None: off."""
+        nat.call("pbx_octree_set_wave_split", self._h, d_cost_orig or None, int(permille))
+
     def _set_cost_kind(self, kind: int) -> None:
         """compute_range's d_cost: 0 interactions per target, 1 the wave's work."""
         nat.call("pbx_octree_set_cost_kind", self._h, int(kind))

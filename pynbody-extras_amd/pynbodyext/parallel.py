@@ -24,6 +24,8 @@ from __future__ import annotations
 import ctypes
 from ctypes import c_int64, c_void_p
 
+import os
+
 import numpy as np
 
 from . import _native as nat
@@ -438,6 +440,9 @@ class ShardedTree:
         self.d_cost = nat.DeviceArray(4 * max(cap, 1))       # leaf order, last walk
         self.d_cost_orig = nat.DeviceArray(4 * max(cap, 1))  # original order, carried
         self.have_costs = False
+        # range walks: split 64-target groups whose earlier wave cost is >=
+        # this fraction (per mille) of the largest (PBX_WAVE_SPLIT=0: off)
+        self.split_permille = int(os.environ.get("PBX_WAVE_SPLIT", "800"))
         self.info = None
         self.d_prof = None  # [counts | moments] of the profile all-reduce
 
@@ -483,6 +488,10 @@ class ShardedTree:
             self.comm.allgatherv(self.d_cost.ptr, [4 * c for _, c in self.ranges],
                                  [4 * f for f, _ in self.ranges])
         self.tree._cost_to_orig_device(self.d_cost.ptr, self.d_cost_orig.ptr)
+        if not self.have_costs and self.split_permille:
+            # later range walks split their heaviest 64-target groups into two
+            # 32-target waves dispatched first (the costs stay in d_cost_orig)
+            self.tree._set_wave_split(self.d_cost_orig.ptr, self.split_permille)
         self.have_costs = True
 
     def profile(self, dev_bins, edges) -> np.ndarray:

@@ -189,6 +189,10 @@ class MockOctree:
     def _set_cost_kind(self, kind):
         self.kind = kind
 
+    def _set_wave_split(self, d_cost_orig, permille=750):
+        # speed only on the device (every target's result unchanged): recorded
+        self.split = (d_cost_orig, permille)
+
     def _rebuild_device(self, d_pos, n, d_mass):
         self.__init__(view(d_pos, 24 * n, np.float64).reshape(n, 3).copy(),
                       view(d_mass, 8 * n, np.float64).copy(), 8, 3)

@@ -730,6 +730,40 @@ def test_radial_equaln_tiled_level0_hint_transitions(gpu):
         h.close()
 
 
+def test_radial_equaln_level0_hint_many_tiles_per_block(gpu):
+    """A span above 765 select blocks x 15 tiles x 4096 (~47M particles):
+    each select_tiles block flushes its u16 level-0 counts to a new row every
+    15 tiles, so the repeated call still takes the hinted
+    histogram — edges, counts and CSR identical to the first (re-read) call,
+    the first call's edges and counts equal to the oracle's."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(47)
+    n = 52_000_000  # 12,696 tiles: 17 per select block -> 2 rows
+    pos = rng.normal(scale=2.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    h = DeviceBins()
+    try:
+        _, e1, c1, m1 = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h)
+        p1, o1 = h.csr()
+        assert h.level0_stats() == {"tiled": 1, "hinted": 0}, h.level0_stats()
+        _, e2, c2, m2 = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h)
+        assert h.level0_stats() == {"tiled": 2, "hinted": 1}, h.level0_stats()
+        p2, o2 = h.csr()
+        assert np.array_equal(e2, e1) and np.array_equal(c2, c1)
+        assert np.array_equal(o2, o1) and np.array_equal(p2, p1)
+        for u, v in zip(m2, m1):
+            np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300)
+        r = np.sqrt((pos[:, 0] * pos[:, 0] + pos[:, 1] * pos[:, 1]) + pos[:, 2] * pos[:, 2])
+        del pos
+        edges = pr.edges_equaln(r, 128)
+        counts = np.bincount(pr.bin_ids(r, edges), minlength=129)[:128]
+        assert np.array_equal(e1, edges) and np.array_equal(c1, counts)
+    finally:
+        h.close()
+
+
 def test_radial_equaln_level0_hint_switch(gpu):
     """set_level0_hint(False) (the bench's cold-handle timing): repeated
     tiled calls on one handle re-read x every time — no call hinted — and

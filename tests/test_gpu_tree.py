@@ -425,7 +425,33 @@ def test_range_walk_wave_costs(gpu):
     wave = cost[:, 0].astype(np.int64)
     assert wave.min() > 0
     assert info["wave_steps"] + info["leaf_wave_steps"] <= wave.sum()
-    for a in (d_pot, d_acc, d_cost):
+    # wave split (speed only): the heaviest 64-target groups walk as two
+    # 32-target waves, dispatched first — every target of the full walk and
+    # of range walks bit-identical, every output written (NaN-filled first)
+    d_orig = nat.DeviceArray(4 * n)
+    dev._cost_to_orig_device(d_cost.ptr, d_orig.ptr)
+
+    def walk_fresh(first, count):
+        d_pot.upload(np.full(n, np.nan))
+        d_acc.upload(np.full((n, 3), np.nan))
+        return walk(first, count)
+
+    for permille in (1000, 750, 1):  # the largest group(s) only / the top / every group (capped)
+        dev._set_wave_split(d_orig.ptr, permille)
+        try:
+            p2, a2 = walk_fresh(0, n)
+            assert np.array_equal(p2, p0) and np.array_equal(a2, a0), permille
+            for first, count in ((0, 1000), (12_345, 64 * 700 + 5), (n - 77, 77), (5, 31)):
+                p3, a3 = walk_fresh(first, count)
+                assert np.array_equal(p3, p0[first:first + count]), (permille, first)
+                assert np.array_equal(a3, a0[first:first + count]), (permille, first)
+        finally:
+            dev._set_wave_split(None, 0)
+    with pytest.raises(ValueError, match="permille"):
+        dev._set_wave_split(d_orig.ptr, 0)
+    p4, a4 = walk_fresh(0, n)
+    assert np.array_equal(p4, p0) and np.array_equal(a4, a0)
+    for a in (d_pot, d_acc, d_cost, d_orig):
         a.free()
 
 
