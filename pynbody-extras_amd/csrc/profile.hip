@@ -929,13 +929,8 @@ constexpr uint32_t SH_RSUB_MAX = 8;  // u16 count rows per block (flushed every 
 // FAM: several family slices (membership tested per particle); else every
 // particle of the span [base, n) is a member (no family, or one slice: the
 // span is that slice) and the 16 slice bounds stay out of the registers.
-#ifdef PBX_ST_3BUF
-#define PBX_SH_WAVES 4  // two blocks per CU
-#else
-#define PBX_SH_WAVES 1
-#endif
 template <bool FAM>
-__global__ void __launch_bounds__(SH_BT, PBX_SH_WAVES)
+__global__ void __launch_bounds__(SH_BT)
     select_tiles(const double *__restrict__ pos, int64_t n, SelectParams p, uint32_t nt,
                  uint32_t G0, double *__restrict__ xo, uint64_t *__restrict__ kw,
                  uint16_t *__restrict__ kpre, uint32_t *__restrict__ wcnt,
@@ -1058,36 +1053,6 @@ __global__ void __launch_bounds__(SH_BT, PBX_SH_WAVES)
       __syncthreads();
     }
   };
-#ifdef PBX_ST_3BUF
-  // three half buffers, two halves in flight while one is selected (twice
-  // the loads in flight per wave at the same occupancy: 2 blocks per CU)
-  const uint32_t nh = 2 * (tb - ta);
-  auto hld = [&](uint32_t k, Half &H) {  // half k of the block's range (past it: the last again)
-    const uint32_t kk = k < nh ? k : nh - 1;
-    ld(ta + kk / 2, (int)(kk & 1), H);
-  };
-  auto hsel = [&](uint32_t k, const Half &H) {
-    const uint32_t tile = ta + k / 2;
-    if ((k & 1) == 0) run = 0;
-    sel(tile, (int)(k & 1), H);
-    if (k & 1) tile_end(tile);
-  };
-  Half A, B, C;
-  if (nh) {
-    hld(0, A);
-    hld(1, B);
-  }
-  for (uint32_t k = 0; k < nh; k += 3) {
-    hld(k + 2, C);
-    hsel(k, A);
-    if (k + 1 >= nh) break;
-    hld(k + 3, A);
-    hsel(k + 1, B);
-    if (k + 2 >= nh) break;
-    hld(k + 4, B);
-    hsel(k + 2, C);
-  }
-#else
   Half A, B;
   if (ta < tb) ld(ta, 0, A);
   for (uint32_t tile = ta; tile < tb; ++tile) {
@@ -1098,7 +1063,8 @@ __global__ void __launch_bounds__(SH_BT, PBX_SH_WAVES)
     sel(tile, 1, B);
     tile_end(tile);
   }
-#endif
+  // (three half buffers with two halves in flight, at the same 2 blocks per
+  // CU: 273 -> 275 us — the loads in flight are not what bounds it: dropped)
   // the block's key range: one atomic pair per block
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1578,17 +1544,13 @@ __device__ __forceinline__ double monomial(int col, double f, double ww) {
 
 // aq[bk[k]] += monomial of slot (op, col, fq, wq) for the K elements whose bin
 // is < nb (LDS atomics)
-// dummy (optional): a per-lane LDS slot that takes the adds of elements
-// whose bin is >= nb, so no add is under a branch (no exec-mask jumps)
 template <int K>
 __device__ __forceinline__ void mom_add(double *aq, int op, int col, int fq, int wq,
                                         const uint32_t *bk, const double *xv, const double *wv,
-                                        uint32_t nb, double *dummy = nullptr) {
-#define PBX_MOM_LOOP(EXPR)                                                          \
-  _Pragma("unroll") for (int k = 0; k < K; ++k) {                                   \
-    if (dummy) atomicAdd(bk[k] < nb ? &aq[bk[k]] : dummy, (EXPR));                  \
-    else if (bk[k] < nb) atomicAdd(&aq[bk[k]], (EXPR));                             \
-  }                                                                                 \
+                                        uint32_t nb) {
+#define PBX_MOM_LOOP(EXPR)                                     \
+  _Pragma("unroll") for (int k = 0; k < K; ++k) if (bk[k] < nb) \
+      atomicAdd(&aq[bk[k]], (EXPR));                           \
   return;
   switch (op) {
     case MO_W: PBX_MOM_LOOP(wv[k])
@@ -2111,7 +2073,6 @@ struct GatherOut {
   AgRec *rec;             // deferred keys, block by block
   const uint32_t *bcnt;   // per block: keys gathered (fused_boff)
   uint32_t *rbase, *rn;   // per block: list start, deferred keys written
-  unsigned long long *rowtot;  // per bin (nb + 1 rows): kept particles, summed over blocks
 };
 
 // exclusive sum of v[0 .. k) over a block (k <= blockDim.x)
@@ -2144,10 +2105,6 @@ __global__ void __launch_bounds__(MS0_TPB)
   __shared__ uint32_t qd[RADIX];
   __shared__ uint32_t red[MS0_TPB / 64];
   __shared__ uint32_t dk;
-#ifdef PBX_AG_BF
-  __shared__ uint32_t thd[64];   // per-lane sinks of the branch-free adds
-  __shared__ double mdummy[64];
-#endif
   const int macc = MOM ? fs.nm * nb : 0;
   double *acc = (double *)smem;
   const int nr = nb + 1, nrs = nr | 1;  // th row stride odd: flush reads bank-conflict free
@@ -2252,23 +2209,14 @@ __global__ void __launch_bounds__(MS0_TPB)
     }
     const uint32_t sbase = t * (uint32_t)TILE + 64u * (uint32_t)(wl * AG_W) + lane;
 #ifndef PBX_DIAG_AG_NOBIN  // (timing diagnostic: no byte stores / tile counts)
-#ifdef PBX_AG_BF
-    // branch-free: every slot's byte is stored (a skipped slot's 0xff is never
-    // read — csr_slots takes kept slots only — and a deferred slot's 0xfe is
-    // overwritten by fix_deferred), counts of non-bins go to a per-lane dummy
-#pragma unroll
-    for (int kk = 0; kk < AG_W; ++kk) {
-      bins[sbase + 64u * kk] = (uint8_t)bk[kk];
-      atomicAdd(bk[kk] <= (uint32_t)nb ? &th[tl * nrs + bk[kk]] : &thd[lane], 1u);
-    }
-#else
+    // (branch-free byte stores and adds — non-bins into per-lane LDS dummies —
+    // measured the same, 179 us at 64M: the branches are not the cost)
 #pragma unroll
     for (int kk = 0; kk < AG_W; ++kk)
       if (bk[kk] <= (uint32_t)nb) {
         bins[sbase + 64u * kk] = (uint8_t)bk[kk];
         atomicAdd(&th[tl * nrs + bk[kk]], 1u);
       }
-#endif
 #endif
 #ifdef PBX_DIAG_AG_NOSUM  // (timing diagnostic: no per-bin sums)
     if (false) {
@@ -2278,42 +2226,22 @@ __global__ void __launch_bounds__(MS0_TPB)
 #pragma unroll
       for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
         if (q >= fs.nm) break;
-#ifdef PBX_AG_BF
-        mom_add<AG_W>(acc + q * nb, fs.op[q], fs.col[q], fs.f[q], fs.w[q], bk, P.v, wv,
-                      (uint32_t)nb, &mdummy[lane]);
-#else
         mom_add<AG_W>(acc + q * nb, fs.op[q], fs.col[q], fs.f[q], fs.w[q], bk, P.v, wv,
                       (uint32_t)nb);
-#endif
       }
     }
-    if (anydef) {  // ~1-3 % of the keys (edge-holding digits), but some lane of almost every
-                   // call: the group segments + the block's deferred list.  One list
-                   // reservation per call for the wave (ballot ranks), the segment slots'
-                   // LDS atomics all issued before any is waited for.
-      uint64_t bal[AG_W], off[AG_W];
-      uint32_t g[AG_W], ss[AG_W], nd = 0;
+    if (anydef) {  // rare (edge-holding digits): the group segment + the block's deferred list
+      // (one list reservation per call for the whole wave, ballot ranks, and
+      // every segment-slot atomic issued before any is waited for: 179 -> 184
+      // us at 64M — dropped)
 #pragma unroll
-      for (int kk = 0; kk < AG_W; ++kk) {
-        const bool d = bk[kk] == DEFER;
-        bal[kk] = __ballot(d);
-        off[kk] = dkey(P.v[kk]) - lo;
-        g[kk] = d ? dtab[(uint32_t)(off[kk] >> s)] & 0x7fffu : 0u;
-        ss[kk] = d ? atomicAdd(&sslot[g[kk]], 1u) : 0u;
-        nd += (uint32_t)__popcll(bal[kk]);
-      }
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&dk, nd);
-      base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-#pragma unroll
-      for (int kk = 0; kk < AG_W; ++kk) {
+      for (int kk = 0; kk < AG_W; ++kk)
         if (bk[kk] == DEFER) {
-          go.seg[ss[kk]] = off[kk];
-          go.rec[rb + base + rank_below(bal[kk])] =
-              AgRec{off[kk], wv[kk], sbase + 64u * kk, t | (g[kk] << AG_TBITS)};
+          const uint64_t off = dkey(P.v[kk]) - lo;
+          const uint32_t g = dtab[(uint32_t)(off >> s)] & 0x7fffu;
+          go.seg[atomicAdd(&sslot[g], 1u)] = off;
+          go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{off, wv[kk], sbase + 64u * kk, t | (g << AG_TBITS)};
         }
-        base += (uint32_t)__popcll(bal[kk]);
-      }
     }
   };
   for (uint32_t r0 = ta; r0 < tb; r0 += AG_TR) {
@@ -2345,12 +2273,6 @@ __global__ void __launch_bounds__(MS0_TPB)
       const int b = k / AG_TR, tl = k - b * AG_TR;
       if (tl < nrt) tile_hist[(int64_t)b * nt + r0 + tl] = th[tl * nrs + b];
     }
-    if (go.rowtot)  // the rows' totals (row_scan's bases): one atomic per bin and flush
-      for (int b = tid; b < nr; b += MS0_TPB) {
-        uint32_t c = 0;
-        for (int tl = 0; tl < nrt; ++tl) c += th[tl * nrs + b];
-        if (c) atomicAdd(&go.rowtot[b], (unsigned long long)c);
-      }
     __syncthreads();
     for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
     __syncthreads();
@@ -2404,9 +2326,8 @@ __global__ void __launch_bounds__(MS0_TPB)
                  const uint32_t *__restrict__ rbase, const uint32_t *__restrict__ rn,
                  const double *__restrict__ edges, const uint32_t *__restrict__ gq, int nb,
                  uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, uint32_t nt,
-                 FusedStats fs, double *__restrict__ slab, unsigned long long *__restrict__ rowtot) {
+                 FusedStats fs, double *__restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ uint32_t dtot[RADIX];  // per-bin totals of the block's deferred keys (rowtot)
   const int macc = MOM ? fs.nm * nb : 0;
   double *acc = (double *)smem;
   double *e = acc + macc;
@@ -2417,10 +2338,7 @@ __global__ void __launch_bounds__(MS0_TPB)
   tile_range(nt, ta, tb);
   const uint32_t wt = (uint32_t)(FD_LDSW / nrs);  // tiles per window
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
-  for (int k = tid; k <= nb; k += MS0_TPB) {
-    e[k] = edges[k];
-    dtot[k] = 0;
-  }
+  for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
   const bool ok_all = !(ctl->err & 2);
   const int64_t r0 = rbase[blockIdx.x], cnt = ok_all ? (int64_t)rn[blockIdx.x] : 0;
   const uint64_t lo = ctl->lo;
@@ -2444,10 +2362,7 @@ __global__ void __launch_bounds__(MS0_TPB)
         const uint32_t t = r[u].tg & ((1u << AG_TBITS) - 1), g = r[u].tg >> AG_TBITS;
         const uint32_t b = ok ? bin_of_in(v, e, nb, (int)gq[g], (int)gq[g + 1]) : (uint32_t)nb;
         if (ok) {
-          if (first) {
-            bins[r[u].pos] = (uint8_t)b;
-            if (rowtot) atomicAdd(&dtot[b], 1u);
-          }
+          if (first) bins[r[u].pos] = (uint8_t)b;
           if (t >= w0 && t < w1) atomicAdd(&tc[(t - w0) * nrs + b], 1u);
         }
         if (MOM && first && ok && b < (uint32_t)nb)
@@ -2469,73 +2384,10 @@ __global__ void __launch_bounds__(MS0_TPB)
     if (w1 >= tb) break;
     __syncthreads();
   }
-  __syncthreads();
-  if (rowtot)
-    for (int k = tid; k <= nb; k += MS0_TPB)
-      if (dtot[k]) atomicAdd(&rowtot[k], (unsigned long long)dtot[k]);
   if (MOM) {
+    __syncthreads();
     double *dst = slab + (int64_t)blockIdx.x * macc;
     for (int k2 = tid; k2 < macc; k2 += MS0_TPB) dst[k2] = acc[k2];
-  }
-}
-
-// The flat exclusive scan of the [bin][tile] table (row-major, nrows x ncols)
-// as nrows independent row scans: block b adds the totals of rows < b
-// (rowtot, summed by assign_gather / fix_deferred) to its row's own
-// exclusive prefix — the same words as scan_u32 over the whole table, with no
-// chain of look-backs across ~nt * nrows / 4096 tiles (11 -> ~3 us at 64M).
-constexpr int RS_TPB = 1024, RS_IPT = 16;  // a row of <= 16K tiles in one pass
-static_assert(RS_TPB >= RADIX, "one thread per row total");
-__global__ void __launch_bounds__(RS_TPB)
-    row_scan(uint32_t *__restrict__ a, uint32_t ncols, const unsigned long long *__restrict__ rowtot) {
-  __shared__ uint32_t wsum[RS_TPB / 64];
-  const int b = blockIdx.x;
-  const uint32_t lane = lane_id();
-  const int wv = threadIdx.x >> 6;
-  uint32_t *row = a + (int64_t)b * ncols;
-  // a 16-wave exclusive scan of one value per thread (+ the block total)
-  auto scan = [&](uint32_t v, uint32_t &tot) {
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t off = 0;
-    tot = 0;
-#pragma unroll
-    for (int k = 0; k < RS_TPB / 64; ++k) {
-      const uint32_t s = wsum[k];
-      off += k < wv ? s : 0u;
-      tot += s;
-    }
-    __syncthreads();
-    return off + x - v;
-  };
-  uint32_t carry;
-  {
-    uint32_t t;
-    scan((int)threadIdx.x < b ? (uint32_t)rowtot[threadIdx.x] : 0u, t);  // rows < b (nrows <= RADIX)
-    carry = t;
-  }
-  for (uint32_t c0 = 0; c0 < ncols; c0 += RS_TPB * RS_IPT) {
-    uint32_t v[RS_IPT], sum = 0;
-    const uint32_t j0 = c0 + threadIdx.x * RS_IPT;
-#pragma unroll
-    for (int k = 0; k < RS_IPT; ++k) {
-      v[k] = j0 + k < ncols ? row[j0 + k] : 0u;
-      sum += v[k];
-    }
-    uint32_t tot;
-    uint32_t run = carry + scan(sum, tot);
-#pragma unroll
-    for (int k = 0; k < RS_IPT; ++k) {
-      if (j0 + k < ncols) row[j0 + k] = run;
-      run += v[k];
-    }
-    carry += tot;
   }
 }
 
@@ -5290,7 +5142,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         bins8 = (uint8_t *)P.bins8.get((size_t)nt * TILE);  // by particle slot
         double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)(2 * g0) * macc) : nullptr;
         go = GatherOut{seg, (AgRec *)P.frec.get(sizeof(AgRec) * (size_t)n_sel), bcnt, bcnt + g0,
-                       bcnt + 2 * g0, cnt};
+                       bcnt + 2 * g0};
         const size_t lds = sizeof(double) * (size_t)macc + sizeof(uint32_t) * (size_t)(nr | 1) * AG_TR;
         auto ag = [&](auto kern) {
           hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, x, (const uint64_t *)P.kw.p,
@@ -5326,14 +5178,15 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
           hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, (const FusedCtl *)ctl,
                              (const AgRec *)go.rec, (const uint32_t *)go.rbase,
                              (const uint32_t *)go.rn, (const double *)de, (const uint32_t *)gq,
-                             (int)nb, bins8, th, nt, fs, maccs2, cnt);
+                             (int)nb, bins8, th, nt, fs, maccs2);
         };
         if (fs.nm) fd(fix_deferred<true>);
         else fd(fix_deferred<false>);
         PBX_HIP(hipGetLastError());
-        // the [bin][tile] table's exclusive scan, row by row (rows' totals in cnt)
-        hipLaunchKernelGGL(row_scan, dim3(nr), dim3(RS_TPB), 0, st, th, nt,
-                           (const unsigned long long *)cnt);
+        // (a row-wise scan — one block per bin row, its base from row totals
+        // summed by assign_gather / fix_deferred — took 15-16 us against this
+        // one-pass look-back scan's 11 us at 64M: dropped)
+        scan_u32(P, st, th, (int64_t)nt * nr);
         cnt_offs = th;
         if (build_csr) {
           int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);

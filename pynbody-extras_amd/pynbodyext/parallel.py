@@ -441,8 +441,10 @@ class ShardedTree:
         self.d_cost_orig = nat.DeviceArray(4 * max(cap, 1))  # original order, carried
         self.have_costs = False
         # range walks: split 64-target groups whose earlier wave cost is >=
-        # this fraction (per mille) of the largest (PBX_WAVE_SPLIT=0: off)
-        self.split_permille = int(os.environ.get("PBX_WAVE_SPLIT", "800"))
+        # this fraction (per mille) of the largest into two 32-target waves
+        # (PBX_WAVE_SPLIT=900, say).  Off by default: at 8 ranks of 4M it
+        # moved the longest range walk by noise only
+        self.split_permille = int(os.environ.get("PBX_WAVE_SPLIT", "0"))
         self.info = None
         self.d_prof = None  # [counts | moments] of the profile all-reduce
 
