@@ -2199,7 +2199,11 @@ __global__ void __launch_bounds__(MS0_TPB)
       const bool kp = (P.k[kk] >> lane) & 1ull;
       const uint64_t key = dkey(P.v[kk]);
       const bool inw = win && key >= ka && key <= kb;  // fused_hist0's window
+#ifdef PBX_DIAG_AG_NOTAB  // timing diagnostic only: no digit-table lookup
+      const uint32_t e = (uint32_t)(key >> 45) & 127u;
+#else
       const uint32_t e = dtab[inw ? (uint32_t)((key - lo) >> s) : 0u];
+#endif
       // (NaN in a digit without edges: no NaN edge, dropped like the table says;
       // NaN in a group's digit is deferred: its bin is below the first NaN edge)
       const bool def = kp && inw && (e & 0x8000u);
@@ -2230,6 +2234,9 @@ __global__ void __launch_bounds__(MS0_TPB)
                       (uint32_t)nb);
       }
     }
+#ifdef PBX_DIAG_AG_NODEFER  // timing diagnostic only: deferred keys dropped
+    anydef = 0;
+#endif
     if (anydef) {  // rare (edge-holding digits): the group segment + the block's deferred list
       // (one list reservation per call for the whole wave, ballot ranks, and
       // every segment-slot atomic issued before any is waited for: 179 -> 184
@@ -2328,6 +2335,7 @@ __global__ void __launch_bounds__(MS0_TPB)
                  uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, uint32_t nt,
                  FusedStats fs, double *__restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t gql[MS_MAXQ + 1];  // the groups' first ranks (gq), ng + 1 of them
   const int macc = MOM ? fs.nm * nb : 0;
   double *acc = (double *)smem;
   double *e = acc + macc;
@@ -2340,6 +2348,7 @@ __global__ void __launch_bounds__(MS0_TPB)
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
   for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
   const bool ok_all = !(ctl->err & 2);
+  for (int k = tid; k <= (ok_all ? ctl->ng : -1); k += MS0_TPB) gql[k] = gq[k];
   const int64_t r0 = rbase[blockIdx.x], cnt = ok_all ? (int64_t)rn[blockIdx.x] : 0;
   const uint64_t lo = ctl->lo;
   for (uint32_t w0 = ta; w0 < tb || (w0 == ta && cnt); w0 += wt) {  // (block-uniform)
@@ -2360,12 +2369,20 @@ __global__ void __launch_bounds__(MS0_TPB)
         const double v = dkey_inv(lo + r[u].off);
         const bool ok = i < cnt;
         const uint32_t t = r[u].tg & ((1u << AG_TBITS) - 1), g = r[u].tg >> AG_TBITS;
-        const uint32_t b = ok ? bin_of_in(v, e, nb, (int)gq[g], (int)gq[g + 1]) : (uint32_t)nb;
+        const uint32_t b = ok ? bin_of_in(v, e, nb, (int)gql[g], (int)gql[g + 1]) : (uint32_t)nb;
         if (ok) {
+#ifdef PBX_DIAG_FD_NOBYTE  // timing diagnostic only: deferred bins not stored
+          if (first && b == 0xdead) bins[r[u].pos] = (uint8_t)b;
+#else
           if (first) bins[r[u].pos] = (uint8_t)b;
+#endif
           if (t >= w0 && t < w1) atomicAdd(&tc[(t - w0) * nrs + b], 1u);
         }
+#ifdef PBX_DIAG_FD_NOSUM  // timing diagnostic only: no sums
+        if (false)
+#else
         if (MOM && first && ok && b < (uint32_t)nb)
+#endif
 #pragma unroll
           for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
             if (q >= fs.nm) break;
@@ -2608,7 +2625,11 @@ __global__ void __launch_bounds__(TPB)
   __syncthreads();
   for (int j = threadIdx.x; j < (int)tn; j += TPB) {
     const uint32_t dgt = sk[j];
+#ifdef PBX_DIAG_CSR_NOSTORE  // timing diagnostic only: the permutation not written
+    if (dgt == 0xdead) perm[0] = (int32_t)(o + sv[j]) + (int32_t)(gofs[dgt] - dstart[dgt]);
+#else
     perm[gofs[dgt] + ((uint32_t)j - dstart[dgt])] = (int32_t)(o + sv[j]);
+#endif
   }
 }
 

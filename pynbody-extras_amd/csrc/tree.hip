@@ -2348,12 +2348,12 @@ static unsigned walk_xcd_chunk() {
   return c;
 }
 
-// small walk grids at 8 waves per SIMD (PBX_WALK_W8=0: off)
+// small walk grids at 8 waves per SIMD (PBX_WALK_W8=0: off; =2: every grid)
 constexpr unsigned kNumSimd = 1024;  // 256 CUs x 4
-static bool walk_w8() {
-  static const bool c = [] {
+static int walk_w8() {
+  static const int c = [] {
     const char *v = std::getenv("PBX_WALK_W8");
-    return !(v && v[0] == '0');
+    return v ? (v[0] == '0' ? 0 : v[0] == '2' ? 2 : 1) : 1;
   }();
   return c;
 }
@@ -2387,7 +2387,7 @@ static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
   else if (raw && lcost)
     hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, true>), dim3(grid), dim3(tpb), 0, st, wp);
   else if (raw && P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC) && tpb == 64 &&
-           waves <= 8u * kNumSimd && walk_w8())  // a range walk (config 5 at >= 8 ranks)
+           ((waves <= 8u * kNumSimd && walk_w8()) || walk_w8() == 2))  // a range walk (config 5, >= 8 ranks)
     hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true>), dim3(grid), dim3(tpb), 0,
                        st, wp);
   else if (raw)
