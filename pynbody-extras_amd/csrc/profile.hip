@@ -467,7 +467,10 @@ __global__ void gather_keys(const uint64_t *__restrict__ keys, const int64_t *__
 // and appends them to a compact list; deeper levels work on that list only,
 // compacting again as they go.  No sort, no host round trip until the edges
 // are done.
-constexpr int MS0_BITS = 14;
+#ifndef PBX_MS0_BITS
+#define PBX_MS0_BITS 14
+#endif
+constexpr int MS0_BITS = PBX_MS0_BITS;
 constexpr int MS0_DIG = 1 << MS0_BITS;
 constexpr int MS0_TPB = 1024;
 constexpr int MS_BITS = 12;
@@ -2102,9 +2105,9 @@ __global__ void __launch_bounds__(MS0_TPB)
   // or 0x8000 | group when the digit holds edges — one LDS read per key
   __shared__ uint16_t dtab[MS0_DIG];
   __shared__ uint32_t sslot[RADIX];
+  __shared__ uint32_t dk;
   __shared__ uint32_t qd[RADIX];
   __shared__ uint32_t red[MS0_TPB / 64];
-  __shared__ uint32_t dk;
   const int macc = MOM ? fs.nm * nb : 0;
   double *acc = (double *)smem;
   const int nr = nb + 1, nrs = nr | 1;  // th row stride odd: flush reads bank-conflict free
@@ -2177,7 +2180,7 @@ __global__ void __launch_bounds__(MS0_TPB)
       P.k[kk] = kw[(s0 >> 6) + kk + vz];
     }
   };
-  constexpr uint32_t SKIP = 0xffffu, DEFER = 0xfffeu;
+  constexpr uint32_t SKIP = 0xffffu, DEFER = 0x10000u;  // DEFER + group: a deferred key
   auto bin = [&](uint32_t t, uint32_t tl, const Part &P) {
 #ifdef PBX_DIAG_AG_LOADONLY  // timing diagnostic only: loads consumed, nothing binned
     {
@@ -2207,7 +2210,8 @@ __global__ void __launch_bounds__(MS0_TPB)
       // (NaN in a digit without edges: no NaN edge, dropped like the table says;
       // NaN in a group's digit is deferred: its bin is below the first NaN edge)
       const bool def = kp && inw && (e & 0x8000u);
-      bk[kk] = !kp ? SKIP : def ? DEFER : inw ? e : (uint32_t)nb;
+      // a deferred key carries its group: DEFER + g (no second table lookup)
+      bk[kk] = !kp ? SKIP : def ? DEFER + (e & 0x7fffu) : inw ? e : (uint32_t)nb;
       wv[kk] = wneed ? P.m[kk] : 1.0;
       anydef |= __ballot(def);
     }
@@ -2243,9 +2247,9 @@ __global__ void __launch_bounds__(MS0_TPB)
       // us at 64M — dropped)
 #pragma unroll
       for (int kk = 0; kk < AG_W; ++kk)
-        if (bk[kk] == DEFER) {
+        if (bk[kk] >= DEFER) {
           const uint64_t off = dkey(P.v[kk]) - lo;
-          const uint32_t g = dtab[(uint32_t)(off >> s)] & 0x7fffu;
+          const uint32_t g = bk[kk] - DEFER;
           go.seg[atomicAdd(&sslot[g], 1u)] = off;
           go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{off, wv[kk], sbase + 64u * kk, t | (g << AG_TBITS)};
         }
@@ -2782,8 +2786,8 @@ __device__ void mono_done(const MonoArgs &a, int tagpos) {
 __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   static_assert(MONO_SI == 4 && MONO_NW == 16, "4 particles per lane, 16 waves");
   MONO_STAMP(0);
-  __shared__ __attribute__((aligned(16))) uint32_t L0[MS0_DIG];  // hist / scan; keys; th partials
-  __shared__ __attribute__((aligned(16))) uint16_t L1[MS0_DIG];  // digit -> group; finish hist; runs + sums
+  __shared__ __attribute__((aligned(16))) uint32_t L0[MONO_DIG];  // hist / scan; keys; th partials
+  __shared__ __attribute__((aligned(16))) uint16_t L1[MONO_DIG];  // digit -> group; finish hist; runs + sums
   __shared__ int64_t q_rr[RADIX];
   __shared__ uint32_t q_dig[RADIX];
   __shared__ uint32_t g_start[RADIX + 1], g_off[RADIX + 1], g_lcnt[RADIX], g_base[RADIX];
@@ -3134,7 +3138,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   // the ranks' peer words (prims.h wave_ranks_lds) in L0: free between the
   // finish (phase 4) and the CSR offsets (phase 6)
   uint64_t *pmask = (uint64_t *)L0;
-  static_assert(sizeof(uint32_t) * MS0_DIG >= sizeof(uint64_t) * MONO_NW * RADIX, "pmask in L0");
+  static_assert(sizeof(uint32_t) * MONO_DIG >= sizeof(uint64_t) * MONO_NW * RADIX, "pmask in L0");
   for (int i = tid; i < MONO_NW * RADIX; i += MONO_BT) {
     runs[i] = 0;
     pmask[i] = 0ull;
@@ -4321,7 +4325,7 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   check_n(n);
   const int nb = (int)nbins, nq = nb + 1, macc = fs.nm * nb;
   if (nb >= RADIX || ndim < 2 || ndim > 3 || nfam < 0 || nfam > MAX_FAM) return nullptr;
-  if (sizeof(double) * (size_t)macc + sizeof(uint32_t) * MONO_NW * RADIX > sizeof(uint16_t) * MS0_DIG)
+  if (sizeof(double) * (size_t)macc + sizeof(uint32_t) * MONO_NW * RADIX > sizeof(uint16_t) * MONO_DIG)
     return nullptr;
   const uint32_t nt = ntiles_of(family_span(n, fam, nfam));
   if (nt == 0 || nt > mono_max_tiles(P.device)) return nullptr;
