@@ -527,12 +527,19 @@ __global__ void __launch_bounds__(TPB)
 // the same over select_tiles' rows (two u16 counts per word) when the call
 // kept the hinted geometry (ctl->hint), else over fused_hist0's u32 rows.
 // Thread = one word (two digits); blockIdx.y takes every gridDim.y-th row.
+// Block (0, 0) also zeroes `zero` (the selection's tail words, whose last
+// reader was fused_hist0) for the next tiled call.
 __global__ void __launch_bounds__(TPB)
     msel_reduce0h(const uint32_t *__restrict__ rows, int nrows, const uint32_t *__restrict__ rows16,
-                  int nrows16, const int32_t *__restrict__ hint, uint32_t *__restrict__ H) {
+                  int nrows16, const int32_t *__restrict__ hint, uint32_t *__restrict__ H,
+                  uint64_t *__restrict__ zero, int nzero) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < nzero) zero[threadIdx.x] = 0ull;
+  __shared__ int32_t shint;  // one load per block (not one per wave)
+  if (threadIdx.x == 0) shint = *hint;
+  __syncthreads();
   const int q = blockIdx.x * TPB + threadIdx.x;  // word q: digits 2q, 2q + 1
   uint32_t a = 0, b = 0;
-  if (*hint) {
+  if (shint) {
     constexpr int U = 8;  // rows in flight per thread
     for (int r0 = blockIdx.y * U; r0 < nrows16; r0 += gridDim.y * U) {
       uint32_t v[U];
@@ -1245,7 +1252,13 @@ __global__ void __launch_bounds__(MS0_TPB)
                 unsigned long long *__restrict__ counts, int nb, uint32_t *__restrict__ H,
                 uint32_t *__restrict__ rows) {
   __shared__ uint32_t lh[MS0_DIG];
-  const FusedCtl ctl = fused_ctl_eff(fsu);
+  // the control record derived once per block and broadcast through LDS
+  // (in every wave, its ~20 scalar loads of the same few lines from all 4096
+  // waves; bimodal 19 / 31 us per process at 64M)
+  __shared__ FusedCtl sctl;
+  if (threadIdx.x == 0) sctl = fused_ctl_eff(fsu);
+  __syncthreads();
+  const FusedCtl ctl = sctl;
   if (blockIdx.x == 0 && threadIdx.x == 0 && fsu.hint_out) {
     // this call's window key range widened by 1/64 of its span on each side
     // (a similar next call still fits), as a level-0 geometry for the next call
@@ -1714,11 +1727,16 @@ __global__ void __launch_bounds__(FR_TPB)
 // columns); the bin counts are then its row-start differences, and are
 // also stored to `counts` (assign_bins skipped its global count atomics).
 constexpr int SLAB_G = 64;  // partial groups of the general (moments) path
+// done (optional): `out` is coherent mapped host memory; every block adds
+// one to *done once its stores have landed, and the block that brings it to
+// done_target stores done_target at out[tagpos] (radial_mono's mono_done
+// protocol): the host polls that word instead of a copy + stream sync.
 __global__ void __launch_bounds__(TPB)
     fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges, int nq,
                unsigned long long *__restrict__ counts, int nb, const double *__restrict__ slab,
                int64_t rows, int nsum, double *__restrict__ out, const uint32_t *__restrict__ offs,
-               uint32_t ntiles, int nhead, const double *__restrict__ slab2, int64_t rows2) {
+               uint32_t ntiles, int nhead, const double *__restrict__ slab2, int64_t rows2,
+               uint64_t *__restrict__ done, uint64_t done_target, int tagpos) {
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
   if ((int)blockIdx.x >= nhead) {
     __shared__ double red[TPB];
@@ -1734,21 +1752,32 @@ __global__ void __launch_bounds__(TPB)
       __syncthreads();
     }
     if (threadIdx.x == 0) out[NC + nq + nb + j] = red[0];
-    return;
-  }
-  const int t = blockIdx.x * TPB + threadIdx.x;
-  if (t < NC) out[t] = ((const double *)ctl)[t];
-  else if (t < NC + nq) out[t] = edges[t - NC];
-  else if (t < NC + nq + nb) {
-    const int b = t - NC - nq;
-    unsigned long long c;
-    if (offs) {
-      c = (unsigned long long)(offs[(int64_t)(b + 1) * ntiles] - offs[(int64_t)b * ntiles]);
-      counts[b] = c;
-    } else {
-      c = counts[b];
+  } else {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    if (t < NC) out[t] = ((const double *)ctl)[t];
+    else if (t < NC + nq) out[t] = edges[t - NC];
+    else if (t < NC + nq + nb) {
+      const int b = t - NC - nq;
+      unsigned long long c;
+      if (offs) {
+        c = (unsigned long long)(offs[(int64_t)(b + 1) * ntiles] - offs[(int64_t)b * ntiles]);
+        counts[b] = c;
+      } else {
+        c = counts[b];
+      }
+      out[t] = __builtin_bit_cast(double, c);
     }
-    out[t] = __builtin_bit_cast(double, c);
+  }
+  if (!done) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pack stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == done_target) {
+      __threadfence_system();
+      __hip_atomic_store((uint64_t *)(out + tagpos), done_target, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -3611,6 +3640,10 @@ struct Profile {
   int64_t sel_base = 0, sel_span = 0;
   uint32_t sel_nt = 0;
   uint32_t sel_rsub = 1;  // select_tiles' u16 level-0 rows per block (hinted calls)
+  // selst's tail words [ctrl][key min / max slots][hint flag] at this address
+  // are zero: the previous tiled call's msel_reduce0h cleared them after
+  // their last reader (fused_hist0), so select_launch skips the fill
+  const uint64_t *sel_tail_zero = nullptr;
   const double *sel_mass = nullptr;
   // one-launch radial path (radial_mono): tile records + group fill, grid
   // barrier words; barrier generation / completion count carried across calls
@@ -3618,7 +3651,9 @@ struct Profile {
   Buf dscal, dlc;  // distributed radial_equaln: global scalars, per-rank group counts
   uint64_t bar_gen = 0, bar_done = 0;
   uint32_t bar_n = 0;  // grid size the barrier words were counted for (0: reset)
-  prim::HostBuf mpin{nullptr, nullptr, 0, true};  // radial_mono's results pack (mapped host)
+  prim::HostBuf mpin{nullptr, nullptr, 0, true};  // radial_mono's / fused_pack's results pack (mapped host)
+  Buf pdone;               // fused_pack's completion counter (monotonic) ...
+  uint64_t pack_done = 0;  // ... and its value after the last call
   // path counters (pbx_profile_path_stats): one-launch calls, of them
   // discarded (re-run by the multi-kernel path), multi-kernel calls
   int64_t n_mono = 0, n_mono_discard = 0, n_multi = 0;
@@ -4025,7 +4060,19 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
   // per-tile look-back status words + ticket / watchdog (selection scratch)
   // [stat nt][ctrl: ticket, watchdog][MM_SLOTS x (~min key, max key)][hint flag]: one zero fill
   const size_t nst = (size_t)nt + 1 + 2 * MM_SLOTS + 1;
+  const size_t sbytes0 = P.selst.bytes;
   uint64_t *stat = (uint64_t *)P.selst.get(sizeof(uint64_t) * nst);
+  // the persistent tiled selection reads none of the per-tile status words:
+  // only the tail needs zeros, and it already holds them when the previous
+  // tiled call cleared it at this address (same buffer, same nt)
+  const bool persist = span && !pos_f32 && nt >= 1024 && lazy && P.x_tiled;
+  static const bool tail_fill = [] {  // A/B: PBX_SEL_TAILFILL=1 fills the tail every call
+    const char *v = std::getenv("PBX_SEL_TAILFILL");
+    return v && v[0] == '1';
+  }();
+  const bool tail_zero = persist && !tail_fill && P.selst.bytes == sbytes0 &&
+                         P.sel_tail_zero == stat + nt;
+  P.sel_tail_zero = nullptr;
   uint32_t *ctrl = (uint32_t *)(stat + nt);
   double *xo = r.xo;
   double *wo = nullptr;
@@ -4037,7 +4084,8 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
     io = (int32_t *)P.idx.get(sizeof(int32_t) * (size_t)(span ? span : 1));
   }
   unsigned long long *mm = (unsigned long long *)(stat + nt + 1);
-  PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * nst, st));
+  if (!persist) PBX_HIP(hipMemsetAsync(stat, 0, sizeof(uint64_t) * nst, st));
+  else if (!tail_zero) PBX_HIP(hipMemsetAsync(stat + nt, 0, sizeof(uint64_t) * (nst - nt), st));
   if (span) {
     auto go = [&](auto kern, int bt, auto tp) {
       using T = decltype(tp);
@@ -4281,6 +4329,36 @@ static bool mono_enabled() {
   return on;
 }
 
+// Completion of a call whose last kernel stores a tag into mapped host
+// memory (radial_mono, fused_pack): the tag is polled (a stream sync wakes
+// the host several microseconds after the kernel ends); the stream is
+// queried now and then, so a call that ends without its tag (a discarded
+// radial_mono, a fault) ends the wait too.  Returns whether the tag arrived.
+// PBX_MONO_SPIN=0: a plain stream sync (A/B).
+static bool wait_tag(hipStream_t st, const double *word, uint64_t want) {
+  static const bool spin = [] {
+    const char *v = std::getenv("PBX_MONO_SPIN");
+    return !(v && v[0] == '0');
+  }();
+  volatile const uint64_t *tag = (volatile const uint64_t *)word;
+  if (spin) {
+    for (uint32_t k = 1; *tag == ~0ull; ++k) {
+      if ((k & 1023u) == 0) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) PBX_HIP(q);
+      }
+      __builtin_ia32_pause();
+    }
+    if (*tag != want) PBX_HIP(hipStreamSynchronize(st));
+  } else {
+    PBX_HIP(hipStreamSynchronize(st));
+  }
+  const bool ok = *tag == want;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the pack's words are read after the tag
+  return ok;
+}
+
 // Tiles (= blocks) the one-launch path may use on a device: every block must
 // be resident at once, one 1024-thread block per CU (0: never)
 static uint32_t mono_max_tiles(int dev) {
@@ -4385,28 +4463,7 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   P.bar_gen += 5;
   P.bar_done += nt;
   ++P.n_mono;
-  // completion: the tag in mapped host memory, polled (a stream sync wakes
-  // the host several microseconds after the kernel ends); the stream is
-  // queried now and then, so a discarded call (no tag) ends the wait too
-  static const bool spin = [] {
-    const char *v = std::getenv("PBX_MONO_SPIN");
-    return !(v && v[0] == '0');
-  }();
-  if (spin) {
-    volatile uint64_t *tag = (volatile uint64_t *)(hp + ntot);
-    for (uint32_t k = 1; *tag == ~0ull; ++k) {
-      if ((k & 1023u) == 0) {
-        const hipError_t q = hipStreamQuery(st);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) PBX_HIP(q);
-      }
-      __builtin_ia32_pause();
-    }
-    if (*tag != a.gen0) PBX_HIP(hipStreamSynchronize(st));
-  } else {
-    PBX_HIP(hipStreamSynchronize(st));
-  }
-  if (__builtin_bit_cast(uint64_t, ((volatile double *)hp)[ntot]) != a.gen0) {
+  if (!wait_tag(st, hp + ntot, a.gen0)) {
     P.bar_n = 0;  // discarded: zero the barrier words before the next call
     ++P.n_mono_discard;
     return nullptr;
@@ -4470,7 +4527,7 @@ int pbx_profile_destroy(void *handle) {
                   &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack, &p->frec, &p->fblk,
                   &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->shint, &p->srows,
                   &p->swc, &p->sbt, &p->mono, &p->bar,
-                  &p->mono_trace, &p->dscal, &p->dlc};
+                  &p->mono_trace, &p->dscal, &p->dlc, &p->pdone};
     for (Buf *b : all) b->release();
     p->pin.release();
     p->mpin.release();
@@ -5104,7 +5161,10 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                          rows);
       hipLaunchKernelGGL(msel_reduce0h, dim3(MS0_DIG / 2 / TPB, 32), dim3(TPB), 0, st,
                          (const uint32_t *)rows, g0, (const uint32_t *)P.srows.p,
-                         hinted ? SH_K * (g0 - 1) * (int)P.sel_rsub : 0, (const int32_t *)&ctl->hint, H);
+                         hinted ? SH_K * (g0 - 1) * (int)P.sel_rsub : 0, (const int32_t *)&ctl->hint, H,
+                         stat + nt, 2 + 2 * MM_SLOTS);
+      PBX_HIP(hipGetLastError());
+      P.sel_tail_zero = stat + nt;  // (select_launch: no fill before the next tiled call)
       int64_t *gsc = nullptr;  // dist: [global kept count][ctl copy]
       uint32_t *lc_all = nullptr;
       if (dist) {
@@ -5340,19 +5400,47 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       const int nloc = dist ? (int)nb : 0;  // dist: this rank's counts after the global ones
       double *dpk = (double *)P.fpack.get(sizeof(double) * (size_t)(ntot + nloc));
       const int nhead = (int)ceil_div(NC + nq + (int)nb, TPB);
-      hipLaunchKernelGGL(fused_pack, dim3(nhead + nsum), dim3(TPB), 0, st, (const FusedCtl *)ctl,
+      const uint32_t npk = (uint32_t)(nhead + nsum);
+      // one rank: the pack lands in mapped host memory with a completion tag
+      // (no D2H copy, no stream sync); dist: all-reduced on the device, copied
+      static const bool map_env = [] {  // A/B: PBX_PACK_MAPPED=0 copies + syncs
+        const char *v = std::getenv("PBX_PACK_MAPPED");
+        return !(v && v[0] == '0');
+      }();
+      const bool mapped = !dist && map_env;
+      uint64_t *pdone = nullptr;
+      if (mapped) {
+        if (!P.pdone.p) {
+          P.pdone.get(sizeof(uint64_t));
+          PBX_HIP(hipMemsetAsync(P.pdone.p, 0, sizeof(uint64_t), st));
+          P.pack_done = 0;
+        }
+        pdone = (uint64_t *)P.pdone.p;
+        hp = (double *)P.mpin.get(sizeof(double) * (size_t)(ntot + 1));
+        hp[ntot] = __builtin_bit_cast(double, ~0ull);
+        dpk = (double *)P.mpin.dev;
+      }
+      hipLaunchKernelGGL(fused_pack, dim3(npk), dim3(TPB), 0, st, (const FusedCtl *)ctl,
                          (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
                          (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead,
-                         (const double *)maccs2, maccs2 ? (int64_t)g0 : 0);
-      if (dist) {
-        PBX_HIP(hipMemcpyAsync(dpk + ntot, dpk + NC + nq, sizeof(double) * nb,
-                               hipMemcpyDeviceToDevice, st));
-        comm_allreduce(comm, dpk + NC + nq, dpk + NC + nq, nb, 2, 0, st);   // counts (u64)
-        comm_allreduce(comm, dpk + NC + nq + nb, dpk + NC + nq + nb, nsum, 0, 0, st);  // sums
+                         (const double *)maccs2, maccs2 ? (int64_t)g0 : 0, pdone,
+                         P.pack_done + npk, ntot);
+      PBX_HIP(hipGetLastError());
+      if (mapped) {
+        P.pack_done += npk;
+        if (!wait_tag(st, hp + ntot, P.pack_done))
+          fail(PBX_ERR_RUNTIME, "the results pack of a radial profile call did not complete");
+      } else {
+        if (dist) {
+          PBX_HIP(hipMemcpyAsync(dpk + ntot, dpk + NC + nq, sizeof(double) * nb,
+                                 hipMemcpyDeviceToDevice, st));
+          comm_allreduce(comm, dpk + NC + nq, dpk + NC + nq, nb, 2, 0, st);   // counts (u64)
+          comm_allreduce(comm, dpk + NC + nq + nb, dpk + NC + nq + nb, nsum, 0, 0, st);  // sums
+        }
+        hp = (double *)P.pin.get(sizeof(double) * (size_t)(ntot + nloc));
+        PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * (ntot + nloc), hipMemcpyDeviceToHost, st));
+        PBX_HIP(hipStreamSynchronize(st));
       }
-      hp = (double *)P.pin.get(sizeof(double) * (size_t)(ntot + nloc));
-      PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * (ntot + nloc), hipMemcpyDeviceToHost, st));
-      PBX_HIP(hipStreamSynchronize(st));
     }
     const FusedCtl *hc = (const FusedCtl *)hp;
     const double *he = hp + NC;
