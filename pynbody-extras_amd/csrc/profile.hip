@@ -960,8 +960,16 @@ __global__ void __launch_bounds__(SH_BT)
   const uint32_t tb0 = (uint32_t)((uint64_t)nt * (ab + 1) / (G0 - 1));
   const uint32_t ta = ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * sub / SH_K);
   const uint32_t tb = ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * (sub + 1) / SH_K);
-  SelHint h{};
-  if (hint) h = *hint;
+  // the hint: one load per block, through LDS (not one per wave from all
+  // the grid's waves at once: the same-line hot spot fused_hist0 had)
+  __shared__ SelHint shh;
+  if (threadIdx.x == 0) {
+    SelHint t{};
+    if (hint) t = *hint;
+    shh = t;
+  }
+  __syncthreads();
+  const SelHint h = shh;
   // rsub rows per block: the u16 counts are flushed to the next row every
   // SH_TMAX tiles (families above ~47M particles)
   const bool hv = h.valid && rows16 && tb - ta <= SH_TMAX * rsub;
@@ -1028,10 +1036,13 @@ __global__ void __launch_bounds__(SH_BT)
       if (keep) {
         if (xv == 1234.5) xt[k * 64 + lane] = xv;
 #else
+      // every slot's x stored (the readers mask by the keep bits): whole
+      // lines, 277 -> 264 us at 64M (same box; measured against kept-only
+      // stores once fused_hist0's timing was stable, see fused_hist0); as
+      // streaming (nt) stores: select 280 -> 274 us and assign_gather's
+      // re-read of x 202 -> 191 us at 64M (same box A/B/A/B)
+      __builtin_nontemporal_store(xv, xt + k * 64 + lane);
       if (keep) {
-        // streaming (nt) stores: select 280 -> 274 us and assign_gather's
-        // re-read of x 202 -> 191 us at 64M (same box A/B/A/B)
-        __builtin_nontemporal_store(xv, xt + k * 64 + lane);
 #endif
         const uint64_t kk = dkey(xv);
         kmin = kk < kmin ? kk : kmin;
@@ -1447,11 +1458,17 @@ __global__ void __launch_bounds__(TPB)
                uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
                uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16, uint32_t rsub) {
   __shared__ uint32_t wsum[NWAVE];
+  __shared__ int c_run, c_hint;  // the control record's fields, one load per block
   const int g = blockIdx.x;
-  if ((ctl->err & 2) || g >= ctl->ng) return;
+  if (threadIdx.x == 0) {
+    c_run = !(ctl->err & 2) && g < ctl->ng;
+    c_hint = ctl->hint;
+  }
+  __syncthreads();
+  if (!c_run) return;
   const int b = threadIdx.x;  // g0 <= TPB
   uint32_t c = 0;
-  if (ctl->hint) {  // select_tiles blocks (b - 1) SH_K .. + SH_K - 1 cover block b's tiles
+  if (c_hint) {  // select_tiles blocks (b - 1) SH_K .. + SH_K - 1 cover block b's tiles
     const uint32_t d = gdig[g];
     if (b >= 1 && b < g0)
       for (uint32_t j = 0; j < SH_K * rsub; ++j)  // the SH_K blocks' rsub rows each
@@ -1685,12 +1702,23 @@ __global__ void __launch_bounds__(FR_TPB)
   __shared__ uint64_t pick[2];
   static_assert(FS_DIG == 2 * FR_TPB, "two digits per thread");
   const int g = blockIdx.x;
-  if ((ctl->err & 2) || g >= ctl->ng) return;
-  const uint64_t base = ctl->lo;
-  const int s = ctl->s0;
-  const int64_t o = goff[g], S = (int64_t)goff[g + 1] - o;
-  const bool in_lds = S <= FS_LDS;
   const int tid = threadIdx.x;
+  __shared__ uint64_t c_lo;  // the control record's fields and the group's
+  __shared__ int c_s, c_run; // segment: one load per block, through LDS
+  __shared__ uint32_t c_o0, c_o1;
+  if (tid == 0) {
+    c_run = !(ctl->err & 2) && g < ctl->ng;
+    c_lo = ctl->lo;
+    c_s = ctl->s0;
+    c_o0 = c_run ? goff[g] : 0u;
+    c_o1 = c_run ? goff[g + 1] : 0u;
+  }
+  __syncthreads();
+  if (!c_run) return;
+  const uint64_t base = c_lo;
+  const int s = c_s;
+  const int64_t o = c_o0, S = (int64_t)c_o1 - o;
+  const bool in_lds = S <= FS_LDS;
   if (in_lds) {
     for (int64_t i = tid; i < S; i += FR_TPB) sk[i] = seg[o + i];
     __syncthreads();
@@ -2142,16 +2170,27 @@ __global__ void __launch_bounds__(MS0_TPB)
   const int nr = nb + 1, nrs = nr | 1;  // th row stride odd: flush reads bank-conflict free
   uint32_t *th = (uint32_t *)(acc + macc);  // [tile][bin]: a wave's atomics hit distinct banks
   const int tid = threadIdx.x;
-  const bool win = !(ctl->err & 2);
-  const int ng = win ? ctl->ng : 0;
-  const uint64_t lo = ctl->lo;
-  const int s = ctl->s0;
+  // the control record's fields: one load per block, broadcast through LDS
+  // (not ~4 scalar loads of one line in each of the grid's 4096 waves)
+  __shared__ uint64_t c_lo;
+  __shared__ int c_ng, c_s, c_win;
+  if (tid == 0) {
+    const bool w0 = !(ctl->err & 2);
+    c_win = w0;
+    c_ng = w0 ? ctl->ng : 0;
+    c_lo = ctl->lo;
+    c_s = ctl->s0;
+    dk = 0;
+  }
   const uint32_t rb = block_prefix(go.bcnt, (int)blockIdx.x, red);
   for (int q = tid; q < nq; q += MS0_TPB) qd[q] = (uint32_t)R[q].prefix;
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
   for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
-  if (tid == 0) dk = 0;
   __syncthreads();
+  const bool win = c_win;
+  const int ng = c_ng;
+  const uint64_t lo = c_lo;
+  const int s = c_s;
   for (int g = tid; g < ng; g += MS0_TPB) sslot[g] = boff[(int64_t)blockIdx.x * MS_MAXQ + g];
   for (int d = tid; d < MS0_DIG; d += MS0_TPB) {  // #{q : digit_q < d}, lower bound
     int a = 0, len = nq;
@@ -2378,12 +2417,20 @@ __global__ void __launch_bounds__(MS0_TPB)
   uint32_t ta, tb;
   tile_range(nt, ta, tb);
   const uint32_t wt = (uint32_t)(FD_LDSW / nrs);  // tiles per window
+  __shared__ uint64_t c_lo;  // the control record's fields, one load per block
+  __shared__ int c_ng;       // (-1: no window)
+  if (tid == 0) {
+    const bool ok = !(ctl->err & 2);
+    c_ng = ok ? ctl->ng : -1;
+    c_lo = ctl->lo;
+  }
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
   for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
-  const bool ok_all = !(ctl->err & 2);
-  for (int k = tid; k <= (ok_all ? ctl->ng : -1); k += MS0_TPB) gql[k] = gq[k];
+  __syncthreads();
+  const bool ok_all = c_ng >= 0;
+  for (int k = tid; k <= c_ng; k += MS0_TPB) gql[k] = gq[k];
   const int64_t r0 = rbase[blockIdx.x], cnt = ok_all ? (int64_t)rn[blockIdx.x] : 0;
-  const uint64_t lo = ctl->lo;
+  const uint64_t lo = c_lo;
   for (uint32_t w0 = ta; w0 < tb || (w0 == ta && cnt); w0 += wt) {  // (block-uniform)
     const uint32_t w1 = min(tb, w0 + wt);
     for (int k = tid; k < (int)(w1 - w0) * nrs; k += MS0_TPB) tc[k] = 0;
@@ -5289,6 +5336,10 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
             const char *v = std::getenv("PBX_CSR_XCD");
             return (v && v[0] == '0') ? 0 : 1;
           }();
+          // (a persistent variant — a block per run of tiles, the next tile's
+          // loads in flight during this one's ranking and stores — took
+          // 105-141 us against 87 at 64M: the prefetch registers cost
+          // occupancy, 8 -> 4-6 blocks per CU; dropped)
           hipLaunchKernelGGL(csrk, dim3(nt), dim3(TPB), 0, st,
                              (const uint32_t *)P.toff.p, (const uint64_t *)P.kw.p,
                              (const uint16_t *)P.kpre.p, (const uint32_t *)P.swc.p,

@@ -6,6 +6,9 @@
 //   rd3w   : rd3 + sqrt(r^2) stored by particle slot (select_tiles' pattern)
 //   rd4    : the same bytes as 16-byte coalesced loads, r^2 from an LDS transpose, summed
 //   rd4w   : rd4 + sqrt(r^2) stored by slot
+//   rd3nt  : rd3w with nt stores
+//   rd2p(w): lane pairs — a lane's two consecutive particles as three 16-byte
+//            loads, their two x as one 16-byte nt store
 //   copy4  : float4 copy of the position bytes (reference rate)
 // usage: probe_stream [n]
 #include <hip/hip_runtime.h>
@@ -88,6 +91,66 @@ __global__ void __launch_bounds__(BT) rd4(const double *__restrict__ pos, int64_
   }
 }
 
+// lane-pair layout: lane l of a wave's 128-particle group holds particles
+// 2l and 2l + 1 (48 contiguous bytes: three 16-byte loads) and stores their
+// two x as one 16-byte store
+template <bool WR>
+__global__ void __launch_bounds__(BT) rd2p(const double *__restrict__ pos, int64_t n,
+                                           double *__restrict__ xo, double *__restrict__ sums) {
+  const int64_t b0 = (int64_t)blockIdx.x * TILE + (threadIdx.x >> 6) * (TILE / (BT / 64));
+  const uint32_t lane = threadIdx.x & 63;
+  constexpr int G = PPL / 2;  // 128-particle groups per wave slice
+  double2 q[G][3];
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const int64_t i = b0 + k * 128 + 2 * lane;
+    const double2 *src = (const double2 *)(pos + 3 * (i + 1 < n ? i : 0));
+    q[k][0] = src[0];
+    q[k][1] = src[1];
+    q[k][2] = src[2];
+  }
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const double x0 = q[k][0].x, y0 = q[k][0].y, z0 = q[k][1].x;
+    const double x1 = q[k][1].y, y1 = q[k][2].x, z1 = q[k][2].y;
+    const double r0 = (x0 * x0 + y0 * y0) + z0 * z0, r1 = (x1 * x1 + y1 * y1) + z1 * z1;
+    const int64_t i = b0 + k * 128 + 2 * lane;
+    if (WR) {
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      d2v o;
+      o.x = __builtin_sqrt(r0);
+      o.y = __builtin_sqrt(r1);
+      if (i + 1 < n) __builtin_nontemporal_store(o, (d2v *)(xo + i));
+    } else {
+      s += r0 + r1;
+    }
+  }
+  if (!WR) {
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) sums[blockIdx.x * (BT / 64) + (threadIdx.x >> 6)] = s;
+  }
+}
+
+// rd3w with nt stores (select_tiles' store flavour)
+__global__ void __launch_bounds__(BT) rd3nt(const double *__restrict__ pos, int64_t n, double *__restrict__ xo) {
+  const int64_t b0 = (int64_t)blockIdx.x * TILE + (threadIdx.x >> 6) * (TILE / (BT / 64));
+  const uint32_t lane = threadIdx.x & 63;
+  double px[PPL], py[PPL], pz[PPL];
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const int64_t i = b0 + k * 64 + lane;
+    const double *q = pos + 3 * (i < n ? i : 0);
+    px[k] = q[0]; py[k] = q[1]; pz[k] = q[2];
+  }
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) {
+    const int64_t i = b0 + k * 64 + lane;
+    const double r2 = (px[k] * px[k] + py[k] * py[k]) + pz[k] * pz[k];
+    if (i < n) __builtin_nontemporal_store(__builtin_sqrt(r2), xo + i);
+  }
+}
+
 __global__ void __launch_bounds__(256) copy4(const double4 *__restrict__ a, double4 *__restrict__ b, int64_t m) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (int64_t)gridDim.x * 256) b[i] = a[i];
 }
@@ -124,6 +187,9 @@ int main(int argc, char **argv) {
   timeit("rd3w", [&] { hipLaunchKernelGGL(rd3<true>, dim3(nt), dim3(BT), 0, 0, pos, n, xo, sums); }, R + W);
   timeit("rd4", [&] { hipLaunchKernelGGL(rd4<false>, dim3(nt), dim3(BT), 0, 0, pos, n, xo, sums); }, R);
   timeit("rd4w", [&] { hipLaunchKernelGGL(rd4<true>, dim3(nt), dim3(BT), 0, 0, pos, n, xo, sums); }, R + W);
+  timeit("rd3nt", [&] { hipLaunchKernelGGL(rd3nt, dim3(nt), dim3(BT), 0, 0, pos, n, xo); }, R + W);
+  timeit("rd2p", [&] { hipLaunchKernelGGL(rd2p<false>, dim3(nt), dim3(BT), 0, 0, pos, n, xo, sums); }, R);
+  timeit("rd2pw", [&] { hipLaunchKernelGGL(rd2p<true>, dim3(nt), dim3(BT), 0, 0, pos, n, xo, sums); }, R + W);
   timeit("copy4", [&] { hipLaunchKernelGGL(copy4, dim3(4096), dim3(256), 0, 0, (const double4 *)pos, (double4 *)cp, (int64_t)(3 * n / 4)); }, 2 * R);
   return 0;
 }
