@@ -1605,6 +1605,7 @@ __device__ __forceinline__ void mom_add(double *aq, int op, int col, int fq, int
 constexpr int FS_BITS = 11;
 constexpr int FS_DIG = 1 << FS_BITS;
 constexpr int FS_LDS = 8192;
+constexpr uint32_t FS_CAND = 256;  // finish_group: keys gathered for the direct rank
 
 // keys of sk[0, S) below / equal to k: 8 keys per step from four 16-B LDS
 // reads (broadcast: every lane reads the same address), counts split over
@@ -1687,7 +1688,51 @@ __device__ void finish_group(const uint64_t *__restrict__ keys, int64_t S, uint6
     __syncthreads();
     pref |= pick[0] << sh;
     rr -= (int64_t)pick[1];
+    const uint32_t left = hist[(uint32_t)pick[0]];  // keys with the new prefix (block-uniform)
     __syncthreads();
+    if (sh > 0 && left <= FS_CAND) {
+      // few keys share the prefix (one 11-bit pass below a level-0 digit of
+      // ~2k keys leaves ~1): gather them into LDS and take the rr-th by
+      // counting, instead of the remaining radix passes (same key: the
+      // rr-th smallest of the keys with this prefix, ties included)
+      const uint64_t m2 = ~((1ull << sh) - 1);
+      uint64_t *cand = (uint64_t *)hist;
+      if (tid == 0) pick[1] = 0ull;
+      __syncthreads();
+      constexpr int FS_U = IN_LDS ? 1 : 8;
+      for (int64_t i0 = 0; i0 < S; i0 += (int64_t)FR_TPB * FS_U) {
+        uint64_t kv[FS_U];
+#pragma unroll
+        for (int u = 0; u < FS_U; ++u) {
+          const int64_t i = i0 + (int64_t)u * FR_TPB + tid;
+          const int64_t ic = i < S ? i : 0;
+          kv[u] = SC1 ? __hip_atomic_load(&keys[ic], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : keys[ic];
+        }
+#pragma unroll
+        for (int u = 0; u < FS_U; ++u) {
+          const int64_t i = i0 + (int64_t)u * FR_TPB + tid;
+          if (i < S && (kv[u] & m2) == pref)
+            cand[atomicAdd((unsigned long long *)&pick[1], 1ull)] = kv[u];
+        }
+      }
+      __syncthreads();
+      const int nc = (int)pick[1];  // == left
+      if (tid < nc) {
+        const uint64_t k = cand[tid];
+        uint32_t less = 0, eq = 0;
+        for (int j = 0; j < nc; ++j) {
+          const uint64_t kj = cand[j];
+          less += kj < k ? 1u : 0u;
+          eq += kj == k ? 1u : 0u;
+        }
+        if ((int64_t)less <= rr && rr < (int64_t)(less + eq)) pick[0] = k;  // ties: same value
+      }
+      __syncthreads();
+      out = pick[0];
+      __syncthreads();  // (pick / hist are reused by the caller's next rank)
+      return;
+    }
   }
   out = pref;
 }
@@ -1697,7 +1742,7 @@ __global__ void __launch_bounds__(FR_TPB)
                  const uint32_t *__restrict__ gq, const uint32_t *__restrict__ goff,
                  const uint64_t *__restrict__ seg, double *__restrict__ edges) {
   __shared__ __attribute__((aligned(16))) uint64_t sk[FS_LDS];
-  __shared__ uint32_t hist[FS_DIG];
+  __shared__ __attribute__((aligned(16))) uint32_t hist[FS_DIG];  // (u64 candidates, finish_group)
   __shared__ uint32_t wsum[FR_TPB / 64];
   __shared__ uint64_t pick[2];
   static_assert(FS_DIG == 2 * FR_TPB, "two digits per thread");
