@@ -2690,6 +2690,20 @@ __global__ void __launch_bounds__(TPB)
   }
   __syncthreads();
   uint32_t lp[16];
+#ifdef PBX_DIAG_CSR_LOADONLY  // timing diagnostic only: the loads, nothing else
+  {
+    uint32_t z = o + go + tn + sbase1;
+    for (int k = 0; k < 16; ++k) z ^= key[k] ^ (uint32_t)wds[k] ^ (uint32_t)kpt[k];
+    if (z == 0x12345u) perm[0] = (int32_t)z;
+    return;
+  }
+#endif
+#ifdef PBX_DIAG_CSR_NORANK  // timing diagnostic only: no wave-local ranks
+  if (true) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lp[k] = 0;
+  } else
+#endif
   if (LDSM) {
     uint32_t dg[16];
     bool okk[16];
