@@ -237,18 +237,26 @@ __global__ void __launch_bounds__(TPB) scan_tiles(const uint32_t *in, int64_t le
 // ready", so the status array is zeroed only when it is (re)allocated.
 // The look-back is wave 0's: lane l inspects tile (hi - l).
 constexpr uint64_t kScAgg = 1ull << 32, kScPre = 2ull << 32;
+// ticket = 0 (a grid that is resident at once): tile = workgroup id, no
+// ticket — every tile it waits for is running too, and publishes its sum
+// before it waits.  The ticket is one same-address atomic per block, issued
+// before the block's loads: at 1184 tiles (the 256M profile's [bin][tile]
+// table) they serialised into most of the kernel's time.
 __global__ void __launch_bounds__(TPB)
     scan_onepass(uint32_t *a, int64_t len, uint64_t *__restrict__ status,
-                 unsigned long long *__restrict__ ctr, uint32_t epoch) {
+                 unsigned long long *__restrict__ ctr, uint32_t epoch, int ticket) {
   __shared__ uint32_t wsum[NWAVE];
   __shared__ uint32_t s_tile, s_excl;
-  if (threadIdx.x == 0) {
-    const uint32_t t = (uint32_t)atomicAdd(&ctr[0], 1ull);
-    if (t == gridDim.x - 1) atomicExch(&ctr[0], 0ull);  // every ticket is out
-    s_tile = t;
+  uint32_t tile = blockIdx.x;
+  if (ticket) {
+    if (threadIdx.x == 0) {
+      const uint32_t t = (uint32_t)atomicAdd(&ctr[0], 1ull);
+      if (t == gridDim.x - 1) atomicExch(&ctr[0], 0ull);  // every ticket is out
+      s_tile = t;
+    }
+    __syncthreads();
+    tile = s_tile;
   }
-  __syncthreads();
-  const uint32_t tile = s_tile;
   const int64_t base = (int64_t)tile * TILE + (int64_t)threadIdx.x * IPT;
   uint32_t v[IPT];
   uint32_t sum = 0;
@@ -522,8 +530,21 @@ static inline void scan_u32(Buf &ws, hipStream_t st, uint32_t *a, int64_t len) {
     ws.epoch = 1;
   }
   uint64_t *w = (uint64_t *)ws.p;
+  static const int ticket_env = [] {  // A/B: PBX_SCAN_TICKET=1 always draws tickets
+    const char *v = std::getenv("PBX_SCAN_TICKET");
+    return v ? std::atoi(v) : -1;
+  }();
+  static const int64_t resident = [] {  // blocks resident at once on this device
+    int dev = 0, cus = 0, per = 0;
+    PBX_HIP(hipGetDevice(&dev));
+    PBX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    PBX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per, reinterpret_cast<const void *>(&scan_onepass), TPB, 0));
+    return (int64_t)cus * per;
+  }();
+  const int ticket = ticket_env >= 0 ? ticket_env : (nt > resident ? 1 : 0);
   hipLaunchKernelGGL(scan_onepass, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, w + 2,
-                     (unsigned long long *)w, ws.epoch);
+                     (unsigned long long *)w, ws.epoch, ticket);
   PBX_HIP(hipGetLastError());
 }
 
