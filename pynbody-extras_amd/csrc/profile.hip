@@ -51,7 +51,6 @@ struct SelectParams {
   int mass_f32;  // masses are float (else double)
   int tiled;     // lazy + tiled: x of tile t at xo[t * TILE ..], no look-back
   int sphere_origin;  // the Sphere is centred at (0, 0, 0) (and ndim == 3): its test IS r^2 < R^2
-  int noticket;  // select_onepass: the grid is resident at once, tile = workgroup id (no ticket)
   double cx, cy, cz, r2max;
   int64_t fam_lo[MAX_FAM];
   int64_t fam_hi[MAX_FAM];
@@ -136,12 +135,7 @@ __global__ void __launch_bounds__(BT)
   __shared__ uint32_t s_tile, s_excl;
   // the ticket (a returning device atomic before any load can be issued)
   // orders the look-back; a tiled selection has none: block = tile
-  // (a grid resident at once needs none either: every tile a block waits
-  // for is running and publishes its count before it looks back — the
-  // ticket, one same-address atomic per block, serialised the [bin][tile]
-  // scan's start the same way, prims.h scan_onepass)
-  if (threadIdx.x == 0)
-    s_tile = ((LAZY && p.tiled) || p.noticket) ? blockIdx.x : atomicAdd(&ctrl[0], 1u);
+  if (threadIdx.x == 0) s_tile = (LAZY && p.tiled) ? blockIdx.x : atomicAdd(&ctrl[0], 1u);
   __syncthreads();
   const uint32_t tile = s_tile;
   const int w = threadIdx.x >> 6;
@@ -4158,21 +4152,6 @@ struct TileHist {  // select_tiles' hinted level-0 histogram (null hint: none)
   uint64_t ka = 0, kb = ~0ull;
 };
 
-// blocks of `fn` (bt threads) resident at once on the current device
-static int64_t resident_blocks(const void *fn, int bt) {
-  static std::mutex mu;
-  static std::vector<std::pair<const void *, int64_t>> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const auto &e : cache)
-    if (e.first == fn) return e.second;
-  int dev = 0, cus = 0, per = 0;
-  PBX_HIP(hipGetDevice(&dev));
-  PBX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  PBX_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, bt, 0));
-  cache.emplace_back(fn, (int64_t)cus * per);
-  return (int64_t)cus * per;
-}
-
 static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
                               int64_t n, int on_device, int use_sphere, const double *sphere,
                               const int64_t *fam, int nfam, int ndim, bool lazy = false,
@@ -4216,13 +4195,7 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
   if (span) {
     auto go = [&](auto kern, int bt, auto tp) {
       using T = decltype(tp);
-      static const int ticket_env = [] {  // A/B: PBX_SEL_TICKET=1 always draws tickets
-        const char *v = std::getenv("PBX_SEL_TICKET");
-        return v ? std::atoi(v) : -1;
-      }();
-      SelectParams spt = sp;
-      spt.noticket = ticket_env == 1 ? 0 : (nt <= resident_blocks((const void *)kern, bt) ? 1 : 0);
-      hipLaunchKernelGGL(kern, dim3(nt), dim3(bt), 0, st, (const T *)d_pos, d_mass, hi, spt, stat,
+      hipLaunchKernelGGL(kern, dim3(nt), dim3(bt), 0, st, (const T *)d_pos, d_mass, hi, sp, stat,
                          ctrl, xo, wo, io, mm, kw, toff, r.kpre);
     };
     if (pos_f32) {  // float32 snapshots: eager only
