@@ -1790,7 +1790,7 @@ __global__ void __launch_bounds__(FR_TPB)
   }
 }
 
-// the step's results in one contiguous staging block (one D2H copy):
+// the step's results in one contiguous block (mapped host memory for one rank, else one D2H copy):
 // [ctl][edges nq][counts nb][monomial sums nm x nb].  Blocks [0, nhead)
 // copy the head; block nhead + j sums column j of the assign slab (`rows`
 // block rows, then the rows2 rows of slab2, fixed order: thread
@@ -5501,7 +5501,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
             PBX_HIP(hipMemcpyAsync(P.perm.p, va, sizeof(int32_t) * n_sel, hipMemcpyDeviceToDevice, st));
         }
       }
-      // the results packed on the device, one copy, one sync
+      // the results packed into one block: mapped host memory + tag (one rank), or a device block, one copy, one sync (dist)
       // (dist: every rank packs the fused sums' columns, zeros without
       // particles, so the all-reduced regions have the same length)
       nsum = (maccs || (dist && fs.nm)) ? fs.nm * (int)nb : 0;
