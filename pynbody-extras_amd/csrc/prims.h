@@ -115,12 +115,24 @@ __device__ __forceinline__ void wave_ranks_lds(const uint32_t (&dig)[IPT], const
     uint32_t l = 0;
     if (ok[k]) {
       const uint32_t d = dig[k];
+#ifdef PBX_RANK_HALF  // A/B: a 32-bit peer word per half-wave (4-byte ORs and clears)
+      uint32_t *pw = (uint32_t *)&pmask[d];
+      const uint32_t h = lane_id() >> 5;
+      __hip_atomic_fetch_or(pw + h, 1u << (lane_id() & 31u), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint64_t m = __hip_atomic_load(&pmask[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      const uint32_t base = __hip_atomic_load(&run[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __hip_atomic_store(&run[d], base + (uint32_t)__popcll(m), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __hip_atomic_store(pw + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
       __hip_atomic_fetch_or(&pmask[d], lbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       const uint64_t m = __hip_atomic_load(&pmask[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       const uint32_t base = __hip_atomic_load(&run[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       __hip_atomic_store(&run[d], base + (uint32_t)__popcll(m), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_WAVEFRONT);
       __hip_atomic_store(&pmask[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
       l = base + rank_below(m);
     }
     lp[k] = l;
