@@ -55,6 +55,9 @@ _SIGS = {
                                          _i64p]),
     "pbx_profile_assign": (c_int, [c_void_p, _dp, c_int64, _i64p, _i64p]),
     "pbx_profile_csr": (c_int, [c_void_p, _i64p, _i64p]),
+    "pbx_profile_binned_equaln": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double,
+                                          c_int, c_int, c_void_p, c_void_p, c_void_p, _dp, _i64p,
+                                          _i64p, _i64p, _dp]),
     "pbx_profile_moments_cols": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_uint32,
                                          _dp]),
     "pbx_profile_percentiles": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
@@ -91,18 +94,65 @@ def _call(name, *args):
 
 class DeviceBinsHandle:
     """One binned quantity x in HBM (a pbx_profile handle) and what the
-    device derived from it: edges, assignment, CSR."""
+    device derived from it: edges, assignment, CSR.
+
+    x is uploaded by ``upload`` once per BinsSet materialisation (the
+    equaln seam, or the assignment seam when no equaln call preceded it):
+    a BinsSet re-materialised in place over the same, mutated array object
+    sees the array's current values, as the reference's numpy code does."""
+
+    # the fused one-round-trip pass (pbx_profile_binned_equaln) takes nbins <= 1024
+    FUSED_MAX_BINS = 1024
 
     def __init__(self, x):
         h = c_void_p()
         _call("pbx_profile_create", byref(h))
         self._h = h
-        self.x_ref = x
+        self.x_ref = None
+        self.n = 0
+        self.nbins = None
+        self.n_valid = 0
+        self.pending = None  # (edges, counts) of a fused equaln pass not yet consumed
+        self.upload(x)
+
+    def upload(self, x):
         a = np.ascontiguousarray(np.asarray(x), dtype=np.float64).reshape(-1)
         _call("pbx_profile_set_x", self._h, a.ctypes.data_as(_dp), a.shape[0])
+        self.x_ref = x
         self.n = a.shape[0]
         self.nbins = None
         self.n_valid = 0
+        self.pending = None
+
+    def equaln_fused(self, nbins, bin_min, bin_max) -> np.ndarray:
+        """equaln edges, their assignment, counts and the device CSR in one
+        host round trip (pbx_profile_binned_equaln); the counts wait in
+        ``pending`` for the assignment seam that follows (bins.py:386-387)."""
+        nb = int(nbins)
+        edges = np.empty(nb + 1)
+        counts = np.zeros(nb, dtype=np.int64)
+        ne, nv = c_int64(0), c_int64(0)
+        _call("pbx_profile_binned_equaln", self._h, nb, int(bin_min is not None),
+              float(bin_min) if bin_min is not None else 0.0, int(bin_max is not None),
+              float(bin_max) if bin_max is not None else 0.0, 1, 0, None, None, None,
+              edges.ctypes.data_as(_dp), byref(ne), counts.ctypes.data_as(_i64p), byref(nv), None)
+        edges = edges[: ne.value].copy()
+        counts = counts[: ne.value - 1].copy()
+        self.nbins, self.n_valid = counts.shape[0], nv.value
+        self.pending = (edges, counts)
+        return edges
+
+    def take_pending(self, edges):
+        """The counts of the fused pass whose edges are exactly ``edges``
+        (then the device assignment and CSR are already those of edges), or
+        None.  Consumed either way."""
+        p, self.pending = self.pending, None
+        if p is None:
+            return None
+        e = np.asarray(edges, dtype=np.float64).reshape(-1)
+        if e.shape != p[0].shape or not np.array_equal(e.view(np.uint64), p[0].view(np.uint64)):
+            return None
+        return p[1]
 
     def edges_equaln(self, nbins, bin_min, bin_max) -> np.ndarray:
         out = np.empty(int(nbins) + 1)
@@ -162,14 +212,13 @@ class DeviceBinsHandle:
 
 
 def _handle_for(binsset, x) -> DeviceBinsHandle:
-    """The BinsSet's device handle for x (one per materialised BinsSet;
-    a new x replaces it)."""
+    """The BinsSet's device handle, with x uploaded for this materialisation."""
     h = binsset.__dict__.get("_pbx_handle")
-    if h is None or h.x_ref is not x:
-        if h is not None:
-            h.close()
+    if h is None:
         h = DeviceBinsHandle(x)
         binsset.__dict__["_pbx_handle"] = h
+    else:
+        h.upload(x)
     return h
 
 
@@ -180,8 +229,15 @@ def _assign_particles(self, x, bin_edges):
     nbins = len(arr_edges) - 1
     if nbins <= 0:
         return [], np.array([], dtype=int)
-    h = _handle_for(self, x)
-    counts = h.assign(arr_edges)
+    h = self.__dict__.get("_pbx_handle")
+    counts = None
+    if h is not None and h.x_ref is x:
+        # the equaln seam of this same materialisation already assigned and
+        # built the CSR with exactly these edges (one host round trip)
+        counts = h.take_pending(arr_edges)
+    if counts is None:
+        h = _handle_for(self, x)
+        counts = h.assign(arr_edges)
     if not counts.any():
         return [np.empty(0, dtype=int) for _ in range(nbins)], np.zeros(nbins, dtype=int)
     perm, offs = h.csr()
@@ -190,8 +246,14 @@ def _assign_particles(self, x, bin_edges):
 
 
 def _equal_number_bins_algorithm(self, x):
-    """bins.py:720-746 on the device (the same edges, bit for bit)."""
-    return _handle_for(self, x).edges_equaln(self.nbins, self._bin_min, self._bin_max)
+    """bins.py:720-746 on the device (the same edges, bit for bit), fused
+    with the assignment and CSR the next seam of the same materialisation
+    asks for (bins.py:386-387)."""
+    h = _handle_for(self, x)
+    nb = int(self.nbins)
+    if 1 <= nb <= DeviceBinsHandle.FUSED_MAX_BINS:
+        return h.equaln_fused(nb, self._bin_min, self._bin_max)
+    return h.edges_equaln(nb, self._bin_min, self._bin_max)
 
 
 def _stat_plan(calc):

@@ -239,21 +239,27 @@ __global__ void __launch_bounds__(TPB) scan_tiles(const uint32_t *in, int64_t le
   }
 }
 
-// Single-pass exclusive scan in place (decoupled look-back).  Tiles are
-// claimed in launch order by a ticket, so every predecessor a tile waits for
-// is already running (workgroup ids alone do not promise that: the XCDs
-// dispatch their shares independently); the block drawing the last ticket
-// re-arms the counter for the next launch.  Status word of a tile:
-// epoch (30 bits) | flag (2: 1 = tile sum, 2 = inclusive prefix) | value
-// (32); words of an earlier call carry another epoch and read as "not
-// ready", so the status array is zeroed only when it is (re)allocated.
-// The look-back is wave 0's: lane l inspects tile (hi - l).
+// Single-pass exclusive scan in place (decoupled look-back).  Status word of
+// a tile: epoch (30 bits) | flag (2: 1 = tile sum, 2 = inclusive prefix) |
+// value (32); words of an earlier call carry another epoch and read as "not
+// ready", so the status array is zeroed only when it is (re)allocated.  The
+// look-back is wave 0's: lane l inspects tile (hi - l).
+// Tile order: with ticket = 1 tiles are claimed in dispatch order by a
+// ticket (one same-address atomic per block, issued before the block's
+// loads — at 1184 tiles, the 256M profile's [bin][tile] table, they
+// serialised into most of the kernel's time), and the block drawing the last
+// ticket re-arms the counter.  With ticket = 0 (the host's choice when the
+// whole grid fits the device at once) tile = workgroup id.  Progress then
+// rests on each XCD dispatching its workgroups in id order: a running tile's
+// predecessors on its own XCD were dispatched before it, and those on other
+// XCDs come before any later id there, so no tile waits for one that our own
+// waiting tiles keep from being dispatched; kernels of other streams or
+// processes can only delay a predecessor until they release its XCD.
+// Watchdog: a look-back still waiting after 2^24 sleeps (~10 s; only a
+// foreign kernel holding an XCD that long) gives up and sets ctr[1]; the
+// scan's result is then incomplete, and the pipelines that read it check
+// that word (scan_watchdog) at their next host read-back and fail loudly.
 constexpr uint64_t kScAgg = 1ull << 32, kScPre = 2ull << 32;
-// ticket = 0 (a grid that is resident at once): tile = workgroup id, no
-// ticket — every tile it waits for is running too, and publishes its sum
-// before it waits.  The ticket is one same-address atomic per block, issued
-// before the block's loads: at 1184 tiles (the 256M profile's [bin][tile]
-// table) they serialised into most of the kernel's time.
 __global__ void __launch_bounds__(TPB)
     scan_onepass(uint32_t *a, int64_t len, uint64_t *__restrict__ status,
                  unsigned long long *__restrict__ ctr, uint32_t epoch, int ticket) {
@@ -307,7 +313,7 @@ __global__ void __launch_bounds__(TPB)
       const uint64_t notready = __ballot(fl == 0);
       const uint64_t need = pre ? (((pre & -pre) << 1) - 1) : ~0ull;  // lanes up to the nearest prefix
       if (notready & need) {
-        if (++spins > (1u << 24)) {  // watchdog (the ticket order makes it unreachable)
+        if (++spins > (1u << 24)) {  // watchdog (see above): ctr[1], checked by the caller
           if (lane == 0) atomicOr(&ctr[1], 1ull);
           break;
         }
@@ -512,7 +518,20 @@ struct HostBuf {
     size_t want = need < 4096 ? 4096 : need;
     PBX_HIP(hipHostMalloc(&p, want,
                           mapped ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault));
-    if (mapped) PBX_HIP(hipHostGetDevicePointer(&dev, p, 0));
+    if (mapped) {
+      // The completion-tag protocols that write here (fused_pack, radial_mono)
+      // rely on the mapping being coherent (fine-grained: the device does not
+      // cache it, so a store is performed at the fabric once its vmcnt
+      // drains, and the tag is the last posted write): check, fail loudly.
+      unsigned int fl = 0;
+      PBX_HIP(hipHostGetFlags(&fl, p));
+      if (!(fl & hipHostMallocCoherent) || !(fl & hipHostMallocMapped)) {
+        (void)hipHostFree(p);
+        p = nullptr;
+        fail(PBX_ERR_RUNTIME, "mapped results buffer is not coherent host memory (flags 0x%x)", fl);
+      }
+      PBX_HIP(hipHostGetDevicePointer(&dev, p, 0));
+    }
     bytes = want;
     return p;
   }
@@ -524,6 +543,10 @@ struct HostBuf {
 };
 
 static inline uint32_t ntiles_of(int64_t n) { return (uint32_t)((n + TILE - 1) / TILE); }
+
+// The sticky watchdog word of a scan workspace (scan_onepass ctr[1]):
+// non-zero once a look-back gave up; cleared by the reader that reports it.
+static inline unsigned long long *scan_watchdog(Buf &ws) { return (unsigned long long *)ws.p + 1; }
 
 // Exclusive scan of len u32 in place, any length: one launch (scan_onepass).
 // `ws` holds [ticket counter, watchdog][status word per tile]; its host-side

@@ -1809,8 +1809,10 @@ __global__ void __launch_bounds__(TPB)
                unsigned long long *__restrict__ counts, int nb, const double *__restrict__ slab,
                int64_t rows, int nsum, double *__restrict__ out, const uint32_t *__restrict__ offs,
                uint32_t ntiles, int nhead, const double *__restrict__ slab2, int64_t rows2,
-               uint64_t *__restrict__ done, uint64_t done_target, int tagpos) {
+               uint64_t *__restrict__ done, uint64_t done_target, int tagpos,
+               const unsigned long long *__restrict__ scan_wd) {
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
+  constexpr int ERRW = (int)(offsetof(FusedCtl, err) / sizeof(double));  // the word holding err
   if ((int)blockIdx.x >= nhead) {
     __shared__ double red[TPB];
     const int j = (int)blockIdx.x - nhead;
@@ -1827,8 +1829,17 @@ __global__ void __launch_bounds__(TPB)
     if (threadIdx.x == 0) out[NC + nq + nb + j] = red[0];
   } else {
     const int t = blockIdx.x * TPB + threadIdx.x;
-    if (t < NC) out[t] = ((const double *)ctl)[t];
-    else if (t < NC + nq) out[t] = edges[t - NC];
+    if (t < NC) {
+      double v = ((const double *)ctl)[t];
+      if (t == ERRW && scan_wd && *scan_wd) {  // a scan of this step gave up: err bit 4
+        const uint64_t b = __builtin_bit_cast(uint64_t, v) |
+                           ((uint64_t)4u << (8 * (offsetof(FusedCtl, err) % sizeof(double))));
+        v = __builtin_bit_cast(double, b);
+      }
+      out[t] = v;
+    } else if (t < NC + nq) {
+      out[t] = edges[t - NC];
+    }
     else if (t < NC + nq + nb) {
       const int b = t - NC - nq;
       unsigned long long c;
@@ -5513,10 +5524,10 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       const uint32_t npk = (uint32_t)(nhead + nsum);
       // one rank: the pack lands in mapped host memory with a completion tag
       // (no D2H copy, no stream sync); dist: all-reduced on the device, copied
-      static const bool map_env = [] {  // A/B: PBX_PACK_MAPPED=0 copies + syncs
-        const char *v = std::getenv("PBX_PACK_MAPPED");
-        return !(v && v[0] == '0');
-      }();
+      // PBX_PACK_MAPPED=0: the copy + sync protocol (read per call: the
+      // mapped-vs-copied test switches it between calls)
+      const char *map_v = std::getenv("PBX_PACK_MAPPED");
+      const bool map_env = !(map_v && map_v[0] == '0');
       const bool mapped = !dist && map_env;
       uint64_t *pdone = nullptr;
       if (mapped) {
@@ -5534,7 +5545,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                          (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
                          (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead,
                          (const double *)maccs2, maccs2 ? (int64_t)g0 : 0, pdone,
-                         P.pack_done + npk, ntot);
+                         P.pack_done + npk, ntot,
+                         P.tsum.p ? (const unsigned long long *)prim::scan_watchdog(P.tsum) : nullptr);
       PBX_HIP(hipGetLastError());
       if (mapped) {
         P.pack_done += npk;
@@ -5558,6 +5570,10 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
     const double *hmo = (const double *)(hcn + nb);
     const FusedCtl c = *hc;
     if (c.err & 1) fail(PBX_ERR_RUNTIME, "selection look-back did not complete");
+    if (c.err & 4) {  // (the watchdog word is sticky: cleared as it is reported)
+      PBX_HIP(hipMemsetAsync(prim::scan_watchdog(P.tsum), 0, sizeof(uint64_t), st));
+      fail(PBX_ERR_RUNTIME, "a device scan of the profile step did not complete (look-back watchdog)");
+    }
     if (tiled_call) {
       ++P.n_tiled_calls;
       if (c.hint) ++P.n_hinted;

@@ -2001,8 +2001,14 @@ static bool split_parallel(Octree &T, hipStream_t st, int sorted_levels) {
   scan_u32(T.tsum, st, S, n + 1);
   PBX_HIP(hipMemcpyAsync(ctl + (nctl - 1), S + n, 4, hipMemcpyDeviceToDevice, st));  // nn
   std::vector<unsigned int> h(nctl);
+  unsigned long long wd = 0;  // the scan's look-back watchdog (prims.h), read in the same batch
   PBX_HIP(hipMemcpyAsync(h.data(), ctl, 4 * nctl, hipMemcpyDeviceToHost, st));
+  PBX_HIP(hipMemcpyAsync(&wd, prim::scan_watchdog(T.tsum), sizeof(wd), hipMemcpyDeviceToHost, st));
   PBX_HIP(hipStreamSynchronize(st));
+  if (wd) {
+    PBX_HIP(hipMemsetAsync(prim::scan_watchdog(T.tsum), 0, sizeof(wd), st));
+    fail(PBX_ERR_RUNTIME, "a device scan of the octree build did not complete (look-back watchdog)");
+  }
   if (h[0]) return false;
   const int64_t nn = h[nctl - 1];
   // levels: nodes per level -> breadth-first id ranges

@@ -49,7 +49,10 @@ class NativeLibraryMissing(ImportError):
 
 
 def lib_path() -> Path:
-    override = os.environ.get("PBX_LIBRARY")
+    """The library this process loads: $PBX_AB_LIBRARY (a same-box A/B build,
+    bound leniently), else $PBX_LIBRARY (strict, like the built product),
+    else the in-tree product build."""
+    override = os.environ.get("PBX_AB_LIBRARY") or os.environ.get("PBX_LIBRARY")
     if override:
         return Path(override)
     return Path(__file__).resolve().parent / "lib" / _LIB_NAME
@@ -181,10 +184,11 @@ def load() -> ctypes.CDLL:
             f"{path} not found: the HIP engine is not built "
             "(python -c 'import __graft_entry__ as g; g.build()')")
     lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
-    # an A/B build named by PBX_LIBRARY may predate a symbol: bind what it has
-    # (calling a missing one raises AttributeError); the product library must
-    # export every declared symbol (tests/test_abi.py)
-    lenient = os.environ.get("PBX_LIBRARY") is not None
+    # an A/B build named by PBX_AB_LIBRARY may predate a symbol: bind what it
+    # has (calling a missing one raises AttributeError); any other library —
+    # the product build, or one named by PBX_LIBRARY — must export every
+    # declared symbol (tests/test_abi.py)
+    lenient = bool(os.environ.get("PBX_AB_LIBRARY"))
     for name, (res, args) in _SIGNATURES.items():
         if lenient and not hasattr(lib, name):
             continue

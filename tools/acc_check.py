@@ -1,6 +1,6 @@
 """Accuracy of the all-particles direct sum (symmetric kernel) against the C
 oracle on a 1M Plummer sphere: 4096 random targets + the 64 innermost ones.
-Run with PBX_LIBRARY=... to check a variant build (GPU box diagnostic)."""
+Run with PBX_AB_LIBRARY=... to check a variant build (GPU box diagnostic)."""
 import os
 import sys
 
@@ -22,7 +22,7 @@ rp, ra = og.direct_subset(pos, mass, idx)
 ep = np.abs(pot[idx] - rp) / np.abs(rp)
 ea = np.linalg.norm(acc[idx] - ra, axis=1) / np.linalg.norm(ra, axis=1)
 w = np.argmax(ea)
-print(f"lib={os.environ.get('PBX_LIBRARY', 'default')} n={n}")
+print(f"lib={os.environ.get('PBX_AB_LIBRARY', 'default')} n={n}")
 print(f"pot rel err: max {ep.max():.3e}  p99.9 {np.quantile(ep, 0.999):.3e}  median {np.median(ep):.3e}")
 print(f"acc rel err: max {ea.max():.3e}  p99.9 {np.quantile(ea, 0.999):.3e}  median {np.median(ea):.3e}"
       f"  (worst at r={r[idx][w]:.3e}, |a|={np.linalg.norm(ra[w]):.3e})")

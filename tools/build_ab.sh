@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Builds pynbodyext/lib/libpbx_ab.so from git revision $1 (default HEAD) for
-# same-box A/B timing: PBX_LIBRARY=<path> python tools/run_leg.py ...
+# same-box A/B timing: PBX_AB_LIBRARY=<path> python tools/run_leg.py ...
 set -euo pipefail
 rev=${1:-HEAD}
 root=$(cd "$(dirname "$0")/.." && pwd)
