@@ -249,6 +249,19 @@ int pbx_octree_set_cost_kind(pbx_octree *tree, int kind);
  * longest wave, and a smaller wave walks a shorter union of its targets'
  * walks.  NULL disables it; the array must stay valid while it is set. */
 int pbx_octree_set_wave_split(pbx_octree *tree, const int32_t *d_cost_orig, int permille);
+/* Preorder pieces (config 5's critical path; no reference counterpart — the
+ * reference parallelises over targets only, tree.rs:1443-1450): self-mode
+ * walks of order 3 without softening, potential + acceleration, run their
+ * 64-target waves from a table, and a wave whose previous walk took more than
+ * permille / 1000 of the longest one's steps is cut into up to kmax pieces by
+ * DFS preorder id interval at its previous walk's node checkpoints
+ * (tree.rs:736-776: the walk visits nodes in preorder, so each piece is the
+ * lane's own walk restricted to an id interval; opening decisions and
+ * interaction counts are those of the whole walk, the sums of a split wave
+ * are added in piece order).  Pieces are listed longest first.  permille 0:
+ * the table and checkpoints only (no split); -1: off (default).  Per-group
+ * state is keyed by leaf-order position / 64. */
+int pbx_octree_set_walk_pieces(pbx_octree *tree, int permille, int kmax);
 /* out[13] = {n, nodes, levels, has_mass_payload, has_hmax,
  *            accepted node interactions and leaf pairs of the last walk,
  *            path words, wave steps and active-lane steps of the last walk

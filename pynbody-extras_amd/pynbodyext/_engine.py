@@ -323,6 +323,11 @@ class Octree:
         two 32-target waves dispatched first (speed only); None: off."""
         nat.call("pbx_octree_set_wave_split", self._h, d_cost_orig or None, int(permille))
 
+    def _set_walk_pieces(self, permille: int = -1, kmax: int = 2) -> None:
+        """Preorder pieces of the heaviest waves in self-mode walks
+        (pbx_octree_set_walk_pieces; -1 = off)."""
+        nat.call("pbx_octree_set_walk_pieces", self._h, int(permille), int(kmax))
+
     def _set_cost_kind(self, kind: int) -> None:
         """compute_range's d_cost: 0 interactions per target, 1 the wave's work."""
         nat.call("pbx_octree_set_cost_kind", self._h, int(kind))
