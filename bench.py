@@ -153,6 +153,28 @@ def cpu_baseline(pos, mass, seconds: float, cores: int | None = None):
     }
 
 
+def cpu_rows(many: dict, one: dict) -> dict:
+    """The CPU baseline rows of a gravity leg: `many` (the box's CPU share,
+    host_cores() threads) carries the line; the single-core run and the
+    all-affinity-cores figure sit beside it.  The reference's threads=0 is
+    rayon's global pool = every core of the machine
+    (crates/pynbodyext-rust/src/gravity.rs:87-101); the GPU boxes show 256
+    affinity cores but give one GPU's job a share of 16 (OMP_NUM_THREADS,
+    the harness's rule for worker pools), so the all-cores row is the
+    16-thread rate scaled linearly to the affinity count — an upper bound
+    on what rayon could reach there (perfect scaling), not a run."""
+    many["single_core"] = {k: one[k] for k in ("value", "cores", "sample")}
+    aff = len(os.sched_getaffinity(0))
+    many["threads_scaling_efficiency"] = many["value"] / (many["cores"] * one["value"])
+    many["all_affinity_cores_bound"] = {
+        "value": many["value"] * aff / many["cores"], "cores": aff,
+        "kind": "linear extrapolation (upper bound), not run",
+        "note": f"{many['cores']}-thread rate x {aff}/{many['cores']}: the reference's rayon "
+                "pool on every affinity core with perfect scaling; not run because a one-GPU "
+                "job's CPU share on the box is OMP_NUM_THREADS threads"}
+    return many
+
+
 PROFILE_BYTES_PER_PARTICLE = 49  # SURVEY.md §8d: equaln profile, algorithmic HBM bytes / input particle
 HBM_PEAK_GBS = 8000.0
 
@@ -446,6 +468,14 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
     build_ms, bal_ms, walk_ms, share_ms, prof_ms = (float(np.median([p[i] for p in parts]))
                                                     for i in range(5))
     info = solver.info
+    with nat.precise_mode(True):  # the walk in precise mode, beside the fast headline
+        pw = []
+        for _ in range(3):
+            step()
+            nat.synchronize()
+            dist.barrier()
+            pw.append(ev[2].elapsed_ms(ev[3]))
+        walk_precise_ms = dist.max(float(np.median(pw[1:])))
     first, count = solver.ranges[dist.rank] if solver.ranges else (0, n)
     flops = info["node_interactions"] * TREE_FLOP_NODE + info["leaf_pairs"] * TREE_FLOP_PP
     achieved = flops / (walk_ms * 1e-3) / 1e12
@@ -479,7 +509,8 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
                      "traffic": pmc_traffic("tree")[0], "kernel": "walk_kernel<order 3, pot+acc>",
                      "flop_per_node": TREE_FLOP_NODE, "flop_per_leaf_pair": TREE_FLOP_PP,
                      "kernel_ms": walk_ms, "mode": "precise" if nat.get_precise() else "fast",
-                     "traffic_source": pmc_traffic("tree")[1]},
+                     "traffic_source": pmc_traffic("tree")[1],
+                     "precise": precise_row(flops, walk_precise_ms)},
         "profile_check": {"bins_nonempty": int(np.sum(mom[:, 0] > 0)),
                           "phi_innermost_bin": float(phi_profile[mom[:, 0] > 0][0]),
                           "phi_outermost_bin": float(phi_profile[mom[:, 0] > 0][-1])},
@@ -499,10 +530,9 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
         solver.d_acc.download(tmp3)
         acc[order] = tmp3
         idx.free()
-        out["cpu_baseline"], out["parity_vs_oracle"] = tree_cpu_baseline(
-            pos, mass, cpu_seconds, theta, pot, acc)
+        many, out["parity_vs_oracle"] = tree_cpu_baseline(pos, mass, cpu_seconds, theta, pot, acc)
         one, _ = tree_cpu_baseline(pos, mass, cpu_seconds / 2, theta, pot, acc, cores=1)
-        out["cpu_baseline"]["single_core"] = {k: one[k] for k in ("value", "cores", "sample")}
+        out["cpu_baseline"] = cpu_rows(many, one)
     solver.close()
     prof.close()
     d_pos.free()
@@ -535,6 +565,82 @@ def bench_api(pos, mass, reps: int = 2) -> dict:
             "potentials_pairs_per_s": pairs / p, "accelerations_pairs_per_s": pairs / a,
             "note": "host numpy arrays in and out (PCIe-inclusive), one call per quantity as the "
                     "reference API has; the bench's value is the device-resident fused solve"}
+
+
+def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
+    """Config 3 through the API a reference user calls, on HOST arrays
+    (PCIe-inclusive; the bench's profile value is the device-resident
+    pipeline): RadialProfileBuilder(ndim=3, weight="mass", bins_type="equaln",
+    nbins=128).filter(Sphere(10) & FamilyFilter("dm"))(sim) with the two
+    statistics read (profiles/base.py:75-140, spatial_profile.py:30-35), and
+    the profile drop-in's seams (integration/pynbodyext_mi355x_profiles.py:
+    bins.py:720-746 equaln fused with :346-395 assignment + CSR read-back,
+    and the Σ mass of proarray.py:272-334) on the host r of the kept
+    particles, as the reference's BinsSet calls them."""
+    import importlib.util
+    from types import SimpleNamespace
+
+    from pynbodyext.filters import FamilyFilter, Sphere
+    from pynbodyext.profiles import RadialProfileBuilder
+    from pynbodyext.synthetic import family_slices, plummer_snapshot
+
+    spec = importlib.util.spec_from_file_location(
+        "pbx_integration_bench", ROOT / "integration" / "pynbodyext_mi355x_profiles.py")
+    integ = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(integ)
+    integ._load(str(nat.lib_path()))
+    rows = []
+    for n in sizes:
+        sim = plummer_snapshot(n, seed=SEEDS.get(n, 1002))
+        builder = RadialProfileBuilder(ndim=3, weight="mass", bins_type="equaln",
+                                       nbins=128).filter(Sphere(10.0) & FamilyFilter("dm"))
+
+        def call():
+            prof = builder(sim)
+            return prof, np.asarray(prof["mass"]["sum"]), np.asarray(prof["r"])
+
+        call()
+        tb = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            prof, msum, rmean = call()
+            tb.append(time.perf_counter() - t0)
+        kept = len(prof.sim)
+        # the seams on the host r of the same kept particles
+        pos, mass = np.asarray(sim["pos"]), np.asarray(sim["mass"])
+        dm = family_slices(n)["dm"]
+        p = pos[dm]
+        r2 = (p[:, 0] * p[:, 0] + p[:, 1] * p[:, 1]) + p[:, 2] * p[:, 2]
+        keep = r2 < 100.0
+        x = np.sqrt(r2[keep])
+        w = np.asarray(mass[dm])[keep]
+
+        def seams():
+            bs = SimpleNamespace(nbins=128, _bin_min=None, _bin_max=None)
+            edges = integ._equal_number_bins_algorithm(bs, x)
+            binind, counts = integ._assign_particles(bs, x, edges)
+            m = bs.__dict__["_pbx_handle"].moments(w, None, 1 << 3)
+            bs.__dict__["_pbx_handle"].close()
+            return edges, counts, m
+
+        seams()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            edges, counts, m = seams()
+            ts.append(time.perf_counter() - t0)
+        same = (np.array_equal(edges, np.asarray(prof.bin_edges)) and
+                np.array_equal(counts, np.asarray(prof.npart_bins)))
+        b, sm = float(np.median(tb)), float(np.median(ts))
+        rows.append({"n": n, "kept": kept,
+                     "builder_ms": b * 1e3, "builder_particles_per_s": n / b,
+                     "seams_ms": sm * 1e3, "seams_kept_per_s": kept / sm,
+                     "seams_equal_builder": bool(same)})
+        del sim, prof
+    return {"rows": rows,
+            "note": "host numpy in and out (positions / masses staged to HBM inside the call "
+                    "for the builder; r uploaded, the int64 CSR read back for the seams): "
+                    "PCIe-inclusive user-facing times, not the bench value"}
 
 
 def pmc_profile_step_bytes(n: int):
@@ -602,6 +708,14 @@ def cpu_host() -> dict:
 # 2.4 GHz = 39.3e12 lane-instructions/s (78.6 TF counts an FMA as 2).
 SYM_INSTR_PER_UNORDERED_PAIR = 19
 FP64_LANE_INSTR_PEAK = 256 * 4 * 16 * 2.4e9
+
+
+def precise_row(flop: float, kernel_ms: float) -> dict:
+    """The kernel in precise mode (pbx_set_precise(1): 1/r Newton-refined,
+    the reference's arithmetic to rounding) beside the fast-mode headline."""
+    tf = flop / (kernel_ms * 1e-3) / 1e12
+    return {"kernel_ms": kernel_ms, "achieved": tf, "frac": tf / FP64_VECTOR_PEAK_TFLOPS,
+            "mode": "precise", "note": "same launch, pbx_set_precise(1); not the headline"}
 
 
 def executed_issue(symmetric: bool, pairs_launch: float, kern_ms: float) -> dict:
@@ -672,6 +786,19 @@ def main():
     kernel_ms = [a.elapsed_ms(b) for a, b in events]
     kern_avg_ms = dist.max(float(np.mean(kernel_ms)))
 
+    # the same solve in precise mode (reference arithmetic, direct.rs:173-179:
+    # 1/r refined by a Newton step), kernel time only, beside the fast headline
+    with nat.precise_mode(True):
+        step(False)
+        pe = [(nat.Event(), nat.Event()) for _ in range(2)]
+        for a, b in pe:
+            solver.gather_sources()
+            a.record()
+            solver.solve()
+            b.record()
+        nat.synchronize()
+    precise_ms = dist.max(float(np.mean([a.elapsed_ms(b) for a, b in pe])))
+
     pairs_per_step = float(n_tot) * float(n_tot - 1)   # all ranks together
     value = pairs_per_step * args.steps / elapsed
     # roofline: this rank's kernel does n_loc * (n_tot - 1) pairs per launch
@@ -694,17 +821,18 @@ def main():
         sweep = bench_profile(sizes, steps=max(200, args.steps), warmup=max(5, args.warmup),
                               cpu=not args.no_cpu_baseline and rank == 0 and world == 1,
                               dist=dist if dist.comm is not None else None)
-    api = None
+    api = prof_api = None
     if world == 1 and not args.no_api:
         api = bench_api(pos, mass)
+        if not args.no_profile:
+            prof_api = bench_profile_api()
     dist.close()
     if rank != 0:
         return
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(pos, mass, args.cpu_seconds)
-        one = cpu_baseline(pos, mass, args.cpu_seconds / 2, cores=1)
-        cpu["single_core"] = {k: one[k] for k in ("value", "cores", "sample")}
+        cpu = cpu_rows(cpu_baseline(pos, mass, args.cpu_seconds),
+                       cpu_baseline(pos, mass, args.cpu_seconds / 2, cores=1))
     out = {
         "metric": "particle-pairs/sec (direct-sum gravity, force+potential)",
         "value": value,
@@ -743,6 +871,7 @@ def main():
             "kernel_ms": kern_avg_ms,
             "frac_is": "algorithmic: 22 flop per ORDERED pair delivered (SURVEY.md §8d)",
             **executed_issue(solver.symmetric, pairs_launch, kern_avg_ms),
+            "precise": precise_row(pairs_launch * FLOP_PER_PAIR, precise_ms),
         },
         "cpu_baseline": cpu,
         "api_level": api,
@@ -788,6 +917,7 @@ def main():
                                           (big["cold_stream_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
                             if big.get("cold_stream_ms") else None},
             "parity_at_roofline_point": big.get("parity_vs_oracle"),
+            "api_level": prof_api,
             "one_launch_discards": (head.get("path") or {}).get("mono_discarded"),
             "sweep": sweep,
             "cpu_baseline": head.get("cpu_baseline"),
