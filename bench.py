@@ -646,14 +646,17 @@ def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
 def pmc_profile_step_bytes(n: int):
     """HBM bytes of one n-particle profile step from the committed PMC
     summary (profiles/pmc_profile_latest.json, collected at its "n")."""
-    f = ROOT / "profiles" / "pmc_profile_latest.json"
-    if not f.exists():
-        return None
-    try:
-        d = json.loads(f.read_text())
-        return d.get("hbm_bytes_per_step") if int(d.get("n", 64_000_000)) == n else None
-    except Exception:
-        return None
+    for f in (ROOT / "profiles" / f"pmc_profile_{n // 1_000_000}M.json",
+              ROOT / "profiles" / "pmc_profile_latest.json"):
+        if not f.exists():
+            continue
+        try:
+            d = json.loads(f.read_text())
+            if int(d.get("n", 64_000_000)) == n:
+                return d.get("hbm_bytes_per_step")
+        except Exception:
+            continue
+    return None
 
 
 def pmc_traffic(which: str = "direct"):
@@ -908,8 +911,9 @@ def main():
                          "at_n_per_gpu": big["n_per_gpu"],
                          "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE,
                          "traffic": pmc_profile_step_bytes(big["n_per_gpu"]),
-                         "traffic_note": "HBM bytes per 64M step (all profile kernels, PMC "
-                                         "run committed in profiles/pmc_profile_latest.json)"},
+                         "traffic_note": "HBM bytes per step at at_n_per_gpu (all profile "
+                                         "kernels: 2 x FETCH_SIZE + WRITE_SIZE, PMC runs "
+                                         "committed as profiles/pmc_profile_<N>M.json)"},
             "counter_roofline": counter,
             "cold_handle": {"n_per_gpu": big["n_per_gpu"], "stream_ms": big.get("cold_stream_ms"),
                             "ms": big.get("cold_ms"), "warm_stream_ms": big["stream_ms"],

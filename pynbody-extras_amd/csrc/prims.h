@@ -94,9 +94,10 @@ __device__ __forceinline__ uint64_t peers8(uint32_t d, uint64_t valid) {
 
 // Stable wave-local ranks from LDS instead of ballots (peers8 costs ~85 VALU
 // per item and made the CSR / radix scatters VALU-bound): for item k every
-// valid lane ORs its lane bit into its digit's 64-bit word of this wave's
-// pmask row (ds_or_b64: OR commutes, the lanes' order inside the instruction
-// does not matter), reads the word back (= its peers), reads the digit's
+// valid lane ORs its lane bit into its half-wave's 32-bit half of its
+// digit's 64-bit word of this wave's pmask row (ds_or_b32: OR commutes, the
+// lanes' order inside the instruction does not matter), reads the whole word
+// back (= its peers), reads the digit's
 // running count run[d], and the group writes count + popcount back and
 // clears the word.  One wave's LDS instructions execute in issue order, so
 // each read sees all of item k's ORs and none of item k + 1's.  Relaxed
@@ -109,13 +110,14 @@ template <int IPT>
 __device__ __forceinline__ void wave_ranks_lds(const uint32_t (&dig)[IPT], const bool (&ok)[IPT],
                                                uint32_t *run, uint64_t *pmask,
                                                uint32_t (&lp)[IPT]) {
-  const uint64_t lbit = 1ull << lane_id();
 #pragma unroll
   for (int k = 0; k < IPT; ++k) {
     uint32_t l = 0;
     if (ok[k]) {
       const uint32_t d = dig[k];
-#ifdef PBX_RANK_HALF  // A/B: a 32-bit peer word per half-wave (4-byte ORs and clears)
+      // a 32-bit peer word per half-wave: 4-byte ORs and clears (half the
+      // LDS bytes of one 64-bit word per wave; csr_slots 91 -> 86 us at
+      // 64M, same-box A/B/A/B, profiles/r5/r5a)
       uint32_t *pw = (uint32_t *)&pmask[d];
       const uint32_t h = lane_id() >> 5;
       __hip_atomic_fetch_or(pw + h, 1u << (lane_id() & 31u), __ATOMIC_RELAXED,
@@ -125,14 +127,6 @@ __device__ __forceinline__ void wave_ranks_lds(const uint32_t (&dig)[IPT], const
       __hip_atomic_store(&run[d], base + (uint32_t)__popcll(m), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_WAVEFRONT);
       __hip_atomic_store(pw + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#else
-      __hip_atomic_fetch_or(&pmask[d], lbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      const uint64_t m = __hip_atomic_load(&pmask[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      const uint32_t base = __hip_atomic_load(&run[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      __hip_atomic_store(&run[d], base + (uint32_t)__popcll(m), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_WAVEFRONT);
-      __hip_atomic_store(&pmask[d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#endif
       l = base + rank_below(m);
     }
     lp[k] = l;

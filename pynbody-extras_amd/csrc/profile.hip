@@ -212,12 +212,7 @@ __global__ void __launch_bounds__(BT)
     uint32_t spins = 0;
     // lane l inspects tile (hi - l): lane 0 is the nearest predecessor;
     // tiles before 0 read as an inclusive prefix of 0
-#ifdef PBX_DIAG_SEL_NOLB  // timing diagnostic only: no look-back (offsets wrong)
-    excl = (uint64_t)tile * (TILE / 2);
-    for (int64_t hi = -2; false;) {
-#else
     for (int64_t hi = (int64_t)tile - 1; tile != 0 && !p.tiled && hi >= -1;) {
-#endif
       const int64_t q = hi - (int64_t)lane;
       const uint64_t s = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT)
@@ -264,11 +259,7 @@ __global__ void __launch_bounds__(BT)
       kw[(int64_t)tile * (TILE / 64) + w * SI + k] = b;
       kpre[(int64_t)tile * (TILE / 64) + w * SI + k] = (uint16_t)(run - s_excl);
     }
-#ifdef PBX_DIAG_SEL_NOWRITE  // timing diagnostic only: r not written
-    if (keep && xv[k] == -1.0) {
-#else
     if (keep) {
-#endif
       int64_t i = wbase + k * 64 + lane;
       uint32_t pos_out = slots ? (uint32_t)(k * 64) + lane : run + rank_below(b);
       xo[pos_out] = xv[k];
@@ -1017,25 +1008,13 @@ __global__ void __launch_bounds__(SH_BT)
 #pragma unroll
     for (int k = 0; k < SH_HALF; ++k) {
       double xv = 0.0;
-#ifdef PBX_DIAG_ST_NOSQRT  // timing diagnostic only: x = r^2 (no sqrt)
-      xv = (H.x[k] * H.x[k] + H.y[k] * H.y[k]) + H.z[k] * H.z[k];
-      const bool keep = ((H.in >> k) & 1u) && xv < p.r2max;
-#else
       const bool keep = ((H.in >> k) & 1u) && select_xyz(H.x[k], H.y[k], H.z[k], p, xv);
-#endif
       const uint64_t bal = __ballot(keep);
       if (lane == 0) {  // (one store per half from lane k instead: csr_slots +19 us, dropped)
         kw[wj + k] = bal;
         kpre[wj + k] = (uint16_t)run;  // kept particles before the word in this wave's slice
       }
       run += (uint32_t)__popcll(bal);
-#ifdef PBX_DIAG_ST_NOKEY  // timing diagnostic only: x stored, no key range / digit counts
-      if (keep) xt[k * 64 + lane] = xv;
-      if (false) {
-#elif defined(PBX_DIAG_ST_NOSTORE)  // timing diagnostic only: x not stored
-      if (keep) {
-        if (xv == 1234.5) xt[k * 64 + lane] = xv;
-#else
       // every slot's x stored (the readers mask by the keep bits): whole
       // lines, 277 -> 264 us at 64M (same box; measured against kept-only
       // stores once fused_hist0's timing was stable, see fused_hist0); as
@@ -1043,7 +1022,6 @@ __global__ void __launch_bounds__(SH_BT)
       // re-read of x 202 -> 191 us at 64M (same box A/B/A/B)
       __builtin_nontemporal_store(xv, xt + k * 64 + lane);
       if (keep) {
-#endif
         const uint64_t kk = dkey(xv);
         kmin = kk < kmin ? kk : kmin;
         kmax = kk > kmax ? kk : kmax;
@@ -1953,17 +1931,7 @@ __global__ void __launch_bounds__(BT)
         if (q >= fs.nm) break;
         const int col = fs.col[q], fq = fs.f[q], wq = fs.w[q];
         double *aq = acc + (int64_t)q * nb;
-#ifdef PBX_DIAG_NO_MOM_ATOMICS  // timing diagnostic only: sums not accumulated
-#pragma unroll
-        for (int k = 0; k < AS_IPT; ++k) {
-          if (b[k] >= (uint32_t)nb) continue;
-          const double f = fq == 0 ? v[k] : wv[k];
-          const double ww = wq == 0 ? v[k] : wv[k];
-          if (monomial(col, f, ww) == 1234.5) aq[0] = 0.0;
-        }
-#else
         mom_add<AS_IPT>(aq, fs.op[q], col, fq, wq, b, v, wv, (uint32_t)nb);
-#endif
       }
     }
   }
@@ -2114,24 +2082,13 @@ __global__ void __launch_bounds__(BT)
       for (int kk = 0; kk < CH; ++kk)
         b[kk] = ((keep >> kk) & 1u) ? (LDSE ? bin_of(v[kk], e, nb) : bin_of(v[kk], edges, nb))
                                     : (uint32_t)nb + 1;
-#ifndef PBX_DIAG_NO_HIST
 #pragma unroll
       for (int kk = 0; kk < CH; ++kk)
         if (b[kk] <= (uint32_t)nb) atomicAdd(&hrow[b[kk]], 1u);
-#endif
 #pragma unroll
       for (int kk = 0; kk < CH; ++kk)
         if ((keep >> kk) & 1u) bins[pos[kk]] = b[kk];
-#ifdef PBX_DIAG_NO_MOM_ATOMICS
       if (MOM) {
-        double sacc = 0.0;
-        for (int kk = 0; kk < CH; ++kk) sacc += v[kk] * wv[kk];
-        if (sacc == 1234.5) acc[0] = 0.0;
-      }
-      if (false) {
-#else
-      if (MOM) {
-#endif
 #pragma unroll
         for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
           if (q >= fs.nm) break;
@@ -2287,13 +2244,6 @@ __global__ void __launch_bounds__(MS0_TPB)
   // wait for the keep words of the tiles in flight
   const uint32_t vz = vgpr_zero();
   auto issue = [&](uint32_t t, Part &P) {
-#ifdef PBX_DIAG_AG_ILV  // timing diagnostic only: tiles interleaved over the blocks
-    {
-      const uint32_t G = gridDim.x - 1, b = blockIdx.x - 1;
-      const uint32_t t2 = b + (t - ta) * G;
-      t = t2 < nt ? t2 : nt - 1;
-    }
-#endif
     const int64_t s0 = (int64_t)t * TILE + 64 * (wl * AG_W);
 #pragma unroll
     for (int kk = 0; kk < AG_W; ++kk) {
@@ -2306,18 +2256,6 @@ __global__ void __launch_bounds__(MS0_TPB)
   };
   constexpr uint32_t SKIP = 0xffffu, DEFER = 0x10000u;  // DEFER + group: a deferred key
   auto bin = [&](uint32_t t, uint32_t tl, const Part &P) {
-#ifdef PBX_DIAG_AG_LOADONLY  // timing diagnostic only: loads consumed, nothing binned
-    {
-      double z = 0.0;
-      uint64_t kz = 0;
-      for (int kk = 0; kk < AG_W; ++kk) {
-        z += P.v[kk] * P.m[kk];
-        kz ^= P.k[kk];
-      }
-      if (z == 1234.5 && kz == 7) acc[0] = z;
-      return;
-    }
-#endif
     uint32_t bk[AG_W];
     double wv[AG_W];
     uint64_t anydef = 0;
@@ -2326,11 +2264,7 @@ __global__ void __launch_bounds__(MS0_TPB)
       const bool kp = (P.k[kk] >> lane) & 1ull;
       const uint64_t key = dkey(P.v[kk]);
       const bool inw = win && key >= ka && key <= kb;  // fused_hist0's window
-#ifdef PBX_DIAG_AG_NOTAB  // timing diagnostic only: no digit-table lookup
-      const uint32_t e = (uint32_t)(key >> 45) & 127u;
-#else
       const uint32_t e = dtab[inw ? (uint32_t)((key - lo) >> s) : 0u];
-#endif
       // (NaN in a digit without edges: no NaN edge, dropped like the table says;
       // NaN in a group's digit is deferred: its bin is below the first NaN edge)
       const bool def = kp && inw && (e & 0x8000u);
@@ -2340,7 +2274,6 @@ __global__ void __launch_bounds__(MS0_TPB)
       anydef |= __ballot(def);
     }
     const uint32_t sbase = t * (uint32_t)TILE + 64u * (uint32_t)(wl * AG_W) + lane;
-#ifndef PBX_DIAG_AG_NOBIN  // (timing diagnostic: no byte stores / tile counts)
     // (branch-free byte stores and adds — non-bins into per-lane LDS dummies —
     // measured the same, 179 us at 64M: the branches are not the cost)
 #pragma unroll
@@ -2349,12 +2282,7 @@ __global__ void __launch_bounds__(MS0_TPB)
         bins[sbase + 64u * kk] = (uint8_t)bk[kk];
         atomicAdd(&th[tl * nrs + bk[kk]], 1u);
       }
-#endif
-#ifdef PBX_DIAG_AG_NOSUM  // (timing diagnostic: no per-bin sums)
-    if (false) {
-#else
     if (MOM) {
-#endif
 #pragma unroll
       for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
         if (q >= fs.nm) break;
@@ -2362,9 +2290,6 @@ __global__ void __launch_bounds__(MS0_TPB)
                       (uint32_t)nb);
       }
     }
-#ifdef PBX_DIAG_AG_NODEFER  // timing diagnostic only: deferred keys dropped
-    anydef = 0;
-#endif
     if (anydef) {  // rare (edge-holding digits): the group segment + the block's deferred list
       // (one list reservation per call for the whole wave, ballot ranks, and
       // every segment-slot atomic issued before any is waited for: 179 -> 184
@@ -2507,18 +2432,10 @@ __global__ void __launch_bounds__(MS0_TPB)
         const uint32_t t = r[u].tg & ((1u << AG_TBITS) - 1), g = r[u].tg >> AG_TBITS;
         const uint32_t b = ok ? bin_of_in(v, e, nb, (int)gql[g], (int)gql[g + 1]) : (uint32_t)nb;
         if (ok) {
-#ifdef PBX_DIAG_FD_NOBYTE  // timing diagnostic only: deferred bins not stored
-          if (first && b == 0xdead) bins[r[u].pos] = (uint8_t)b;
-#else
           if (first) bins[r[u].pos] = (uint8_t)b;
-#endif
           if (t >= w0 && t < w1) atomicAdd(&tc[(t - w0) * nrs + b], 1u);
         }
-#ifdef PBX_DIAG_FD_NOSUM  // timing diagnostic only: no sums
-        if (false)
-#else
         if (MOM && first && ok && b < (uint32_t)nb)
-#endif
 #pragma unroll
           for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
             if (q >= fs.nm) break;
@@ -2701,20 +2618,6 @@ __global__ void __launch_bounds__(TPB)
   }
   __syncthreads();
   uint32_t lp[16];
-#ifdef PBX_DIAG_CSR_LOADONLY  // timing diagnostic only: the loads, nothing else
-  {
-    uint32_t z = o + go + tn + sbase1;
-    for (int k = 0; k < 16; ++k) z ^= key[k] ^ (uint32_t)wds[k] ^ (uint32_t)kpt[k];
-    if (z == 0x12345u) perm[0] = (int32_t)z;
-    return;
-  }
-#endif
-#ifdef PBX_DIAG_CSR_NORANK  // timing diagnostic only: no wave-local ranks
-  if (true) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) lp[k] = 0;
-  } else
-#endif
   if (LDSM) {
     uint32_t dg[16];
     bool okk[16];
@@ -2775,11 +2678,7 @@ __global__ void __launch_bounds__(TPB)
   __syncthreads();
   for (int j = threadIdx.x; j < (int)tn; j += TPB) {
     const uint32_t dgt = sk[j];
-#ifdef PBX_DIAG_CSR_NOSTORE  // timing diagnostic only: the permutation not written
-    if (dgt == 0xdead) perm[0] = (int32_t)(o + sv[j]) + (int32_t)(gofs[dgt] - dstart[dgt]);
-#else
     perm[gofs[dgt] + ((uint32_t)j - dstart[dgt])] = (int32_t)(o + sv[j]);
-#endif
   }
 }
 

@@ -1419,7 +1419,6 @@ __global__ void __launch_bounds__(WALK_TPB)
       n_pp += (unsigned long long)na * (unsigned long long)(e - s);
       if (act) {
         if (LCOST) cost += e - s;
-#ifndef PBX_DIAG_SKIP_LEAF  // timing diagnostic: leaves visited, pairs not evaluated
         // only a target's own leaf needs the self-pair mask (an int compare
         // and four selects per pair): every other leaf takes the plain loop
         const bool own = (uint32_t)(self32 - s) < (uint32_t)(e - s);
@@ -1427,7 +1426,6 @@ __global__ void __launch_bounds__(WALK_TPB)
           leaf_sum<WANT, SOFT, RAW, false>(wp, s, e, -1, tx, ty, tz, th, ph, ax, ay, az);
         else
           leaf_sum<WANT, SOFT, RAW, true>(wp, s, e, self32, tx, ty, tz, th, ph, ax, ay, az);
-#endif
       }
     }
     p = act ? (open ? first : next) : p;
@@ -2664,7 +2662,7 @@ static unsigned walk_tpb() {
 template <int P, int WANT>
 static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
   const unsigned tpb = walk_tpb();
-  unsigned grid = wp.wtab ? wp.nwt_max : (unsigned)((wp.m + tpb - 1) / tpb);
+  unsigned grid = (wp.wtab || wp.ptab) ? wp.nwt_max : (unsigned)((wp.m + tpb - 1) / tpb);
   const unsigned waves = grid;  // (before the rounding: blocks past the work exit at once)
   wp.xcd_chunk = walk_xcd_chunk();
   if (wp.xcd_chunk) {  // whole rounds of kNumXcd chunks; the extra blocks find no targets
