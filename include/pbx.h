@@ -262,6 +262,12 @@ int pbx_octree_set_wave_split(pbx_octree *tree, const int32_t *d_cost_orig, int 
  * the table and checkpoints only (no split); -1: off (default).  Per-group
  * state is keyed by leaf-order position / 64. */
 int pbx_octree_set_walk_pieces(pbx_octree *tree, int permille, int kmax);
+/* Walk statistics on (1, default) or off (0) for this tree's later walks of
+ * order 3 with potential + acceleration, no softening, in fast mode (no
+ * reference counterpart: instrumentation).  Off, pbx_octree_info reports zero
+ * interaction and step counts for those walks; decisions and values are
+ * unchanged. */
+int pbx_octree_set_walk_counters(pbx_octree *tree, int enabled);
 /* out[13] = {n, nodes, levels, has_mass_payload, has_hmax,
  *            accepted node interactions and leaf pairs of the last walk,
  *            path words, wave steps and active-lane steps of the last walk

@@ -1170,8 +1170,12 @@ __device__ __forceinline__ bool node_accept(const WalkParams &wp, const u32x16 &
 // starts at its lanes' lowest first node and stops at a_hi.  Every node is
 // decided and evaluated exactly as in the whole walk; only the sums are
 // split (added in piece order).
+// CNT: the walk statistics (interaction counts, SIMD-efficiency counters:
+// pbx_octree_info) are accumulated; a walk whose caller turned them off
+// (pbx_octree_set_walk_counters) runs without their ~7 scalar operations per
+// wave step — the same decisions and sums, only the instrumentation is gone.
 template <int P, int WANT, bool SOFT, bool RAW, bool LCOST = true, bool W8 = false,
-          bool PIECES = false>
+          bool PIECES = false, bool CNT = true>
 __global__ void __launch_bounds__(WALK_TPB)
     __attribute__((amdgpu_waves_per_eu(W8 ? 8 : ((P <= 3 && !SOFT) ? 7 : 1), W8 ? 8 : 7)))
     walk_kernel(WalkParams wp) {
@@ -1312,8 +1316,8 @@ __global__ void __launch_bounds__(WALK_TPB)
     const uint32_t wflags = (uint32_t)chunk_i(c[0], 15);
     uint32_t nleaf = wflags & WF_NEXT_LEAF;
     const bool act = (p == w);
-    const unsigned na = (unsigned)__popcll(__ballot(act));
-    n_active += na;  // SIMD efficiency counter
+    const unsigned na = CNT ? (unsigned)__popcll(__ballot(act)) : 0u;
+    if (CNT) n_active += na;  // SIMD efficiency counter
     bool open = false;
     int32_t nw = next;
     // tree.rs:1087-1090: empty nodes are skipped — their records say "leaf
@@ -1405,18 +1409,23 @@ __global__ void __launch_bounds__(WALK_TPB)
         }
       }
     }
-    const unsigned no = (unsigned)__popcll(__ballot(open));
-    n_node += na - no;  // active lanes accept or open
-    open_steps += no ? 1u : 0u;
+    const uint64_t bo = __ballot(open);
+    const unsigned no = CNT ? (unsigned)__popcll(bo) : (bo != 0ull ? 1u : 0u);
+    if (CNT) {
+      n_node += na - no;  // active lanes accept or open
+      open_steps += no ? 1u : 0u;
+    }
     nw = no ? first : next;
     nleaf = no ? (wflags & WF_FIRST_LEAF) : nleaf;
     }
     if (first < 0) {  // leaf: direct sum in ascending index order
       const int32_t s = chunk_i(c[0], 14), e = s + (int32_t)(wflags & WF_COUNT);
-      ++leaf_steps;
-      leaf_rounds += (uint32_t)(e - s + 3) >> 2;
-      leaf_active += na;
-      n_pp += (unsigned long long)na * (unsigned long long)(e - s);
+      if (CNT) {
+        ++leaf_steps;
+        leaf_active += na;
+        n_pp += (unsigned long long)na * (unsigned long long)(e - s);
+      }
+      if (CNT || wp.cost_kind) leaf_rounds += (uint32_t)(e - s + 3) >> 2;
       if (act) {
         if (LCOST) cost += e - s;
         // only a target's own leaf needs the self-pair mask (an int compare
@@ -1480,7 +1489,7 @@ __global__ void __launch_bounds__(WALK_TPB)
     wp.acc[3 * o + 1] = ay;
     wp.acc[3 * o + 2] = az;
   }
-  if (wp.counters) {
+  if (CNT && wp.counters) {
     if (lane0) {
       atomicAdd(&wp.counters[0], (unsigned long long)n_node);
       atomicAdd(&wp.counters[1], n_pp);
@@ -2136,6 +2145,7 @@ struct Octree {
   int32_t split_permille = 0;
   Buf wtab;                             // the wave table + its length
   int piece_permille = -1, piece_kmax = 2;  // preorder pieces (pbx_octree_set_walk_pieces), -1 off
+  bool walk_counts = true;                  // pbx_octree_set_walk_counters
   Buf ck, kbuf, pbuf, pcost, pctr;          // their checkpoints, scratch, partial sums, counters
   int64_t ck_groups = 0, p_slots = 0;
   Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
@@ -2671,14 +2681,29 @@ static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
   }
   const bool raw = !precise_mode();
   const bool lcost = wp.cost && !wp.cost_kind;  // per-lane counts wanted
+  const bool cnt = wp.counters != nullptr;  // (walk() clears it only where a CNT=false variant exists)
   if (wp.ptab) {  // preorder pieces (walk() enables them for this configuration only)
     if constexpr (P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC)) {
-      if (raw)
+      if (raw && cnt)
         hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true, true>), dim3(grid),
                            dim3(tpb), 0, st, wp);
+      else if (raw)
+        hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true, true, false>),
+                           dim3(grid), dim3(tpb), 0, st, wp);
       else
         hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false, true, true>), dim3(grid),
                            dim3(tpb), 0, st, wp);
+    }
+    return;
+  }
+  if (!cnt) {  // order 3, potential + acceleration, no softening, fast mode (walk())
+    if constexpr (P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC)) {
+      if (tpb == 64 && ((waves <= 8u * kNumSimd && walk_w8()) || walk_w8() == 2))
+        hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true, false, false>),
+                           dim3(grid), dim3(tpb), 0, st, wp);
+      else
+        hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, false, false, false>),
+                           dim3(grid), dim3(tpb), 0, st, wp);
     }
     return;
   }
@@ -2735,7 +2760,13 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   wp.has_hmax = T.has_hmax ? 1 : 0;
   wp.pot = d_pot;
   wp.acc = d_acc;
-  wp.counters = ctr;
+  // the walk statistics, unless the caller turned them off for a walk that
+  // has a CNT=false variant (order 3, pot + acc, no softening, fast mode,
+  // no per-lane interaction counts)
+  const bool nocnt = !T.walk_counts && T.moment_order() == 3 && !(T.has_hmax || T.soft_set) &&
+                     want == (PBX_WANT_POT | PBX_WANT_ACC) && !precise_mode() &&
+                     !(d_cost && T.cost_kind == 0);
+  wp.counters = nocnt ? nullptr : ctr;
   wp.max_steps = T.nn + 16;
   wp.fault = (unsigned int *)(ctr + 2);
   wp.cost_kind = T.cost_kind;
@@ -3305,6 +3336,13 @@ int pbx_octree_set_walk_pieces(pbx_octree *t, int permille, int kmax) {
     if (permille >= 0 && (kmax < 2 || kmax > 8)) fail(PBX_ERR_VALUE, "kmax must be in [2, 8]");
     T.piece_permille = permille < 0 ? -1 : permille;
     T.piece_kmax = kmax;
+  });
+}
+
+int pbx_octree_set_walk_counters(pbx_octree *t, int enabled) {
+  return guard([&] {
+    Octree &T = as_tree(t);
+    T.walk_counts = enabled != 0;
   });
 }
 

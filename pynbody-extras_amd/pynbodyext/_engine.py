@@ -328,6 +328,11 @@ class Octree:
         (pbx_octree_set_walk_pieces; -1 = off)."""
         nat.call("pbx_octree_set_walk_pieces", self._h, int(permille), int(kmax))
 
+    def _set_walk_counters(self, enabled: bool = True) -> None:
+        """Walk statistics (info()'s interaction / step counts) on or off for
+        later fast-mode order-3 walks (pbx_octree_set_walk_counters)."""
+        nat.call("pbx_octree_set_walk_counters", self._h, int(bool(enabled)))
+
     def _set_cost_kind(self, kind: int) -> None:
         """compute_range's d_cost: 0 interactions per target, 1 the wave's work."""
         nat.call("pbx_octree_set_cost_kind", self._h, int(kind))

@@ -479,6 +479,7 @@ class ShardedTree:
         # (PBX_WALK_PIECES="permille,kmax"; "off" or -1 disables)
         self.pieces = parse_pieces(os.environ.get("PBX_WALK_PIECES", PIECES_DEFAULT))
         self.info = None
+        self.count_walks = True  # walk statistics (set_walk_counters)
         self.d_prof = None  # [counts | moments] of the profile all-reduce
 
     def build(self):
@@ -492,6 +493,13 @@ class ShardedTree:
                 self.tree._set_walk_pieces(*self.pieces)
         else:  # next step / snapshot: same handle, HBM buffers reused
             self.tree._rebuild_device(self.d_pos.ptr, self.n, self.d_mass.ptr)
+
+    def set_walk_counters(self, enabled: bool) -> None:
+        """Walk statistics on / off for the later walks (info keeps the last
+        counted walk's); the walk's decisions and sums do not change."""
+        self.count_walks = bool(enabled)
+        if self.tree is not None:
+            self.tree._set_walk_counters(self.count_walks)
 
     def balance(self):
         """This step's target ranges (see the class docstring)."""
@@ -514,7 +522,9 @@ class ShardedTree:
         self.tree._compute_range_device(self.theta, want, first, count, 1, self.d_pot.ptr,
                                         self.d_acc.ptr,
                                         self.d_cost.offset(4 * first) if multi else None)
-        self.info = self.tree.info()
+        info = self.tree.info()
+        if self.count_walks or self.info is None:  # (uncounted walks report zeros)
+            self.info = info
         if multi and share:
             self.share_costs()
         return first, count

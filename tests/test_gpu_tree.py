@@ -593,3 +593,38 @@ def test_walk_pieces(gpu, mode):
     assert np.array_equal(p4, p0) and np.array_equal(a4, a0)
     for a in (d_pot, d_acc, d_cost):
         a.free()
+
+
+@pytest.mark.fast
+def test_walk_counters_off(gpu):
+    """pbx_octree_set_walk_counters(0): the fast order-3 walk without its
+    statistics — every target bit-identical, info() counts zero, a walk with
+    them back on counts again (full walk and a range walk at 8 waves per
+    SIMD)."""
+    from pynbodyext import _native as nat
+
+    n = 64 * 3000
+    pos, mass = plummer(n, seed=151)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    want = nat.WANT_POT | nat.WANT_ACC
+    d_pot, d_acc = nat.DeviceArray(8 * n), nat.DeviceArray(24 * n)
+
+    def walk(first, count):
+        dev._compute_range_device(0.5, want, first, count, 1, d_pot.ptr, d_acc.ptr, None)
+        p, a = np.empty(count), np.empty((count, 3))
+        d_pot.download(p)
+        d_acc.download(a)
+        return p, a, dev.info()
+
+    for first, count in ((0, n), (64 * 100, 64 * 1000 + 3)):
+        p0, a0, i0 = walk(first, count)
+        assert i0["node_interactions"] > 0 and i0["leaf_pairs"] > 0
+        dev._set_walk_counters(False)
+        p1, a1, i1 = walk(first, count)
+        dev._set_walk_counters(True)
+        assert np.array_equal(p1, p0) and np.array_equal(a1, a0)
+        assert i1["node_interactions"] == 0 and i1["leaf_pairs"] == 0 and i1["wave_steps"] == 0
+        _, _, i2 = walk(first, count)
+        assert i2["node_interactions"] == i0["node_interactions"]
+    d_pot.free()
+    d_acc.free()
