@@ -523,11 +523,12 @@ __global__ void __launch_bounds__(TPB)
 __global__ void __launch_bounds__(TPB)
     msel_reduce0h(const uint32_t *__restrict__ rows, int nrows, const uint32_t *__restrict__ rows16,
                   int nrows16, const int32_t *__restrict__ hint, uint32_t *__restrict__ H,
-                  uint64_t *__restrict__ zero, int nzero) {
+                  uint64_t *__restrict__ zero, int nzero, int rows16_done) {
   if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < nzero) zero[threadIdx.x] = 0ull;
   __shared__ int32_t shint;  // one load per block (not one per wave)
   if (threadIdx.x == 0) shint = *hint;
   __syncthreads();
+  if (shint && rows16_done) return;  // fused_hist0 summed the u16 rows already
   const int q = blockIdx.x * TPB + threadIdx.x;  // word q: digits 2q, 2q + 1
   uint32_t a = 0, b = 0;
   if (shint) {
@@ -831,7 +832,7 @@ struct FusedSetup {
   int empty_bounds;
   int tiled;  // tiled selection: x of tile t at x[t * TILE ..], its count in stat[t]
   uint32_t *toff;  // tiled: the tile offsets block 0 writes
-  uint32_t *zero;  // words block 0 zeroes for later kernels (fused_boff's per-block counts)
+  uint32_t *zero;  // words block 0 zeroes for later kernels (fused_resolve's per-block counts)
   int nzero;
   int dist;  // one rank of several: the key range (mm slots) is global, no keys here is no error
   const uint64_t *kw;  // tiled: the selection's keep words (slot i holds a key iff its bit is set)
@@ -839,6 +840,8 @@ struct FusedSetup {
   const uint32_t *hflag; // select_tiles: a window key fell outside the hint (or null)
   SelHint *hint_out;     // fused_hist0 block 0: this call's own geometry, for the next call
   const uint32_t *btot;  // tiled: select_tiles' block totals (SH_K (gridDim - 1) blocks)
+  const uint32_t *rows16;  // tiled, hinted: select_tiles' u16 digit rows (two per word)
+  int nrows16;             // their number (SH_K (gridDim - 1) rsub)
 };
 
 // Element range of fused_hist0 / fused_gather: the kept x [0, n), or with
@@ -938,8 +941,13 @@ __global__ void __launch_bounds__(SH_BT)
                  uint32_t *__restrict__ toff, uint32_t *__restrict__ btot,
                  unsigned long long *__restrict__ minmax, const SelHint *__restrict__ hint,
                  uint64_t ka, uint64_t kb, uint32_t *__restrict__ rows16, uint32_t rsub,
-                 uint32_t *__restrict__ hflag) {
+                 uint32_t *__restrict__ hflag, uint32_t *__restrict__ H) {
   constexpr int SI = TILE / SH_BT;
+  {  // the level-0 histogram H of this call, zeroed slice by slice (fused_hist0 /
+     // msel_reduce0h fill it after this launch)
+    const uint32_t per = (MS0_DIG + gridDim.x - 1) / gridDim.x, h0 = blockIdx.x * per;
+    for (uint32_t i = h0 + threadIdx.x; i < min<uint32_t>(h0 + per, MS0_DIG); i += SH_BT) H[i] = 0u;
+  }
   __shared__ uint32_t lh[MS0_DIG / 2];
   __shared__ uint32_t tcnt[SH_MAXT][SH_NW];
   __shared__ unsigned long long wmin[SH_NW], wmax[SH_NW];
@@ -1288,10 +1296,43 @@ __global__ void __launch_bounds__(MS0_TPB)
       *ctl_out = ctl;
     }
     for (int k = threadIdx.x; k <= nb; k += MS0_TPB) counts[k] = 0;  // for assign_bins
-    for (int k = threadIdx.x; k < MS0_DIG; k += MS0_TPB) H[k] = 0;   // for msel_reduce0
+    if (!fsu.tiled)  // (a tiled call's H was zeroed by select_tiles)
+      for (int k = threadIdx.x; k < MS0_DIG; k += MS0_TPB) H[k] = 0;   // for msel_reduce0
     for (int k = threadIdx.x; k < fsu.nzero; k += MS0_TPB) fsu.zero[k] = 0;
   }
   if (fsu.tiled) tile_offsets_fix(fsu.btot, fsu.nt, fsu.toff, red);  // (blocks >= 1)
+  if (ctl.hint && fsu.tiled && fsu.rows16) {
+    // select_tiles counted the keys: this block sums its slice of H's words
+    // over every u16 row (a block owns its words: plain stores, no atomics;
+    // msel_reduce0h then has nothing to add).  Thread t: word h0 + t % 32,
+    // rows t / 32, t / 32 + 32, ... (32 threads read one 128-byte piece)
+    __shared__ uint32_t pa[MS0_TPB], pb[MS0_TPB];
+    constexpr int WPB = 32;  // words per block step
+    const int nw = MS0_DIG / 2;
+    for (int h0 = blockIdx.x * WPB; h0 < nw; h0 += gridDim.x * WPB) {
+      const int q = h0 + (threadIdx.x & (WPB - 1));
+      uint32_t a = 0, b = 0;
+      if (q < nw)
+        for (int r = threadIdx.x / WPB; r < fsu.nrows16; r += MS0_TPB / WPB) {
+          const uint32_t v = fsu.rows16[(int64_t)r * nw + q];
+          a += v & 0xffffu;
+          b += v >> 16;
+        }
+      pa[threadIdx.x] = a;
+      pb[threadIdx.x] = b;
+      __syncthreads();
+      if (threadIdx.x < WPB && q < nw) {
+        for (int k = threadIdx.x + WPB; k < MS0_TPB; k += WPB) {
+          a += pa[k];
+          b += pb[k];
+        }
+        H[2 * q] = a;
+        H[2 * q + 1] = b;
+      }
+      __syncthreads();
+    }
+    return;
+  }
   if (ctl.hint) return;  // select_tiles counted the keys (msel_reduce0 sums its rows)
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
   __syncthreads();
@@ -1309,28 +1350,41 @@ __global__ void __launch_bounds__(MS0_TPB)
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) row[i] = lh[i];
 }
 
-// Level-0 resolve + groups, one block of 1024: the window size m, each
-// rank's level-0 digit and residual rank (bins.py:738-744 ranks), the
-// distinct chosen digits in rank order (= ascending), their key counts and
-// segment offsets.  H is left zeroed.
+// Level-0 resolve + groups and the per-block segment offsets, one launch of
+// nq blocks x 1024 (was fused_resolve0 + fused_boff): EVERY block scans H
+// (64 KB, L2-resident) and derives the window size m, each rank's level-0
+// digit and residual rank (bins.py:738-744 ranks), the distinct chosen
+// digits in rank order (= ascending) — the groups — with their key counts
+// and segment offsets, identically; block 0 publishes them (R, gdig, goff,
+// gq, ctl->ng / m / total), and block g then gives group g its per-block
+// offsets: block b of fused_hist0 / select_tiles counted rows[b][digit of g]
+// keys of group g, so its keys go to goff[g] + the exclusive sum over
+// earlier blocks.  H is left as it is (the next call's select_tiles or
+// fused_hist0 zeroes it).
 constexpr int FR_TPB = 1024;
 __global__ void __launch_bounds__(FR_TPB)
-    fused_resolve0(uint32_t *__restrict__ H, FusedCtl *__restrict__ ctl, int64_t nbins, int nq,
-                   MsRank *__restrict__ R, uint32_t *__restrict__ gdig, uint32_t *__restrict__ goff,
-                   uint32_t *__restrict__ gq) {
+    fused_resolve(const uint32_t *__restrict__ H, FusedCtl *__restrict__ ctl, int64_t nbins, int nq,
+                  MsRank *__restrict__ R, uint32_t *__restrict__ gdig, uint32_t *__restrict__ goff,
+                  uint32_t *__restrict__ gq, const uint32_t *__restrict__ rows, int g0,
+                  uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
+                  uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16, uint32_t rsub) {
   constexpr int PT = MS0_DIG / FR_TPB;
   __shared__ uint32_t incl[MS0_DIG];
   __shared__ uint32_t wsum[FR_TPB / 64];
   __shared__ uint32_t qdig[MS_MAXQ];
   __shared__ uint32_t gstart[MS_MAXQ + 1];
-  __shared__ int sng;
+  __shared__ uint32_t gd[MS_MAXQ], go[MS_MAXQ + 1];
+  __shared__ int sng, s_err, s_w0, s_hint;
   const int tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const int wv = tid >> 6;
-  for (int k = tid; k < MS0_DIG; k += FR_TPB) {  // coalesced, via LDS
-    incl[k] = H[k];
-    H[k] = 0;
+  const bool pub = blockIdx.x == 0;  // the block that publishes the shared results
+  if (tid == 0) {  // the control record's fields: one load per block
+    s_err = ctl->err;
+    s_w0 = ctl->w0;
+    s_hint = ctl->hint;
   }
+  for (int k = tid; k < MS0_DIG; k += FR_TPB) incl[k] = H[k];  // coalesced, via LDS
   __syncthreads();
   uint32_t v[PT], tot = 0;
 #pragma unroll
@@ -1356,8 +1410,8 @@ __global__ void __launch_bounds__(FR_TPB)
     incl[tid * PT + k] = run;
   }
   __syncthreads();
-  const int64_t m = (ctl->err & 2) ? 0 : (int64_t)incl[MS0_DIG - 1];
-  const int top = (1 << ctl->w0) - 1;
+  const int64_t m = (s_err & 2) ? 0 : (int64_t)incl[MS0_DIG - 1];
+  const int top = (1 << s_w0) - 1;
   for (int q = tid; q < nq; q += FR_TPB) {
     int64_t r = 0;
     if (m >= 2) r = (q == nq - 1) ? m - 1 : (int64_t)((double)(q * m) / (double)nbins);
@@ -1366,8 +1420,10 @@ __global__ void __launch_bounds__(FR_TPB)
       const int mid = (a + b) >> 1;
       if ((int64_t)incl[mid] <= r) a = mid + 1; else b = mid;
     }
-    R[q].prefix = (uint64_t)a;
-    R[q].rr = r - (a ? (int64_t)incl[a - 1] : 0);
+    if (pub) {
+      R[q].prefix = (uint64_t)a;
+      R[q].rr = r - (a ? (int64_t)incl[a - 1] : 0);
+    }
     qdig[q] = (uint32_t)a;
   }
   __syncthreads();
@@ -1384,8 +1440,10 @@ __global__ void __launch_bounds__(FR_TPB)
     if (lane == 0) {
       gstart[ng] = (uint32_t)nq;
       sng = (int)ng;
-      ctl->ng = (int32_t)ng;
-      ctl->m = m;
+      if (pub) {
+        ctl->ng = (int32_t)ng;
+        ctl->m = m;
+      }
     }
   }
   __syncthreads();
@@ -1393,13 +1451,14 @@ __global__ void __launch_bounds__(FR_TPB)
   // group g: digit, count, segment offset (prefix over groups: one wave)
   if (wv == 0) {
     uint32_t base = 0;
-    for (int g0 = 0; g0 < ng; g0 += 64) {
-      const int g = g0 + (int)lane;
+    for (int gg0 = 0; gg0 < ng; gg0 += 64) {
+      const int g = gg0 + (int)lane;
       uint32_t c = 0, d = 0;
       if (g < ng) {
         d = qdig[gstart[g]];
         c = incl[d] - (d ? incl[d - 1] : 0u);
-        gdig[g] = d;
+        gd[g] = d;
+        if (pub) gdig[g] = d;
       }
       uint32_t ys = c;
 #pragma unroll
@@ -1407,60 +1466,64 @@ __global__ void __launch_bounds__(FR_TPB)
         const uint32_t y = __shfl_up(ys, o, 64);
         if (lane >= (uint32_t)o) ys += y;
       }
-      if (g < ng) goff[g] = base + ys - c;
+      if (g < ng) {
+        go[g] = base + ys - c;
+        if (pub) goff[g] = base + ys - c;
+      }
       base += __shfl(ys, 63, 64);
     }
     if (lane == 0) {
-      goff[ng] = base;
-      ctl->total = base;
+      go[ng] = base;
+      if (pub) {
+        goff[ng] = base;
+        ctl->total = base;
+      }
     }
   }
-  for (int g = tid; g <= ng; g += FR_TPB) gq[g] = gstart[g];  // each group's ranks
-  for (int q = tid; q < nq; q += FR_TPB) {  // every rank's group: last start <= q
-    int a = 0, b = ng - 1;
-    while (a < b) {
-      const int mid = (a + b + 1) >> 1;
-      if ((int)gstart[mid] <= q) a = mid; else b = mid - 1;
+  if (pub) {
+    for (int g = tid; g <= ng; g += FR_TPB) gq[g] = gstart[g];  // each group's ranks
+    for (int q = tid; q < nq; q += FR_TPB) {  // every rank's group: last start <= q
+      int a = 0, b = ng - 1;
+      while (a < b) {
+        const int mid = (a + b + 1) >> 1;
+        if ((int)gstart[mid] <= q) a = mid; else b = mid - 1;
+      }
+      R[q].group = a;
     }
-    R[q].group = a;
-  }
-}
-
-// Per-block segment offsets of every group: block b of fused_hist0 counted
-// rows[b][digit of g] keys of group g, so its keys go to goff[g] + the
-// exclusive sum over earlier blocks (one block per group, one thread per
-// level-0 block).
-__global__ void __launch_bounds__(TPB)
-    fused_boff(const uint32_t *__restrict__ rows, int g0, const FusedCtl *__restrict__ ctl,
-               const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ goff,
-               uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
-               uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16, uint32_t rsub) {
-  __shared__ uint32_t wsum[NWAVE];
-  __shared__ int c_run, c_hint;  // the control record's fields, one load per block
-  const int g = blockIdx.x;
-  if (threadIdx.x == 0) {
-    c_run = !(ctl->err & 2) && g < ctl->ng;
-    c_hint = ctl->hint;
   }
   __syncthreads();
-  if (!c_run) return;
-  const int b = threadIdx.x;  // g0 <= TPB
+  // this block's group: per-block segment offsets (one thread per level-0 block)
+  const int g = blockIdx.x;
+  if ((s_err & 2) || g >= ng) return;
+  const uint32_t d = gd[g];
   uint32_t c = 0;
-  if (c_hint) {  // select_tiles blocks (b - 1) SH_K .. + SH_K - 1 cover block b's tiles
-    const uint32_t d = gdig[g];
+  const int b = tid;  // g0 <= FR_TPB
+  if (s_hint) {  // select_tiles blocks (b - 1) SH_K .. + SH_K - 1 cover block b's tiles
     if (b >= 1 && b < g0)
       for (uint32_t j = 0; j < SH_K * rsub; ++j)  // the SH_K blocks' rsub rows each
         c += (rows16[((int64_t)(b - 1) * SH_K * rsub + j) * (MS0_DIG / 2) + (d >> 1)] >>
               (16 * (d & 1))) &
              0xffffu;
   } else if (b < g0) {
-    c = rows[(int64_t)b * MS0_DIG + gdig[g]];
+    c = rows[(int64_t)b * MS0_DIG + d];
   }
-  uint32_t tot;
-  const uint32_t ex = block_excl_scan(c, wsum, &tot);
-  if (b < g0) boff[(int64_t)b * MS_MAXQ + g] = goff[g] + ex;
+  // exclusive scan of c over the block's 16 waves (block_excl_scan is 4-wave)
+  uint32_t xc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(xc, o, 64);
+    if (lane >= (uint32_t)o) xc += y;
+  }
+  if (lane == 63) wsum[wv] = xc;
+  __syncthreads();
+  uint32_t ex = xc - c, btot = 0;
+  for (int k = 0; k < FR_TPB / 64; ++k) {
+    ex += k < wv ? wsum[k] : 0u;
+    btot += wsum[k];
+  }
+  if (b < g0) boff[(int64_t)b * MS_MAXQ + g] = go[g] + ex;
   if (bcnt && b < g0 && c) atomicAdd(&bcnt[b], c);  // keys block b gathers, all groups
-  if (lc && b == 0) lc[g] = tot;  // distributed: this rank's keys of group g
+  if (lc && b == 0) lc[g] = btot;  // distributed: this rank's keys of group g
 }
 
 // Distributed equaln: every rank's keys of group g occupy one slice of the
@@ -1488,7 +1551,7 @@ __global__ void dist_status(const FusedCtl *__restrict__ ctl, int64_t *__restric
 
 // keys of the chosen level-0 buckets -> their group's segment (key - base).
 // Same grid and element order as fused_hist0, so block b owns exactly the
-// slots fused_boff gave it; inside the block an LDS counter per group hands
+// slots fused_resolve gave it; inside the block an LDS counter per group hands
 // them out (no global atomics: the keys of one group are few and were
 // contended on a handful of addresses).
 __global__ void __launch_bounds__(MS0_TPB)
@@ -1782,21 +1845,76 @@ constexpr int SLAB_G = 64;  // partial groups of the general (moments) path
 // one to *done once its stores have landed, and the block that brings it to
 // done_target stores done_target at out[tagpos] (radial_mono's mono_done
 // protocol): the host polls that word instead of a copy + stream sync.
-__global__ void __launch_bounds__(TPB)
-    fused_pack(const FusedCtl *__restrict__ ctl, const double *__restrict__ edges, int nq,
-               unsigned long long *__restrict__ counts, int nb, const double *__restrict__ slab,
-               int64_t rows, int nsum, double *__restrict__ out, const uint32_t *__restrict__ offs,
-               uint32_t ntiles, int nhead, const double *__restrict__ slab2, int64_t rows2,
-               uint64_t *__restrict__ done, uint64_t done_target, int tagpos,
-               const unsigned long long *__restrict__ scan_wd) {
+struct PackArgs {
+  const FusedCtl *ctl;
+  const double *edges;
+  int nq;
+  unsigned long long *counts;
+  int nb;
+  const double *slab;
+  int64_t rows;
+  int nsum;
+  double *out;
+  const uint32_t *offs;
+  uint32_t ntiles;
+  int nhead;
+  const double *slab2;
+  int64_t rows2;
+  uint64_t *done;
+  uint64_t done_target;
+  int tagpos;
+  const unsigned long long *scan_wd;
+  double *stage;  // done != null: the pack in device memory (sc1), copied out by the last block
+};
+
+// The completion-tag hand-off into coherent mapped host memory (fused_pack,
+// csr_slots' pack blocks, radial_mono): each block stores its part of the
+// pack into a DEVICE staging copy with sc1 stores and drains them (vmcnt)
+// before a relaxed agent-scope count — the hand-off form of
+// MI355X_MICROARCH.md's table, no L2 write-back per block; the block whose
+// count completes the target loads the whole stage with sc1 loads, writes it
+// to the host pack, drains, then issues the one system-scope fence and the
+// tag.  Only that block writes host memory, so its fence orders every pack
+// word before the tag.  (Round 4 let every block write the host pack
+// directly and fenced only in the last block: with no ordering between
+// different blocks' posted writes and the tag, a pack whose blocks ran
+// beside heavy HBM traffic — the pack riding in csr_slots — was read with
+// words missing.)  Returns in the last block only after the tag.
+__device__ void pack_complete(uint64_t *done, uint64_t target, const double *stage, double *out,
+                              int ntot, int tagpos, uint64_t tag) {
+  __shared__ int s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's sc1 stage stores performed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old + 1 == target;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int i = threadIdx.x; i < ntot; i += blockDim.x) out[i] = ld_sc1d(&stage[i]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store((uint64_t *)(out + tagpos), tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// pack block pb of the a.nhead + a.nsum blocks (red: TPB doubles of LDS)
+__device__ void pack_block(const PackArgs &a, int pb, double *red) {
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
   constexpr int ERRW = (int)(offsetof(FusedCtl, err) / sizeof(double));  // the word holding err
-  if ((int)blockIdx.x >= nhead) {
-    __shared__ double red[TPB];
-    const int j = (int)blockIdx.x - nhead;
+  const int nq = a.nq, nb = a.nb;
+  // mapped: the staging copy (sc1), else the device pack itself (copied by the host)
+  auto put = [&](int i, double v) {
+    if (a.done) st_sc1d(&a.stage[i], v);
+    else a.out[i] = v;
+  };
+  if (pb >= a.nhead) {
+    const int j = pb - a.nhead;
     double v = 0.0;
-    for (int64_t r = threadIdx.x; r < rows; r += TPB) v += slab[r * nsum + j];
-    for (int64_t r = threadIdx.x; r < rows2; r += TPB) v += slab2[r * nsum + j];  // fix_deferred
+    for (int64_t r = threadIdx.x; r < a.rows; r += TPB) v += a.slab[r * a.nsum + j];
+    for (int64_t r = threadIdx.x; r < a.rows2; r += TPB) v += a.slab2[r * a.nsum + j];  // fix_deferred
     red[threadIdx.x] = v;
     __syncthreads();
 #pragma unroll
@@ -1804,43 +1922,37 @@ __global__ void __launch_bounds__(TPB)
       if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
       __syncthreads();
     }
-    if (threadIdx.x == 0) out[NC + nq + nb + j] = red[0];
+    if (threadIdx.x == 0) put(NC + nq + nb + j, red[0]);
   } else {
-    const int t = blockIdx.x * TPB + threadIdx.x;
+    const int t = pb * TPB + threadIdx.x;
     if (t < NC) {
-      double v = ((const double *)ctl)[t];
-      if (t == ERRW && scan_wd && *scan_wd) {  // a scan of this step gave up: err bit 4
+      double v = ((const double *)a.ctl)[t];
+      if (t == ERRW && a.scan_wd && *a.scan_wd) {  // a scan of this step gave up: err bit 4
         const uint64_t b = __builtin_bit_cast(uint64_t, v) |
                            ((uint64_t)4u << (8 * (offsetof(FusedCtl, err) % sizeof(double))));
         v = __builtin_bit_cast(double, b);
       }
-      out[t] = v;
+      put(t, v);
     } else if (t < NC + nq) {
-      out[t] = edges[t - NC];
-    }
-    else if (t < NC + nq + nb) {
+      put(t, a.edges[t - NC]);
+    } else if (t < NC + nq + nb) {
       const int b = t - NC - nq;
       unsigned long long c;
-      if (offs) {
-        c = (unsigned long long)(offs[(int64_t)(b + 1) * ntiles] - offs[(int64_t)b * ntiles]);
-        counts[b] = c;
+      if (a.offs) {
+        c = (unsigned long long)(a.offs[(int64_t)(b + 1) * a.ntiles] - a.offs[(int64_t)b * a.ntiles]);
+        a.counts[b] = c;
       } else {
-        c = counts[b];
+        c = a.counts[b];
       }
-      out[t] = __builtin_bit_cast(double, c);
+      put(t, __builtin_bit_cast(double, c));
     }
   }
-  if (!done) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pack stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t old = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == done_target) {
-      __threadfence_system();
-      __hip_atomic_store((uint64_t *)(out + tagpos), done_target, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  if (a.done) pack_complete(a.done, a.done_target, a.stage, a.out, a.tagpos, a.tagpos, a.done_target);
+}
+
+__global__ void __launch_bounds__(TPB) fused_pack(PackArgs a) {
+  __shared__ double red[TPB];
+  pack_block(a, (int)blockIdx.x, red);
 }
 
 // ----------------------------------------------------------------- assign
@@ -2123,7 +2235,7 @@ __global__ void __launch_bounds__(BT)
 // edges are known, block by block, so its writes stay inside the block's
 // own tiles).  NaN keys are binned like the others (bin_of's NaN rule: the
 // bin below the first NaN edge, else dropped).  Blocks walk fused_hist0's tile
-// ranges (tile_range), so block b fills exactly the segment slots fused_boff
+// ranges (tile_range), so block b fills exactly the segment slots fused_resolve
 // gave it, and its list lies at the exclusive sum of the earlier blocks'
 // gathered counts (bcnt).  Bins are bytes (nb < 256; invalid = nb).
 // Per-tile counts for the CSR pass ([bin][tile], nb + 1 rows) stay in LDS
@@ -2144,7 +2256,7 @@ constexpr uint32_t AG_TBITS = 24;  // tiles < 2^24 (profiles hold < 2^31 particl
 struct GatherOut {
   uint64_t *seg;          // key - window base, by segment slot
   AgRec *rec;             // deferred keys, block by block
-  const uint32_t *bcnt;   // per block: keys gathered (fused_boff)
+  const uint32_t *bcnt;   // per block: keys gathered (fused_resolve)
   uint32_t *rbase, *rn;   // per block: list start, deferred keys written
 };
 
@@ -2553,36 +2665,40 @@ __global__ void __launch_bounds__(TPB)
 // bytes): csr_sel's scheme with element e = slot (wave, iteration, lane) =
 // particle order, valid iff its keep bit is set (keep words loaded up front
 // into SGPRs: every load address is known at launch), value = the selection
-// index toff[t] + kpre + rank in the word.  Each element's wave-local rank
-// is taken right after its peer leader's returning LDS atomic.
-// STAGE: the tile is sorted by bin in LDS and written out run by run
-// (coalesced); else every element is stored at its CSR position directly
-// (a (bin, tile) run is one block's, so L2 merges its lines; no 12 KB of LDS).
-// LDSM: the wave-local stable ranks from LDS (prims.h wave_ranks_lds) instead
-// of ballots: ~12 VALU + 5 LDS instructions per 64 slots instead of peers8's
-// ~85 VALU, which made csr_slots VALU-bound (SQ_ACTIVE_INST_VALU = 94 of its
-// 107 us at 64M, profiles/r4/pmc_r4b; 105.5 -> 90.6 us same box).
-template <bool STAGE, bool LDSM>
+// index toff[t] + kpre + rank in the word.  Wave-local stable ranks from LDS
+// (prims.h wave_ranks_lds: ~12 VALU + 5 LDS instructions per 64 slots
+// instead of peers8's ~85 VALU, which made this pass VALU-bound, 105.5 ->
+// 90.6 us at 64M), the tile sorted by bin in LDS and written out run by run
+// (coalesced; storing each element at its CSR position directly was 194 vs
+// 128 us).  Tiles are XCD-contiguous (xcd_swizzle: a (bin, tile) run's
+// output lines shared with the next tile's run, and the [bin][tile] offset
+// words 16 tiles share, stay in one L2).
+// pack / npk: the step's results pack (fused_pack's work, PackArgs) rides in
+// the first npk blocks, before their tile — one launch less per step.
 __global__ void __launch_bounds__(TPB)
     csr_slots(const uint32_t *__restrict__ toff, const uint64_t *__restrict__ kw,
               const uint16_t *__restrict__ kpre, const uint32_t *__restrict__ wcnt,
               const uint8_t *__restrict__ bins, const uint32_t *__restrict__ offs,
-              uint32_t ntiles, int32_t *__restrict__ perm, uint32_t nrows, int xcd) {
+              uint32_t ntiles, int32_t *__restrict__ perm, uint32_t nrows, PackArgs pack,
+              int npk) {
   __shared__ uint32_t run[NWAVE][RADIX];
   __shared__ uint32_t dstart[RADIX];
   __shared__ uint32_t gofs[RADIX];
   __shared__ uint32_t wsum[NWAVE];
-  __shared__ uint8_t sk[STAGE ? TILE : 1];
-  // sv, and during the ranking the [NWAVE][RADIX] peer words (8 KB either way)
+  __shared__ uint8_t sk[TILE];
+  // sv, and during the ranking the [NWAVE][RADIX] peer words (8 KB either
+  // way); before both, the pack's reduction buffer (TPB doubles)
   __shared__ __attribute__((aligned(16))) uint16_t sv[TILE];
   static_assert(sizeof(uint16_t) * TILE == sizeof(uint64_t) * NWAVE * RADIX, "pmask aliases sv");
+  static_assert(sizeof(uint16_t) * TILE >= sizeof(double) * TPB, "the pack's buffer fits sv");
   uint64_t *pmask = (uint64_t *)sv;
+  if ((int)blockIdx.x < npk) {
+    pack_block(pack, (int)blockIdx.x, (double *)sv);
+    __syncthreads();
+  }
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // keep words: scalar loads
   const uint32_t lane = lane_id();
-  // xcd: each XCD takes one contiguous run of tiles (xcd_swizzle), so a
-  // (bin, tile) run's output lines shared with the next tile's run, and the
-  // [bin][tile] offset words 16 tiles share, stay in one L2 (speed only)
-  const uint32_t t = xcd ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t t = xcd_swizzle(blockIdx.x, gridDim.x);
   const int d0 = threadIdx.x;  // TPB == RADIX
   const uint32_t dr = (uint32_t)d0 < nrows ? (uint32_t)d0 : nrows - 1;  // no branch around the load
   const uint32_t go0 = offs[(int64_t)dr * ntiles + t];
@@ -2614,11 +2730,11 @@ __global__ void __launch_bounds__(TPB)
   }
   for (int d = threadIdx.x; d < NWAVE * RADIX; d += TPB) {
     (&run[0][0])[d] = 0;
-    if (LDSM) pmask[d] = 0ull;
+    pmask[d] = 0ull;
   }
   __syncthreads();
   uint32_t lp[16];
-  if (LDSM) {
+  {
     uint32_t dg[16];
     bool okk[16];
 #pragma unroll
@@ -2627,19 +2743,6 @@ __global__ void __launch_bounds__(TPB)
       dg[k] = key[k] & 255u;
     }
     wave_ranks_lds<16>(dg, okk, &run[w][0], pmask + w * RADIX, lp);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint64_t wd = wds[k];
-      const bool ok = (wd >> lane) & 1ull;
-      const uint32_t dgt = key[k] & 255u;
-      uint64_t m = peers8(dgt, wd);
-      m = ok ? m : 0ull;
-      const uint32_t ret =
-          (ok && rank_below(m) == 0) ? atomicAdd(&run[w][dgt], (uint32_t)__popcll(m)) : 0u;
-      const int leader = m ? __builtin_ctzll(m) : (int)lane;
-      lp[k] = (uint32_t)__shfl((int)ret, leader, 64) + rank_below(m);
-    }
   }
   __syncthreads();
   {
@@ -2649,8 +2752,7 @@ __global__ void __launch_bounds__(TPB)
     const uint32_t st = block_excl_scan(tot, wsum, nullptr);
     dstart[d0] = st;
     gofs[d0] = go;
-    // STAGE: tile-local sorted position; else the CSR position itself
-    uint32_t a = STAGE ? st : go;
+    uint32_t a = st;  // tile-local sorted position
 #pragma unroll
     for (int ww = 0; ww < NWAVE; ++ww) {
       const uint32_t c = run[ww][d0];
@@ -2666,15 +2768,10 @@ __global__ void __launch_bounds__(TPB)
       const uint32_t dgt = key[k] & 255u;
       const uint32_t q = run[w][dgt] + lp[k];
       const uint32_t v = (k < 8 ? sbase0 : sbase1) + (uint32_t)kpt[k] + rank_below(wd);
-      if (STAGE) {
-        sk[q] = (uint8_t)dgt;
-        sv[q] = (uint16_t)v;
-      } else {
-        perm[q] = (int32_t)(o + v);
-      }
+      sk[q] = (uint8_t)dgt;
+      sv[q] = (uint16_t)v;
     }
   }
-  if (!STAGE) return;
   __syncthreads();
   for (int j = threadIdx.x; j < (int)tn; j += TPB) {
     const uint32_t dgt = sk[j];
@@ -2698,7 +2795,7 @@ __global__ void __launch_bounds__(TPB)
 //     this tile's offset; compacted x; level-0 histogram of the tile's
 //     window keys in LDS, its non-zero bins added to H
 //   3 every block: scan of H, each rank's level-0 digit and residual rank
-//     (fused_resolve0's rules), the groups; the tile's keys of chosen
+//     (fused_resolve's rules), the groups; the tile's keys of chosen
 //     buckets -> the group segments (one global atomic per tile and group)
 //   4 block g (and g + grid, ...): group g's ranks (fused_finish) -> edges
 //   5 bins (bin_of), per-bin monomial sums in LDS (one slab row per tile),
@@ -2716,8 +2813,9 @@ constexpr int MONO_BITS = 14;
 constexpr int MONO_DIG = 1 << MONO_BITS;
 static_assert(MONO_DIG <= MS0_DIG, "the LDS arrays are MS0_DIG long");
 constexpr int BAR_LINE = 16;             // u64 words per 128-B line
-// lines 0-7 group counters, 8 top counter, 9 generation, 10 completions
-constexpr size_t BAR_WORDS = (size_t)BAR_LINE * 11;
+// lines 0-7 group counters, 8 top counter, 9 generation, 10 completions,
+// 11 the call (gen0 + 1) in which a window key fell outside the hint
+constexpr size_t BAR_WORDS = (size_t)BAR_LINE * 12;
 
 // Hand-off loads / stores of the one-launch path: sc1 (relaxed agent-scope
 // atomics: global_load / global_store ... sc1), so no fence is needed at a
@@ -2764,6 +2862,25 @@ __device__ bool grid_sync(uint64_t *bar, uint64_t gen, uint32_t nblk, int *ok) {
   return *ok != 0;
 }
 
+// A grid_sync arrival without the wait: keeps the counters at the
+// generation the host carries when a call skips a barrier it does not need
+// (every block skips it: the decision is grid-uniform).
+__device__ void grid_arrive(uint64_t *bar, uint64_t gen, uint32_t nblk) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t g = blockIdx.x % 8, ngrp = nblk < 8 ? nblk : 8;
+    const uint64_t gs = nblk / 8 + (g < nblk % 8 ? 1 : 0);
+    const uint64_t old = __hip_atomic_fetch_add(bar + BAR_LINE * g, 1ull, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == gen * gs) {
+      const uint64_t o2 = __hip_atomic_fetch_add(bar + BAR_LINE * 8, 1ull, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      if (o2 + 1 == gen * ngrp) st_sc1(bar + BAR_LINE * 9, gen);
+    }
+  }
+}
+
 struct MonoRec {  // a tile's selection result (phase 1)
   uint64_t cnt, kmin, kmax, pad;
 };
@@ -2779,7 +2896,10 @@ struct MonoArgs {
   int64_t nbins;
   FusedStats fs;
   MonoRec *rec;
-  uint32_t *H;      // level-0 histogram (MS0_DIG)
+  uint32_t *H;      // level-0 histogram counted in phase 1 with the hint's geometry (MS0_DIG)
+  uint32_t *H2;     // ... or in phase 2 with this call's own (both zero on entry and exit)
+  const SelHint *hin;  // the previous call's level-0 geometry (null: none)
+  SelHint *hout;       // this call's, for the next call
   uint32_t *gcnt;   // per-group segment fill (MS_MAXQ)
   uint64_t *seg;    // group segments (keys - lo)
   double *x;        // compacted kept x
@@ -2791,37 +2911,23 @@ struct MonoArgs {
   uint32_t *th;     // [RADIX][nt] bin counts per tile
   double *slab;     // [nt][nm * nb] per-tile monomial sums
   unsigned long long *counts;
-  double *pack;     // [ctl][edges nq][counts nb][sums nm x nb][tag]
+  double *pack;     // [ctl][edges nq][counts nb][sums nm x nb][tag] (mapped host memory)
+  double *stage;    // the same in device memory (sc1 stores; pack_complete copies it out)
   uint64_t *bar;
   uint64_t gen0;         // generations gen0 + 1 .. gen0 + 5; tag of this call
   uint64_t done_target;  // the completion counter's value once every block is done
   uint64_t *trace;       // PBX_MONO_TRACE diagnostic: 8 wall-clock stamps per block, or null
 };
 
-// End of a block's part of the call: the block whose completion brings the
-// (monotonic) counter to its target writes the pack's tag.  A call in which
-// a block gave up at a barrier never reaches the target: no tag, and the
-// host discards the call.  The host may read the pack as soon as it sees
-// the tag (radial_mono_run spins on it).  The pack lives in coherent mapped
-// host memory (uncached on the device): a block's pack stores are performed
-// once its waves' vmcnt drains, before its agent-scope count; only the
-// block that completes the count issues the system-scope fence and the tag.
-// (A system-scope fence in EVERY block — an L2 write-back each — cost the
-// kernel 65 -> 73 us at 1M, round 3.)
+// End of a block's part of the call (pack_complete): the block whose
+// completion brings the (monotonic) counter to its target copies the staged
+// pack to the host pack and writes the tag.  A call in which a block gave up
+// at a barrier never reaches the target: no tag, and the host discards the
+// call.  The host may read the pack as soon as it sees the tag (radial_mono_run
+// spins on it).  (A system-scope fence in EVERY block — an L2 write-back each
+// — cost the kernel 65 -> 73 us at 1M, round 3: only the last block fences.)
 __device__ void mono_done(const MonoArgs &a, int tagpos) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's pack stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // relaxed: an acq_rel agent-scope add is an L2 write-back per block too
-    // (the pack stores are already performed: uncached memory, vmcnt drained)
-    const uint64_t old = __hip_atomic_fetch_add(a.bar + BAR_LINE * 10, 1ull, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == a.done_target) {
-      __threadfence_system();
-      __hip_atomic_store((uint64_t *)(a.pack + tagpos), a.gen0, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  pack_complete(a.bar + BAR_LINE * 10, a.done_target, a.stage, a.pack, tagpos, tagpos, a.gen0);
 }
 
 #define MONO_STAMP(k)                                                       \
@@ -2848,12 +2954,29 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   const int tid = threadIdx.x, w = tid >> 6;
   const uint32_t lane = lane_id();
   const int nb = a.nb, nq = a.nq;
-  if (tid == 0) s_ok = 1;
-  for (int i = tid; i < MONO_DIG; i += MONO_BT) L0[i] = 0;
-  if (t == 0) {  // zeroed here, used after barrier 1
-    for (int i = tid; i < MONO_DIG; i += MONO_BT) st_sc1(&a.H[i], 0u);
-    for (int i = tid; i < RADIX; i += MONO_BT) st_sc1(&a.gcnt[i], 0u);
+  __shared__ SelHint s_hint;
+  __shared__ int s_hinted;
+  if (tid == 0) {
+    s_ok = 1;
+    SelHint h{};
+    if (a.hin) h = *a.hin;  // (one load per block)
+    s_hint = h;
   }
+  for (int i = tid; i < MONO_DIG; i += MONO_BT) L0[i] = 0;
+  if (t == 0)  // zeroed here, used after barrier 1
+    for (int i = tid; i < RADIX; i += MONO_BT) st_sc1(&a.gcnt[i], 0u);
+  __syncthreads();
+  // the previous call's level-0 geometry: this call's window keys are counted
+  // with it while x is in registers (phase 1, into H); if every window key of
+  // the call falls inside it (no block sets the bar's line 11), the digits of
+  // that geometry rank the keys exactly as this call's own would (any base <=
+  // the lowest window key and any width covering the highest: same groups,
+  // same edges) and phase 2's count and barrier are skipped
+  const SelHint hint = s_hint;
+  const bool hv = hint.valid != 0;
+  const int hb = hint.s + hint.w;
+  const uint64_t hspan = hb >= 64 ? ~0ull : ((1ull << hb) - 1);
+  const uint64_t hhi = hint.lo + hspan < hint.lo ? ~0ull : hint.lo + hspan;
   // ---- 1: selection (select_onepass) -------------------------------------
   const int64_t wbase = a.sp.base + (int64_t)t * TILE + (int64_t)w * (TILE / MONO_NW);
   double xv[MONO_SI], mv[MONO_SI];
@@ -2873,6 +2996,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       py[k] = q[1];
       pz[k] = q[2];
     }
+    bool esc = false;
 #pragma unroll
     for (int k = 0; k < MONO_SI; ++k) {
       const bool keep = ((inbits >> k) & 1u) && select_xyz(px[k], py[k], pz[k], a.sp, xv[k]);
@@ -2882,8 +3006,13 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
         const unsigned long long kk = dkey(xv[k]);
         kmin = kk < kmin ? kk : kmin;
         kmax = kk > kmax ? kk : kmax;
+        if (hv && kk >= a.ka && kk <= a.kb) {
+          if (kk >= hint.lo && kk <= hhi) atomicAdd(&L0[(uint32_t)((kk - hint.lo) >> hint.s)], 1u);
+          else esc = true;
+        }
       }
     }
+    if (__ballot(esc) && lane == 0) st_sc1(a.bar + BAR_LINE * 11, a.gen0 + 1);
 #pragma unroll
     for (int k = 0; k < MONO_SI; ++k) {
       const int64_t i = wbase + k * 64 + lane;
@@ -2908,6 +3037,11 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     wmax[w] = kmax;
   }
   __syncthreads();
+  if (hv)  // the hinted counts -> H (complete at barrier 1)
+    for (int i = tid; i < MONO_DIG; i += MONO_BT) {
+      const uint32_t v = L0[i];
+      if (v) atomicAdd(&a.H[i], v);
+    }
   if (tid == 0) {
     MonoRec r{0, ~0ull, 0ull, 0};
     for (int k = 0; k < MONO_NW; ++k) {
@@ -2965,6 +3099,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       cl.n = (int64_t)tot;
       const uint64_t lo = a.ka > cl.kmin ? a.ka : cl.kmin;
       const uint64_t hi = a.kb < cl.kmax ? a.kb : cl.kmax;
+      SelHint ho{};
       if (cl.n == 0 || a.empty_bounds || lo > hi) {
         cl.err |= 2;
         cl.w0 = 1;
@@ -2974,7 +3109,26 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
         cl.w0 = B < MONO_BITS ? B : MONO_BITS;
         cl.s0 = B - cl.w0;
         cl.lo = lo;
+        // the next call's hint: this window widened by 1/64 of its span each side
+        const uint64_t mg = span >> 6;
+        const uint64_t lo2 = lo >= mg ? lo - mg : 0ull;
+        const uint64_t hi2 = hi + mg < hi ? ~0ull : hi + mg;
+        const uint64_t sp2 = hi2 - lo2;
+        const int B2 = sp2 ? 64 - __builtin_clzll(sp2) : 1;
+        ho.w = B2 < MONO_BITS ? B2 : MONO_BITS;
+        ho.s = B2 - ho.w;
+        ho.lo = lo2;
+        ho.valid = 1;
       }
+      if (t == 0 && a.hout) *a.hout = ho;
+      const bool hinted = hv && !(cl.err & 2) && ld_sc1(a.bar + BAR_LINE * 11) != a.gen0 + 1;
+      if (hinted) {
+        cl.lo = hint.lo;
+        cl.s0 = hint.s;
+        cl.w0 = hint.w;
+        cl.hint = 1;
+      }
+      s_hinted = hinted ? 1 : 0;
       s_ctl = cl;
     }
   }
@@ -2993,21 +3147,31 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     }
     if (tid == 0) a.toff[t] = s_toff;
   }
-  if (ok2) {
+  const bool hinted = s_hinted != 0;
+  if (hinted) {  // H is complete: no second count, no wait
+    grid_arrive(a.bar, a.gen0 + 2, nt);
+  } else {
+    if (hv) {  // (phase 1 counted into L0 with the hint's geometry)
+      for (int i = tid; i < MONO_DIG; i += MONO_BT) L0[i] = 0;
+      __syncthreads();
+    }
+    if (ok2) {
 #pragma unroll
-    for (int k = 0; k < MONO_SI; ++k) {
-      const uint64_t key = dkey(xv[k]);
-      if (((keepbits >> k) & 1u) && key >= a.ka && key <= a.kb)
-        atomicAdd(&L0[(uint32_t)((key - ctl0.lo) >> ctl0.s0)], 1u);
+      for (int k = 0; k < MONO_SI; ++k) {
+        const uint64_t key = dkey(xv[k]);
+        if (((keepbits >> k) & 1u) && key >= a.ka && key <= a.kb)
+          atomicAdd(&L0[(uint32_t)((key - ctl0.lo) >> ctl0.s0)], 1u);
+      }
     }
+    __syncthreads();
+    if (ok2)
+      for (int i = tid; i < MONO_DIG; i += MONO_BT) {
+        const uint32_t v = L0[i];
+        if (v) atomicAdd(&a.H2[i], v);
+      }
+    if (!grid_sync(a.bar, a.gen0 + 2, nt, &s_ok)) return;
   }
-  __syncthreads();
-  if (ok2)
-    for (int i = tid; i < MONO_DIG; i += MONO_BT) {
-      const uint32_t v = L0[i];
-      if (v) atomicAdd(&a.H[i], v);
-    }
-  if (!grid_sync(a.bar, a.gen0 + 2, nt, &s_ok)) return;
+  const uint32_t *Hs = hinted ? a.H : a.H2;
   MONO_STAMP(2);
 
   // ---- 3: ranks -> level-0 digits and groups; keys -> group segments -----
@@ -3021,7 +3185,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     {
       uint32_t h[PT];
 #pragma unroll
-      for (int k = 0; k < PT; ++k) h[k] = ld_sc1(&a.H[k * MONO_BT + tid]);
+      for (int k = 0; k < PT; ++k) h[k] = ld_sc1(&Hs[k * MONO_BT + tid]);
 #pragma unroll
       for (int k = 0; k < PT; ++k) L0[k * MONO_BT + tid] = h[k];
     }
@@ -3128,6 +3292,13 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   }
   if (!grid_sync(a.bar, a.gen0 + 3, nt, &s_ok)) return;
   MONO_STAMP(3);
+  {  // H / H2 read for the last time: zeroed for the next call, slice by slice
+    const uint32_t per = (MONO_DIG + nt - 1) / nt, h0 = t * per;
+    for (uint32_t i = h0 + tid; i < min<uint32_t>(h0 + per, MONO_DIG); i += MONO_BT) {
+      if (hv) a.H[i] = 0u;
+      if (!hinted) a.H2[i] = 0u;
+    }
+  }
 
   // ---- 4: each group's ranks (fused_finish) -> edges ---------------------
   if (ok2) {
@@ -3170,7 +3341,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     // (gen0 + 5), or the next call on this handle would wait one short
     if (!grid_sync(a.bar, a.gen0 + 5, nt, &s_ok)) return;
     constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
-    if (t == 0 && tid < NC) a.pack[tid] = ((const double *)&s_ctl)[tid];
+    if (t == 0 && tid < NC) st_sc1d(&a.stage[tid], ((const double *)&s_ctl)[tid]);
     mono_done(a, NC + nq + nb + a.fs.nm * nb);
     return;
   }
@@ -3291,7 +3462,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       if (t == 0 && d < nb) {
         a.counts[d] = tot;
         constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
-        a.pack[NC + nq + d] = __builtin_bit_cast(double, (unsigned long long)tot);
+        st_sc1d(&a.stage[NC + nq + d], __builtin_bit_cast(double, (unsigned long long)tot));
       }
       s_gofs[d] = ex + xs - tot + bl;  // bin start + this bin's keys in tiles before t
     }
@@ -3305,8 +3476,8 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   }
   constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
   if (t == 0) {
-    if (tid < NC) a.pack[tid] = ((const double *)&s_ctl)[tid];
-    for (int i = tid; i < nq; i += MONO_BT) a.pack[NC + i] = e_lds[i];
+    if (tid < NC) st_sc1d(&a.stage[tid], ((const double *)&s_ctl)[tid]);
+    for (int i = tid; i < nq; i += MONO_BT) st_sc1d(&a.stage[NC + i], e_lds[i]);
   }
   // per-bin sums: column j summed over the tiles in a fixed order by one
   // wave; columns spread over the blocks first (its 4 loads per lane are 64
@@ -3322,7 +3493,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     double s = ((v[0] + v[1]) + v[2]) + v[3];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (lane == 0) a.pack[NC + nq + nb + j] = s;
+    if (lane == 0) st_sc1d(&a.stage[NC + nq + nb + j], s);
   }
   MONO_STAMP(6);
   mono_done(a, NC + nq + nb + nsum);
@@ -3664,10 +3835,13 @@ struct Profile {
   // one-launch radial path (radial_mono): tile records + group fill, grid
   // barrier words; barrier generation / completion count carried across calls
   Buf mono, bar, mono_trace;
+  Buf mH, mhint;  // radial_mono: its two level-0 histograms, its level-0 hint slots
+  int64_t n_mhint = 0, n_mono_hinted = 0;
   Buf dscal, dlc;  // distributed radial_equaln: global scalars, per-rank group counts
   uint64_t bar_gen = 0, bar_done = 0;
   uint32_t bar_n = 0;  // grid size the barrier words were counted for (0: reset)
   prim::HostBuf mpin{nullptr, nullptr, 0, true};  // radial_mono's / fused_pack's results pack (mapped host)
+  Buf pstage;              // the results pack staged in device memory (pack_complete)
   Buf pdone;               // fused_pack's completion counter (monotonic) ...
   uint64_t pack_done = 0;  // ... and its value after the last call
   // path counters (pbx_profile_path_stats): one-launch calls, of them
@@ -4140,7 +4314,8 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
                            dim3(SH_BT), 0, st, (const double *)d_pos, hi,
                            sp, nt, (uint32_t)G0, xo, kw, r.kpre, wc, toff, bt, mm,
                            th ? th->hint : nullptr, th ? th->ka : 0ull, th ? th->kb : ~0ull, rows16, rsub,
-                           (uint32_t *)(mm + 2 * MM_SLOTS));
+                           (uint32_t *)(mm + 2 * MM_SLOTS),
+                           (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG));
       } else if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
       else if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
       else if (sel512) go(select_onepass<512, false, double>, 512, 0.0);
@@ -4337,6 +4512,14 @@ static bool agather_off() {
   return off;
 }
 
+static bool mono_hint_env() {  // A/B: PBX_MONO_HINT=0 counts level 0 in phase 2 always
+  static const bool on = [] {
+    const char *v = std::getenv("PBX_MONO_HINT");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 static bool mono_enabled() {
   static const bool on = [] {
     const char *v = std::getenv("PBX_RADIAL_MONO");
@@ -4441,7 +4624,16 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   char *scr = (char *)P.mono.get(sizeof(MonoRec) * MONO_MAXT + sizeof(uint32_t) * RADIX);
   a.rec = (MonoRec *)scr;
   a.gcnt = (uint32_t *)(scr + sizeof(MonoRec) * MONO_MAXT);
-  a.H = (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG);
+  const bool fresh_h = !P.mH.p;
+  a.H = (uint32_t *)P.mH.get(sizeof(uint32_t) * 2 * MS0_DIG);
+  a.H2 = a.H + MS0_DIG;
+  if (!P.mhint.p) {
+    P.mhint.get(2 * sizeof(SelHint));
+    PBX_HIP(hipMemsetAsync(P.mhint.p, 0, 2 * sizeof(SelHint), st));
+  }
+  SelHint *mh = (SelHint *)P.mhint.p;
+  a.hin = (P.hint_off || !mono_hint_env()) ? nullptr : mh + (P.n_mhint & 1);
+  a.hout = mh + ((P.n_mhint + 1) & 1);
   a.seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)ns);
   a.x = r.xo;
   a.kw = r.kw;
@@ -4459,10 +4651,13 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   // readback (no copy on the stream), the host reads it after the sync
   double *hp = (double *)P.mpin.get(sizeof(double) * (size_t)(ntot + 1));
   a.pack = (double *)P.mpin.dev;
+  a.stage = (double *)P.pstage.get(sizeof(double) * (size_t)ntot);
   hp[ntot] = __builtin_bit_cast(double, ~0ull);
-  if (P.bar_n != nt || !P.bar.p) {  // counters are counted for one grid size
+  if (P.bar_n != nt || !P.bar.p || fresh_h) {  // counters are counted for one grid size
     P.bar.get(sizeof(uint64_t) * BAR_WORDS);
     PBX_HIP(hipMemsetAsync(P.bar.p, 0, sizeof(uint64_t) * BAR_WORDS, st));
+    // (after a discarded call H / H2 may hold counts: both zero on entry)
+    PBX_HIP(hipMemsetAsync(a.H, 0, sizeof(uint32_t) * 2 * MS0_DIG, st));
     P.bar_gen = P.bar_done = 0;
     P.bar_n = nt;
   }
@@ -4479,6 +4674,7 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   P.bar_gen += 5;
   P.bar_done += nt;
   ++P.n_mono;
+  ++P.n_mhint;
   if (!wait_tag(st, hp + ntot, a.gen0)) {
     P.bar_n = 0;  // discarded: zero the barrier words before the next call
     ++P.n_mono_discard;
@@ -4501,6 +4697,7 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
     std::fprintf(stderr, "\n");
   }
   P.csrh_ready = false;
+  if (((const FusedCtl *)hp)->hint) ++P.n_mono_hinted;
   *nsum = macc;
   return hp;
 }
@@ -4543,7 +4740,8 @@ int pbx_profile_destroy(void *handle) {
                   &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack, &p->frec, &p->fblk,
                   &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->shint, &p->srows,
                   &p->swc, &p->sbt, &p->mono, &p->bar,
-                  &p->mono_trace, &p->dscal, &p->dlc, &p->pdone};
+                  &p->mono_trace, &p->dscal, &p->dlc, &p->pdone, &p->pstage, &p->mH,
+                  &p->mhint};
     for (Buf *b : all) b->release();
     p->pin.release();
     p->mpin.release();
@@ -4564,6 +4762,15 @@ int pbx_profile_set_level0_hint(void *handle, int enabled) {
   return guard([&] {
     Profile &P = as_profile(handle);
     P.hint_off = enabled == 0;
+  });
+}
+
+int pbx_profile_mono_stats(void *handle, int64_t *out) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (!out) fail(PBX_ERR_VALUE, "null output");
+    out[0] = P.n_mono;
+    out[1] = P.n_mono_hinted;
   });
 }
 
@@ -5172,13 +5379,15 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                            (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0, (int)dist,
                            (const uint64_t *)P.kw.p,
                            hinted ? hints + ((P.n_tiled - 1) & 1) : nullptr, hflag,
-                           hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p};
+                           hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p,
+                           hinted ? (const uint32_t *)P.srows.p : nullptr,
+                           hinted ? SH_K * (g0 - 1) * (int)P.sel_rsub : 0};
       hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
                          rows);
       hipLaunchKernelGGL(msel_reduce0h, dim3(MS0_DIG / 2 / TPB, 32), dim3(TPB), 0, st,
                          (const uint32_t *)rows, g0, (const uint32_t *)P.srows.p,
                          hinted ? SH_K * (g0 - 1) * (int)P.sel_rsub : 0, (const int32_t *)&ctl->hint, H,
-                         stat + nt, 2 + 2 * MM_SLOTS);
+                         stat + nt, 2 + 2 * MM_SLOTS, (hinted && tiled) ? 1 : 0);
       PBX_HIP(hipGetLastError());
       P.sel_tail_zero = stat + nt;  // (select_launch: no fill before the next tiled call)
       int64_t *gsc = nullptr;  // dist: [global kept count][ctl copy]
@@ -5196,11 +5405,9 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)g0) * (MS_MAXQ + 1));
       uint32_t *goff = gdig + (MS_MAXQ + 1), *gq = goff + (MS_MAXQ + 1);
       uint32_t *boff = gq + (MS_MAXQ + 1);
-      hipLaunchKernelGGL(fused_resolve0, dim3(1), dim3(FR_TPB), 0, st, H, ctl, nbins, nq, R, gdig,
-                         goff, gq);
-      hipLaunchKernelGGL(fused_boff, dim3(nq), dim3(TPB), 0, st, (const uint32_t *)rows, g0,
-                         (const FusedCtl *)ctl, (const uint32_t *)gdig, (const uint32_t *)goff, boff,
-                         bcnt, dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr,
+      hipLaunchKernelGGL(fused_resolve, dim3(nq), dim3(FR_TPB), 0, st, (const uint32_t *)H, ctl,
+                         nbins, nq, R, gdig, goff, gq, (const uint32_t *)rows, g0, boff, bcnt,
+                         dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr,
                          (const uint32_t *)P.srows.p, P.sel_rsub);
       int64_t seg_total = 0;  // dist: keys in all ranks' group segments
       if (dist) {
@@ -5233,6 +5440,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       P.csrh_ready = false;
       uint32_t ablocks = 0;
       const uint32_t *cnt_offs = nullptr;  // scanned CSR histogram the counts come from
+      bool csr_pack = false;  // tiled: csr_slots launched with the pack
       uint32_t *th = nullptr;
       uint8_t *bins8 = nullptr;
       GatherOut go{};
@@ -5289,32 +5497,9 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         // one-pass look-back scan's 11 us at 64M: dropped)
         scan_u32(P, st, th, (int64_t)nt * nr);
         cnt_offs = th;
-        if (build_csr) {
-          int32_t *perm = (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel);
-          static const bool stage = [] {  // A/B: PBX_CSR_DIRECT=1 stores without LDS staging
-            const char *v = std::getenv("PBX_CSR_DIRECT");
-            return !(v && v[0] == '1');
-          }();
-          static const bool peers_env = [] {  // A/B: PBX_CSR_PEERS=1 ranks with peers8 ballots
-            const char *v = std::getenv("PBX_CSR_PEERS");
-            return v && v[0] == '1';
-          }();
-          auto csrk = stage ? (peers_env ? csr_slots<true, false> : csr_slots<true, true>)
-                            : (peers_env ? csr_slots<false, false> : csr_slots<false, true>);
-          static const int xcd_env = [] {  // A/B: PBX_CSR_XCD=0 keeps launch order
-            const char *v = std::getenv("PBX_CSR_XCD");
-            return (v && v[0] == '0') ? 0 : 1;
-          }();
-          // (a persistent variant — a block per run of tiles, the next tile's
-          // loads in flight during this one's ranking and stores — took
-          // 105-141 us against 87 at 64M: the prefetch registers cost
-          // occupancy, 8 -> 4-6 blocks per CU; dropped)
-          hipLaunchKernelGGL(csrk, dim3(nt), dim3(TPB), 0, st,
-                             (const uint32_t *)P.toff.p, (const uint64_t *)P.kw.p,
-                             (const uint16_t *)P.kpre.p, (const uint32_t *)P.swc.p,
-                             (const uint8_t *)bins8, (const uint32_t *)th, nt, perm, nr, xcd_env);
-          PBX_HIP(hipGetLastError());
-        }
+        // the CSR pass (csr_slots) is launched with the results pack below
+        // (its first blocks carry the pack)
+        csr_pack = build_csr;
       } else if (n_sel && lazy) {
         // tile-walking assignment over the lazy selection + its CSR pass
         const int64_t macc = (int64_t)fs.nm * nb;
@@ -5440,12 +5625,25 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         hp[ntot] = __builtin_bit_cast(double, ~0ull);
         dpk = (double *)P.mpin.dev;
       }
-      hipLaunchKernelGGL(fused_pack, dim3(npk), dim3(TPB), 0, st, (const FusedCtl *)ctl,
-                         (const double *)de, nq, cnt, (int)nb, (const double *)maccs,
-                         (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead,
-                         (const double *)maccs2, maccs2 ? (int64_t)g0 : 0, pdone,
-                         P.pack_done + npk, ntot,
-                         P.tsum.p ? (const unsigned long long *)prim::scan_watchdog(P.tsum) : nullptr);
+      const PackArgs pk{(const FusedCtl *)ctl, (const double *)de, nq, cnt, (int)nb,
+                        (const double *)maccs, (int64_t)ablocks, nsum, dpk, cnt_offs, nt, nhead,
+                        (const double *)maccs2, maccs2 ? (int64_t)g0 : 0, pdone,
+                        P.pack_done + npk, ntot,
+                        P.tsum.p ? (const unsigned long long *)prim::scan_watchdog(P.tsum) : nullptr,
+                        mapped ? (double *)P.pstage.get(sizeof(double) * (size_t)ntot) : nullptr};
+      auto csr = [&](int np) {
+        hipLaunchKernelGGL(csr_slots, dim3(nt), dim3(TPB), 0, st, (const uint32_t *)P.toff.p,
+                           (const uint64_t *)P.kw.p, (const uint16_t *)P.kpre.p,
+                           (const uint32_t *)P.swc.p, (const uint8_t *)bins8, (const uint32_t *)th,
+                           nt, (int32_t *)P.perm.get(sizeof(int32_t) * (size_t)n_sel),
+                           (uint32_t)nb + 1, pk, np);
+      };
+      if (csr_pack && npk <= nt) {  // the pack rides in csr_slots' first npk blocks
+        csr((int)npk);
+      } else {
+        if (csr_pack) csr(0);
+        hipLaunchKernelGGL(fused_pack, dim3(npk), dim3(TPB), 0, st, pk);
+      }
       PBX_HIP(hipGetLastError());
       if (mapped) {
         P.pack_done += npk;

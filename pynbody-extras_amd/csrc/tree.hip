@@ -988,7 +988,8 @@ struct WalkParams {
   // in piece order (the last piece to finish does it)
   const struct WavePiece *ptab;
   int32_t *ck;                   // per global group g = gfirst + t0 / 64: [CK_N + 1] ints,
-                                 // [0] the walk's steps, [1 + j] its node at step j * CK_STEP
+                                 // [0] the walk's cost (node steps + leaf rounds), [1 + j]
+                                 // its node at cost j * CK_STEP
   int64_t gfirst;
   double *pbuf;                  // [slot][64 lanes][pot, ax, ay, az] partial sums
   int32_t *pcost;                // [slot] the piece's wave cost (steps + leaf rounds)
@@ -1003,8 +1004,8 @@ struct WalkParams {
 struct WavePiece {
   int32_t t0, cnt, a_lo, a_hi, pslot, gbase, npc, ck0;
 };
-constexpr int CK_STEP = 64;   // checkpoint spacing in wave steps
-constexpr int CK_N = 128;     // checkpoints per group (walks of up to 8192 steps)
+constexpr int CK_STEP = 64;   // checkpoint spacing in wave cost units (node steps + leaf rounds)
+constexpr int CK_N = 160;     // checkpoints per group (walks of up to 10240 cost units)
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
@@ -1262,6 +1263,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   // phi registers: ~20 v_mov_b64 per wave step, as many VALU issues as the
   // opening test itself).
   const uint32_t max_steps = (uint32_t)wp.max_steps;
+  uint32_t ck_next = 0;  // PIECES: cost of the next checkpoint
   // theta^2 in a VGPR pair: left a kernel argument, it was reloaded from the
   // kernarg segment every step (a scalar load and its wait; SGPRs are full)
   const uint64_t th2b = __builtin_bit_cast(uint64_t, wp.theta2);
@@ -1305,9 +1307,12 @@ __global__ void __launch_bounds__(WALK_TPB)
     // bit 30 of w: the node is a leaf (walk-record flags; set only below)
     const uint32_t wleaf = ((uint32_t)w >> 30) & 1u;
     w &= 0x3fffffff;
-    if (PIECES && wp.ck && ((steps - 1) & (CK_STEP - 1)) == 0) {  // checkpoint (uniform)
-      const uint32_t j = (uint32_t)ck0 + (steps - 1) / CK_STEP;
+    if (PIECES && wp.ck && steps - 1 + leaf_rounds >= ck_next) {  // checkpoint (uniform)
+      // the wave's node at every CK_STEP units of its cost (node steps + leaf
+      // rounds, what its time follows): the next walk's piece boundaries
+      const uint32_t j = (uint32_t)ck0 + ck_next / CK_STEP;
       if (j < (uint32_t)CK_N && lane0) wp.ck[gidx * (CK_N + 1) + 1 + j] = w;
+      ck_next += CK_STEP;
     }
     u32x16 c[NCH];
     load_chunks_node<NCH>(wp.walk + (int64_t)w * RS, c, wleaf);
@@ -1318,7 +1323,8 @@ __global__ void __launch_bounds__(WALK_TPB)
     const bool act = (p == w);
     const unsigned na = CNT ? (unsigned)__popcll(__ballot(act)) : 0u;
     if (CNT) n_active += na;  // SIMD efficiency counter
-    bool open = false;
+    uint64_t bo = 0ull;  // the lanes that open this node
+    int32_t pn = act ? next : p;  // this lane's next node (a leaf: next)
     int32_t nw = next;
     // tree.rs:1087-1090: empty nodes are skipped — their records say "leaf
     // of no records" (walk_record), so the sign of `first` alone decides.
@@ -1340,7 +1346,12 @@ __global__ void __launch_bounds__(WALK_TPB)
         }
       }
       const bool accept = act && soft_ok && chunk_d(c[0], 4) < theta2 * dist2;
-      open = act && !accept;
+      // this lane's next node, and the lanes that open w as the ballot of ONE
+      // compare (pn == first holds exactly for the lanes that opened w: a lane
+      // not at w cannot have its next node inside w's subtree) — a ballot of
+      // the bool `open` is rebuilt from a VGPR copy (v_cndmask + v_cmp)
+      pn = act ? (accept ? next : first) : p;
+      bo = __ballot(pn == first);
       if (LCOST) cost += accept ? 1 : 0;
       if (accept) {
         if constexpr (P == 0) {  // monopole without multipoles (tree.rs:1126-1129, 1284-1291)
@@ -1409,7 +1420,6 @@ __global__ void __launch_bounds__(WALK_TPB)
         }
       }
     }
-    const uint64_t bo = __ballot(open);
     const unsigned no = CNT ? (unsigned)__popcll(bo) : (bo != 0ull ? 1u : 0u);
     if (CNT) {
       n_node += na - no;  // active lanes accept or open
@@ -1425,7 +1435,7 @@ __global__ void __launch_bounds__(WALK_TPB)
         leaf_active += na;
         n_pp += (unsigned long long)na * (unsigned long long)(e - s);
       }
-      if (CNT || wp.cost_kind) leaf_rounds += (uint32_t)(e - s + 3) >> 2;
+      if (CNT || PIECES || wp.cost_kind) leaf_rounds += (uint32_t)(e - s + 3) >> 2;
       if (act) {
         if (LCOST) cost += e - s;
         // only a target's own leaf needs the self-pair mask (an int compare
@@ -1437,7 +1447,7 @@ __global__ void __launch_bounds__(WALK_TPB)
           leaf_sum<WANT, SOFT, RAW, true>(wp, s, e, self32, tx, ty, tz, th, ph, ax, ay, az);
       }
     }
-    p = act ? (open ? first : next) : p;
+    p = pn;
     // (nleaf is set only for a real node: nw >= 0)
     w = nw | (nleaf ? 0x40000000 : 0);
   }
@@ -1448,11 +1458,23 @@ __global__ void __launch_bounds__(WALK_TPB)
     wp.trace[3 * wv + 1] = (unsigned long long)wall_clock64();
     wp.trace[3 * wv + 2] = (unsigned long long)steps;
   }
+  // (before the pieces' early exits: every piece's counts are added)
+  if (CNT && wp.counters) {
+    if (lane0) {
+      atomicAdd(&wp.counters[0], (unsigned long long)n_node);
+      atomicAdd(&wp.counters[1], n_pp);
+      atomicAdd(&wp.counters[3], (unsigned long long)steps);
+      atomicAdd(&wp.counters[4], (unsigned long long)n_active);
+      atomicAdd(&wp.counters[5], (unsigned long long)leaf_steps);
+      atomicAdd(&wp.counters[6], (unsigned long long)leaf_active);
+      atomicAdd(&wp.counters[7], (unsigned long long)open_steps);
+    }
+  }
   int32_t wcost = (int32_t)(steps + leaf_rounds);
   if (PIECES) {
-    if (wp.ck && lane0) {  // the group's steps in this walk (split: summed over its pieces)
-      if (pslot < 0) wp.ck[gidx * (CK_N + 1)] = (int32_t)steps;
-      else atomicAdd(&wp.ck[gidx * (CK_N + 1)], (int32_t)steps);
+    if (wp.ck && lane0) {  // the group's cost in this walk (split: summed over its pieces)
+      if (pslot < 0) wp.ck[gidx * (CK_N + 1)] = wcost;
+      else atomicAdd(&wp.ck[gidx * (CK_N + 1)], wcost);
     }
     if (pslot >= 0) {  // a piece of a split group: partial sums, the last piece adds them
       double *pb = wp.pbuf + ((int64_t)pslot * 64 + (threadIdx.x & 63)) * 4;
@@ -1488,17 +1510,6 @@ __global__ void __launch_bounds__(WALK_TPB)
     wp.acc[3 * o] = ax;
     wp.acc[3 * o + 1] = ay;
     wp.acc[3 * o + 2] = az;
-  }
-  if (CNT && wp.counters) {
-    if (lane0) {
-      atomicAdd(&wp.counters[0], (unsigned long long)n_node);
-      atomicAdd(&wp.counters[1], n_pp);
-      atomicAdd(&wp.counters[3], (unsigned long long)steps);
-      atomicAdd(&wp.counters[4], (unsigned long long)n_active);
-      atomicAdd(&wp.counters[5], (unsigned long long)leaf_steps);
-      atomicAdd(&wp.counters[6], (unsigned long long)leaf_active);
-      atomicAdd(&wp.counters[7], (unsigned long long)open_steps);
-    }
   }
 }
 
@@ -1585,15 +1596,15 @@ __global__ void __launch_bounds__(1024)
 
 // Piece table of a self-mode walk of targets [first, first + m) (leaf order),
 // one block of 1024 threads.  Group g = targets 64g .. 64g + 63 of the walk,
-// global group gg = gfirst + g; S = ck[gg][0], its steps in the previous walk
-// (0: none recorded).  With permille > 0 a group whose S exceeds
+// global group gg = gfirst + g; S = ck[gg][0], its cost (node steps + leaf
+// rounds) in the previous walk (0: none recorded).  With permille > 0 a group whose S exceeds
 // T = permille / 1000 of the largest is cut into K = min(kmax, ceil(S / T))
-// pieces at its previous walk's checkpoints nearest to the steps k S / K
+// pieces at its previous walk's checkpoints nearest to the cost k S / K
 // (strictly increasing node ids inside the tree; a split that would not be
 // is dropped), at most `cap` extra waves in all (groups in order).  The
 // entries are listed longest piece first (32 buckets of S / K), so the
 // longest chains start first; a split group's counter slots are handed out
-// here and its step count is zeroed (its pieces add theirs).  kbuf: one
+// here and its cost is zeroed (its pieces add theirs).  kbuf: one
 // byte per group (its piece count), scratch.
 constexpr int PT_NB = 32;
 __device__ __forceinline__ int pt_split(const int32_t *__restrict__ ckg, int32_t S, int K, int k,

@@ -235,6 +235,14 @@ class DeviceBins:
         nat.call("pbx_profile_path_stats", self._h, _i64(out))
         return {"mono": int(out[0]), "mono_discarded": int(out[1]), "multi": int(out[2])}
 
+    def mono_stats(self) -> dict:
+        """One-launch radial_equaln calls on this handle, and of them those
+        whose level-0 digits were counted with the previous one-launch call's
+        geometry (one grid barrier less; pbx_profile_mono_stats)."""
+        out = np.zeros(2, dtype=np.int64)
+        nat.call("pbx_profile_mono_stats", self._h, _i64(out))
+        return {"mono": int(out[0]), "hinted": int(out[1])}
+
     def level0_stats(self) -> dict:
         """Tiled multi-kernel radial_equaln calls on this handle, and of them
         those whose level-0 digit histogram the selection kernel counted with

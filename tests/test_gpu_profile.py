@@ -730,6 +730,72 @@ def test_radial_equaln_tiled_level0_hint_transitions(gpu):
         h.close()
 
 
+@pytest.mark.parametrize("n", [400_000, 1_000_000])
+def test_radial_equaln_one_launch_level0_hint_transitions(gpu, n):
+    """The one-launch path (radial_mono, <= 256 selection tiles) counts the
+    level-0 digits with the previous one-launch call's geometry while x is in
+    registers and, when every window key of the call fell inside it, skips
+    its second count and one grid barrier (pbx_profile_mono_stats counts
+    those calls); a key outside it (a wider or shifted radius range, a NaN, a
+    clipped window) falls back — either way edges, counts and CSR equal the
+    oracle's and the sums agree to 1e-12."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(35)
+    base = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    nanpos = base.copy()
+    nanpos[::997] = np.nan
+    calls = [(base, None, None, False),
+             (base, None, None, True),
+             (base * 0.999, None, None, True),
+             (base * 1e6, None, None, False),
+             (base * 1e6, None, None, True),
+             (base * 1e-6, None, None, False),
+             (nanpos * 1e-6, None, None, False),
+             (nanpos * 1e-6, None, None, True),
+             (base, 1.0, 4.0, None),
+             (base, 1.0, 4.0, True),
+             (base, 2.0, None, None),
+             (base, 1e9, 2e9, None)]  # an empty window: the ValueError of bins.py
+    h = DeviceBins()
+    try:
+        hinted = 0
+        for k, (pos, lo, hi, want_hint) in enumerate(calls):
+            if lo == 1e9:
+                with pytest.raises((ValueError, IndexError)):
+                    DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h,
+                                             bin_min=lo, bin_max=hi)
+                continue
+            _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h,
+                                                  bin_min=lo, bin_max=hi)
+            st = h.mono_stats()
+            assert h.path_stats()["mono"] == k + 1 and h.path_stats()["mono_discarded"] == 0
+            got_hint = st["hinted"] - hinted
+            hinted = st["hinted"]
+            if want_hint is not None:
+                assert got_hint == int(want_hint), (k, st)
+            ref = _oracle_radial(pos, mass, None, None, 128, lo, hi)
+            assert np.array_equal(e, ref["edges"], equal_nan=True), k
+            assert np.array_equal(c, ref["counts"]), k
+            pp, o = h.csr()
+            assert np.array_equal(o, ref["offsets"]) and np.array_equal(pp, ref["perm"]), k
+            ne = c > 0
+            for (f, w, cols), got in zip(stats, m):
+                for col in range(7):
+                    if (cols >> col) & 1 and not (w == -1 and col in (0, 1, 2, 5)):
+                        want = _oracle_col(ref, f, w, col)
+                        np.testing.assert_allclose(got[ne, col], want[ne], rtol=1e-12,
+                                                   atol=1e-12 * np.nanmax(np.abs(want[ne])))
+        # after the failed (empty-window) call the next one is still exact
+        _, e, c, _ = DeviceBins.radial_equaln(base, mass, nbins=128, stats=stats, into=h)
+        ref = _oracle_radial(base, mass, None, None, 128, None, None)
+        assert np.array_equal(e, ref["edges"]) and np.array_equal(c, ref["counts"])
+    finally:
+        h.close()
+
+
 def test_radial_equaln_level0_hint_many_tiles_per_block(gpu):
     """A span above 765 select blocks x 15 tiles x 4096 (~47M particles):
     each select_tiles block flushes its u16 level-0 counts to a new row every
