@@ -426,6 +426,14 @@ int pbx_profile_mono_stats(void *handle, int64_t *out);
  * was counted by the selection kernel with the previous tiled call's digit
  * geometry (every window key inside it), so x was not read a second time}. */
 int pbx_profile_level0_stats(void *handle, int64_t *out);
+/* Telemetry of the speculative assignment of the tiled calls (no reference
+ * counterpart): out[2] = {calls whose selection kernel also binned every key
+ * with the bin table stored by an earlier call (launched when the previous
+ * tiled call's level-0 digits of every rank matched that table), of those the
+ * calls whose own digits matched it too, so the assignment pass (a second
+ * read of x and the masses) was skipped}.  A miss re-runs the assignment;
+ * results are identical either way.  PBX_SPEC=0 disables the speculation. */
+int pbx_profile_spec_stats(void *handle, int64_t *out);
 /* enabled = 0: this handle's tiled calls never use the previous call's
  * level-0 digit geometry (every call re-reads x for its level-0 histogram:
  * the cost of a first call / a new snapshot); 1 (default): use it when it

@@ -77,28 +77,29 @@ static void *host_stage(Comm *c, size_t bytes) {
   return c->hstage;
 }
 
-// Call the host transport.  `locked`: the caller holds d.mu (a library
-// pipeline issuing a collective between its kernels); it is released while
-// the transport waits for the other ranks, which may be threads of this
-// process driving the same device.
-static void host_call(Comm *c, Device &d, bool locked, int kind, void *h, int64_t count, int dtype,
-                      int op, const int64_t *counts, const int64_t *displs) {
-  if (locked) d.mu.unlock();
+// Call the host transport.  `lk`: the caller's hold on the device lock d.mu
+// (a library pipeline issuing a collective between its kernels), or null;
+// it is released while the transport waits for the other ranks, which may be
+// threads of this process driving the same device (pbx_common.h states what
+// such a pipeline may not keep across the wait).
+static void host_call(Comm *c, std::unique_lock<std::mutex> *lk, int kind, void *h, int64_t count,
+                      int dtype, int op, const int64_t *counts, const int64_t *displs) {
+  if (lk) lk->unlock();
   const int r = c->host(c->host_ctx, kind, h, count, dtype, op, counts, displs);
-  if (locked) d.mu.lock();
+  if (lk) lk->lock();
   if (r != 0) fail(PBX_ERR_RUNTIME, "host collective (kind %d, rank %d of %d) failed: %d", kind,
                    c->rank, c->nranks, r);
 }
 
 // Device all-reduce through the host transport: D2H, transport, H2D, each
 // step drained (the staging is reused by the next collective).
-static void host_allreduce_dev(Comm *c, Device &d, bool locked, const void *send, void *recv,
-                               int64_t count, int dtype, int op) {
+static void host_allreduce_dev(Comm *c, Device &d, std::unique_lock<std::mutex> *lk,
+                               const void *send, void *recv, int64_t count, int dtype, int op) {
   const size_t bytes = dtype_size(dtype) * (size_t)count;
   void *h = host_stage(c, bytes);
   PBX_HIP(hipMemcpyAsync(h, send, bytes, hipMemcpyDeviceToHost, d.stream));
   PBX_HIP(hipStreamSynchronize(d.stream));
-  host_call(c, d, locked, PBX_COLL_ALLREDUCE, h, count, dtype, op, nullptr, nullptr);
+  host_call(c, lk, PBX_COLL_ALLREDUCE, h, count, dtype, op, nullptr, nullptr);
   PBX_HIP(hipMemcpyAsync(recv, h, bytes, hipMemcpyHostToDevice, d.stream));
   PBX_HIP(hipStreamSynchronize(d.stream));
 }
@@ -109,14 +110,16 @@ CommRanks comm_ranks(void *comm) {
   return CommRanks{c->nranks, c->rank};
 }
 
-// (called by library pipelines that hold the device lock)
+// (called by library pipelines that hold the device lock: `lk`)
 void comm_allreduce(void *comm, const void *send, void *recv, int64_t count, int dtype, int op,
-                    hipStream_t st) {
+                    hipStream_t st, std::unique_lock<std::mutex> &lk) {
   Comm *c = as_comm(comm);
   check_codes(dtype, op);
   if (count <= 0) return;
   if (c->host) {
-    host_allreduce_dev(c, comm_device(c), true, send, recv, count, dtype, op);
+    if (!lk.owns_lock() || lk.mutex() != &comm_device(c).mu)
+      fail(PBX_ERR_RUNTIME, "comm_allreduce: the caller does not hold the device lock");
+    host_allreduce_dev(c, comm_device(c), &lk, send, recv, count, dtype, op);
     return;
   }
   PBX_NCCL(ncclAllReduce(send, recv, (size_t)count, kTypes[dtype], kOps[op], c->nccl, st));
@@ -209,7 +212,7 @@ int pbx_comm_allgatherv(void *comm, void *d_buf, const int64_t *counts, const in
       char *h = (char *)host_stage(c, (size_t)(hi - lo));
       PBX_HIP(hipMemcpyAsync(h, base + lo, (size_t)(hi - lo), hipMemcpyDeviceToHost, d.stream));
       PBX_HIP(hipStreamSynchronize(d.stream));
-      host_call(c, d, false, PBX_COLL_ALLGATHERV, h, c->nranks, 0, 0, counts, dl.data());
+      host_call(c, nullptr, PBX_COLL_ALLGATHERV, h, c->nranks, 0, 0, counts, dl.data());
       PBX_HIP(hipMemcpyAsync(base + lo, h, (size_t)(hi - lo), hipMemcpyHostToDevice, d.stream));
       PBX_HIP(hipStreamSynchronize(d.stream));
       return;
@@ -234,7 +237,7 @@ static void allreduce_dev(void *comm, const void *d_send, void *d_recv, int64_t 
   if (count < 0) fail(PBX_ERR_VALUE, "negative count");
   Device &d = comm_device(c);
   if (c->host) {
-    if (count) host_allreduce_dev(c, d, false, d_send, d_recv, count, dtype, op);
+    if (count) host_allreduce_dev(c, d, nullptr, d_send, d_recv, count, dtype, op);
     return;
   }
   PBX_NCCL(ncclAllReduce(d_send, d_recv, (size_t)count, kTypes[dtype], kOps[op], c->nccl, d.stream));
@@ -264,7 +267,7 @@ static void allreduce_host(Comm *c, void *h_buf, int64_t count, int dtype, int o
   const size_t bytes = dtype_size(dtype) * (size_t)count;
   if (bytes == 0) return;
   if (c->host) {
-    host_call(c, d, false, PBX_COLL_ALLREDUCE, h_buf, count, dtype, op, nullptr, nullptr);
+    host_call(c, nullptr, PBX_COLL_ALLREDUCE, h_buf, count, dtype, op, nullptr, nullptr);
     return;
   }
   host_stage(c, bytes);

@@ -131,9 +131,18 @@ struct ScopedTimer {
 struct CommRanks {
   int nranks, rank;
 };
+// `lk` is the caller's hold on the device's lock: with a host-transport
+// communicator (pbx_comm_init_host) comm_allreduce releases it while the
+// transport waits for the other ranks — they may be threads of this process
+// driving the same device — and takes it back before returning.  So another
+// library call can run on this device and stream in that window: a pipeline
+// that issues comm_allreduce must keep its state in its own (per-handle)
+// buffers, never in workspace another call may use (Device::slot()), across
+// the collective.  (radial_equaln, the one such pipeline, keeps all of it in
+// its Profile.)
 CommRanks comm_ranks(void *comm);
 void comm_allreduce(void *comm, const void *send, void *recv, int64_t count, int dtype, int op,
-                    hipStream_t st);
+                    hipStream_t st, std::unique_lock<std::mutex> &lk);
 
 // Direct-sum precision mode (pbx_set_precise): true -> Newton-refined
 // 1/sqrt everywhere (~1e-16); false (default, or PBX_PRECISE=0) -> the

@@ -515,43 +515,86 @@ __global__ void __launch_bounds__(TPB)
   if (s) atomicAdd(&H[d], s);
 }
 
-// the same over select_tiles' rows (two u16 counts per word) when the call
-// kept the hinted geometry (ctl->hint), else over fused_hist0's u32 rows.
-// Thread = one word (two digits); blockIdx.y takes every gridDim.y-th row.
-// Block (0, 0) also zeroes `zero` (the selection's tail words, whose last
-// reader was fused_hist0) for the next tiled call.
-__global__ void __launch_bounds__(TPB)
+// H from the level-0 rows: select_tiles' u16 rows (two counts per word)
+// when the call kept the hinted geometry (ctl->hint), else fused_hist0's
+// u32 rows.  Block = 64 digits (32 words) of H, which it stores whole (no
+// atomics, no zeroed H needed).  u16 rows: thread t loads 16 bytes (4 words,
+// 8 digits) of rows t / 8, t / 8 + 128, ..., four rows in flight; u32 rows:
+// one digit of rows t / 64, t / 64 + 16, ...; the row groups' partial sums
+// are added through LDS.  (The u16 sums as 4-byte words, one row in flight
+// per thread, inside fused_hist0: 16 us at 64M, load latency bound; as
+// atomics from 1024 blocks of 256 threads: 7 us.)  Block 0 also zeroes
+// `zero` (the selection's tail words, whose last reader was fused_hist0)
+// for the next tiled call.
+constexpr int R0_DIG = 64;  // digits per msel_reduce0h block
+__global__ void __launch_bounds__(MS0_TPB)
     msel_reduce0h(const uint32_t *__restrict__ rows, int nrows, const uint32_t *__restrict__ rows16,
                   int nrows16, const int32_t *__restrict__ hint, uint32_t *__restrict__ H,
-                  uint64_t *__restrict__ zero, int nzero, int rows16_done) {
-  if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < nzero) zero[threadIdx.x] = 0ull;
+                  uint64_t *__restrict__ zero, int nzero) {
+  if (blockIdx.x == 0 && (int)threadIdx.x < nzero) zero[threadIdx.x] = 0ull;
   __shared__ int32_t shint;  // one load per block (not one per wave)
+  __shared__ uint32_t part[MS0_TPB * 8];
   if (threadIdx.x == 0) shint = *hint;
   __syncthreads();
-  if (shint && rows16_done) return;  // fused_hist0 summed the u16 rows already
-  const int q = blockIdx.x * TPB + threadIdx.x;  // word q: digits 2q, 2q + 1
-  uint32_t a = 0, b = 0;
-  if (shint) {
-    constexpr int U = 8;  // rows in flight per thread
-    for (int r0 = blockIdx.y * U; r0 < nrows16; r0 += gridDim.y * U) {
-      uint32_t v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        v[u] = r0 + u < nrows16 ? rows16[(int64_t)(r0 + u) * (MS0_DIG / 2) + q] : 0u;
+  const int d0 = blockIdx.x * R0_DIG;
+  if (shint && rows16) {
+    constexpr int RG = MS0_TPB / 8, U = 4, NW = MS0_DIG / 2;
+    const int c = threadIdx.x & 7, rg = threadIdx.x >> 3;
+    uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t *base = rows16 + d0 / 2 + 4 * c;
+    for (int r0 = rg; r0 < nrows16; r0 += RG * U) {
+      uint4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        a += v[u] & 0xffffu;
-        b += v[u] >> 16;
+        const int r = r0 + u * RG;
+        v[u] = r < nrows16 ? *(const uint4 *)(base + (int64_t)r * NW) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s[0] += v[u].x & 0xffffu;
+        s[1] += v[u].x >> 16;
+        s[2] += v[u].y & 0xffffu;
+        s[3] += v[u].y >> 16;
+        s[4] += v[u].z & 0xffffu;
+        s[5] += v[u].z >> 16;
+        s[6] += v[u].w & 0xffffu;
+        s[7] += v[u].w >> 16;
       }
     }
-  } else {
-    for (int r = blockIdx.y; r < nrows; r += gridDim.y) {
-      a += rows[(int64_t)r * MS0_DIG + 2 * q];
-      b += rows[(int64_t)r * MS0_DIG + 2 * q + 1];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[rg * R0_DIG + 8 * c + j] = s[j];
+    __syncthreads();
+    {  // digit t % 64, row groups 8 (t / 64) .. + 7
+      const int k = threadIdx.x & 63, p = threadIdx.x >> 6;
+      uint32_t a = 0;
+#pragma unroll
+      for (int j = 0; j < RG / 16; ++j) a += part[(p * (RG / 16) + j) * R0_DIG + k];
+      __syncthreads();
+      part[threadIdx.x] = a;
     }
+  } else {
+    constexpr int RG = MS0_TPB / R0_DIG, U = 8;
+    const int k = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    uint32_t a = 0;
+    for (int r0 = rg; r0 < nrows; r0 += RG * U) {
+      uint32_t v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = r0 + u * RG;
+        v[u] = r < nrows ? rows[(int64_t)r * MS0_DIG + d0 + k] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) a += v[u];
+    }
+    part[threadIdx.x] = a;
   }
-  if (a) atomicAdd(&H[2 * q], a);
-  if (b) atomicAdd(&H[2 * q + 1], b);
+  __syncthreads();
+  if (threadIdx.x < R0_DIG) {  // 16 partials per digit
+    uint32_t a = 0;
+#pragma unroll
+    for (int p = 0; p < MS0_TPB / 64; ++p) a += part[p * 64 + threadIdx.x];
+    H[d0 + threadIdx.x] = a;
+  }
 }
 
 // levels >= 1: keys whose prefix is an active group add to that group's
@@ -800,8 +843,10 @@ struct FusedCtl {
   uint64_t kmin, kmax;
   int32_t hint;    // 1: the level-0 geometry (lo, s0, w0) is the previous call's, its
                    // histogram was built by select_tiles (no re-read of x)
-  int32_t pad_;
+  int32_t spec;    // SPEC_MATCH: this call's level-0 ranks equal the stored bin table's;
+                   // SPEC_HIT: select_tiles binned with that table (no assignment pass)
 };
+constexpr int32_t SPEC_MATCH = 1, SPEC_HIT = 2;
 
 // Level-0 digit geometry of a handle's previous tiled call (select_tiles
 // counts this call's keys with it while they are still in registers; the
@@ -812,6 +857,98 @@ struct SelHint {
   int32_t s, w;
   int32_t valid, pad;
 };
+constexpr int AS_MAXM = 8;
+struct FusedStats {
+  int nm;
+  int f[AS_MAXM];
+  int w[AS_MAXM];
+  int col[AS_MAXM];
+  int op[AS_MAXM];  // MO_* when the slot's monomial has a dedicated form, else MO_GEN
+};
+struct AgRec {  // a deferred key: key - window base, weight, particle slot, tile | group << 24
+  uint64_t off;
+  double w;
+  uint32_t pos, tg;
+};
+constexpr uint32_t AG_TBITS = 24;  // tiles < 2^24 (profiles hold < 2^31 particles); groups < 256
+
+// the common monomials in their own (uniform-branch) loops: the generic
+// form selects a(f), f, ww per element (~14 VALU), these are 0-2 VALU.
+// Each is the value monomial() computes for that slot, bit for bit (the
+// products are the same products; x*1.0 is exact)
+enum : int { MO_GEN = 0, MO_W = 1, MO_X = 2, MO_XW = 3, MO_XXW = 4, MO_XX = 5, MO_WW = 6 };
+
+// monomial value of column `col` (the expression moments_kernel sums):
+// a(f) in {1, f, f*f, |f|} times b in {1, ww}; x*1.0 is exact, so this is
+// bit-identical to the per-column expressions
+__device__ __forceinline__ double monomial(int col, double f, double ww) {
+  const int am = (col == 0) ? 0 : (col == 1 || col == 3) ? 1 : (col == 2 || col == 4) ? 2 : 3;
+  const bool wb = (col == 0 || col == 1 || col == 2 || col == 5);
+  const double a = am == 0 ? 1.0 : am == 1 ? f : am == 2 ? f * f : __builtin_fabs(f);
+  return wb ? a * ww : a;
+}
+
+// aq[bk[k]] += monomial of slot (op, col, fq, wq) for the K elements whose bin
+// is < nb (LDS atomics)
+template <int K>
+__device__ __forceinline__ void mom_add(double *aq, int op, int col, int fq, int wq,
+                                        const uint32_t *bk, const double *xv, const double *wv,
+                                        uint32_t nb) {
+#define PBX_MOM_LOOP(EXPR)                                     \
+  _Pragma("unroll") for (int k = 0; k < K; ++k) if (bk[k] < nb) \
+      atomicAdd(&aq[bk[k]], (EXPR));                           \
+  return;
+  switch (op) {
+    case MO_W: PBX_MOM_LOOP(wv[k])
+    case MO_X: PBX_MOM_LOOP(xv[k])
+    case MO_XW: PBX_MOM_LOOP(xv[k] * wv[k])
+    case MO_XXW: PBX_MOM_LOOP((xv[k] * xv[k]) * wv[k])
+    case MO_XX: PBX_MOM_LOOP(xv[k] * xv[k])
+    case MO_WW: PBX_MOM_LOOP(wv[k] * wv[k])
+    default:
+      PBX_MOM_LOOP(monomial(col, fq == 0 ? xv[k] : wv[k], wq == 0 ? xv[k] : wv[k]))
+  }
+#undef PBX_MOM_LOOP
+}
+
+// Speculative assignment (tiled one-rank calls).  The bin of a key whose
+// level-0 digit holds no edge depends only on the digit: bin = #{ranks q
+// with digit_q < digit} - 1 (assign_gather's table).  So when this call's
+// level-0 digit of every rank q equals the previous full call's (same
+// geometry, same nq), that call's digit -> bin table bins this call's keys
+// exactly, and select_tiles can bin every key while x is still in registers
+// (byte bins, per-bin sums, and the keys of edge-holding digits into a
+// deferred list) — the assignment pass that re-reads x and the masses is
+// skipped.  fused_resolve compares the digits (SPEC_MATCH) once the level-0
+// histogram is known; on a mismatch assign_gather runs as before and stores
+// the new table.  The table: written by assign_gather's block 0 (which has
+// no tiles of its own), read by the next call's select_tiles and
+// fused_resolve (before that call's assign_gather may rewrite it).
+struct SpecTab {
+  uint64_t lo;             // level-0 geometry the digits are taken in
+  int32_t s0, w0;
+  int32_t nb, nq, ng, valid;
+  uint32_t qd[MS_MAXQ];    // level-0 digit of each rank q
+  uint8_t bin[MS0_DIG];    // digit -> bin (nb: outside the edges); SPEC_DEFER: the digit holds edges
+};
+constexpr uint8_t SPEC_DEFER = 0xff;
+constexpr int SPEC_MAXB = 254;   // bins (and groups <= nq = nb + 1 < 256) a byte table holds
+constexpr int SPEC_MACC = 256;   // per-bin sums (nm * nb doubles) select_tiles keeps in LDS
+constexpr int SPEC_LIST = 4;     // deferred-list capacity: 1 / SPEC_LIST of a block's slots
+struct SpecArgs {
+  const SpecTab *tab;      // null: no speculation (select_tiles<FAM, false>)
+  const double *mass;      // f64 masses by particle (null: unit weights)
+  uint8_t *bins;           // byte bins by particle slot (assign_gather's bins8)
+  uint32_t *th;            // [bin][tile] counts of the CSR pass (deferred keys: fix_deferred adds)
+  double *slab;            // per select block: nm * nb sums
+  AgRec *rec;              // deferred lists: select block j's at rbase[j]
+  uint32_t *rbase, *rn;    // per select block: list start, length
+  uint32_t *flag;          // set when a block could not bin (table / hint geometry differ,
+                           // a list overflowed): the call takes the assignment pass
+  FusedStats fs;
+  int nb;
+};
+
 // select_tiles blocks per assign_gather block (tile sub-ranges): 3 x 255
 // blocks of 8 waves at <= 80 VGPRs (6 waves per SIMD) are all resident at once
 #ifndef PBX_SH_K
@@ -840,8 +977,6 @@ struct FusedSetup {
   const uint32_t *hflag; // select_tiles: a window key fell outside the hint (or null)
   SelHint *hint_out;     // fused_hist0 block 0: this call's own geometry, for the next call
   const uint32_t *btot;  // tiled: select_tiles' block totals (SH_K (gridDim - 1) blocks)
-  const uint32_t *rows16;  // tiled, hinted: select_tiles' u16 digit rows (two per word)
-  int nrows16;             // their number (SH_K (gridDim - 1) rsub)
 };
 
 // Element range of fused_hist0 / fused_gather: the kept x [0, n), or with
@@ -933,21 +1068,20 @@ constexpr uint32_t SH_RSUB_MAX = 8;  // u16 count rows per block (flushed every 
 // FAM: several family slices (membership tested per particle); else every
 // particle of the span [base, n) is a member (no family, or one slice: the
 // span is that slice) and the 16 slice bounds stay out of the registers.
-template <bool FAM>
-__global__ void __launch_bounds__(SH_BT)
+// SPEC: the speculative assignment (SpecArgs above) — with a stored table
+// whose geometry is the hint's, every kept key is also binned here: byte bin
+// by slot, per-bin sums in LDS (one slab row per block), the keys of
+// edge-holding digits into the block's deferred list.
+template <bool FAM, bool SPEC>
+__global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
     select_tiles(const double *__restrict__ pos, int64_t n, SelectParams p, uint32_t nt,
                  uint32_t G0, double *__restrict__ xo, uint64_t *__restrict__ kw,
                  uint16_t *__restrict__ kpre, uint32_t *__restrict__ wcnt,
                  uint32_t *__restrict__ toff, uint32_t *__restrict__ btot,
                  unsigned long long *__restrict__ minmax, const SelHint *__restrict__ hint,
                  uint64_t ka, uint64_t kb, uint32_t *__restrict__ rows16, uint32_t rsub,
-                 uint32_t *__restrict__ hflag, uint32_t *__restrict__ H) {
+                 uint32_t *__restrict__ hflag, SpecArgs sa) {
   constexpr int SI = TILE / SH_BT;
-  {  // the level-0 histogram H of this call, zeroed slice by slice (fused_hist0 /
-     // msel_reduce0h fill it after this launch)
-    const uint32_t per = (MS0_DIG + gridDim.x - 1) / gridDim.x, h0 = blockIdx.x * per;
-    for (uint32_t i = h0 + threadIdx.x; i < min<uint32_t>(h0 + per, MS0_DIG); i += SH_BT) H[i] = 0u;
-  }
   __shared__ uint32_t lh[MS0_DIG / 2];
   __shared__ uint32_t tcnt[SH_MAXT][SH_NW];
   __shared__ unsigned long long wmin[SH_NW], wmax[SH_NW];
@@ -962,10 +1096,22 @@ __global__ void __launch_bounds__(SH_BT)
   // the hint: one load per block, through LDS (not one per wave from all
   // the grid's waves at once: the same-line hot spot fused_hist0 had)
   __shared__ SelHint shh;
+  __shared__ uint8_t sdt[SPEC ? MS0_DIG : 1];      // the table's digit -> bin
+  __shared__ double sacc[SPEC ? SPEC_MACC : 1];    // per-bin sums
+  // per-(tile, bin) counts of the current SH_TMAX tiles (flushed with the u16 rows)
+  __shared__ uint32_t tcs[SPEC ? SH_TMAX * ((SPEC_MAXB + 1) | 1) : 1];
+  __shared__ uint32_t sdk;                         // deferred keys listed
+  __shared__ int s_spec;
   if (threadIdx.x == 0) {
     SelHint t{};
     if (hint) t = *hint;
     shh = t;
+    if (SPEC) {
+      const SpecTab *tb = sa.tab;
+      s_spec = tb->valid && t.valid && tb->lo == t.lo && tb->s0 == t.s && tb->w0 == t.w &&
+               tb->nb == sa.nb;
+      sdk = 0;
+    }
   }
   __syncthreads();
   const SelHint h = shh;
@@ -978,6 +1124,36 @@ __global__ void __launch_bounds__(SH_BT)
   const int hb = h.s + h.w;
   const uint64_t hspan = hb >= 64 ? ~0ull : ((1ull << hb) - 1);
   const uint64_t hhi = hlo + hspan < hlo ? ~0ull : hlo + hspan;
+  const bool spec = SPEC && hv && s_spec;
+  const int nb = SPEC ? sa.nb : 0;
+  const int macc = SPEC ? sa.fs.nm * nb : 0;
+  uint32_t mfl = 0;  // SPEC: per monomial q, factors x, x, w, w present (bits 4q ..)
+  if constexpr (SPEC) {
+#pragma unroll
+    for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+      if (q >= sa.fs.nm) break;
+      const int op = sa.fs.op[q];
+      const uint32_t f = ((op == MO_X || op == MO_XW || op == MO_XXW || op == MO_XX) ? 1u : 0u) |
+                         ((op == MO_XXW || op == MO_XX) ? 2u : 0u) |
+                         ((op == MO_W || op == MO_XW || op == MO_XXW || op == MO_WW) ? 4u : 0u) |
+                         ((op == MO_WW) ? 8u : 0u);
+      mfl |= f << (4 * q);
+    }
+  }
+  const int nrs = (nb + 1) | 1;
+  // the block's deferred list: 1 / SPEC_LIST of its slots (an overflow fails the speculation)
+  const uint64_t lbase = (uint64_t)ta * TILE / SPEC_LIST;
+  const uint32_t lcap = (uint32_t)((uint64_t)(tb - ta) * TILE / SPEC_LIST);
+  if (SPEC) {
+    if (spec) {
+      const uint4 *src = (const uint4 *)sa.tab->bin;
+      for (int i = threadIdx.x; i < MS0_DIG / 16; i += SH_BT) ((uint4 *)sdt)[i] = src[i];
+      for (int i = threadIdx.x; i < macc; i += SH_BT) sacc[i] = 0.0;
+      for (int i = threadIdx.x; i < SH_TMAX * nrs; i += SH_BT) tcs[i] = 0;
+    } else if (threadIdx.x == 0) {
+      atomicOr(sa.flag, 1u);
+    }
+  }
   if (hv) {
     for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) lh[i] = 0;
     __syncthreads();
@@ -993,6 +1169,7 @@ __global__ void __launch_bounds__(SH_BT)
   constexpr int SH_HALF = SI / 2;
   struct Half {
     double x[SH_HALF], y[SH_HALF], z[SH_HALF];
+    double m[SPEC ? SH_HALF : 1];  // SPEC: the masses (loaded with the positions)
     uint32_t in;
   };
   auto ld = [&](uint32_t tile, int h, Half &H) {
@@ -1007,12 +1184,15 @@ __global__ void __launch_bounds__(SH_BT)
       H.x[k] = q[0];
       H.y[k] = q[1];
       H.z[k] = q[2];
+      if constexpr (SPEC) H.m[k] = (spec && sa.mass) ? sa.mass[in ? i : 0] : 1.0;
     }
   };
   uint32_t run = 0;
   auto sel = [&](uint32_t tile, int h, const Half &H) {
     double *xt = xo + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW) + h * SH_HALF * 64;
     const int64_t wj = (int64_t)tile * (TILE / 64) + w * SI + h * SH_HALF;
+    const uint32_t slot0 = tile * (uint32_t)TILE + (uint32_t)w * (TILE / SH_NW) + h * SH_HALF * 64 + lane;
+    const double *mh = H.m;
 #pragma unroll
     for (int k = 0; k < SH_HALF; ++k) {
       double xv = 0.0;
@@ -1042,6 +1222,65 @@ __global__ void __launch_bounds__(SH_BT)
           }
         }
       }
+      if constexpr (SPEC) {
+        if (spec) {  // the table's bin (AgRec / bins8 conventions of assign_gather)
+        const int kq = k;
+        const uint64_t kk = dkey(xv);
+        uint32_t code = 0xffffu, dd = 0;
+        bool def = false;
+        if (keep) {
+          code = (uint32_t)nb;  // kept, outside the window: the dropped bin
+          if (kk >= ka && kk <= kb && kk >= hlo && kk <= hhi) {
+            dd = (uint32_t)((kk - hlo) >> hsh);
+            const uint32_t c8 = sdt[dd];
+            def = c8 == SPEC_DEFER;
+            code = def ? 0xffffu : c8;
+          }
+          if (!def) {
+            sa.bins[slot0 + 64u * k] = (uint8_t)code;
+            atomicAdd(&tcs[((tile - ta) % SH_TMAX) * nrs + code], 1u);
+          }
+        }
+        if (macc && code < (uint32_t)nb) {
+          // the dedicated monomials only (the host checks): (a1 a2)(b1 b2) with
+          // a = x or 1, b = w or 1 — the same products as mom_add's forms
+          // (x * 1.0 is exact); the factors of monomial q are bits 4q .. 4q + 3
+          // of mfl (one short loop, not mom_add's switch unrolled per key)
+#pragma unroll 1
+          for (int q = 0; q < sa.fs.nm; ++q) {
+            const uint32_t f = mfl >> (4 * q);
+            const double a = ((f & 1u) ? xv : 1.0) * ((f & 2u) ? xv : 1.0);
+            const double b = ((f & 4u) ? mh[kq] : 1.0) * ((f & 8u) ? mh[kq] : 1.0);
+            atomicAdd(&sacc[q * nb + code], a * b);
+          }
+        }
+        const uint64_t bd = __ballot(def);
+        if (bd) {  // rare: keys of edge-holding digits, into the block's list
+          uint32_t b0 = 0;
+          if (lane == 0) b0 = atomicAdd(&sdk, (uint32_t)__popcll(bd));
+          b0 = __shfl(b0, 0, 64);
+          if (def) {
+            const uint32_t idx = b0 + rank_below(bd);
+            // (the group: filled in by assign_gather from the digit — a
+            // global table lookup here stalled almost every wave step)
+            if (idx < lcap) sa.rec[lbase + idx] = AgRec{kk - hlo, mh[kq], slot0 + 64u * k, tile};
+          }
+        }
+        }
+      }
+    }
+  };
+  // SPEC: tiles [t0, t1) of the current SH_TMAX group are complete (after a
+  // block barrier): their [bin][tile] counts out, the LDS counts zeroed
+  auto flush_tc = [&](uint32_t t0, uint32_t t1) {
+    if constexpr (SPEC) {
+      const int ntl = (int)(t1 - t0), nr = nb + 1;
+      for (int k = threadIdx.x; k < ntl * nr; k += SH_BT) {
+        const int b = k / ntl, tl = k - b * ntl;
+        uint32_t &c = tcs[((t0 - ta + tl) % SH_TMAX) * nrs + b];
+        sa.th[(int64_t)b * nt + t0 + tl] = c;
+        c = 0;
+      }
     }
   };
   // end of a tile: the wave's count; every SH_TMAX tiles the u16 digit rows
@@ -1052,6 +1291,7 @@ __global__ void __launch_bounds__(SH_BT)
     }
     if (hv && (tile - ta) % SH_TMAX == SH_TMAX - 1 && tile + 1 < tb) {  // (block-uniform)
       __syncthreads();  // every wave's counts of this row's tiles are in
+      if (spec) flush_tc(tile + 1 - SH_TMAX, tile + 1);
       uint32_t *row = rows16 + ((int64_t)blockIdx.x * rsub + (tile - ta) / SH_TMAX) * (MS0_DIG / 2);
       for (int i = threadIdx.x; i < MS0_DIG / 2; i += SH_BT) {
         row[i] = lh[i];
@@ -1087,6 +1327,16 @@ __global__ void __launch_bounds__(SH_BT)
   const uint64_t anyoob = __ballot(oob);
   if (anyoob && lane == 0) atomicOr(hflag, 1u);
   __syncthreads();
+  if (SPEC && spec) {  // the block's sums row and list, its last tiles' counts
+    if (tb > ta) flush_tc(ta + ((tb - ta - 1) / SH_TMAX) * SH_TMAX, tb);
+    for (int i = threadIdx.x; i < macc; i += SH_BT) sa.slab[(int64_t)blockIdx.x * macc + i] = sacc[i];
+    if (threadIdx.x == 0) {
+      const uint32_t c = sdk;
+      sa.rbase[blockIdx.x] = (uint32_t)lbase;
+      sa.rn[blockIdx.x] = c < lcap ? c : lcap;
+      if (c > lcap) atomicOr(sa.flag, 1u);
+    }
+  }
   if (w == 0) {
     // block-local exclusive tile offsets (lane = tile, 64 at a time) and the block total
     uint32_t carry = 0;
@@ -1246,8 +1496,7 @@ static_assert(MS0_TPB == TS_TPB, "fused_hist0's block 0 runs the tile scan");
 // level-0 histogram rows (msel_hist0 with the base / shift / length from ctl)
 __global__ void __launch_bounds__(MS0_TPB)
     fused_hist0(const double *__restrict__ x, FusedSetup fsu, FusedCtl *__restrict__ ctl_out,
-                unsigned long long *__restrict__ counts, int nb, uint32_t *__restrict__ H,
-                uint32_t *__restrict__ rows) {
+                unsigned long long *__restrict__ counts, int nb, uint32_t *__restrict__ rows) {
   __shared__ uint32_t lh[MS0_DIG];
   // the control record derived once per block and broadcast through LDS
   // (in every wave, its ~20 scalar loads of the same few lines from all 4096
@@ -1272,6 +1521,11 @@ __global__ void __launch_bounds__(MS0_TPB)
       h.s = B - h.w;
       h.lo = lo2;
       h.valid = 1;
+      // this call kept the hinted geometry (every window key inside it): when
+      // the fresh one has the same digit width, keep it — the level-0 digits
+      // (and the stored bin table's, SpecTab) stay comparable from call to
+      // call of a slowly changing snapshot
+      if (ctl.hint && fsu.hint->s == h.s && fsu.hint->w == h.w) h = *fsu.hint;
     }
     *fsu.hint_out = h;
   }
@@ -1296,44 +1550,10 @@ __global__ void __launch_bounds__(MS0_TPB)
       *ctl_out = ctl;
     }
     for (int k = threadIdx.x; k <= nb; k += MS0_TPB) counts[k] = 0;  // for assign_bins
-    if (!fsu.tiled)  // (a tiled call's H was zeroed by select_tiles)
-      for (int k = threadIdx.x; k < MS0_DIG; k += MS0_TPB) H[k] = 0;   // for msel_reduce0
     for (int k = threadIdx.x; k < fsu.nzero; k += MS0_TPB) fsu.zero[k] = 0;
   }
   if (fsu.tiled) tile_offsets_fix(fsu.btot, fsu.nt, fsu.toff, red);  // (blocks >= 1)
-  if (ctl.hint && fsu.tiled && fsu.rows16) {
-    // select_tiles counted the keys: this block sums its slice of H's words
-    // over every u16 row (a block owns its words: plain stores, no atomics;
-    // msel_reduce0h then has nothing to add).  Thread t: word h0 + t % 32,
-    // rows t / 32, t / 32 + 32, ... (32 threads read one 128-byte piece)
-    __shared__ uint32_t pa[MS0_TPB], pb[MS0_TPB];
-    constexpr int WPB = 32;  // words per block step
-    const int nw = MS0_DIG / 2;
-    for (int h0 = blockIdx.x * WPB; h0 < nw; h0 += gridDim.x * WPB) {
-      const int q = h0 + (threadIdx.x & (WPB - 1));
-      uint32_t a = 0, b = 0;
-      if (q < nw)
-        for (int r = threadIdx.x / WPB; r < fsu.nrows16; r += MS0_TPB / WPB) {
-          const uint32_t v = fsu.rows16[(int64_t)r * nw + q];
-          a += v & 0xffffu;
-          b += v >> 16;
-        }
-      pa[threadIdx.x] = a;
-      pb[threadIdx.x] = b;
-      __syncthreads();
-      if (threadIdx.x < WPB && q < nw) {
-        for (int k = threadIdx.x + WPB; k < MS0_TPB; k += WPB) {
-          a += pa[k];
-          b += pb[k];
-        }
-        H[2 * q] = a;
-        H[2 * q + 1] = b;
-      }
-      __syncthreads();
-    }
-    return;
-  }
-  if (ctl.hint) return;  // select_tiles counted the keys (msel_reduce0 sums its rows)
+  if (ctl.hint) return;  // select_tiles counted the keys (msel_reduce0h sums its rows)
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
   __syncthreads();
   const uint64_t ka = fsu.ka, kb = fsu.kb;
@@ -1359,22 +1579,23 @@ __global__ void __launch_bounds__(MS0_TPB)
 // gq, ctl->ng / m / total), and block g then gives group g its per-block
 // offsets: block b of fused_hist0 / select_tiles counted rows[b][digit of g]
 // keys of group g, so its keys go to goff[g] + the exclusive sum over
-// earlier blocks.  H is left as it is (the next call's select_tiles or
-// fused_hist0 zeroes it).
+// earlier blocks.  H is left as it is (the next call's msel_reduce0h
+// overwrites every word).
 constexpr int FR_TPB = 1024;
 __global__ void __launch_bounds__(FR_TPB)
     fused_resolve(const uint32_t *__restrict__ H, FusedCtl *__restrict__ ctl, int64_t nbins, int nq,
                   MsRank *__restrict__ R, uint32_t *__restrict__ gdig, uint32_t *__restrict__ goff,
                   uint32_t *__restrict__ gq, const uint32_t *__restrict__ rows, int g0,
                   uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
-                  uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16, uint32_t rsub) {
+                  uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16, uint32_t rsub,
+                  const SpecTab *__restrict__ tab, uint32_t *__restrict__ sflag, int nb) {
   constexpr int PT = MS0_DIG / FR_TPB;
   __shared__ uint32_t incl[MS0_DIG];
   __shared__ uint32_t wsum[FR_TPB / 64];
   __shared__ uint32_t qdig[MS_MAXQ];
   __shared__ uint32_t gstart[MS_MAXQ + 1];
   __shared__ uint32_t gd[MS_MAXQ], go[MS_MAXQ + 1];
-  __shared__ int sng, s_err, s_w0, s_hint;
+  __shared__ int sng, s_err, s_w0, s_hint, s_spec;
   const int tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const int wv = tid >> 6;
@@ -1383,6 +1604,12 @@ __global__ void __launch_bounds__(FR_TPB)
     s_err = ctl->err;
     s_w0 = ctl->w0;
     s_hint = ctl->hint;
+    // the stored bin table (SpecTab) applies iff this call's geometry and
+    // every rank's level-0 digit are its own (compared below, block 0)
+    s_spec = 0;
+    if (pub && tab && tab->valid && !(s_err & 2) && tab->nb == nb && tab->nq == nq &&
+        tab->lo == ctl->lo && tab->s0 == ctl->s0 && tab->w0 == s_w0)
+      s_spec = 1;
   }
   for (int k = tid; k < MS0_DIG; k += FR_TPB) incl[k] = H[k];  // coalesced, via LDS
   __syncthreads();
@@ -1425,8 +1652,15 @@ __global__ void __launch_bounds__(FR_TPB)
       R[q].rr = r - (a ? (int64_t)incl[a - 1] : 0);
     }
     qdig[q] = (uint32_t)a;
+    if (pub && s_spec && tab->qd[q] != (uint32_t)a) s_spec = 0;  // (benign race: all write 0)
   }
   __syncthreads();
+  if (pub && tid == 0) {
+    const int m = s_spec ? SPEC_MATCH : 0;
+    // a hit: select_tiles binned every key with the table (no block gave up)
+    ctl->spec = m | ((m && sflag && *sflag == 0u) ? SPEC_HIT : 0);
+    if (sflag) *sflag = 0u;  // (for the next speculating call)
+  }
   // groups: run starts of the (non-decreasing) digits; one wave numbers them
   if (wv == 0) {
     uint32_t ng = 0;
@@ -1592,52 +1826,6 @@ __global__ void __launch_bounds__(MS0_TPB)
 // column col[q] of pbx_profile_moments_cols for field f[q] (0 = x, 1 =
 // weights) and weights w[q] (0 = x, 1 = weights, -1 = none); block sums in
 // LDS, one slab row (nm x nb) per block.
-constexpr int AS_MAXM = 8;
-struct FusedStats {
-  int nm;
-  int f[AS_MAXM];
-  int w[AS_MAXM];
-  int col[AS_MAXM];
-  int op[AS_MAXM];  // MO_* when the slot's monomial has a dedicated form, else MO_GEN
-};
-// the common monomials in their own (uniform-branch) loops: the generic
-// form selects a(f), f, ww per element (~14 VALU), these are 0-2 VALU.
-// Each is the value monomial() computes for that slot, bit for bit (the
-// products are the same products; x*1.0 is exact)
-enum : int { MO_GEN = 0, MO_W = 1, MO_X = 2, MO_XW = 3, MO_XXW = 4, MO_XX = 5, MO_WW = 6 };
-
-// monomial value of column `col` (the expression moments_kernel sums):
-// a(f) in {1, f, f*f, |f|} times b in {1, ww}; x*1.0 is exact, so this is
-// bit-identical to the per-column expressions
-__device__ __forceinline__ double monomial(int col, double f, double ww) {
-  const int am = (col == 0) ? 0 : (col == 1 || col == 3) ? 1 : (col == 2 || col == 4) ? 2 : 3;
-  const bool wb = (col == 0 || col == 1 || col == 2 || col == 5);
-  const double a = am == 0 ? 1.0 : am == 1 ? f : am == 2 ? f * f : __builtin_fabs(f);
-  return wb ? a * ww : a;
-}
-
-// aq[bk[k]] += monomial of slot (op, col, fq, wq) for the K elements whose bin
-// is < nb (LDS atomics)
-template <int K>
-__device__ __forceinline__ void mom_add(double *aq, int op, int col, int fq, int wq,
-                                        const uint32_t *bk, const double *xv, const double *wv,
-                                        uint32_t nb) {
-#define PBX_MOM_LOOP(EXPR)                                     \
-  _Pragma("unroll") for (int k = 0; k < K; ++k) if (bk[k] < nb) \
-      atomicAdd(&aq[bk[k]], (EXPR));                           \
-  return;
-  switch (op) {
-    case MO_W: PBX_MOM_LOOP(wv[k])
-    case MO_X: PBX_MOM_LOOP(xv[k])
-    case MO_XW: PBX_MOM_LOOP(xv[k] * wv[k])
-    case MO_XXW: PBX_MOM_LOOP((xv[k] * xv[k]) * wv[k])
-    case MO_XX: PBX_MOM_LOOP(xv[k] * xv[k])
-    case MO_WW: PBX_MOM_LOOP(wv[k] * wv[k])
-    default:
-      PBX_MOM_LOOP(monomial(col, fq == 0 ? xv[k] : wv[k], wq == 0 ? xv[k] : wv[k]))
-  }
-#undef PBX_MOM_LOOP
-}
 
 // One block (FR_TPB threads) per group: for each of its ranks, an MSD radix
 // select (FS_BITS-bit digits, LDS histogram, parallel scan) over the group's
@@ -2247,12 +2435,6 @@ constexpr int AG_TR = 64;
 #endif
 constexpr int AG_W = PBX_AG_W;                // keep words of a tile per wave
 constexpr int AG_TPS = AG_W * (MS0_TPB / 64) / 64;  // tiles per step (the block's waves)
-struct AgRec {  // a deferred key: key - window base, weight, particle slot, tile | group << 24
-  uint64_t off;
-  double w;
-  uint32_t pos, tg;
-};
-constexpr uint32_t AG_TBITS = 24;  // tiles < 2^24 (profiles hold < 2^31 particles); groups < 256
 struct GatherOut {
   uint64_t *seg;          // key - window base, by segment slot
   AgRec *rec;             // deferred keys, block by block
@@ -2273,6 +2455,17 @@ __device__ __forceinline__ uint32_t block_prefix(const uint32_t *__restrict__ v,
   return t;
 }
 
+// The speculative assignment's hand-over (select_tiles<FAM, true>): on a hit
+// (ctl->spec & SPEC_HIT) assign_gather only moves the select blocks' deferred
+// keys into their groups' segments and sums their slab rows; on a miss it
+// assigns as before and (block 0) stores the table for the next call.
+struct SpecIO {
+  SpecTab *tab;            // written by block 0 of a full assignment
+  AgRec *srec;             // select blocks' deferred lists (their groups filled in) ...
+  const uint32_t *srbase, *srn;
+  const double *sslab;     // ... and per-bin sums (SH_K rows per assign block)
+};
+
 template <bool MOM>
 __global__ void __launch_bounds__(MS0_TPB)
     assign_gather(const double *__restrict__ x, const uint64_t *__restrict__ kw, int64_t base,
@@ -2281,7 +2474,7 @@ __global__ void __launch_bounds__(MS0_TPB)
                   const MsRank *__restrict__ R, int nq,
                   const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ boff, int nb,
                   uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
-                  double *__restrict__ slab, GatherOut go) {
+                  double *__restrict__ slab, GatherOut go, SpecIO sio) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per level-0 digit: the bin of its keys (#{q : digit_q < d} - 1, or nb),
   // or 0x8000 | group when the digit holds edges — one LDS read per key
@@ -2298,14 +2491,48 @@ __global__ void __launch_bounds__(MS0_TPB)
   // the control record's fields: one load per block, broadcast through LDS
   // (not ~4 scalar loads of one line in each of the grid's 4096 waves)
   __shared__ uint64_t c_lo;
-  __shared__ int c_ng, c_s, c_win;
+  __shared__ int c_ng, c_s, c_win, c_w0, c_hit;
   if (tid == 0) {
     const bool w0 = !(ctl->err & 2);
     c_win = w0;
     c_ng = w0 ? ctl->ng : 0;
     c_lo = ctl->lo;
     c_s = ctl->s0;
+    c_w0 = ctl->w0;
+    c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
     dk = 0;
+  }
+  __syncthreads();
+  const int ng = c_ng;
+  for (int g = tid; g < ng; g += MS0_TPB) sslot[g] = boff[(int64_t)blockIdx.x * MS_MAXQ + g];
+  if (c_hit) {  // select_tiles binned the keys: its lists -> the group segments, its sums
+    // digit -> group of the edge-holding digits (the records carry key - lo)
+    for (int g = tid; g < ng; g += MS0_TPB) dtab[gdig[g]] = (uint16_t)g;
+    __syncthreads();
+    const int s = c_s;
+    if (blockIdx.x >= 1) {
+      for (uint32_t j = SH_K * (blockIdx.x - 1); j < SH_K * blockIdx.x; ++j) {
+        const uint32_t r0 = sio.srbase[j], cnt = sio.srn[j];
+        for (uint32_t i = tid; i < cnt; i += MS0_TPB) {
+          AgRec *rp = sio.srec + r0 + i;
+          const uint64_t off = rp->off;
+          const uint32_t g = dtab[(uint32_t)(off >> s)];
+          go.seg[atomicAdd(&sslot[g], 1u)] = off;
+          rp->tg |= g << AG_TBITS;  // (fix_deferred reads the group)
+        }
+      }
+    }
+    if (MOM) {
+      double *dst = slab + (int64_t)blockIdx.x * macc;
+      for (int k = tid; k < macc; k += MS0_TPB) {
+        double v = 0.0;
+        if (blockIdx.x >= 1)
+          for (uint32_t j = SH_K * (blockIdx.x - 1); j < SH_K * blockIdx.x; ++j)
+            v += sio.sslab[(int64_t)j * macc + k];
+        dst[k] = v;
+      }
+    }
+    return;
   }
   const uint32_t rb = block_prefix(go.bcnt, (int)blockIdx.x, red);
   for (int q = tid; q < nq; q += MS0_TPB) qd[q] = (uint32_t)R[q].prefix;
@@ -2313,10 +2540,8 @@ __global__ void __launch_bounds__(MS0_TPB)
   for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
   __syncthreads();
   const bool win = c_win;
-  const int ng = c_ng;
   const uint64_t lo = c_lo;
   const int s = c_s;
-  for (int g = tid; g < ng; g += MS0_TPB) sslot[g] = boff[(int64_t)blockIdx.x * MS_MAXQ + g];
   for (int d = tid; d < MS0_DIG; d += MS0_TPB) {  // #{q : digit_q < d}, lower bound
     int a = 0, len = nq;
     while (len > 0) {
@@ -2334,9 +2559,27 @@ __global__ void __launch_bounds__(MS0_TPB)
   __syncthreads();
   for (int g = tid; g < ng; g += MS0_TPB) dtab[gdig[g]] = (uint16_t)(0x8000u | (uint32_t)g);
   __syncthreads();
+  if (blockIdx.x == 0 && sio.tab) {  // (block 0 has no tiles) the table for the next call
+    SpecTab *T = sio.tab;
+    const bool ok = win && nb <= SPEC_MAXB && ng < 256;
+    for (int d = tid; d < MS0_DIG; d += MS0_TPB) {
+      const uint32_t e = dtab[d];
+      T->bin[d] = (e & 0x8000u) ? SPEC_DEFER : (uint8_t)e;
+    }
+    for (int q = tid; q < nq; q += MS0_TPB) T->qd[q] = qd[q];
+    if (tid == 0) {
+      T->lo = lo;
+      T->s0 = s;
+      T->w0 = c_w0;
+      T->nb = nb;
+      T->nq = nq;
+      T->ng = ng;
+      T->valid = ok ? 1 : 0;
+    }
+  }
   uint32_t ta, tb;
   tile_range(nt, ta, tb);
-  // wave w: words [AG_W wl, AG_W (wl + 1)) of tiles r0 + sub, r0 + sub + AG_TPS, ...
+  // wave w: words [AG_W wl, AG_W (wl + 1)) of tiles ta + sub, ta + sub + AG_TPS, ...
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wl = w % (64 / AG_W), sub = w / (64 / AG_W);
   const uint32_t lane = lane_id();
@@ -2498,7 +2741,7 @@ __global__ void __launch_bounds__(MS0_TPB)
                  const uint32_t *__restrict__ rbase, const uint32_t *__restrict__ rn,
                  const double *__restrict__ edges, const uint32_t *__restrict__ gq, int nb,
                  uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, uint32_t nt,
-                 FusedStats fs, double *__restrict__ slab) {
+                 FusedStats fs, double *__restrict__ slab, SpecIO sio) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t gql[MS_MAXQ + 1];  // the groups' first ranks (gq), ng + 1 of them
   const int macc = MOM ? fs.nm * nb : 0;
@@ -2511,50 +2754,71 @@ __global__ void __launch_bounds__(MS0_TPB)
   tile_range(nt, ta, tb);
   const uint32_t wt = (uint32_t)(FD_LDSW / nrs);  // tiles per window
   __shared__ uint64_t c_lo;  // the control record's fields, one load per block
-  __shared__ int c_ng;       // (-1: no window)
+  __shared__ int c_ng, c_hit;  // (c_ng -1: no window)
   if (tid == 0) {
     const bool ok = !(ctl->err & 2);
     c_ng = ok ? ctl->ng : -1;
     c_lo = ctl->lo;
+    c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
   }
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
   for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
   __syncthreads();
   const bool ok_all = c_ng >= 0;
   for (int k = tid; k <= c_ng; k += MS0_TPB) gql[k] = gq[k];
-  const int64_t r0 = rbase[blockIdx.x], cnt = ok_all ? (int64_t)rn[blockIdx.x] : 0;
   const uint64_t lo = c_lo;
-  for (uint32_t w0 = ta; w0 < tb || (w0 == ta && cnt); w0 += wt) {  // (block-uniform)
+  // this block's deferred keys: assign_gather's list of the block, or on a
+  // speculation hit the lists of its SH_K select blocks (keys of its own tiles)
+  const bool hit = c_hit != 0;
+  const int nl = hit ? (blockIdx.x >= 1 ? SH_K : 0) : 1;
+  int64_t lb[SH_K], lc[SH_K];
+  int64_t cnt_all = 0;
+#pragma unroll
+  for (int l = 0; l < SH_K; ++l) {
+    lb[l] = 0;
+    lc[l] = 0;
+    if (l < nl && ok_all) {
+      const uint32_t j = hit ? SH_K * (blockIdx.x - 1) + l : blockIdx.x;
+      lb[l] = hit ? sio.srbase[j] : rbase[j];
+      lc[l] = hit ? sio.srn[j] : rn[j];
+      cnt_all += lc[l];
+    }
+  }
+  const AgRec *lr = hit ? sio.srec : rec;
+  for (uint32_t w0 = ta; w0 < tb || (w0 == ta && cnt_all); w0 += wt) {  // (block-uniform)
     const uint32_t w1 = min(tb, w0 + wt);
     for (int k = tid; k < (int)(w1 - w0) * nrs; k += MS0_TPB) tc[k] = 0;
     __syncthreads();
     const bool first = w0 == ta;  // bytes and sums on the first pass only
-    for (int64_t i0 = 0; i0 < cnt; i0 += (int64_t)MS0_TPB * FD_U) {
-      AgRec r[FD_U];
+    for (int l = 0; l < nl; ++l) {
+      const int64_t r0 = lb[l], cnt = lc[l];
+      for (int64_t i0 = 0; i0 < cnt; i0 += (int64_t)MS0_TPB * FD_U) {
+        AgRec r[FD_U];
 #pragma unroll
-      for (int u = 0; u < FD_U; ++u) {
-        const int64_t i = i0 + u * MS0_TPB + tid;
-        r[u] = rec[r0 + (i < cnt ? i : 0)];  // unconditional loads
-      }
-#pragma unroll
-      for (int u = 0; u < FD_U; ++u) {
-        const int64_t i = i0 + u * MS0_TPB + tid;
-        const double v = dkey_inv(lo + r[u].off);
-        const bool ok = i < cnt;
-        const uint32_t t = r[u].tg & ((1u << AG_TBITS) - 1), g = r[u].tg >> AG_TBITS;
-        const uint32_t b = ok ? bin_of_in(v, e, nb, (int)gql[g], (int)gql[g + 1]) : (uint32_t)nb;
-        if (ok) {
-          if (first) bins[r[u].pos] = (uint8_t)b;
-          if (t >= w0 && t < w1) atomicAdd(&tc[(t - w0) * nrs + b], 1u);
+        for (int u = 0; u < FD_U; ++u) {
+          const int64_t i = i0 + u * MS0_TPB + tid;
+          r[u] = lr[r0 + (i < cnt ? i : 0)];  // unconditional loads
         }
-        if (MOM && first && ok && b < (uint32_t)nb)
 #pragma unroll
-          for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
-            if (q >= fs.nm) break;
-            const double f = fs.f[q] == 0 ? v : r[u].w;
-            const double ww = fs.w[q] == 0 ? v : r[u].w;
-            atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
+        for (int u = 0; u < FD_U; ++u) {
+          const int64_t i = i0 + u * MS0_TPB + tid;
+          const double v = dkey_inv(lo + r[u].off);
+          const bool ok = i < cnt;
+          const uint32_t t = r[u].tg & ((1u << AG_TBITS) - 1), g = r[u].tg >> AG_TBITS;
+          const uint32_t b = ok ? bin_of_in(v, e, nb, (int)gql[g], (int)gql[g + 1]) : (uint32_t)nb;
+          if (ok) {
+            if (first) bins[r[u].pos] = (uint8_t)b;
+            if (t >= w0 && t < w1) atomicAdd(&tc[(t - w0) * nrs + b], 1u);
           }
+          if (MOM && first && ok && b < (uint32_t)nb)
+#pragma unroll
+            for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+              if (q >= fs.nm) break;
+              const double f = fs.f[q] == 0 ? v : r[u].w;
+              const double ww = fs.w[q] == 0 ? v : r[u].w;
+              atomicAdd(&acc[q * nb + b], monomial(fs.col[q], f, ww));
+            }
+        }
       }
     }
     __syncthreads();
@@ -3109,15 +3373,29 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
         cl.w0 = B < MONO_BITS ? B : MONO_BITS;
         cl.s0 = B - cl.w0;
         cl.lo = lo;
-        // the next call's hint: this window widened by 1/64 of its span each side
-        const uint64_t mg = span >> 6;
-        const uint64_t lo2 = lo >= mg ? lo - mg : 0ull;
-        const uint64_t hi2 = hi + mg < hi ? ~0ull : hi + mg;
-        const uint64_t sp2 = hi2 - lo2;
-        const int B2 = sp2 ? 64 - __builtin_clzll(sp2) : 1;
-        ho.w = B2 < MONO_BITS ? B2 : MONO_BITS;
-        ho.s = B2 - ho.w;
-        ho.lo = lo2;
+        // the next call's hint: this call's digit width with the base moved
+        // down by half the room the width leaves above the window, when that
+        // room is at least 1/32 of the span (a similar next call still fits
+        // with digits as fine as its own); else the window widened by 1/64
+        // of its span each side (one more key bit: digits twice as wide,
+        // groups twice as large — the finish took +5 us at 1M that way)
+        const uint64_t cap = B >= 64 ? ~0ull : ((1ull << B) - 1);
+        const uint64_t room = cap - span;
+        if (room >= (span >> 5)) {
+          const uint64_t mg = room >> 1;
+          ho.w = cl.w0;
+          ho.s = cl.s0;
+          ho.lo = lo >= mg ? lo - mg : 0ull;
+        } else {
+          const uint64_t mg = span >> 6;
+          const uint64_t lo2 = lo >= mg ? lo - mg : 0ull;
+          const uint64_t hi2 = hi + mg < hi ? ~0ull : hi + mg;
+          const uint64_t sp2 = hi2 - lo2;
+          const int B2 = sp2 ? 64 - __builtin_clzll(sp2) : 1;
+          ho.w = B2 < MONO_BITS ? B2 : MONO_BITS;
+          ho.s = B2 - ho.w;
+          ho.lo = lo2;
+        }
         ho.valid = 1;
       }
       if (t == 0 && a.hout) *a.hout = ho;
@@ -3821,6 +4099,11 @@ struct Profile {
   // tiled radial calls: level-0 geometry hints (two SelHint slots, by call
   // parity) and select_tiles' digit rows
   Buf shint, srows, swc, sbt;  // + select_tiles' per-(tile, wave) counts and block totals
+  // speculative assignment: the stored bin table, select_tiles' deferred
+  // lists, their [start, length] per select block, per-block sums
+  Buf stab, srec, sspec, sslab, sflag;
+  bool spec_next = false;  // the last tiled call's ranks matched the table: speculate
+  int64_t n_spec = 0, n_spec_hit = 0;  // tiled calls that speculated, of them hits
   uint64_t n_tiled = 0;
   bool lazy = false, w_ready = false, idx_ready = false;
   bool x_tiled = false;  // x holds a tiled selection (tile t at x[t * TILE ..]): ensure_x
@@ -4234,13 +4517,17 @@ static int fused_grid(int64_t n_sel) {
 struct TileHist {  // select_tiles' hinted level-0 histogram (null hint: none)
   const SelHint *hint = nullptr;
   uint64_t ka = 0, kb = ~0ull;
+  // the speculative assignment (tab non-null: wanted); select_launch fills
+  // the rest and sets `spec` when it launched select_tiles<FAM, true>
+  SpecArgs sa{};
+  bool spec = false;
 };
 
 static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
                               int64_t n, int on_device, int use_sphere, const double *sphere,
                               const int64_t *fam, int nfam, int ndim, bool lazy = false,
                               int pos_f32 = 0, int mass_f32 = 0, bool tiled = false,
-                              const TileHist *th = nullptr) {
+                              TileHist *th = nullptr) {
   const SelPrep r = select_prep(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
                                 lazy, pos_f32, mass_f32, tiled);
   const SelectParams &sp = r.sp;
@@ -4310,12 +4597,33 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
           rows16 = (uint32_t *)P.srows.get(sizeof(uint32_t) * (size_t)G1 * rsub * (MS0_DIG / 2));
         uint32_t *wc = (uint32_t *)P.swc.get(sizeof(uint32_t) * (size_t)nt * SH_NW);
         uint32_t *bt = (uint32_t *)P.sbt.get(sizeof(uint32_t) * (size_t)G1);
-        hipLaunchKernelGGL(sp.nfam > 1 ? select_tiles<true> : select_tiles<false>, dim3(G1),
+        SpecArgs sa{};
+        const bool spec = th && th->sa.tab && rows16;
+        if (spec) {  // select_tiles bins with the stored table too
+          sa = th->sa;
+          sa.mass = (const double *)d_mass;
+          sa.bins = (uint8_t *)P.bins8.get((size_t)nt * TILE);
+          sa.th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * (sa.nb + 1));
+          sa.slab = (double *)P.sslab.get(sizeof(double) * (size_t)G1 * std::max(1, sa.fs.nm * sa.nb));
+          sa.rec = (AgRec *)P.srec.get(sizeof(AgRec) * ((size_t)nt * TILE / SPEC_LIST + 1));
+          sa.rbase = (uint32_t *)P.sspec.get(sizeof(uint32_t) * 2 * (size_t)G1);
+          sa.rn = sa.rbase + G1;
+          // (zeroed once; fused_resolve resets it after reading it)
+          if (!P.sflag.p) {
+            P.sflag.get(sizeof(uint32_t));
+            PBX_HIP(hipMemsetAsync(P.sflag.p, 0, sizeof(uint32_t), st));
+          }
+          sa.flag = (uint32_t *)P.sflag.p;
+          th->sa = sa;
+        }
+        if (th) th->spec = spec;
+        auto kern = spec ? (sp.nfam > 1 ? select_tiles<true, true> : select_tiles<false, true>)
+                         : (sp.nfam > 1 ? select_tiles<true, false> : select_tiles<false, false>);
+        hipLaunchKernelGGL(kern, dim3(G1),
                            dim3(SH_BT), 0, st, (const double *)d_pos, hi,
                            sp, nt, (uint32_t)G0, xo, kw, r.kpre, wc, toff, bt, mm,
                            th ? th->hint : nullptr, th ? th->ka : 0ull, th ? th->kb : ~0ull, rows16, rsub,
-                           (uint32_t *)(mm + 2 * MM_SLOTS),
-                           (uint32_t *)P.msH.get(sizeof(uint32_t) * MS0_DIG));
+                           (uint32_t *)(mm + 2 * MM_SLOTS), sa);
       } else if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
       else if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
       else if (sel512) go(select_onepass<512, false, double>, 512, 0.0);
@@ -4755,6 +5063,15 @@ int pbx_profile_level0_stats(void *handle, int64_t *out) {
     if (!out) fail(PBX_ERR_VALUE, "null output");
     out[0] = P.n_tiled_calls;
     out[1] = P.n_hinted;
+  });
+}
+
+int pbx_profile_spec_stats(void *handle, int64_t *out) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    if (!out) fail(PBX_ERR_VALUE, "null output");
+    out[0] = P.n_spec;
+    out[1] = P.n_spec_hit;
   });
 }
 
@@ -5254,7 +5571,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       if (f_src[k] < 0 || f_src[k] > 1 || w_src[k] < -1 || w_src[k] > 1)
         fail(PBX_ERR_VALUE, "the fused path takes the profile's x / weights only");
     Device &d = current_device();
-    std::lock_guard<std::mutex> lk(d.mu);
+    std::unique_lock<std::mutex> lk(d.mu);  // (released inside comm_allreduce's host wait)
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.radial_equaln");
     // bins < 256: the lazy selection + tile-walking assignment / CSR passes
@@ -5350,14 +5667,30 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       thist.hint = hints ? hints + (P.n_tiled & 1) : nullptr;
       thist.ka = ka;
       thist.kb = empty_bounds ? 0ull : kb;
+      // the speculative assignment: when the last tiled call's level-0 ranks
+      // matched the stored table (a repeated or similar call), select_tiles
+      // bins with it (checked by fused_resolve; a miss takes assign_gather)
+      static const bool spec_env = [] {  // A/B: PBX_SPEC=0 never speculates
+        const char *v = std::getenv("PBX_SPEC");
+        return !(v && v[0] == '0');
+      }();
+      bool spec_ops = true;  // select_tiles' sums take the dedicated monomials only
+      for (int q = 0; q < fs.nm; ++q) spec_ops = spec_ops && fs.op[q] != MO_GEN;
+      if (hints && spec_env && P.spec_next && P.stab.p && nb <= SPEC_MAXB &&
+          fs.nm * nb <= SPEC_MACC && spec_ops && !agather_off()) {
+        thist.sa.tab = (const SpecTab *)P.stab.p;
+        thist.sa.fs = fs;
+        thist.sa.nb = (int)nb;
+      }
       const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
                                         nfam, ndim, lazy, 0, 0, /*tiled=*/true, &thist);
+      if (thist.spec) ++P.n_spec;
       const bool hinted = hints && P.x_tiled;
       tiled_call = P.x_tiled;
       if (hinted) ++P.n_tiled;  // (the next tiled call reads the slot this one writes)
       if (dist)  // global key range: every min / max slot pair (~min, max) max-reduced
         comm_allreduce(comm, (uint64_t *)P.selst.p + nt + 1, (uint64_t *)P.selst.p + nt + 1,
-                       2 * MM_SLOTS, 2, 2, st);
+                       2 * MM_SLOTS, 2, 2, st, lk);
       const int64_t n_sel = nt ? P.sel_span : 0;  // tiled particles (the families' span)
       const bool tiled = P.x_tiled;  // x by tile (large inputs): tile offsets from fused_hist0
       uint64_t *stat = (uint64_t *)P.selst.p;
@@ -5379,15 +5712,13 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                            (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0, (int)dist,
                            (const uint64_t *)P.kw.p,
                            hinted ? hints + ((P.n_tiled - 1) & 1) : nullptr, hflag,
-                           hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p,
-                           hinted ? (const uint32_t *)P.srows.p : nullptr,
-                           hinted ? SH_K * (g0 - 1) * (int)P.sel_rsub : 0};
-      hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb, H,
+                           hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p};
+      hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb,
                          rows);
-      hipLaunchKernelGGL(msel_reduce0h, dim3(MS0_DIG / 2 / TPB, 32), dim3(TPB), 0, st,
-                         (const uint32_t *)rows, g0, (const uint32_t *)P.srows.p,
+      hipLaunchKernelGGL(msel_reduce0h, dim3(MS0_DIG / R0_DIG), dim3(MS0_TPB), 0, st,
+                         (const uint32_t *)rows, g0, hinted ? (const uint32_t *)P.srows.p : nullptr,
                          hinted ? SH_K * (g0 - 1) * (int)P.sel_rsub : 0, (const int32_t *)&ctl->hint, H,
-                         stat + nt, 2 + 2 * MM_SLOTS, (hinted && tiled) ? 1 : 0);
+                         stat + nt, 2 + 2 * MM_SLOTS);
       PBX_HIP(hipGetLastError());
       P.sel_tail_zero = stat + nt;  // (select_launch: no fill before the next tiled call)
       int64_t *gsc = nullptr;  // dist: [global kept count][ctl copy]
@@ -5398,20 +5729,30 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         PBX_HIP(hipMemsetAsync(lc_all, 0, sizeof(uint32_t) * (size_t)cr.nranks * MS_MAXQ, st));
         // [global kept count, ranks whose look-back failed]
         hipLaunchKernelGGL(dist_status, dim3(1), dim3(1), 0, st, (const FusedCtl *)ctl, gsc + 2);
-        comm_allreduce(comm, gsc + 2, gsc, 2, 1, 0, st);
-        comm_allreduce(comm, H, H, MS0_DIG, 3, 0, st);
+        comm_allreduce(comm, gsc + 2, gsc, 2, 1, 0, st, lk);
+        comm_allreduce(comm, H, H, MS0_DIG, 3, 0, st, lk);
       }
       MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
       uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)g0) * (MS_MAXQ + 1));
       uint32_t *goff = gdig + (MS_MAXQ + 1), *gq = goff + (MS_MAXQ + 1);
       uint32_t *boff = gq + (MS_MAXQ + 1);
+      // the stored bin table (one rank, tiled assignment): allocated zeroed (invalid)
+      SpecTab *stab = nullptr;
+      if (agath && !dist) {
+        if (!P.stab.p) {
+          P.stab.get(sizeof(SpecTab));
+          PBX_HIP(hipMemsetAsync(P.stab.p, 0, sizeof(SpecTab), st));
+        }
+        stab = (SpecTab *)P.stab.p;
+      }
       hipLaunchKernelGGL(fused_resolve, dim3(nq), dim3(FR_TPB), 0, st, (const uint32_t *)H, ctl,
                          nbins, nq, R, gdig, goff, gq, (const uint32_t *)rows, g0, boff, bcnt,
                          dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr,
-                         (const uint32_t *)P.srows.p, P.sel_rsub);
+                         (const uint32_t *)P.srows.p, P.sel_rsub, (const SpecTab *)stab,
+                         thist.spec ? thist.sa.flag : nullptr, (int)nb);
       int64_t seg_total = 0;  // dist: keys in all ranks' group segments
       if (dist) {
-        comm_allreduce(comm, lc_all, lc_all, (int64_t)cr.nranks * MS_MAXQ, 3, 0, st);
+        comm_allreduce(comm, lc_all, lc_all, (int64_t)cr.nranks * MS_MAXQ, 3, 0, st, lk);
         hipLaunchKernelGGL(dist_rank_offsets, dim3(nq), dim3(TPB), 0, st, (const FusedCtl *)ctl,
                            (const uint32_t *)lc_all, cr.rank, g0, boff);
         PBX_HIP(hipGetLastError());
@@ -5444,6 +5785,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       uint32_t *th = nullptr;
       uint8_t *bins8 = nullptr;
       GatherOut go{};
+      SpecIO sio{};
       if (agath) {
         const int nr = (int)nb + 1;
         const int64_t macc = (int64_t)fs.nm * nb;
@@ -5453,12 +5795,16 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         go = GatherOut{seg, (AgRec *)P.frec.get(sizeof(AgRec) * (size_t)n_sel), bcnt, bcnt + g0,
                        bcnt + 2 * g0};
         const size_t lds = sizeof(double) * (size_t)macc + sizeof(uint32_t) * (size_t)(nr | 1) * AG_TR;
+        sio = SpecIO{stab, thist.spec ? thist.sa.rec : nullptr,
+                     thist.spec ? (const uint32_t *)thist.sa.rbase : nullptr,
+                     thist.spec ? (const uint32_t *)thist.sa.rn : nullptr,
+                     thist.spec ? (const double *)thist.sa.slab : nullptr};
         auto ag = [&](auto kern) {
           hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, x, (const uint64_t *)P.kw.p,
                              P.sel_base, P.sel_span, nt, P.sel_mass,
                              (const FusedCtl *)ctl, ka, kb, (const MsRank *)R, nq,
                              (const uint32_t *)gdig, (const uint32_t *)boff, (int)nb, bins8, th,
-                             fs, slab, go);
+                             fs, slab, go, sio);
         };
         if (fs.nm) ag(assign_gather<true>);
         else ag(assign_gather<false>);
@@ -5474,7 +5820,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                            seg, tiled ? (const uint64_t *)P.kw.p : nullptr, nt);
       }
       if (dist)  // every rank's group keys, each in its own slice: the all-gather
-        comm_allreduce(comm, seg, seg, seg_total, 2, 0, st);
+        comm_allreduce(comm, seg, seg, seg_total, 2, 0, st, lk);
       hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
                          (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
                          (const uint64_t *)seg, de);
@@ -5487,7 +5833,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
           hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, (const FusedCtl *)ctl,
                              (const AgRec *)go.rec, (const uint32_t *)go.rbase,
                              (const uint32_t *)go.rn, (const double *)de, (const uint32_t *)gq,
-                             (int)nb, bins8, th, nt, fs, maccs2);
+                             (int)nb, bins8, th, nt, fs, maccs2, sio);
         };
         if (fs.nm) fd(fix_deferred<true>);
         else fd(fix_deferred<false>);
@@ -5653,8 +5999,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         if (dist) {
           PBX_HIP(hipMemcpyAsync(dpk + ntot, dpk + NC + nq, sizeof(double) * nb,
                                  hipMemcpyDeviceToDevice, st));
-          comm_allreduce(comm, dpk + NC + nq, dpk + NC + nq, nb, 2, 0, st);   // counts (u64)
-          comm_allreduce(comm, dpk + NC + nq + nb, dpk + NC + nq + nb, nsum, 0, 0, st);  // sums
+          comm_allreduce(comm, dpk + NC + nq, dpk + NC + nq, nb, 2, 0, st, lk);   // counts (u64)
+          comm_allreduce(comm, dpk + NC + nq + nb, dpk + NC + nq + nb, nsum, 0, 0, st, lk);  // sums
         }
         hp = (double *)P.pin.get(sizeof(double) * (size_t)(ntot + nloc));
         PBX_HIP(hipMemcpyAsync(hp, dpk, sizeof(double) * (ntot + nloc), hipMemcpyDeviceToHost, st));
@@ -5674,6 +6020,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
     if (tiled_call) {
       ++P.n_tiled_calls;
       if (c.hint) ++P.n_hinted;
+      if (c.spec & SPEC_HIT) ++P.n_spec_hit;
+      P.spec_next = !dist && (c.spec & SPEC_MATCH);
     }
     P.mm[0] = c.kmin;
     P.mm[1] = c.kmax;
@@ -5699,8 +6047,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         PBX_HIP(hipStreamSynchronize(st));
         int64_t *gc = (int64_t *)P.dscal.get(sizeof(int64_t) * 4 + sizeof(FusedCtl));
         PBX_HIP(hipMemcpyAsync(gc, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
-        comm_allreduce(comm, gc, gc, 1, 1, 0, st);
-        comm_allreduce(comm, accs, accs, (int64_t)n_stats * NMOM, 0, 0, st);
+        comm_allreduce(comm, gc, gc, 1, 1, 0, st, lk);
+        comm_allreduce(comm, accs, accs, (int64_t)n_stats * NMOM, 0, 0, st, lk);
         PBX_HIP(hipMemcpyAsync(h_counts, gc, sizeof(int64_t), hipMemcpyDeviceToHost, st));
       } else {
         PBX_HIP(hipMemcpyAsync(h_counts, P.counts.p, sizeof(int64_t), hipMemcpyDeviceToHost, st));
@@ -5730,7 +6078,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         for (int k = 0; k < n_stats; ++k)
           moments_device(P, st, f_src[k], nullptr, P.field, w_src[k], nullptr, P.weight, cols[k],
                          accs + k * len);
-        if (dist) comm_allreduce(comm, accs, accs, (int64_t)n_stats * len, 0, 0, st);
+        if (dist) comm_allreduce(comm, accs, accs, (int64_t)n_stats * len, 0, 0, st, lk);
         PBX_HIP(hipMemcpyAsync(h_moments, accs, sizeof(double) * n_stats * len,
                                hipMemcpyDeviceToHost, st));
         PBX_HIP(hipStreamSynchronize(st));

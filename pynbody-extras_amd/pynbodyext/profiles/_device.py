@@ -252,6 +252,14 @@ class DeviceBins:
         nat.call("pbx_profile_level0_stats", self._h, _i64(out))
         return {"tiled": int(out[0]), "hinted": int(out[1])}
 
+    def spec_stats(self) -> dict:
+        """Tiled radial_equaln calls whose selection kernel also binned the
+        keys with the stored bin table, and of them the hits (the assignment
+        pass skipped; pbx_profile_spec_stats)."""
+        out = np.zeros(2, dtype=np.int64)
+        nat.call("pbx_profile_spec_stats", self._h, _i64(out))
+        return {"speculated": int(out[0]), "hits": int(out[1])}
+
     def set_level0_hint(self, enabled: bool) -> None:
         """False: every tiled radial_equaln call on this handle re-reads x for
         its level-0 histogram (what a first call or a new snapshot costs);

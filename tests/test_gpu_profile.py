@@ -830,6 +830,62 @@ def test_radial_equaln_level0_hint_many_tiles_per_block(gpu):
         h.close()
 
 
+def test_radial_equaln_speculative_assignment(gpu):
+    """The speculative assignment of tiled calls (select_tiles binning every
+    key with the bin table an earlier call stored, checked by fused_resolve
+    against this call's level-0 digits).  On one handle: a repeated call
+    speculates once two calls in a row had the same digits, and hits; a
+    snapshot scaled by 1 + 1e-12 and a reshuffled one (same radii, every
+    particle elsewhere) still hit — their keys bin exactly with the table; a
+    changed window or bin count misses first (the assignment pass runs) and
+    hits again once repeated; with a family slice and an offset sphere
+    (select_tiles<FAM = true>) too.  Every call equals the same call on a
+    handle that never speculates (level-0 hint off): edges, counts and CSR
+    bit-identical, sums to rounding."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(51)
+    n = 4_400_000
+    pos = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    win = {"bin_min": 0.5, "bin_max": 6.0}
+    fam = {"sphere": ((0.5, 0.0, 0.0), 7.0), "families": [(100_000, 4_300_000)]}
+    h, ref = DeviceBins(), DeviceBins()
+    ref.set_level0_hint(False)
+
+    def call(p_, kw):
+        kw = dict(kw)
+        nb = kw.pop("nbins", 128)
+        _, e, c, m = DeviceBins.radial_equaln(p_, mass, nbins=nb, stats=stats, into=h, **kw)
+        pp, o = h.csr()
+        _, e0, c0, m0 = DeviceBins.radial_equaln(p_, mass, nbins=nb, stats=stats, into=ref, **kw)
+        pp0, o0 = ref.csr()
+        assert np.array_equal(e, e0) and np.array_equal(c, c0), kw
+        assert np.array_equal(o, o0) and np.array_equal(pp, pp0), kw
+        for u, v in zip(m, m0):
+            np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300, err_msg=str(kw))
+        st = h.spec_stats()
+        return st["speculated"], st["hits"]
+
+    try:
+        got = [call(pos, {}) for _ in range(5)]
+        # calls 0, 1: no table / the table in call 0's unhinted geometry; call
+        # 2 matches (no speculation yet); calls 3, 4 speculate and hit
+        assert got == [(0, 0), (0, 0), (0, 0), (1, 1), (2, 2)], got
+        assert call(pos * (1.0 + 1e-12), {}) == (3, 3)
+        assert call(pos[rng.permutation(n)], {}) == (4, 4)
+        for kw in (win, {"nbins": 64}, fam):
+            s0, h0 = h.spec_stats().values()
+            got = [call(pos, kw) for _ in range(5)]
+            assert got[0] == (s0 + 1, h0), (kw, got)  # speculated with the old table: a miss
+            assert got[-1][1] - got[-2][1] == 1, (kw, got)  # repeated: hits again
+        assert ref.spec_stats() == {"speculated": 0, "hits": 0}
+    finally:
+        h.close()
+        ref.close()
+
+
 def test_radial_equaln_level0_hint_switch(gpu):
     """set_level0_hint(False) (the bench's cold-handle timing): repeated
     tiled calls on one handle re-read x every time — no call hinted — and
