@@ -846,7 +846,7 @@ struct FusedCtl {
   int32_t spec;    // SPEC_MATCH: this call's level-0 ranks equal the stored bin table's;
                    // SPEC_HIT: select_tiles binned with that table (no assignment pass)
 };
-constexpr int32_t SPEC_MATCH = 1, SPEC_HIT = 2;
+constexpr int32_t SPEC_MATCH = 1, SPEC_HIT = 2, SPEC_NOX = 4;
 
 // Level-0 digit geometry of a handle's previous tiled call (select_tiles
 // counts this call's keys with it while they are still in registers; the
@@ -943,8 +943,9 @@ struct SpecArgs {
   double *slab;            // per select block: nm * nb sums
   AgRec *rec;              // deferred lists: select block j's at rbase[j]
   uint32_t *rbase, *rn;    // per select block: list start, length
-  uint32_t *flag;          // set when a block could not bin (table / hint geometry differ,
-                           // a list overflowed): the call takes the assignment pass
+  uint32_t *flag;          // bit 0: a block could not bin (table / hint geometry differ, a
+                           // list overflowed): the call takes the assignment pass;
+                           // bit 1: the blocks binned and stored no x (SPEC_NOX)
   FusedStats fs;
   int nb;
 };
@@ -956,6 +957,15 @@ struct SpecArgs {
 #endif
 constexpr int SH_K = PBX_SH_K;
 
+
+// the inputs x is recomputed from when a speculating selection stored none (xsrc_tiles)
+struct XSrc {
+  const double *pos;  // the selection's positions (null: x was stored)
+  int64_t n_hi;       // particles [sp.base, n_hi) are tiled
+  SelectParams sp;
+  double *x;          // x by slot
+  const uint64_t *kw;
+};
 
 // The step's control record from the selection's status words: kept count
 // (inclusive prefix of the last tile), key range (min over the slot pairs),
@@ -977,6 +987,8 @@ struct FusedSetup {
   const uint32_t *hflag; // select_tiles: a window key fell outside the hint (or null)
   SelHint *hint_out;     // fused_hist0 block 0: this call's own geometry, for the next call
   const uint32_t *btot;  // tiled: select_tiles' block totals (SH_K (gridDim - 1) blocks)
+  const uint32_t *sflag; // tiled, speculating: select_tiles' flags (bit 1: no x stored)
+  XSrc xs;               // ... and what x is recomputed from then
 };
 
 // Element range of fused_hist0 / fused_gather: the kept x [0, n), or with
@@ -1146,6 +1158,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   const uint32_t lcap = (uint32_t)((uint64_t)(tb - ta) * TILE / SPEC_LIST);
   if (SPEC) {
     if (spec) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(sa.flag, 2u);  // no x stored (SPEC_NOX)
       const uint4 *src = (const uint4 *)sa.tab->bin;
       for (int i = threadIdx.x; i < MS0_DIG / 16; i += SH_BT) ((uint4 *)sdt)[i] = src[i];
       for (int i = threadIdx.x; i < macc; i += SH_BT) sacc[i] = 0.0;
@@ -1208,7 +1221,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       // stores once fused_hist0's timing was stable, see fused_hist0); as
       // streaming (nt) stores: select 280 -> 274 us and assign_gather's
       // re-read of x 202 -> 191 us at 64M (same box A/B/A/B)
-      __builtin_nontemporal_store(xv, xt + k * 64 + lane);
+      if (!(SPEC && spec)) __builtin_nontemporal_store(xv, xt + k * 64 + lane);
       if (keep) {
         const uint64_t kk = dkey(xv);
         kmin = kk < kmin ? kk : kmin;
@@ -1386,6 +1399,42 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   }
 }
 
+// A speculating select_tiles stores no x (SPEC_NOX): a hit never reads it.
+// When a call does need it after all — a key escaped the level-0 hint
+// (fused_hist0 counts x again) or the digits missed the table (assign_gather
+// bins x) — each block of those kernels first recomputes x for its own
+// tiles from the positions (the kept slots, by the keep words; select_xyz:
+// the same value select_tiles computed); after a hit the host marks x
+// missing and ensure_x rebuilds it the same way (xsrc_kernel) for a later
+// consumer.
+__device__ void xsrc_tiles(const XSrc &xs, uint32_t ta, uint32_t tb) {
+  constexpr int U = 4;  // slots per thread in flight
+  const int bt = blockDim.x;
+  const int64_t s0 = (int64_t)ta * TILE, s1 = (int64_t)tb * TILE;
+  for (int64_t a = s0 + threadIdx.x; a < s1; a += (int64_t)bt * U) {
+    double px[U], py[U], pz[U];
+    bool kp[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t sl = a + (int64_t)u * bt;
+      kp[u] = sl < s1 && ((xs.kw[sl >> 6] >> (sl & 63)) & 1ull);
+      const double *q = xs.pos + 3 * (kp[u] ? xs.sp.base + sl : 0);
+      px[u] = q[0];
+      py[u] = q[1];
+      pz[u] = q[2];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double xv = 0.0;
+      if (kp[u] && select_xyz(px[u], py[u], pz[u], xs.sp, xv)) xs.x[a + (int64_t)u * bt] = xv;
+    }
+  }
+}
+__global__ void __launch_bounds__(TPB) xsrc_kernel(XSrc xs, uint32_t nt, uint32_t tiles_per_block) {
+  const uint32_t ta = blockIdx.x * tiles_per_block;
+  xsrc_tiles(xs, ta, min(nt, ta + tiles_per_block));
+}
+
 // fused_hist0 blocks >= 1 (tiled): the global tile offsets, select_tiles'
 // block-local ones plus each select block's base (the sum of the block
 // totals before it); block 0: the kept count
@@ -1554,6 +1603,16 @@ __global__ void __launch_bounds__(MS0_TPB)
   }
   if (fsu.tiled) tile_offsets_fix(fsu.btot, fsu.nt, fsu.toff, red);  // (blocks >= 1)
   if (ctl.hint) return;  // select_tiles counted the keys (msel_reduce0h sums its rows)
+  __shared__ int s_nox;
+  if (threadIdx.x == 0) s_nox = (fsu.tiled && fsu.sflag && (*fsu.sflag & 2u)) ? 1 : 0;
+  __syncthreads();
+  if (s_nox) {  // a speculating selection stored no x and a key escaped the hint: x of this block's tiles
+    uint32_t ta, tb;
+    tile_range(fsu.nt, ta, tb);
+    xsrc_tiles(fsu.xs, ta, tb);
+    __threadfence();
+    __syncthreads();
+  }
   for (int i = threadIdx.x; i < MS0_DIG; i += MS0_TPB) lh[i] = 0;
   __syncthreads();
   const uint64_t ka = fsu.ka, kb = fsu.kb;
@@ -1658,7 +1717,8 @@ __global__ void __launch_bounds__(FR_TPB)
   if (pub && tid == 0) {
     const int m = s_spec ? SPEC_MATCH : 0;
     // a hit: select_tiles binned every key with the table (no block gave up)
-    ctl->spec = m | ((m && sflag && *sflag == 0u) ? SPEC_HIT : 0);
+    const uint32_t f = sflag ? *sflag : 0u;
+    ctl->spec = m | ((m && sflag && !(f & 1u)) ? SPEC_HIT : 0) | ((f & 2u) ? SPEC_NOX : 0);
     if (sflag) *sflag = 0u;  // (for the next speculating call)
   }
   // groups: run starts of the (non-decreasing) digits; one wave numbers them
@@ -2459,6 +2519,7 @@ __device__ __forceinline__ uint32_t block_prefix(const uint32_t *__restrict__ v,
 // (ctl->spec & SPEC_HIT) assign_gather only moves the select blocks' deferred
 // keys into their groups' segments and sums their slab rows; on a miss it
 // assigns as before and (block 0) stores the table for the next call.
+constexpr int AG_HU = 4;  // assign_gather on a hit: records per thread in flight
 struct SpecIO {
   SpecTab *tab;            // written by block 0 of a full assignment
   AgRec *srec;             // select blocks' deferred lists (their groups filled in) ...
@@ -2474,7 +2535,7 @@ __global__ void __launch_bounds__(MS0_TPB)
                   const MsRank *__restrict__ R, int nq,
                   const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ boff, int nb,
                   uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
-                  double *__restrict__ slab, GatherOut go, SpecIO sio) {
+                  double *__restrict__ slab, GatherOut go, SpecIO sio, XSrc xs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per level-0 digit: the bin of its keys (#{q : digit_q < d} - 1, or nb),
   // or 0x8000 | group when the digit holds edges — one LDS read per key
@@ -2491,9 +2552,12 @@ __global__ void __launch_bounds__(MS0_TPB)
   // the control record's fields: one load per block, broadcast through LDS
   // (not ~4 scalar loads of one line in each of the grid's 4096 waves)
   __shared__ uint64_t c_lo;
-  __shared__ int c_ng, c_s, c_win, c_w0, c_hit;
+  __shared__ int c_ng, c_s, c_win, c_w0, c_hit, c_xsrc;
   if (tid == 0) {
     const bool w0 = !(ctl->err & 2);
+    // x to recompute first: a speculating selection stored none, the call
+    // missed, and fused_hist0 did not rebuild it (the hint held)
+    c_xsrc = ((ctl->spec & SPEC_NOX) && !(ctl->spec & SPEC_HIT) && ctl->hint) ? 1 : 0;
     c_win = w0;
     c_ng = w0 ? ctl->ng : 0;
     c_lo = ctl->lo;
@@ -2510,15 +2574,34 @@ __global__ void __launch_bounds__(MS0_TPB)
     for (int g = tid; g < ng; g += MS0_TPB) dtab[gdig[g]] = (uint16_t)g;
     __syncthreads();
     const int s = c_s;
-    if (blockIdx.x >= 1) {
-      for (uint32_t j = SH_K * (blockIdx.x - 1); j < SH_K * blockIdx.x; ++j) {
-        const uint32_t r0 = sio.srbase[j], cnt = sio.srn[j];
-        for (uint32_t i = tid; i < cnt; i += MS0_TPB) {
-          AgRec *rp = sio.srec + r0 + i;
-          const uint64_t off = rp->off;
-          const uint32_t g = dtab[(uint32_t)(off >> s)];
-          go.seg[atomicAdd(&sslot[g], 1u)] = off;
-          rp->tg |= g << AG_TBITS;  // (fix_deferred reads the group)
+    if (blockIdx.x >= 1) {  // the SH_K lists as one index range, AG_HU records in flight
+      uint32_t lb[SH_K], le[SH_K], tot = 0;
+#pragma unroll
+      for (int l = 0; l < SH_K; ++l) {
+        const uint32_t j = SH_K * (blockIdx.x - 1) + l;
+        lb[l] = sio.srbase[j] - tot;  // record of list l at index i: lb[l] + i
+        tot += sio.srn[j];
+        le[l] = tot;
+      }
+      for (uint32_t i0 = 0; i0 < tot; i0 += MS0_TPB * AG_HU) {
+        AgRec *rp[AG_HU];
+        uint64_t off[AG_HU];
+#pragma unroll
+        for (int u = 0; u < AG_HU; ++u) {
+          const uint32_t i = i0 + u * MS0_TPB + tid;
+          const uint32_t ii = i < tot ? i : 0u;
+          uint32_t base = lb[SH_K - 1];
+#pragma unroll
+          for (int l = SH_K - 2; l >= 0; --l) base = ii < le[l] ? lb[l] : base;
+          rp[u] = sio.srec + base + ii;
+          off[u] = rp[u]->off;
+        }
+#pragma unroll
+        for (int u = 0; u < AG_HU; ++u) {
+          if (i0 + u * MS0_TPB + tid >= tot) break;
+          const uint32_t g = dtab[(uint32_t)(off[u] >> s)];
+          go.seg[atomicAdd(&sslot[g], 1u)] = off[u];
+          rp[u]->tg |= g << AG_TBITS;  // (fix_deferred reads the group)
         }
       }
     }
@@ -2579,6 +2662,11 @@ __global__ void __launch_bounds__(MS0_TPB)
   }
   uint32_t ta, tb;
   tile_range(nt, ta, tb);
+  if (c_xsrc) {
+    xsrc_tiles(xs, ta, tb);
+    __threadfence();
+    __syncthreads();
+  }
   // wave w: words [AG_W wl, AG_W (wl + 1)) of tiles ta + sub, ta + sub + AG_TPS, ...
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wl = w % (64 / AG_W), sub = w / (64 / AG_W);
@@ -4103,6 +4191,9 @@ struct Profile {
   // lists, their [start, length] per select block, per-block sums
   Buf stab, srec, sspec, sslab, sflag;
   bool spec_next = false;  // the last tiled call's ranks matched the table: speculate
+  bool x_missing = false;  // the last selection stored no x (a speculation hit): ensure_x rebuilds it
+  XSrc xsrc{};             // ... from these positions / parameters
+  Buf posst;               // lazy selections of host arrays: the staged positions (kept for xsrc)
   int64_t n_spec = 0, n_spec_hit = 0;  // tiled calls that speculated, of them hits
   uint64_t n_tiled = 0;
   bool lazy = false, w_ready = false, idx_ready = false;
@@ -4471,8 +4562,11 @@ static SelPrep select_prep(Profile &P, hipStream_t st, const void *pos, const vo
   const size_t ps = pos_f32 ? sizeof(float) : sizeof(double);
   const size_t ms = mass_f32 ? sizeof(float) : sizeof(double);
   const void *d_pos = pos, *d_mass = mass;
+  P.x_missing = false;
   if (!on_device && n) {
-    void *tp = P.keys0.get(ps * 3 * (size_t)n);
+    // (lazy: kept for the selection's lifetime — a speculating tiled call may
+    // have to recompute x from them later, ensure_x)
+    void *tp = (lazy ? P.posst : P.keys0).get(ps * 3 * (size_t)n);
     PBX_HIP(hipMemcpyAsync(tp, pos, ps * 3 * n, hipMemcpyHostToDevice, st));
     d_pos = tp;
     if (mass) {
@@ -4518,9 +4612,11 @@ struct TileHist {  // select_tiles' hinted level-0 histogram (null hint: none)
   const SelHint *hint = nullptr;
   uint64_t ka = 0, kb = ~0ull;
   // the speculative assignment (tab non-null: wanted); select_launch fills
-  // the rest and sets `spec` when it launched select_tiles<FAM, true>
+  // the rest and sets `spec` when it launched select_tiles<FAM, true>, and
+  // `xs`: what x is recomputed from when that kernel stored none
   SpecArgs sa{};
   bool spec = false;
+  XSrc xs{};
 };
 
 static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const void *mass,
@@ -4616,7 +4712,14 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
           sa.flag = (uint32_t *)P.sflag.p;
           th->sa = sa;
         }
-        if (th) th->spec = spec;
+        if (th) {
+          th->spec = spec;
+          th->xs = XSrc{spec ? (const double *)d_pos : nullptr, hi, sp, xo, kw};
+        }
+        if (spec) {  // (x missing until the call's pack says it missed: x rebuilt)
+          P.x_missing = true;
+          P.xsrc = th->xs;
+        }
         auto kern = spec ? (sp.nfam > 1 ? select_tiles<true, true> : select_tiles<false, true>)
                          : (sp.nfam > 1 ? select_tiles<true, false> : select_tiles<false, false>);
         hipLaunchKernelGGL(kern, dim3(G1),
@@ -4658,6 +4761,17 @@ static void ensure_idx(Profile &P, hipStream_t st) {
 
 // compact a tiled selection's x (consumers that index x by selection index)
 static void ensure_x(Profile &P, hipStream_t st) {
+  if (P.x_missing) {  // a speculation hit stored no x: recompute it from the positions
+    const uint32_t tpb = 4;
+    XSrc xs = P.xsrc;
+    xs.x = (double *)P.x.p;
+    xs.kw = (const uint64_t *)P.kw.p;
+    if (P.sel_nt)
+      hipLaunchKernelGGL(xsrc_kernel, dim3(ceil_div(P.sel_nt, tpb)), dim3(TPB), 0, st, xs,
+                         P.sel_nt, tpb);
+    PBX_HIP(hipGetLastError());
+    P.x_missing = false;
+  }
   if (!P.x_tiled) return;
   double *xc = (double *)P.xc.get(sizeof(double) * (size_t)std::max<int64_t>(P.n, 1));
   if (P.sel_nt && P.n)
@@ -5114,6 +5228,7 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
     P.has_idx = false;
     P.lazy = false;
     P.x_tiled = false;
+    P.x_missing = false;
     P.csr_ready = false;
     P.csrh_ready = false;
     P.ms.active = false;
@@ -5712,7 +5827,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                            (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0, (int)dist,
                            (const uint64_t *)P.kw.p,
                            hinted ? hints + ((P.n_tiled - 1) & 1) : nullptr, hflag,
-                           hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p};
+                           hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p,
+                           thist.spec ? (const uint32_t *)thist.sa.flag : nullptr, thist.xs};
       hipLaunchKernelGGL(fused_hist0, dim3(g0), dim3(MS0_TPB), 0, st, x, fsu, ctl, cnt, (int)nb,
                          rows);
       hipLaunchKernelGGL(msel_reduce0h, dim3(MS0_DIG / R0_DIG), dim3(MS0_TPB), 0, st,
@@ -5804,7 +5920,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                              P.sel_base, P.sel_span, nt, P.sel_mass,
                              (const FusedCtl *)ctl, ka, kb, (const MsRank *)R, nq,
                              (const uint32_t *)gdig, (const uint32_t *)boff, (int)nb, bins8, th,
-                             fs, slab, go, sio);
+                             fs, slab, go, sio, thist.xs);
         };
         if (fs.nm) ag(assign_gather<true>);
         else ag(assign_gather<false>);
@@ -6022,6 +6138,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       if (c.hint) ++P.n_hinted;
       if (c.spec & SPEC_HIT) ++P.n_spec_hit;
       P.spec_next = !dist && (c.spec & SPEC_MATCH);
+      // a hit stored no x (ensure_x rebuilds it on demand); a miss rebuilt it
+      P.x_missing = (c.spec & SPEC_NOX) && (c.spec & SPEC_HIT);
     }
     P.mm[0] = c.kmin;
     P.mm[1] = c.kmax;

@@ -868,11 +868,19 @@ def test_radial_equaln_speculative_assignment(gpu):
         st = h.spec_stats()
         return st["speculated"], st["hits"]
 
+    def x_consumers():
+        # a hit stores no x: the next consumer of x rebuilds it from the positions
+        np.testing.assert_array_equal(h.percentiles([0.5]), ref.percentiles([0.5]))
+        xi, xx, _ = h.selection(idx=True, x=True, w=False)
+        yi, yx, _ = ref.selection(idx=True, x=True, w=False)
+        assert np.array_equal(xi, yi) and np.array_equal(xx, yx)
+
     try:
         got = [call(pos, {}) for _ in range(5)]
         # calls 0, 1: no table / the table in call 0's unhinted geometry; call
         # 2 matches (no speculation yet); calls 3, 4 speculate and hit
         assert got == [(0, 0), (0, 0), (0, 0), (1, 1), (2, 2)], got
+        x_consumers()
         assert call(pos * (1.0 + 1e-12), {}) == (3, 3)
         assert call(pos[rng.permutation(n)], {}) == (4, 4)
         for kw in (win, {"nbins": 64}, fam):
@@ -880,6 +888,12 @@ def test_radial_equaln_speculative_assignment(gpu):
             got = [call(pos, kw) for _ in range(5)]
             assert got[0] == (s0 + 1, h0), (kw, got)  # speculated with the old table: a miss
             assert got[-1][1] - got[-2][1] == 1, (kw, got)  # repeated: hits again
+            x_consumers()
+        # speculating, and the keys escape the level-0 hint: fused_hist0
+        # rebuilds x from the positions before it counts
+        s0, h0 = h.spec_stats().values()
+        assert call(pos * 2.0, {}) == (s0 + 1, h0)
+        x_consumers()
         assert ref.spec_stats() == {"speculated": 0, "hits": 0}
     finally:
         h.close()
