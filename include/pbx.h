@@ -381,8 +381,12 @@ int pbx_profile_binned_equaln(void *handle, int64_t nbins, int has_min, double b
  * first later call on this handle that needs them (pbx_profile_moments*,
  * pbx_profile_get_selection with h_w, weighted percentiles) and held by the
  * handle from then on, so that array must stay allocated and unchanged
- * until that call (or the next selection).  Host inputs (on_device = 0) are
- * staged into the handle. */
+ * until that call (or the next selection).  The same holds for `pos`: a
+ * repeated large (tiled) call that bins with the stored table
+ * (pbx_profile_spec_stats) keeps no copy of x, and the first later call that
+ * reads x (pbx_profile_get_selection with h_x, statistics or percentiles of
+ * x, pbx_profile_edges_equaln / assign on this selection) recomputes it from
+ * `pos`.  Host inputs (on_device = 0) are staged into the handle. */
 int pbx_profile_radial_equaln(void *handle, const double *pos, const double *mass, int64_t n,
                               int on_device, int use_sphere, const double *sphere,
                               const int64_t *fam, int nfam, int ndim, int64_t nbins, int has_min,

@@ -143,7 +143,10 @@ class DeviceBins:
         first later call that needs them (moments(), selection(w=True),
         weighted percentiles) and held by the handle from then on, so that
         array must stay alive and unchanged until that call or the next
-        selection on this handle (pbx.h, pbx_profile_radial_equaln).  Host
+        selection on this handle (pbx.h, pbx_profile_radial_equaln).  So must
+        ``pos``: a repeated large call that bins with the stored table keeps
+        no copy of x, and the first later reader of x (selection(x=True),
+        statistics of x, percentiles) recomputes it from ``pos``.  Host
         arrays are staged into the handle and carry no such contract."""
         if comm is None and not on_device and (
                 np.asarray(pos).dtype == np.float32 or
