@@ -321,9 +321,13 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
             lv = dev.level0_stats()
             if lv["tiled"]:
                 # the steps above reuse the previous call's level-0 digit
-                # geometry (same snapshot every call); a first call or a new
-                # snapshot re-reads x for its level-0 histogram: time that too
+                # geometry and, once two calls in a row had the same level-0
+                # digits, bin with the stored table inside the selection (same
+                # snapshot every call); a first call or a new snapshot re-reads
+                # x for its level-0 histogram and takes the assignment pass:
+                # time that too
                 row["level0_hinted_calls"] = lv
+                row["speculated_calls"] = dev.spec_stats()
                 dev.set_level0_hint(False)
                 ct, cd = [], []
                 for _ in range(max(20, steps // 10)):
@@ -338,7 +342,9 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                 row["cold_ms"] = float(np.median(ct)) * 1e3
                 row["cold_stream_ms"] = float(np.median(cd))
                 row["cold_note"] = ("level-0 geometry hint off (pbx_profile_set_level0_hint 0): "
-                                    "every call re-reads x, as a first call / new snapshot does")
+                                    "every call re-reads x for its level-0 histogram and runs the "
+                                    "assignment pass (no speculation), as a first call / new "
+                                    "snapshot does")
         out.append(row)
         if cpu and world == 1:
             from oracle import profile_ref as pr
@@ -660,10 +666,10 @@ def pmc_profile_step_bytes(n: int):
         try:
             d = json.loads(f.read_text())
             if int(d.get("n", 64_000_000)) == n:
-                return d.get("hbm_bytes_per_step")
+                return d.get("hbm_bytes_per_step"), str(f.relative_to(ROOT))
         except Exception:
             continue
-    return None
+    return None, None
 
 
 def pmc_traffic(which: str = "direct"):
@@ -892,14 +898,14 @@ def main():
         # counter-based: the PMC run's HBM bytes per step over this run's stream time
         counter = None
         for r in sweep:
-            b = pmc_profile_step_bytes(r["n_per_gpu"])
+            b, bsrc = pmc_profile_step_bytes(r["n_per_gpu"])
             if b:
                 gbs = b / (r["stream_ms"] * 1e-3) / 1e9
                 counter = {"n_per_gpu": r["n_per_gpu"], "hbm_bytes_per_step": b,
                            "achieved_gbs": gbs, "frac_of_spec": gbs / HBM_PEAK_GBS,
                            "frac_of_measured_copy_6290": gbs / 6290.0,
-                           "source": "profiles/pmc_profile_latest.json (2 x FETCH_SIZE + "
-                                     "WRITE_SIZE of every profile kernel) / this run's stream_ms"}
+                           "source": f"{bsrc} (2 x FETCH_SIZE + WRITE_SIZE of every profile "
+                                     "kernel, steady-state calls) / this run's stream_ms"}
         out["profile"] = {
             "metric": "particles/sec (RadialProfileBuilder equaln 128, Sphere&FamilyFilter, "
                       "weight=mass)",
@@ -917,7 +923,7 @@ def main():
                          "frac": big["hbm_gbs_algorithmic_per_gpu"] / HBM_PEAK_GBS,
                          "at_n_per_gpu": big["n_per_gpu"],
                          "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE,
-                         "traffic": pmc_profile_step_bytes(big["n_per_gpu"]),
+                         "traffic": pmc_profile_step_bytes(big["n_per_gpu"])[0],
                          "traffic_note": "HBM bytes per step at at_n_per_gpu (all profile "
                                          "kernels: 2 x FETCH_SIZE + WRITE_SIZE, PMC runs "
                                          "committed as profiles/pmc_profile_<N>M.json)"},
