@@ -1140,6 +1140,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   const int nb = SPEC ? sa.nb : 0;
   const int macc = SPEC ? sa.fs.nm * nb : 0;
   uint32_t mfl = 0;  // SPEC: per monomial q, factors x, x, w, w present (bits 4q ..)
+  int mmode = 0;     // SPEC: 1 = {Σw, Σx·w}, 2 = {Σw} (dedicated adds), else the factor loop
   if constexpr (SPEC) {
 #pragma unroll
     for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
@@ -1151,6 +1152,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
                          ((op == MO_WW) ? 8u : 0u);
       mfl |= f << (4 * q);
     }
+    mmode = (sa.fs.nm == 2 && mfl == 0x54u) ? 1 : (sa.fs.nm == 1 && mfl == 0x4u) ? 2 : 0;
   }
   const int nrs = (nb + 1) | 1;
   // the block's deferred list: 1 / SPEC_LIST of its slots (an overflow fails the speculation)
@@ -1201,11 +1203,101 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
     }
   };
   uint32_t run = 0;
+  // SPEC, speculating: the selection of a half (as sel below, without the x
+  // stores), then the bins of its kept keys — the table lookups of the
+  // half's four keys issued together, one LDS wait — then their bytes,
+  // per-tile counts, sums and deferred list entries
+  auto sel_spec = [&](uint32_t tile, int h, const Half &H) {
+    if constexpr (SPEC) {
+      const int64_t wj = (int64_t)tile * (TILE / 64) + w * SI + h * SH_HALF;
+      const uint32_t slot0 = tile * (uint32_t)TILE + (uint32_t)w * (TILE / SH_NW) + h * SH_HALF * 64 + lane;
+      double xk[SH_HALF];
+      uint64_t kk[SH_HALF];
+      uint32_t kb4 = 0, in4 = 0;  // kept / kept and in the hinted window, per key
+#pragma unroll
+      for (int k = 0; k < SH_HALF; ++k) {
+        double xv = 0.0;
+        const bool keep = ((H.in >> k) & 1u) && select_xyz(H.x[k], H.y[k], H.z[k], p, xv);
+        const uint64_t bal = __ballot(keep);
+        if (lane == 0) {
+          kw[wj + k] = bal;
+          kpre[wj + k] = (uint16_t)run;
+        }
+        run += (uint32_t)__popcll(bal);
+        xk[k] = xv;
+        kk[k] = dkey(xv);
+        kb4 |= (uint32_t)keep << k;
+        if (keep) {
+          kmin = kk[k] < kmin ? kk[k] : kmin;
+          kmax = kk[k] > kmax ? kk[k] : kmax;
+          if (kk[k] >= ka && kk[k] <= kb) {
+            if (kk[k] >= hlo && kk[k] <= hhi) {
+              const uint32_t d = (uint32_t)((kk[k] - hlo) >> hsh);
+              atomicAdd(&lh[d >> 1], 1u << (16 * (d & 1)));
+              in4 |= 1u << k;
+            } else {
+              oob = true;
+            }
+          }
+        }
+      }
+      uint32_t c8[SH_HALF];
+#pragma unroll
+      for (int k = 0; k < SH_HALF; ++k)
+        c8[k] = ((in4 >> k) & 1u) ? (uint32_t)sdt[(uint32_t)((kk[k] - hlo) >> hsh)] : (uint32_t)nb;
+      uint32_t *trow = tcs + ((tile - ta) % SH_TMAX) * nrs;
+#pragma unroll
+      for (int k = 0; k < SH_HALF; ++k) {
+        const bool keep = (kb4 >> k) & 1u;
+        const bool def = keep && c8[k] == SPEC_DEFER;
+        const uint32_t code = c8[k];
+        if (keep && !def) {  // (kept, outside the window: c8 = nb, the dropped bin)
+          sa.bins[slot0 + 64u * k] = (uint8_t)code;
+          atomicAdd(&trow[code], 1u);
+          if (code < (uint32_t)nb) {
+            if (mmode == 1) {  // Σw, Σx·w (mass / mean profiles)
+              atomicAdd(&sacc[code], H.m[k]);
+              atomicAdd(&sacc[nb + code], xk[k] * H.m[k]);
+            } else if (mmode == 2) {  // Σw
+              atomicAdd(&sacc[code], H.m[k]);
+            } else if (macc) {
+              // the dedicated monomials only (the host checks): (a1 a2)(b1 b2)
+              // with a = x or 1, b = w or 1 — mom_add's products (x * 1.0 is
+              // exact); monomial q's factors are bits 4q .. 4q + 3 of mfl
+#pragma unroll 1
+              for (int q = 0; q < sa.fs.nm; ++q) {
+                const uint32_t f = mfl >> (4 * q);
+                const double a = ((f & 1u) ? xk[k] : 1.0) * ((f & 2u) ? xk[k] : 1.0);
+                const double b = ((f & 4u) ? H.m[k] : 1.0) * ((f & 8u) ? H.m[k] : 1.0);
+                atomicAdd(&sacc[q * nb + code], a * b);
+              }
+            }
+          }
+        }
+        const uint64_t bd = __ballot(def);
+        if (bd) {  // rare: keys of edge-holding digits, into the block's list
+          uint32_t b0 = 0;
+          if (lane == 0) b0 = atomicAdd(&sdk, (uint32_t)__popcll(bd));
+          b0 = __shfl(b0, 0, 64);
+          if (def) {
+            const uint32_t idx = b0 + rank_below(bd);
+            // (the group: filled in by assign_gather from the key — a global
+            // table lookup here stalled almost every wave step)
+            if (idx < lcap) sa.rec[lbase + idx] = AgRec{kk[k] - hlo, H.m[k], slot0 + 64u * k, tile};
+          }
+        }
+      }
+    }
+  };
   auto sel = [&](uint32_t tile, int h, const Half &H) {
+    if constexpr (SPEC) {
+      if (spec) {
+        sel_spec(tile, h, H);
+        return;
+      }
+    }
     double *xt = xo + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW) + h * SH_HALF * 64;
     const int64_t wj = (int64_t)tile * (TILE / 64) + w * SI + h * SH_HALF;
-    const uint32_t slot0 = tile * (uint32_t)TILE + (uint32_t)w * (TILE / SH_NW) + h * SH_HALF * 64 + lane;
-    const double *mh = H.m;
 #pragma unroll
     for (int k = 0; k < SH_HALF; ++k) {
       double xv = 0.0;
@@ -1221,7 +1313,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       // stores once fused_hist0's timing was stable, see fused_hist0); as
       // streaming (nt) stores: select 280 -> 274 us and assign_gather's
       // re-read of x 202 -> 191 us at 64M (same box A/B/A/B)
-      if (!(SPEC && spec)) __builtin_nontemporal_store(xv, xt + k * 64 + lane);
+      __builtin_nontemporal_store(xv, xt + k * 64 + lane);
       if (keep) {
         const uint64_t kk = dkey(xv);
         kmin = kk < kmin ? kk : kmin;
@@ -1233,52 +1325,6 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
           } else {
             oob = true;
           }
-        }
-      }
-      if constexpr (SPEC) {
-        if (spec) {  // the table's bin (AgRec / bins8 conventions of assign_gather)
-        const int kq = k;
-        const uint64_t kk = dkey(xv);
-        uint32_t code = 0xffffu, dd = 0;
-        bool def = false;
-        if (keep) {
-          code = (uint32_t)nb;  // kept, outside the window: the dropped bin
-          if (kk >= ka && kk <= kb && kk >= hlo && kk <= hhi) {
-            dd = (uint32_t)((kk - hlo) >> hsh);
-            const uint32_t c8 = sdt[dd];
-            def = c8 == SPEC_DEFER;
-            code = def ? 0xffffu : c8;
-          }
-          if (!def) {
-            sa.bins[slot0 + 64u * k] = (uint8_t)code;
-            atomicAdd(&tcs[((tile - ta) % SH_TMAX) * nrs + code], 1u);
-          }
-        }
-        if (macc && code < (uint32_t)nb) {
-          // the dedicated monomials only (the host checks): (a1 a2)(b1 b2) with
-          // a = x or 1, b = w or 1 — the same products as mom_add's forms
-          // (x * 1.0 is exact); the factors of monomial q are bits 4q .. 4q + 3
-          // of mfl (one short loop, not mom_add's switch unrolled per key)
-#pragma unroll 1
-          for (int q = 0; q < sa.fs.nm; ++q) {
-            const uint32_t f = mfl >> (4 * q);
-            const double a = ((f & 1u) ? xv : 1.0) * ((f & 2u) ? xv : 1.0);
-            const double b = ((f & 4u) ? mh[kq] : 1.0) * ((f & 8u) ? mh[kq] : 1.0);
-            atomicAdd(&sacc[q * nb + code], a * b);
-          }
-        }
-        const uint64_t bd = __ballot(def);
-        if (bd) {  // rare: keys of edge-holding digits, into the block's list
-          uint32_t b0 = 0;
-          if (lane == 0) b0 = atomicAdd(&sdk, (uint32_t)__popcll(bd));
-          b0 = __shfl(b0, 0, 64);
-          if (def) {
-            const uint32_t idx = b0 + rank_below(bd);
-            // (the group: filled in by assign_gather from the digit — a
-            // global table lookup here stalled almost every wave step)
-            if (idx < lcap) sa.rec[lbase + idx] = AgRec{kk - hlo, mh[kq], slot0 + 64u * k, tile};
-          }
-        }
         }
       }
     }
