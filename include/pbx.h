@@ -431,12 +431,16 @@ int pbx_profile_mono_stats(void *handle, int64_t *out);
  * geometry (every window key inside it), so x was not read a second time}. */
 int pbx_profile_level0_stats(void *handle, int64_t *out);
 /* Telemetry of the speculative assignment of the tiled calls (no reference
- * counterpart): out[2] = {calls whose selection kernel also binned every key
+ * counterpart): out[3] = {calls whose selection kernel also binned every key
  * with the bin table stored by an earlier call (launched when the previous
  * tiled call's level-0 digits of every rank matched that table), of those the
  * calls whose own digits matched it too, so the assignment pass (a second
- * read of x and the masses) was skipped}.  A miss re-runs the assignment;
- * results are identical either way.  PBX_SPEC=0 disables the speculation. */
+ * read of x and the masses) was skipped, and of those the calls that also
+ * binned the keys of edge-holding digits with the previous call's edges
+ * (launched when the last two calls' edges were identical) and found every
+ * edge at its rank: no deferred keys and no order-statistic finish}.  A
+ * miss re-runs the assignment; results are identical either way.
+ * PBX_SPEC=0 disables the speculation. */
 int pbx_profile_spec_stats(void *handle, int64_t *out);
 /* enabled = 0: this handle's tiled calls never use the previous call's
  * level-0 digit geometry (every call re-reads x for its level-0 histogram:

@@ -846,7 +846,7 @@ struct FusedCtl {
   int32_t spec;    // SPEC_MATCH: this call's level-0 ranks equal the stored bin table's;
                    // SPEC_HIT: select_tiles binned with that table (no assignment pass)
 };
-constexpr int32_t SPEC_MATCH = 1, SPEC_HIT = 2, SPEC_NOX = 4;
+constexpr int32_t SPEC_MATCH = 1, SPEC_HIT = 2, SPEC_NOX = 4, SPEC_EDGE = 8;
 
 // Level-0 digit geometry of a handle's previous tiled call (select_tiles
 // counts this call's keys with it while they are still in registers; the
@@ -911,6 +911,22 @@ __device__ __forceinline__ void mom_add(double *aq, int op, int col, int fq, int
 #undef PBX_MOM_LOOP
 }
 
+// bin_of(v, e, nb) for a v whose lower bound lies in [qa, qb]
+__device__ __forceinline__ uint32_t bin_of_in(double v, const double *e, int nb, int qa, int qb) {
+  if (v != v) return bin_of(v, e, nb);  // rare: the first NaN edge
+  int l = qa, h = qb;  // first k in [qa, qb) with !(e[k] < v), qb if none
+  while (l < h) {
+    const int m = (l + h) >> 1;
+    if (e[m] < v) l = m + 1;
+    else h = m;
+  }
+  const int lo = l;
+  int b = lo - 1;
+  if (v == e[0]) b = 0;
+  if (v == e[nb]) b = nb - 1;
+  return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
+}
+
 // Speculative assignment (tiled one-rank calls).  The bin of a key whose
 // level-0 digit holds no edge depends only on the digit: bin = #{ranks q
 // with digit_q < digit} - 1 (assign_gather's table).  So when this call's
@@ -930,6 +946,14 @@ struct SpecTab {
   int32_t nb, nq, ng, valid;
   uint32_t qd[MS_MAXQ];    // level-0 digit of each rank q
   uint8_t bin[MS0_DIG];    // digit -> bin (nb: outside the edges); SPEC_DEFER: the digit holds edges
+  // the edges of the last call with these digits (fix_deferred) and the
+  // groups (gdig: assign_gather, gq: fix_deferred), for the edge speculation
+  uint32_t gdig[MS_MAXQ];  // the edge-holding digits, ascending
+  uint32_t gq[MS_MAXQ + 1];  // group g's ranks gq[g] .. gq[g + 1]
+  double edges[MS_MAXQ];
+  int32_t edges_valid;
+  int32_t enc;  // 1 (nb <= 128): an edge-holding digit's byte is 128 + its group (255: group
+                // >= 127, found by search); 0: SPEC_DEFER for all of them
 };
 constexpr uint8_t SPEC_DEFER = 0xff;
 constexpr int SPEC_MAXB = 254;   // bins (and groups <= nq = nb + 1 < 256) a byte table holds
@@ -945,9 +969,12 @@ struct SpecArgs {
   uint32_t *rbase, *rn;    // per select block: list start, length
   uint32_t *flag;          // bit 0: a block could not bin (table / hint geometry differ, a
                            // list overflowed): the call takes the assignment pass;
-                           // bit 1: the blocks binned and stored no x (SPEC_NOX)
+                           // bit 1: the blocks binned and stored no x (SPEC_NOX);
+                           // bit 2: edge speculation (every key binned with the table's edges)
+  uint32_t *lteq;          // edge speculation: per rank q, window keys of its digit < / == edge q
   FusedStats fs;
   int nb;
+  int edge;                // 1: the edge speculation (the host saw the last call's edges repeat)
 };
 
 // select_tiles blocks per assign_gather block (tile sub-ranges): 3 x 255
@@ -1113,7 +1140,13 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   // per-(tile, bin) counts of the current SH_TMAX tiles (flushed with the u16 rows)
   __shared__ uint32_t tcs[SPEC ? SH_TMAX * ((SPEC_MAXB + 1) | 1) : 1];
   __shared__ uint32_t sdk;                         // deferred keys listed
-  __shared__ int s_spec;
+  __shared__ int s_spec, s_edge, s_enc;
+  // edge speculation: the table's edges (and their keys), groups, and per
+  // rank the window keys of its digit below / equal to its edge
+  __shared__ double sedg[SPEC ? SPEC_MAXB + 1 : 1];
+  __shared__ uint64_t sek[SPEC ? SPEC_MAXB + 1 : 1];
+  __shared__ uint32_t sgq[SPEC ? SPEC_MAXB + 2 : 1], sgd[SPEC ? SPEC_MAXB + 1 : 1];
+  __shared__ uint32_t slt[SPEC ? 2 * (SPEC_MAXB + 1) : 1];
   if (threadIdx.x == 0) {
     SelHint t{};
     if (hint) t = *hint;
@@ -1122,6 +1155,8 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       const SpecTab *tb = sa.tab;
       s_spec = tb->valid && t.valid && tb->lo == t.lo && tb->s0 == t.s && tb->w0 == t.w &&
                tb->nb == sa.nb;
+      s_edge = s_spec && sa.edge && tb->edges_valid;
+      s_enc = tb->enc;
       sdk = 0;
     }
   }
@@ -1160,7 +1195,20 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   const uint32_t lcap = (uint32_t)((uint64_t)(tb - ta) * TILE / SPEC_LIST);
   if (SPEC) {
     if (spec) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(sa.flag, 2u);  // no x stored (SPEC_NOX)
+      if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(sa.flag, s_edge ? 6u : 2u);  // NOX, EDGE
+      if (s_edge) {
+        const int nq = nb + 1, ng = sa.tab->ng;
+        for (int q = threadIdx.x; q < nq; q += SH_BT) {
+          const double e = sa.tab->edges[q];
+          sedg[q] = e;
+          sek[q] = dkey(e);
+          slt[2 * q] = slt[2 * q + 1] = 0;
+        }
+        for (int g = threadIdx.x; g <= ng; g += SH_BT) {
+          sgq[g] = sa.tab->gq[g];
+          if (g < ng) sgd[g] = sa.tab->gdig[g];
+        }
+      }
       const uint4 *src = (const uint4 *)sa.tab->bin;
       for (int i = threadIdx.x; i < MS0_DIG / 16; i += SH_BT) ((uint4 *)sdt)[i] = src[i];
       for (int i = threadIdx.x; i < macc; i += SH_BT) sacc[i] = 0.0;
@@ -1246,11 +1294,37 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       for (int k = 0; k < SH_HALF; ++k)
         c8[k] = ((in4 >> k) & 1u) ? (uint32_t)sdt[(uint32_t)((kk[k] - hlo) >> hsh)] : (uint32_t)nb;
       uint32_t *trow = tcs + ((tile - ta) % SH_TMAX) * nrs;
+      const bool edge = s_edge != 0;
+      const uint32_t gmin = s_enc ? 128u : (uint32_t)SPEC_DEFER;  // bytes >= gmin: edge-holding digit
 #pragma unroll
       for (int k = 0; k < SH_HALF; ++k) {
         const bool keep = (kb4 >> k) & 1u;
-        const bool def = keep && c8[k] == SPEC_DEFER;
-        const uint32_t code = c8[k];
+        uint32_t code = c8[k];
+        if (((in4 >> k) & 1u) && code >= gmin) code = SPEC_DEFER;  // (out of the window: nb)
+        if (edge && keep && code == SPEC_DEFER) {
+          // an edge-holding digit: the bin among its group's edges (the
+          // table's), and per edge the keys below / equal to it (the
+          // edges are checked against this call's ranks by fused_resolve)
+          int g;
+          if (c8[k] != SPEC_DEFER) {
+            g = (int)c8[k] - 128;  // (the byte carries the group)
+          } else {  // search the group by its digit
+            const uint32_t dd = (uint32_t)((kk[k] - hlo) >> hsh);
+            int lo = 0, hi = sa.tab->ng - 1;
+            while (lo < hi) {
+              const int mid = (lo + hi) >> 1;
+              if (sgd[mid] < dd) lo = mid + 1; else hi = mid;
+            }
+            g = lo;
+          }
+          const int qa = (int)sgq[g], qb = (int)sgq[g + 1];
+          code = bin_of_in(xk[k], sedg, nb, qa, qb);
+          for (int q = qa; q < qb; ++q) {
+            if (kk[k] < sek[q]) atomicAdd(&slt[2 * q], 1u);
+            else if (kk[k] == sek[q]) atomicAdd(&slt[2 * q + 1], 1u);
+          }
+        }
+        const bool def = keep && code == SPEC_DEFER;
         if (keep && !def) {  // (kept, outside the window: c8 = nb, the dropped bin)
           sa.bins[slot0 + 64u * k] = (uint8_t)code;
           atomicAdd(&trow[code], 1u);
@@ -1388,6 +1462,9 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   __syncthreads();
   if (SPEC && spec) {  // the block's sums row and list, its last tiles' counts
     if (tb > ta) flush_tc(ta + ((tb - ta - 1) / SH_TMAX) * SH_TMAX, tb);
+    if (s_edge)
+      for (int i = threadIdx.x; i < 2 * (nb + 1); i += SH_BT)
+        if (slt[i]) atomicAdd(&sa.lteq[i], slt[i]);
     for (int i = threadIdx.x; i < macc; i += SH_BT) sa.slab[(int64_t)blockIdx.x * macc + i] = sacc[i];
     if (threadIdx.x == 0) {
       const uint32_t c = sdk;
@@ -1693,14 +1770,15 @@ __global__ void __launch_bounds__(FR_TPB)
                   uint32_t *__restrict__ gq, const uint32_t *__restrict__ rows, int g0,
                   uint32_t *__restrict__ boff, uint32_t *__restrict__ bcnt,
                   uint32_t *__restrict__ lc, const uint32_t *__restrict__ rows16, uint32_t rsub,
-                  const SpecTab *__restrict__ tab, uint32_t *__restrict__ sflag, int nb) {
+                  const SpecTab *__restrict__ tab, uint32_t *__restrict__ sflag, int nb,
+                  uint32_t *__restrict__ lteq) {
   constexpr int PT = MS0_DIG / FR_TPB;
   __shared__ uint32_t incl[MS0_DIG];
   __shared__ uint32_t wsum[FR_TPB / 64];
   __shared__ uint32_t qdig[MS_MAXQ];
   __shared__ uint32_t gstart[MS_MAXQ + 1];
   __shared__ uint32_t gd[MS_MAXQ], go[MS_MAXQ + 1];
-  __shared__ int sng, s_err, s_w0, s_hint, s_spec;
+  __shared__ int sng, s_err, s_w0, s_hint, s_spec, s_eok;
   const int tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const int wv = tid >> 6;
@@ -1715,6 +1793,7 @@ __global__ void __launch_bounds__(FR_TPB)
     if (pub && tab && tab->valid && !(s_err & 2) && tab->nb == nb && tab->nq == nq &&
         tab->lo == ctl->lo && tab->s0 == ctl->s0 && tab->w0 == s_w0)
       s_spec = 1;
+    s_eok = 1;  // (edge speculation: every edge at its rank, below)
   }
   for (int k = tid; k < MS0_DIG; k += FR_TPB) incl[k] = H[k];  // coalesced, via LDS
   __syncthreads();
@@ -1758,13 +1837,24 @@ __global__ void __launch_bounds__(FR_TPB)
     }
     qdig[q] = (uint32_t)a;
     if (pub && s_spec && tab->qd[q] != (uint32_t)a) s_spec = 0;  // (benign race: all write 0)
+    if (pub && lteq) {  // the table's edge q is this call's iff rank r is among its equals
+      const int64_t rr = r - (a ? (int64_t)incl[a - 1] : 0);
+      const uint32_t lt = lteq[2 * q], eq = lteq[2 * q + 1];
+      if (!((int64_t)lt <= rr && rr < (int64_t)lt + (int64_t)eq)) s_eok = 0;
+    }
   }
   __syncthreads();
+  if (pub && lteq)  // read: zeroed for the next edge-speculating call
+    for (int i = tid; i < 2 * nq; i += FR_TPB) lteq[i] = 0u;
   if (pub && tid == 0) {
     const int m = s_spec ? SPEC_MATCH : 0;
-    // a hit: select_tiles binned every key with the table (no block gave up)
+    // a hit: select_tiles binned every key with the table (no block gave up);
+    // an edge-speculating call (it listed no deferred keys) only when its
+    // edges hold too — otherwise the assignment runs
     const uint32_t f = sflag ? *sflag : 0u;
-    ctl->spec = m | ((m && sflag && !(f & 1u)) ? SPEC_HIT : 0) | ((f & 2u) ? SPEC_NOX : 0);
+    const bool hit = m && sflag && !(f & 1u) && (!(f & 4u) || s_eok);
+    ctl->spec = m | (hit ? SPEC_HIT : 0) | ((f & 2u) ? SPEC_NOX : 0) |
+                ((hit && (f & 4u)) ? SPEC_EDGE : 0);
     if (sflag) *sflag = 0u;  // (for the next speculating call)
   }
   // groups: run starts of the (non-decreasing) digits; one wave numbers them
@@ -2075,7 +2165,8 @@ __device__ void finish_group(const uint64_t *__restrict__ keys, int64_t S, uint6
 __global__ void __launch_bounds__(FR_TPB)
     fused_finish(const FusedCtl *__restrict__ ctl, const MsRank *__restrict__ R,
                  const uint32_t *__restrict__ gq, const uint32_t *__restrict__ goff,
-                 const uint64_t *__restrict__ seg, double *__restrict__ edges) {
+                 const uint64_t *__restrict__ seg, double *__restrict__ edges,
+                 const SpecTab *__restrict__ tab, int nq) {
   __shared__ __attribute__((aligned(16))) uint64_t sk[FS_LDS];
   __shared__ __attribute__((aligned(16))) uint32_t hist[FS_DIG];  // (u64 candidates, finish_group)
   __shared__ uint32_t wsum[FR_TPB / 64];
@@ -2086,14 +2177,21 @@ __global__ void __launch_bounds__(FR_TPB)
   __shared__ uint64_t c_lo;  // the control record's fields and the group's
   __shared__ int c_s, c_run; // segment: one load per block, through LDS
   __shared__ uint32_t c_o0, c_o1;
+  __shared__ int c_edge;
   if (tid == 0) {
-    c_run = !(ctl->err & 2) && g < ctl->ng;
+    c_edge = (ctl->spec & SPEC_EDGE) ? 1 : 0;
+    c_run = !(ctl->err & 2) && g < ctl->ng && !c_edge;
     c_lo = ctl->lo;
     c_s = ctl->s0;
     c_o0 = c_run ? goff[g] : 0u;
     c_o1 = c_run ? goff[g + 1] : 0u;
   }
   __syncthreads();
+  if (c_edge) {  // the edge speculation held: the table's edges are this call's
+    if (g == 0)
+      for (int q = tid; q < nq; q += FR_TPB) edges[q] = tab->edges[q];
+    return;
+  }
   if (!c_run) return;
   const uint64_t base = c_lo;
   const int s = c_s;
@@ -2691,12 +2789,26 @@ __global__ void __launch_bounds__(MS0_TPB)
   if (blockIdx.x == 0 && sio.tab) {  // (block 0 has no tiles) the table for the next call
     SpecTab *T = sio.tab;
     const bool ok = win && nb <= SPEC_MAXB && ng < 256;
+    // nb <= 128: a window key's digit outside the edges' digits cannot occur
+    // (the lowest / highest window keys ARE the first / last edge), so the
+    // bytes 128 .. 254 carry the groups 0 .. 126 of edge-holding digits
+    const int enc = nb <= 128 ? 1 : 0;
     for (int d = tid; d < MS0_DIG; d += MS0_TPB) {
       const uint32_t e = dtab[d];
-      T->bin[d] = (e & 0x8000u) ? SPEC_DEFER : (uint8_t)e;
+      uint8_t c;
+      if (e & 0x8000u) {
+        const uint32_t g = e & 0x7fffu;
+        c = enc ? (g < 127 ? (uint8_t)(128 + g) : SPEC_DEFER) : SPEC_DEFER;
+      } else {
+        c = enc ? (uint8_t)(e < 128 ? e : 0) : (uint8_t)e;
+      }
+      T->bin[d] = c;
     }
+    if (tid == 0) T->enc = enc;
     for (int q = tid; q < nq; q += MS0_TPB) T->qd[q] = qd[q];
+    for (int g = tid; g < ng; g += MS0_TPB) T->gdig[g] = gdig[g];
     if (tid == 0) {
+      T->edges_valid = 0;  // (fix_deferred stores this call's edges)
       T->lo = lo;
       T->s0 = s;
       T->w0 = c_w0;
@@ -2853,22 +2965,6 @@ __global__ void __launch_bounds__(MS0_TPB)
 constexpr int FD_U = 4;          // keys per thread in flight
 constexpr int FD_LDSW = 28672;   // LDS words for the block's [tile][bin] counts (112 KB)
 
-// bin_of(v, e, nb) for a v whose lower bound lies in [qa, qb]
-__device__ __forceinline__ uint32_t bin_of_in(double v, const double *e, int nb, int qa, int qb) {
-  if (v != v) return bin_of(v, e, nb);  // rare: the first NaN edge
-  int l = qa, h = qb;  // first k in [qa, qb) with !(e[k] < v), qb if none
-  while (l < h) {
-    const int m = (l + h) >> 1;
-    if (e[m] < v) l = m + 1;
-    else h = m;
-  }
-  const int lo = l;
-  int b = lo - 1;
-  if (v == e[0]) b = 0;
-  if (v == e[nb]) b = nb - 1;
-  return (b < 0 || b >= nb) ? (uint32_t)nb : (uint32_t)b;
-}
-
 template <bool MOM>
 __global__ void __launch_bounds__(MS0_TPB)
     fix_deferred(const FusedCtl *__restrict__ ctl, const AgRec *__restrict__ rec,
@@ -2888,19 +2984,37 @@ __global__ void __launch_bounds__(MS0_TPB)
   tile_range(nt, ta, tb);
   const uint32_t wt = (uint32_t)(FD_LDSW / nrs);  // tiles per window
   __shared__ uint64_t c_lo;  // the control record's fields, one load per block
-  __shared__ int c_ng, c_hit;  // (c_ng -1: no window)
+  __shared__ int c_ng, c_hit, c_edge;  // (c_ng -1: no window)
   if (tid == 0) {
     const bool ok = !(ctl->err & 2);
     c_ng = ok ? ctl->ng : -1;
     c_lo = ctl->lo;
     c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
+    c_edge = (ctl->spec & SPEC_EDGE) ? 1 : 0;
   }
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
   for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
   __syncthreads();
   const bool ok_all = c_ng >= 0;
+  const bool c_hit_edge = c_edge != 0;
   for (int k = tid; k <= c_ng; k += MS0_TPB) gql[k] = gq[k];
   const uint64_t lo = c_lo;
+  if (blockIdx.x == 0 && sio.tab && ok_all && !c_hit_edge) {
+    // the table now holds this call's digits: its edges and groups with it
+    // (the next call's edge speculation)
+    SpecTab *T = sio.tab;
+    __shared__ int s_fin;
+    if (tid == 0) s_fin = 1;
+    __syncthreads();
+    for (int q = tid; q <= nb; q += MS0_TPB) {
+      const double v = edges[q];
+      T->edges[q] = v;
+      if (!(v - v == 0.0)) s_fin = 0;  // (NaN / inf edges: no edge speculation)
+    }
+    for (int k = tid; k <= c_ng; k += MS0_TPB) T->gq[k] = gq[k];
+    __syncthreads();
+    if (tid == 0) T->edges_valid = s_fin;
+  }
   // this block's deferred keys: assign_gather's list of the block, or on a
   // speculation hit the lists of its SH_K select blocks (keys of its own tiles)
   const bool hit = c_hit != 0;
@@ -4237,6 +4351,10 @@ struct Profile {
   // lists, their [start, length] per select block, per-block sums
   Buf stab, srec, sspec, sslab, sflag;
   bool spec_next = false;  // the last tiled call's ranks matched the table: speculate
+  bool edge_next = false;  // ... and its edges were the call's before it: speculate on edges too
+  std::vector<double> last_edges;  // the last tiled call's edges
+  Buf slteq;               // edge speculation: per rank, keys below / equal to its edge
+  int64_t n_edge_hit = 0;
   bool x_missing = false;  // the last selection stored no x (a speculation hit): ensure_x rebuilds it
   XSrc xsrc{};             // ... from these positions / parameters
   Buf posst;               // lazy selections of host arrays: the staged positions (kept for xsrc)
@@ -5232,6 +5350,7 @@ int pbx_profile_spec_stats(void *handle, int64_t *out) {
     if (!out) fail(PBX_ERR_VALUE, "null output");
     out[0] = P.n_spec;
     out[1] = P.n_spec_hit;
+    out[2] = P.n_edge_hit;
   });
 }
 
@@ -5842,6 +5961,12 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         thist.sa.tab = (const SpecTab *)P.stab.p;
         thist.sa.fs = fs;
         thist.sa.nb = (int)nb;
+        thist.sa.edge = P.edge_next ? 1 : 0;
+        if (thist.sa.edge && !P.slteq.p) {  // (zero before the first use; fused_resolve re-zeroes)
+          P.slteq.get(sizeof(uint32_t) * 2 * MS_MAXQ);
+          PBX_HIP(hipMemsetAsync(P.slteq.p, 0, sizeof(uint32_t) * 2 * MS_MAXQ, st));
+        }
+        thist.sa.lteq = (uint32_t *)P.slteq.p;
       }
       const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
                                         nfam, ndim, lazy, 0, 0, /*tiled=*/true, &thist);
@@ -5911,7 +6036,8 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
                          nbins, nq, R, gdig, goff, gq, (const uint32_t *)rows, g0, boff, bcnt,
                          dist ? lc_all + (size_t)cr.rank * MS_MAXQ : nullptr,
                          (const uint32_t *)P.srows.p, P.sel_rsub, (const SpecTab *)stab,
-                         thist.spec ? thist.sa.flag : nullptr, (int)nb);
+                         thist.spec ? thist.sa.flag : nullptr, (int)nb,
+                         (thist.spec && thist.sa.edge) ? thist.sa.lteq : nullptr);
       int64_t seg_total = 0;  // dist: keys in all ranks' group segments
       if (dist) {
         comm_allreduce(comm, lc_all, lc_all, (int64_t)cr.nranks * MS_MAXQ, 3, 0, st, lk);
@@ -5985,7 +6111,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         comm_allreduce(comm, seg, seg, seg_total, 2, 0, st, lk);
       hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
                          (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
-                         (const uint64_t *)seg, de);
+                         (const uint64_t *)seg, de, (const SpecTab *)stab, nq);
       PBX_HIP(hipGetLastError());
       // assignment (+ the statistics' distinct sums) with the device edges
       if (agath) {
@@ -6183,7 +6309,14 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       ++P.n_tiled_calls;
       if (c.hint) ++P.n_hinted;
       if (c.spec & SPEC_HIT) ++P.n_spec_hit;
+      if (c.spec & SPEC_EDGE) ++P.n_edge_hit;
       P.spec_next = !dist && (c.spec & SPEC_MATCH);
+      // edge speculation next: this call's digits matched and its edges are
+      // the previous call's, bit for bit
+      const bool same = (int64_t)P.last_edges.size() == nq &&
+                        std::memcmp(P.last_edges.data(), he, sizeof(double) * nq) == 0;
+      P.edge_next = P.spec_next && same;
+      P.last_edges.assign(he, he + nq);
       // a hit stored no x (ensure_x rebuilds it on demand); a miss rebuilt it
       P.x_missing = (c.spec & SPEC_NOX) && (c.spec & SPEC_HIT);
     }

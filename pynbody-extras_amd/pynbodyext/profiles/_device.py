@@ -257,11 +257,12 @@ class DeviceBins:
 
     def spec_stats(self) -> dict:
         """Tiled radial_equaln calls whose selection kernel also binned the
-        keys with the stored bin table, and of them the hits (the assignment
-        pass skipped; pbx_profile_spec_stats)."""
-        out = np.zeros(2, dtype=np.int64)
+        keys with the stored bin table, of them the hits (the assignment
+        pass skipped), and of those the edge hits (the previous call's edges
+        held: no deferred keys, no finish; pbx_profile_spec_stats)."""
+        out = np.zeros(3, dtype=np.int64)
         nat.call("pbx_profile_spec_stats", self._h, _i64(out))
-        return {"speculated": int(out[0]), "hits": int(out[1])}
+        return {"speculated": int(out[0]), "hits": int(out[1]), "edge_hits": int(out[2])}
 
     def set_level0_hint(self, enabled: bool) -> None:
         """False: every tiled radial_equaln call on this handle re-reads x for

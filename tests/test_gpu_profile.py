@@ -866,7 +866,7 @@ def test_radial_equaln_speculative_assignment(gpu):
         for u, v in zip(m, m0):
             np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300, err_msg=str(kw))
         st = h.spec_stats()
-        return st["speculated"], st["hits"]
+        return st["speculated"], st["hits"], st["edge_hits"]
 
     def x_consumers():
         # a hit stores no x: the next consumer of x rebuilds it from the positions
@@ -878,23 +878,30 @@ def test_radial_equaln_speculative_assignment(gpu):
     try:
         got = [call(pos, {}) for _ in range(5)]
         # calls 0, 1: no table / the table in call 0's unhinted geometry; call
-        # 2 matches (no speculation yet); calls 3, 4 speculate and hit
-        assert got == [(0, 0), (0, 0), (0, 0), (1, 1), (2, 2)], got
+        # 2 matches (no speculation yet; its edges repeat call 1's); calls 3, 4
+        # speculate on the digits and the edges, and hit on both
+        assert got == [(0, 0, 0), (0, 0, 0), (0, 0, 0), (1, 1, 1), (2, 2, 2)], got
         x_consumers()
-        assert call(pos * (1.0 + 1e-12), {}) == (3, 3)
-        assert call(pos[rng.permutation(n)], {}) == (4, 4)
+        # the same digits, other edges: the edge speculation misses (the
+        # assignment runs, x rebuilt from the positions) ...
+        assert call(pos * (1.0 + 1e-12), {}) == (3, 2, 2)
+        x_consumers()
+        # ... and the next call speculates on the digits only: a reshuffled
+        # snapshot (same radii, every particle elsewhere) hits
+        assert call(pos[rng.permutation(n)], {}) == (4, 3, 2)
         for kw in (win, {"nbins": 64}, fam):
-            s0, h0 = h.spec_stats().values()
+            s0, h0, e0 = h.spec_stats().values()
             got = [call(pos, kw) for _ in range(5)]
-            assert got[0] == (s0 + 1, h0), (kw, got)  # speculated with the old table: a miss
-            assert got[-1][1] - got[-2][1] == 1, (kw, got)  # repeated: hits again
+            assert got[0] == (s0 + 1, h0, e0), (kw, got)  # speculated with the old table: a miss
+            assert got[-1][1] - got[-2][1] == 1, (kw, got)  # repeated: hits again ...
+            assert got[-1][2] - got[-2][2] == 1, (kw, got)  # ... on the edges too
             x_consumers()
         # speculating, and the keys escape the level-0 hint: fused_hist0
         # rebuilds x from the positions before it counts
-        s0, h0 = h.spec_stats().values()
-        assert call(pos * 2.0, {}) == (s0 + 1, h0)
+        s0, h0, e0 = h.spec_stats().values()
+        assert call(pos * 2.0, {}) == (s0 + 1, h0, e0)
         x_consumers()
-        assert ref.spec_stats() == {"speculated": 0, "hits": 0}
+        assert ref.spec_stats() == {"speculated": 0, "hits": 0, "edge_hits": 0}
     finally:
         h.close()
         ref.close()
