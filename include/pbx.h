@@ -418,11 +418,15 @@ int pbx_profile_radial_equaln_comm(void *comm, void *handle, const double *pos, 
  * multi-kernel path (a silent ~2x slowdown if non-zero), calls that took
  * the multi-kernel path}. */
 int pbx_profile_path_stats(void *handle, int64_t *out);
-/* Telemetry of the one-launch calls (no reference counterpart): out[2] =
+/* Telemetry of the one-launch calls (no reference counterpart): out[3] =
  * {one-launch calls, of those the calls whose level-0 digit histogram was
  * counted during the selection with the previous one-launch call's geometry
  * (every window key inside it: one grid barrier and the second count
- * skipped; the edges are the same either way)}. */
+ * skipped; the edges are the same either way), and the calls that found the
+ * previous call's edges at their ranks (tried when the last two calls' edges
+ * were identical: each edge's keys below / equal counted during the
+ * selection; a hit skips the order-statistic phases and their barriers)}.
+ * PBX_MONO_EDGE=0 disables the edge speculation. */
 int pbx_profile_mono_stats(void *handle, int64_t *out);
 /* Telemetry of the tiled (>= 1024 selection tiles) multi-kernel calls of
  * pbx_profile_radial_equaln on this handle (no reference counterpart):

@@ -3426,7 +3426,14 @@ struct MonoArgs {
   double *pack;     // [ctl][edges nq][counts nb][sums nm x nb][tag] (mapped host memory)
   double *stage;    // the same in device memory (sc1 stores; pack_complete copies it out)
   uint64_t *bar;
-  uint64_t gen0;         // generations gen0 + 1 .. gen0 + 5; tag of this call
+  uint64_t gen0;         // barrier generations gen0 + 1, + 2, ... (the call reports how many
+                         // it used: FusedCtl::spec >> 8); tag of this call
+  // edge speculation: the previous call's edges (rewritten by every call) and
+  // per edge the window keys below (by upper bound) / equal, summed over the
+  // blocks (zero on entry and exit); eg: speculate (the host saw them repeat)
+  double *pedges;
+  uint32_t *eU, *eE;
+  int eg;
   uint64_t done_target;  // the completion counter's value once every block is done
   uint64_t *trace;       // PBX_MONO_TRACE diagnostic: 8 wall-clock stamps per block, or null
 };
@@ -3467,13 +3474,24 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   const uint32_t lane = lane_id();
   const int nb = a.nb, nq = a.nq;
   __shared__ SelHint s_hint;
-  __shared__ int s_hinted;
+  __shared__ int s_hinted, s_edge;
+  __shared__ uint64_t ek_l[RADIX];             // edge speculation: the previous edges' keys,
+  __shared__ uint32_t eUl[RADIX + 1], eEl[RADIX];  // this block's keys by upper bound / equal
   if (tid == 0) {
     s_ok = 1;
     SelHint h{};
     if (a.hin) h = *a.hin;  // (one load per block)
     s_hint = h;
+    s_edge = 0;
   }
+  if (a.eg)
+    for (int i = tid; i <= nq; i += MONO_BT) {
+      if (i < nq) {
+        ek_l[i] = dkey(a.pedges[i]);
+        eEl[i] = 0;
+      }
+      eUl[i] = 0;
+    }
   for (int i = tid; i < MONO_DIG; i += MONO_BT) L0[i] = 0;
   if (t == 0)  // zeroed here, used after barrier 1
     for (int i = tid; i < RADIX; i += MONO_BT) st_sc1(&a.gcnt[i], 0u);
@@ -3485,7 +3503,9 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   // the lowest window key and any width covering the highest: same groups,
   // same edges) and phase 2's count and barrier are skipped
   const SelHint hint = s_hint;
-  const bool hv = hint.valid != 0;
+  // (an edge-speculating call counts no hinted level 0: a hit needs none, a
+  // miss counts this call's own in phase 2)
+  const bool hv = hint.valid != 0 && !a.eg;
   const int hb = hint.s + hint.w;
   const uint64_t hspan = hb >= 64 ? ~0ull : ((1ull << hb) - 1);
   const uint64_t hhi = hint.lo + hspan < hint.lo ? ~0ull : hint.lo + hspan;
@@ -3522,6 +3542,15 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
           if (kk >= hint.lo && kk <= hhi) atomicAdd(&L0[(uint32_t)((kk - hint.lo) >> hint.s)], 1u);
           else esc = true;
         }
+        if (a.eg && kk >= a.ka && kk <= a.kb) {  // edge speculation: upper bound among the edges
+          int lo = 0, hi = nq;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (ek_l[mid] <= kk) lo = mid + 1; else hi = mid;
+          }
+          atomicAdd(&eUl[lo], 1u);
+          if (lo > 0 && ek_l[lo - 1] == kk) atomicAdd(&eEl[lo - 1], 1u);
+        }
       }
     }
     if (__ballot(esc) && lane == 0) st_sc1(a.bar + BAR_LINE * 11, a.gen0 + 1);
@@ -3554,6 +3583,11 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       const uint32_t v = L0[i];
       if (v) atomicAdd(&a.H[i], v);
     }
+  if (a.eg)  // ... and the edge counts
+    for (int i = tid; i <= nq; i += MONO_BT) {
+      if (eUl[i]) atomicAdd(&a.eU[i], eUl[i]);
+      if (i < nq && eEl[i]) atomicAdd(&a.eE[i], eEl[i]);
+    }
   if (tid == 0) {
     MonoRec r{0, ~0ull, 0ull, 0};
     for (int k = 0; k < MONO_NW; ++k) {
@@ -3565,8 +3599,43 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     st_sc1(&a.rec[t].kmin, r.kmin);
     st_sc1(&a.rec[t].kmax, r.kmax);
   }
-  if (!grid_sync(a.bar, a.gen0 + 1, nt, &s_ok)) return;
+  uint64_t gn = a.gen0 + 1;  // the barrier generation (sequential: skipped barriers take none)
+  if (!grid_sync(a.bar, gn, nt, &s_ok)) return;
   MONO_STAMP(1);
+  int64_t m_edge = 0;
+  if (a.eg) {
+    // the previous edges are this call's iff every rank r_q lies among the
+    // keys equal to edge q: #keys < e_q <= r_q < #keys <= e_q (#keys < e_q =
+    // the keys whose upper bound is <= q; equal ones counted at the last of
+    // equal edges); every block decides the same from the same sums
+    uint32_t u = 0;
+    if (tid <= nq) u = ld_sc1(&a.eU[tid]);
+    if (tid < nq) eEl[tid] = ld_sc1(&a.eE[tid]);
+    uint32_t xs = u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(xs, o, 64);
+      if (lane >= (uint32_t)o) xs += y;
+    }
+    if (lane == 63) wsum[w] = xs;
+    __syncthreads();
+    uint32_t incl = xs;
+    for (int k = 0; k < w; ++k) incl += wsum[k];
+    if (tid <= nq) eUl[tid] = incl;  // keys with upper bound <= tid = keys < e_tid
+    if (tid == 0) s_edge = 1;
+    __syncthreads();
+    const int64_t m = (int64_t)eUl[nq];  // every window key
+    m_edge = m;
+    if (tid < nq) {
+      int j = tid;  // the last edge equal to this one
+      while (j + 1 < nq && ek_l[j + 1] == ek_l[tid]) ++j;
+      // #keys < e_q = the keys whose upper bound is <= q (eUl: inclusive prefix)
+      const int64_t below = (int64_t)eUl[tid], eq = (int64_t)eEl[j];
+      const int64_t r = (tid == nq - 1) ? m - 1 : (int64_t)((double)(tid * m) / (double)a.nbins);
+      if (m < 2 || !(below <= r && r < below + eq)) s_edge = 0;
+    }
+    __syncthreads();
+  }
 
   // ---- 2: totals, this tile's offset, compacted x, level-0 histogram -----
   {
@@ -3654,6 +3723,12 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
         cl.w0 = hint.w;
         cl.hint = 1;
       }
+      if (s_edge && !(cl.err & 2)) {  // the previous edges hold: no order statistics to find
+        cl.m = m_edge;
+        cl.spec = SPEC_EDGE;
+      } else {
+        s_edge = 0;
+      }
       s_hinted = hinted ? 1 : 0;
       s_ctl = cl;
     }
@@ -3674,8 +3749,12 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     if (tid == 0) a.toff[t] = s_toff;
   }
   const bool hinted = s_hinted != 0;
-  if (hinted) {  // H is complete: no second count, no wait
-    grid_arrive(a.bar, a.gen0 + 2, nt);
+  const bool edge = s_edge != 0;
+  if (edge) {  // nothing reads the level-0 histogram: zeroed for the next call, slice by slice
+    const uint32_t per = (MONO_DIG + nt - 1) / nt, h0 = t * per;
+    for (uint32_t i = h0 + tid; i < min<uint32_t>(h0 + per, MONO_DIG); i += MONO_BT)
+      if (hv) a.H[i] = 0u;
+  } else if (hinted) {  // H is complete: no second count, no barrier
   } else {
     if (hv) {  // (phase 1 counted into L0 with the hint's geometry)
       for (int i = tid; i < MONO_DIG; i += MONO_BT) L0[i] = 0;
@@ -3695,14 +3774,15 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
         const uint32_t v = L0[i];
         if (v) atomicAdd(&a.H2[i], v);
       }
-    if (!grid_sync(a.bar, a.gen0 + 2, nt, &s_ok)) return;
+    if (!grid_sync(a.bar, ++gn, nt, &s_ok)) return;
   }
   const uint32_t *Hs = hinted ? a.H : a.H2;
   MONO_STAMP(2);
 
   // ---- 3: ranks -> level-0 digits and groups; keys -> group segments -----
+  // (an edge hit skips phases 3 and 4 and their barriers)
   int ng = 0;
-  if (ok2) {
+  if (ok2 && !edge) {
     constexpr int PT = MONO_DIG / MONO_BT;
     static_assert(PT % 4 == 0, "16-B LDS reads");
     // H in with lane-consecutive sc1 loads (a thread's PT consecutive words
@@ -3816,9 +3896,10 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       if (gg[k] != 0xffffu)
         st_sc1(&a.seg[g_off[gg[k]] + g_base[gg[k]] + ls[k]], dkey(xv[k]) - ctl0.lo);
   }
-  if (!grid_sync(a.bar, a.gen0 + 3, nt, &s_ok)) return;
-  MONO_STAMP(3);
-  {  // H / H2 read for the last time: zeroed for the next call, slice by slice
+  if (!edge) {
+    if (!grid_sync(a.bar, ++gn, nt, &s_ok)) return;
+    MONO_STAMP(3);
+    // H / H2 read for the last time: zeroed for the next call, slice by slice
     const uint32_t per = (MONO_DIG + nt - 1) / nt, h0 = t * per;
     for (uint32_t i = h0 + tid; i < min<uint32_t>(h0 + per, MONO_DIG); i += MONO_BT) {
       if (hv) a.H[i] = 0u;
@@ -3827,7 +3908,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   }
 
   // ---- 4: each group's ranks (fused_finish) -> edges ---------------------
-  if (ok2) {
+  if (ok2 && !edge) {
     uint64_t *sk = (uint64_t *)L0;
     uint32_t *hist = (uint32_t *)L1;
     const uint64_t lo = ctl0.lo;
@@ -3859,13 +3940,21 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
       __syncthreads();
     }
   }
-  if (!grid_sync(a.bar, a.gen0 + 4, nt, &s_ok)) return;
-  MONO_STAMP(4);
+  if (!edge) {
+    if (!grid_sync(a.bar, ++gn, nt, &s_ok)) return;
+    MONO_STAMP(4);
+  }
   if (!ok2) {  // nothing to bin: the control record tells the host
-    // every block takes this branch (ctl0 is the same in all of them); the
-    // fifth barrier keeps the counters at the generation the host carries
-    // (gen0 + 5), or the next call on this handle would wait one short
-    if (!grid_sync(a.bar, a.gen0 + 5, nt, &s_ok)) return;
+    // every block takes this branch (ctl0 is the same in all of them); one
+    // more barrier: every block has read the edge sums (a.eU) before block 0
+    // zeroes them
+    if (tid == 0) s_ctl.spec = (int32_t)((gn + 1 - a.gen0) << 8);  // the barriers used
+    if (!grid_sync(a.bar, ++gn, nt, &s_ok)) return;
+    if (t == 0 && a.eg)
+      for (int i = tid; i <= nq; i += MONO_BT) {
+        a.eU[i] = 0u;
+        if (i < nq) a.eE[i] = 0u;
+      }
     constexpr int NC = (int)(sizeof(FusedCtl) / sizeof(double));
     if (t == 0 && tid < NC) st_sc1d(&a.stage[tid], ((const double *)&s_ctl)[tid]);
     mono_done(a, NC + nq + nb + a.fs.nm * nb);
@@ -3876,7 +3965,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
   uint32_t *runs = (uint32_t *)L1;                         // [MONO_NW][RADIX]
   double *acc = (double *)((char *)L1 + sizeof(uint32_t) * MONO_NW * RADIX);
   const int nm = a.fs.nm, macc = nm * nb;
-  for (int i = tid; i < nq; i += MONO_BT) e_lds[i] = ld_sc1d(&a.edges[i]);
+  for (int i = tid; i < nq; i += MONO_BT) e_lds[i] = ld_sc1d(edge ? &a.pedges[i] : &a.edges[i]);
   // the ranks' peer words (prims.h wave_ranks_lds) in L0: free between the
   // finish (phase 4) and the CSR offsets (phase 6)
   uint64_t *pmask = (uint64_t *)L0;
@@ -3922,8 +4011,20 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     st_sc1(&a.th[(int64_t)tid * nt + t], s);
   }
   for (int i = tid; i < macc; i += MONO_BT) st_sc1d(&a.slab[(int64_t)t * macc + i], acc[i]);
-  if (!grid_sync(a.bar, a.gen0 + 5, nt, &s_ok)) return;
+  if (tid == 0) s_ctl.spec = (edge ? SPEC_EDGE : 0) | (int32_t)((gn + 1 - a.gen0) << 8);
+  if (!grid_sync(a.bar, ++gn, nt, &s_ok)) return;
   MONO_STAMP(5);
+  if (t == 0) {  // (every block read the edge sums and the previous edges before barrier 1 / here)
+    for (int i = tid; i < nq; i += MONO_BT) {
+      a.pedges[i] = e_lds[i];  // the next call's speculation
+      a.edges[i] = e_lds[i];
+    }
+    if (a.eg)
+      for (int i = tid; i <= nq; i += MONO_BT) {
+        a.eU[i] = 0u;
+        if (i < nq) a.eE[i] = 0u;
+      }
+  }
 
   // ---- 6: CSR offsets, perm, counts, packed results ----------------------
   {
@@ -4374,7 +4475,11 @@ struct Profile {
   // barrier words; barrier generation / completion count carried across calls
   Buf mono, bar, mono_trace;
   Buf mH, mhint;  // radial_mono: its two level-0 histograms, its level-0 hint slots
-  int64_t n_mhint = 0, n_mono_hinted = 0;
+  int64_t n_mhint = 0, n_mono_hinted = 0, n_mono_edge = 0;
+  Buf mpedges, meue;  // radial_mono's edge speculation: the last edges, the per-edge sums
+  bool medge_next = false;
+  int medge_nq = 0;
+  std::vector<double> mono_last_edges;
   Buf dscal, dlc;  // distributed radial_equaln: global scalars, per-rank group counts
   uint64_t bar_gen = 0, bar_done = 0;
   uint32_t bar_n = 0;  // grid size the barrier words were counted for (0: reset)
@@ -5098,6 +5203,14 @@ static bool agather_off() {
   return off;
 }
 
+static bool mono_edge_env() {  // A/B: PBX_MONO_EDGE=0 never speculates on the edges
+  static const bool on = [] {
+    const char *v = std::getenv("PBX_MONO_EDGE");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 static bool mono_hint_env() {  // A/B: PBX_MONO_HINT=0 counts level 0 in phase 2 always
   static const bool on = [] {
     const char *v = std::getenv("PBX_MONO_HINT");
@@ -5255,16 +5368,42 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   a.trace = trace_env ? (uint64_t *)P.mono_trace.get(sizeof(uint64_t) * 8 * nt) : nullptr;
   a.gen0 = P.bar_gen;
   a.done_target = P.bar_done + nt;
+  // edge speculation: the previous call's edges (every call leaves its own in
+  // P.mpedges) and the per-edge sums (zero on entry and exit); tried when the
+  // last two one-launch calls' edges were identical
+  if (!P.mpedges.p) {
+    P.mpedges.get(sizeof(double) * RADIX);
+    PBX_HIP(hipMemsetAsync(P.mpedges.p, 0, sizeof(double) * RADIX, st));
+    P.meue.get(sizeof(uint32_t) * (2 * RADIX + 1));
+    PBX_HIP(hipMemsetAsync(P.meue.p, 0, sizeof(uint32_t) * (2 * RADIX + 1), st));
+  }
+  a.pedges = (double *)P.mpedges.p;
+  a.eU = (uint32_t *)P.meue.p;
+  a.eE = a.eU + RADIX + 1;
+  a.eg = (P.medge_next && nq == P.medge_nq && mono_edge_env()) ? 1 : 0;
   hipLaunchKernelGGL(radial_mono, dim3(nt), dim3(MONO_BT), 0, st, a);
   PBX_HIP(hipGetLastError());
-  P.bar_gen += 5;
   P.bar_done += nt;
   ++P.n_mono;
   ++P.n_mhint;
   if (!wait_tag(st, hp + ntot, a.gen0)) {
     P.bar_n = 0;  // discarded: zero the barrier words before the next call
+    P.medge_next = false;
     ++P.n_mono_discard;
+    if (P.mpedges.p) {  // (the edge sums may hold counts)
+      PBX_HIP(hipMemsetAsync(P.meue.p, 0, sizeof(uint32_t) * (2 * RADIX + 1), st));
+    }
     return nullptr;
+  }
+  {  // the barriers the call used (skipped phases take none); edges for the next call
+    const FusedCtl *hc = (const FusedCtl *)hp;
+    P.bar_gen += (uint64_t)((hc->spec >> 8) & 0xff);
+    if (hc->spec & SPEC_EDGE) ++P.n_mono_edge;
+    const double *he = hp + NC;
+    P.medge_next = (int)P.mono_last_edges.size() == nq &&
+                   std::memcmp(P.mono_last_edges.data(), he, sizeof(double) * nq) == 0;
+    P.mono_last_edges.assign(he, he + nq);
+    P.medge_nq = nq;
   }
   if (a.trace) {  // per phase: min / max over blocks of the stamp, relative to the earliest start
     std::vector<uint64_t> tr((size_t)8 * nt);
@@ -5327,7 +5466,8 @@ int pbx_profile_destroy(void *handle) {
                   &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->shint, &p->srows,
                   &p->swc, &p->sbt, &p->mono, &p->bar,
                   &p->mono_trace, &p->dscal, &p->dlc, &p->pdone, &p->pstage, &p->mH,
-                  &p->mhint};
+                  &p->mhint, &p->stab, &p->srec, &p->sspec, &p->sslab, &p->sflag, &p->posst,
+                  &p->slteq, &p->mpedges, &p->meue};
     for (Buf *b : all) b->release();
     p->pin.release();
     p->mpin.release();
@@ -5367,6 +5507,7 @@ int pbx_profile_mono_stats(void *handle, int64_t *out) {
     if (!out) fail(PBX_ERR_VALUE, "null output");
     out[0] = P.n_mono;
     out[1] = P.n_mono_hinted;
+    out[2] = P.n_mono_edge;
   });
 }
 

@@ -241,10 +241,12 @@ class DeviceBins:
     def mono_stats(self) -> dict:
         """One-launch radial_equaln calls on this handle, and of them those
         whose level-0 digits were counted with the previous one-launch call's
-        geometry (one grid barrier less; pbx_profile_mono_stats)."""
-        out = np.zeros(2, dtype=np.int64)
+        geometry (one grid barrier less), and of them those that found the
+        previous call's edges at their ranks (no order statistics, three
+        barriers less; pbx_profile_mono_stats)."""
+        out = np.zeros(3, dtype=np.int64)
         nat.call("pbx_profile_mono_stats", self._h, _i64(out))
-        return {"mono": int(out[0]), "hinted": int(out[1])}
+        return {"mono": int(out[0]), "hinted": int(out[1]), "edge_hits": int(out[2])}
 
     def level0_stats(self) -> dict:
         """Tiled multi-kernel radial_equaln calls on this handle, and of them

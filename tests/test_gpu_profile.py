@@ -747,8 +747,11 @@ def test_radial_equaln_one_launch_level0_hint_transitions(gpu, n):
     stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
     nanpos = base.copy()
     nanpos[::997] = np.nan
+    # (consecutive calls never repeat their edges here: two identical edge
+    # sets would make the next call speculate on the edges, which counts no
+    # hinted level 0 — test_radial_equaln_one_launch_edge_speculation)
     calls = [(base, None, None, False),
-             (base, None, None, True),
+             (base * (1.0 + 1e-12), None, None, True),
              (base * 0.999, None, None, True),
              (base * 1e6, None, None, False),
              (base * 1e6, None, None, True),
@@ -792,6 +795,54 @@ def test_radial_equaln_one_launch_level0_hint_transitions(gpu, n):
         _, e, c, _ = DeviceBins.radial_equaln(base, mass, nbins=128, stats=stats, into=h)
         ref = _oracle_radial(base, mass, None, None, 128, None, None)
         assert np.array_equal(e, ref["edges"]) and np.array_equal(c, ref["counts"])
+    finally:
+        h.close()
+
+
+def test_radial_equaln_one_launch_edge_speculation(gpu):
+    """The one-launch path's edge speculation: once two calls on a handle
+    returned identical edges, the next call counts, during its selection,
+    each previous edge's window keys below and equal to it; when every edge
+    sits at its rank the call skips the order-statistic phases (mono_stats
+    edge_hits).  A repeated snapshot hits; a perturbed one, a window, a NaN
+    or a bin-count change misses (or is not tried) — every call equal to the
+    oracle (edges, counts, CSR bit-exact, sums to 1e-12)."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(61)
+    n = 600_000
+    base = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    nanpos = base.copy()
+    nanpos[::991] = np.nan
+    calls = [  # (positions, nbins, bin_min, bin_max, edge hits after the call)
+        (base, 128, None, None, 0), (base, 128, None, None, 0), (base, 128, None, None, 1),
+        (base, 128, None, None, 2), (base * (1.0 + 1e-12), 128, None, None, 2),
+        (base, 128, None, None, 2), (base, 128, None, None, 2), (base, 128, None, None, 3),
+        (base, 128, 1.0, 4.0, 3), (base, 128, 1.0, 4.0, 3), (base, 128, 1.0, 4.0, 4),
+        (base, 64, 1.0, 4.0, 4), (base, 64, 1.0, 4.0, 4), (base, 64, 1.0, 4.0, 5),
+        (nanpos, 128, None, None, 5), (nanpos, 128, None, None, 5), (nanpos, 128, None, None, 6)]
+    h = DeviceBins()
+    try:
+        for k, (pos, nb, lo, hi, want) in enumerate(calls):
+            _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=nb, stats=stats, into=h,
+                                                  bin_min=lo, bin_max=hi)
+            st = h.mono_stats()
+            assert h.path_stats()["mono_discarded"] == 0, k
+            assert st["edge_hits"] == want, (k, st)
+            ref = _oracle_radial(pos, mass, None, None, nb, lo, hi)
+            assert np.array_equal(e, ref["edges"], equal_nan=True), k
+            assert np.array_equal(c, ref["counts"]), k
+            pp, o = h.csr()
+            assert np.array_equal(o, ref["offsets"]) and np.array_equal(pp, ref["perm"]), k
+            ne = c > 0
+            for (f, w, cols), got in zip(stats, m):
+                for col in range(7):
+                    if (cols >> col) & 1 and not (w == -1 and col in (0, 1, 2, 5)):
+                        want_c = _oracle_col(ref, f, w, col)
+                        np.testing.assert_allclose(got[ne, col], want_c[ne], rtol=1e-12,
+                                                   atol=1e-12 * np.nanmax(np.abs(want_c[ne])))
     finally:
         h.close()
 
