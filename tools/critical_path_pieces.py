@@ -6,7 +6,8 @@ and every range walked alone with the per-wave timeline (PBX_WALK_TRACE)
 — first plain, then under each pieces setting "permille,kmax": a range is
 walked three times (the first records its groups' steps and node
 checkpoints, the second is cut at them and records its pieces' own, the
-third — timed — is cut at those), each checked against the full walk
+third — timed, without the walk statistics like the bench's timed steps —
+is cut at those), each checked against the full walk
 (interaction counts identical, values to 1e-12).
 
 Prints one JSON object: per setting the max range span (first wave start to
@@ -46,9 +47,13 @@ want = nat.WANT_POT | nat.WANT_ACC
 ev = [nat.Event() for _ in range(2)]
 
 
-def walk(first, count, cost=None):
+def walk(first, count, cost=None, counted=True):
+    """One range walk; ``counted=False``: without the walk statistics (the
+    fast kernel the timed ShardedTree steps run), counts then reported from
+    the last counted walk."""
     if os.path.exists(trace):
         os.remove(trace)
+    tree._set_walk_counters(counted)
     ev[0].record()
     tree._compute_range_device(0.5, want, first, count, 1, d_pot.ptr, d_acc.ptr, cost)
     ev[1].record()
@@ -59,12 +64,16 @@ def walk(first, count, cost=None):
     s, e, st = h[:, 0].astype(np.int64), h[:, 1].astype(np.int64), h[:, 2].astype(np.int64)
     d = (e - s) / 100.0  # us
     k = int(np.argmax(d))
-    info = tree.info()
+    info = tree.info() if counted else last_info[0]
+    last_info[0] = info
     return ms, {"waves": int(len(d)), "wave_us_max": float(d[k]), "steps_of_longest": int(st[k]),
                 "steps_max": int(st.max()), "wave_us_p99": float(np.percentile(d, 99)),
                 "wave_us_mean": float(d.mean()),
                 "span_us": float((e.max() - s.min()) / 100.0),
                 "counts": (info["node_interactions"], info["leaf_pairs"])}
+
+
+last_info = [None]
 
 
 def outputs(count):
@@ -82,7 +91,7 @@ ev[1].record()
 nat.synchronize()
 build_ms = ev[0].elapsed_ms(ev[1])
 walk(0, n, d_cost.ptr)
-full_ms, full = walk(0, n, d_cost.ptr)
+full_ms, full = walk(0, n, d_cost.ptr, counted=False)
 p_full, a_full = outputs(n)
 tree._cost_to_orig_device(d_cost.ptr, d_cost_orig.ptr)
 ranges = align_ranges(tree._balance_device(d_cost_orig.ptr, world), n, 64)
@@ -93,7 +102,7 @@ def run_ranges(label, reps):
     for first, count in ranges:
         for _ in range(reps - 1):
             walk(first, count, d_cost.offset(4 * first))
-        ms, info = walk(first, count, d_cost.offset(4 * first))
+        ms, info = walk(first, count, d_cost.offset(4 * first), counted=False)
         p, a = outputs(count)
         rp = float(np.max(np.abs(p - p_full[first:first + count]) / np.abs(p_full[first:first + count])))
         ra = float(np.max(np.linalg.norm(a - a_full[first:first + count], axis=1)
