@@ -1779,6 +1779,7 @@ __global__ void __launch_bounds__(FR_TPB)
   __shared__ uint32_t gstart[MS_MAXQ + 1];
   __shared__ uint32_t gd[MS_MAXQ], go[MS_MAXQ + 1];
   __shared__ int sng, s_err, s_w0, s_hint, s_spec, s_eok;
+  __shared__ uint32_t s_flag;
   const int tid = threadIdx.x;
   const uint32_t lane = lane_id();
   const int wv = tid >> 6;
@@ -1788,12 +1789,14 @@ __global__ void __launch_bounds__(FR_TPB)
     s_w0 = ctl->w0;
     s_hint = ctl->hint;
     // the stored bin table (SpecTab) applies iff this call's geometry and
-    // every rank's level-0 digit are its own (compared below, block 0)
+    // every rank's level-0 digit are its own (compared below, in every
+    // block: an edge hit needs no per-block offsets)
     s_spec = 0;
-    if (pub && tab && tab->valid && !(s_err & 2) && tab->nb == nb && tab->nq == nq &&
+    if (tab && tab->valid && !(s_err & 2) && tab->nb == nb && tab->nq == nq &&
         tab->lo == ctl->lo && tab->s0 == ctl->s0 && tab->w0 == s_w0)
       s_spec = 1;
     s_eok = 1;  // (edge speculation: every edge at its rank, below)
+    s_flag = sflag ? *sflag : 0u;  // (reset by fused_finish, after every reader)
   }
   for (int k = tid; k < MS0_DIG; k += FR_TPB) incl[k] = H[k];  // coalesced, via LDS
   __syncthreads();
@@ -1836,27 +1839,23 @@ __global__ void __launch_bounds__(FR_TPB)
       R[q].rr = r - (a ? (int64_t)incl[a - 1] : 0);
     }
     qdig[q] = (uint32_t)a;
-    if (pub && s_spec && tab->qd[q] != (uint32_t)a) s_spec = 0;  // (benign race: all write 0)
-    if (pub && lteq) {  // the table's edge q is this call's iff rank r is among its equals
+    if (s_spec && tab->qd[q] != (uint32_t)a) s_spec = 0;  // (benign race: all write 0)
+    if (lteq) {  // the table's edge q is this call's iff rank r is among its equals
       const int64_t rr = r - (a ? (int64_t)incl[a - 1] : 0);
       const uint32_t lt = lteq[2 * q], eq = lteq[2 * q + 1];
       if (!((int64_t)lt <= rr && rr < (int64_t)lt + (int64_t)eq)) s_eok = 0;
     }
   }
   __syncthreads();
-  if (pub && lteq)  // read: zeroed for the next edge-speculating call
-    for (int i = tid; i < 2 * nq; i += FR_TPB) lteq[i] = 0u;
-  if (pub && tid == 0) {
-    const int m = s_spec ? SPEC_MATCH : 0;
-    // a hit: select_tiles binned every key with the table (no block gave up);
-    // an edge-speculating call (it listed no deferred keys) only when its
-    // edges hold too — otherwise the assignment runs
-    const uint32_t f = sflag ? *sflag : 0u;
-    const bool hit = m && sflag && !(f & 1u) && (!(f & 4u) || s_eok);
-    ctl->spec = m | (hit ? SPEC_HIT : 0) | ((f & 2u) ? SPEC_NOX : 0) |
-                ((hit && (f & 4u)) ? SPEC_EDGE : 0);
-    if (sflag) *sflag = 0u;  // (for the next speculating call)
-  }
+  // a hit: select_tiles binned every key with the table (no block gave up);
+  // an edge-speculating call (it listed no deferred keys) only when its
+  // edges hold too — otherwise the assignment runs
+  const uint32_t f = s_flag;
+  const bool hit = s_spec && sflag && !(f & 1u) && (!(f & 4u) || s_eok);
+  const bool edge_hit = hit && (f & 4u);
+  if (pub && tid == 0)
+    ctl->spec = (s_spec ? SPEC_MATCH : 0) | (hit ? SPEC_HIT : 0) | ((f & 2u) ? SPEC_NOX : 0) |
+                (edge_hit ? SPEC_EDGE : 0);
   // groups: run starts of the (non-decreasing) digits; one wave numbers them
   if (wv == 0) {
     uint32_t ng = 0;
@@ -1922,9 +1921,10 @@ __global__ void __launch_bounds__(FR_TPB)
     }
   }
   __syncthreads();
-  // this block's group: per-block segment offsets (one thread per level-0 block)
+  // this block's group: per-block segment offsets (one thread per level-0
+  // block; an edge hit gathers no keys)
   const int g = blockIdx.x;
-  if ((s_err & 2) || g >= ng) return;
+  if ((s_err & 2) || g >= ng || edge_hit) return;
   const uint32_t d = gd[g];
   uint32_t c = 0;
   const int b = tid;  // g0 <= FR_TPB
@@ -2166,7 +2166,8 @@ __global__ void __launch_bounds__(FR_TPB)
     fused_finish(const FusedCtl *__restrict__ ctl, const MsRank *__restrict__ R,
                  const uint32_t *__restrict__ gq, const uint32_t *__restrict__ goff,
                  const uint64_t *__restrict__ seg, double *__restrict__ edges,
-                 const SpecTab *__restrict__ tab, int nq) {
+                 const SpecTab *__restrict__ tab, int nq, uint32_t *__restrict__ sflag,
+                 uint32_t *__restrict__ lteq) {
   __shared__ __attribute__((aligned(16))) uint64_t sk[FS_LDS];
   __shared__ __attribute__((aligned(16))) uint32_t hist[FS_DIG];  // (u64 candidates, finish_group)
   __shared__ uint32_t wsum[FR_TPB / 64];
@@ -2185,6 +2186,13 @@ __global__ void __launch_bounds__(FR_TPB)
     c_s = ctl->s0;
     c_o0 = c_run ? goff[g] : 0u;
     c_o1 = c_run ? goff[g + 1] : 0u;
+  }
+  // the speculation's flag and edge counts, read by fused_hist0 / fused_resolve:
+  // zeroed for the next speculating call
+  if (g == 0) {
+    if (sflag && tid == 0) *sflag = 0u;
+    if (lteq)
+      for (int i = tid; i < 2 * nq; i += FR_TPB) lteq[i] = 0u;
   }
   __syncthreads();
   if (c_edge) {  // the edge speculation held: the table's edges are this call's
@@ -2306,7 +2314,9 @@ __device__ void pack_block(const PackArgs &a, int pb, double *red) {
     const int j = pb - a.nhead;
     double v = 0.0;
     for (int64_t r = threadIdx.x; r < a.rows; r += TPB) v += a.slab[r * a.nsum + j];
-    for (int64_t r = threadIdx.x; r < a.rows2; r += TPB) v += a.slab2[r * a.nsum + j];  // fix_deferred
+    // fix_deferred's rows (none written on an edge hit)
+    const int64_t rows2 = (a.ctl->spec & SPEC_EDGE) ? 0 : a.rows2;
+    for (int64_t r = threadIdx.x; r < rows2; r += TPB) v += a.slab2[r * a.nsum + j];
     red[threadIdx.x] = v;
     __syncthreads();
 #pragma unroll
@@ -2992,14 +3002,17 @@ __global__ void __launch_bounds__(MS0_TPB)
     c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
     c_edge = (ctl->spec & SPEC_EDGE) ? 1 : 0;
   }
+  __syncthreads();
+  // an edge hit: no deferred keys, and the table keeps its edges (the pack
+  // reads no fix_deferred sums either)
+  if (c_edge) return;
   for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
   for (int k = tid; k <= nb; k += MS0_TPB) e[k] = edges[k];
   __syncthreads();
   const bool ok_all = c_ng >= 0;
-  const bool c_hit_edge = c_edge != 0;
   for (int k = tid; k <= c_ng; k += MS0_TPB) gql[k] = gq[k];
   const uint64_t lo = c_lo;
-  if (blockIdx.x == 0 && sio.tab && ok_all && !c_hit_edge) {
+  if (blockIdx.x == 0 && sio.tab && ok_all) {
     // the table now holds this call's digits: its edges and groups with it
     // (the next call's edge speculation)
     SpecTab *T = sio.tab;
@@ -6252,7 +6265,9 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         comm_allreduce(comm, seg, seg, seg_total, 2, 0, st, lk);
       hipLaunchKernelGGL(fused_finish, dim3(nq), dim3(FR_TPB), 0, st, (const FusedCtl *)ctl,
                          (const MsRank *)R, (const uint32_t *)gq, (const uint32_t *)goff,
-                         (const uint64_t *)seg, de, (const SpecTab *)stab, nq);
+                         (const uint64_t *)seg, de, (const SpecTab *)stab, nq,
+                         thist.spec ? thist.sa.flag : nullptr,
+                         (thist.spec && thist.sa.edge) ? thist.sa.lteq : nullptr);
       PBX_HIP(hipGetLastError());
       // assignment (+ the statistics' distinct sums) with the device edges
       if (agath) {

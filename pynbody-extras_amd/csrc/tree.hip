@@ -1188,7 +1188,7 @@ __global__ void __launch_bounds__(WALK_TPB)
   int64_t t = (int64_t)lb * blockDim.x + threadIdx.x;
   bool valid = t < wp.m;
   int32_t a_lo = 0, a_hi = 0x3fffffff, pslot = -1, gbase = 0, npc = 1, ck0 = 0;
-  int64_t gidx = 0;
+  int32_t *ckrow = nullptr;  // PIECES: the group's checkpoint row (null: none recorded)
   if (PIECES) {  // (one wave per block) this wave's piece from the table
     const uint32_t nwt = *wp.wtab_n;
     if (lb >= nwt) {
@@ -1205,11 +1205,16 @@ __global__ void __launch_bounds__(WALK_TPB)
     valid = ln < __builtin_amdgcn_readfirstlane(e.cnt);
     a_lo = __builtin_amdgcn_readfirstlane(e.a_lo);
     a_hi = __builtin_amdgcn_readfirstlane(e.a_hi);
-    pslot = __builtin_amdgcn_readfirstlane(e.pslot);
-    gbase = __builtin_amdgcn_readfirstlane(e.gbase);
-    npc = __builtin_amdgcn_readfirstlane(e.npc);
-    ck0 = __builtin_amdgcn_readfirstlane(e.ck0);
-    gidx = wp.gfirst + (__builtin_amdgcn_readfirstlane(e.t0) >> 6);
+    // the values used only at a checkpoint or after the loop are kept in
+    // VGPRs (uniform all the same): at 8 waves per SIMD the SGPR budget is
+    // full, and as SGPRs they were spilled to VGPR lanes — ~200 v_readlane
+    // and ~80 v_writelane in the kernel, ~20 % slower per wave than the
+    // plain range walk
+    pslot = e.pslot | (int32_t)vgpr_zero();
+    gbase = e.gbase | (int32_t)vgpr_zero();
+    npc = e.npc | (int32_t)vgpr_zero();
+    ck0 = e.ck0 | (int32_t)vgpr_zero();
+    if (wp.ck) ckrow = wp.ck + (wp.gfirst + ((e.t0 | (int32_t)vgpr_zero()) >> 6)) * (CK_N + 1);
   } else if (wp.wtab) {  // (one wave per block) this wave's targets from the table
     const uint32_t nwt = *wp.wtab_n;
     if (lb >= nwt) {
@@ -1254,7 +1259,9 @@ __global__ void __launch_bounds__(WALK_TPB)
   unsigned long long n_pp = 0;
   int32_t p = valid ? 0 : -2;  // this lane's next node in its own walk
   int32_t w = 0;               // the wave's node (uniform)
-  uint32_t steps = 0;          // the wave moves strictly forward in DFS order
+  // wave steps left before the guard against corrupted links trips, minus
+  // one: the loop runs while (w | budget) >= 0 — one scalar OR and compare
+  // for both exits (steps = max_steps - 1 - budget afterwards)
   uint32_t leaf_rounds = 0;    // 4-record leaf rounds (cost_kind 1)
   // One path through the body, no `continue`: every exit of a divergent
   // region merges into the same accumulator registers, and p takes one
@@ -1263,7 +1270,8 @@ __global__ void __launch_bounds__(WALK_TPB)
   // phi registers: ~20 v_mov_b64 per wave step, as many VALU issues as the
   // opening test itself).
   const uint32_t max_steps = (uint32_t)wp.max_steps;
-  uint32_t ck_next = 0;  // PIECES: cost of the next checkpoint
+  int32_t budget = (int32_t)max_steps - 1;  // (max_steps < 2^31: nodes + 16)
+  uint32_t ck_next = wp.ck ? 0u : ~0u;  // PIECES: cost of the next checkpoint (~0: none)
   // theta^2 in a VGPR pair: left a kernel argument, it was reloaded from the
   // kernarg segment every step (a scalar load and its wait; SGPRs are full)
   const uint64_t th2b = __builtin_bit_cast(uint64_t, wp.theta2);
@@ -1300,18 +1308,18 @@ __global__ void __launch_bounds__(WALK_TPB)
     for (int o = 32; o > 0; o >>= 1) mn = min(mn, __shfl_xor(mn, o, 64));
     w = mn == 0x7fffffff ? -1 : mn;
   }
-  while (w >= 0 && steps < max_steps &&
+  while ((w | budget) >= 0 &&
          (!PIECES || (w & 0x3fffffff) < a_hi)) {  // corrupted links: stop instead of hanging
-    ++steps;
+    --budget;
     w = __builtin_amdgcn_readfirstlane(w);  // uniform: keep it (and the address math) scalar
     // bit 30 of w: the node is a leaf (walk-record flags; set only below)
     const uint32_t wleaf = ((uint32_t)w >> 30) & 1u;
     w &= 0x3fffffff;
-    if (PIECES && wp.ck && steps - 1 + leaf_rounds >= ck_next) {  // checkpoint (uniform)
+    if (PIECES && (uint32_t)((int32_t)max_steps - 2 - budget) + leaf_rounds >= ck_next) {  // checkpoint (uniform)
       // the wave's node at every CK_STEP units of its cost (node steps + leaf
       // rounds, what its time follows): the next walk's piece boundaries
       const uint32_t j = (uint32_t)ck0 + ck_next / CK_STEP;
-      if (j < (uint32_t)CK_N && lane0) wp.ck[gidx * (CK_N + 1) + 1 + j] = w;
+      if (j < (uint32_t)CK_N && lane0) ckrow[1 + j] = w;
       ck_next += CK_STEP;
     }
     u32x16 c[NCH];
@@ -1319,7 +1327,7 @@ __global__ void __launch_bounds__(WALK_TPB)
     const double mass = chunk_d(c[0], 3);
     const int32_t next = chunk_i(c[0], 12), first = chunk_i(c[0], 13);
     const uint32_t wflags = (uint32_t)chunk_i(c[0], 15);
-    uint32_t nleaf = wflags & WF_NEXT_LEAF;
+    uint32_t nleaf = wflags & WF_NEXT_LEAF;  // (bit 30: the flag of w below as it is)
     const bool act = (p == w);
     const unsigned na = CNT ? (unsigned)__popcll(__ballot(act)) : 0u;
     if (CNT) n_active += na;  // SIMD efficiency counter
@@ -1426,7 +1434,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       open_steps += no ? 1u : 0u;
     }
     nw = no ? first : next;
-    nleaf = no ? (wflags & WF_FIRST_LEAF) : nleaf;
+    nleaf = no ? ((wflags & WF_FIRST_LEAF) << 1) : nleaf;
     }
     if (first < 0) {  // leaf: direct sum in ascending index order
       const int32_t s = chunk_i(c[0], 14), e = s + (int32_t)(wflags & WF_COUNT);
@@ -1449,8 +1457,10 @@ __global__ void __launch_bounds__(WALK_TPB)
     }
     p = pn;
     // (nleaf is set only for a real node: nw >= 0)
-    w = nw | (nleaf ? 0x40000000 : 0);
+    static_assert(WF_NEXT_LEAF == 0x40000000u && WF_FIRST_LEAF << 1 == WF_NEXT_LEAF, "w's leaf bit");
+    w = nw | (int32_t)nleaf;
   }
+  const uint32_t steps = (uint32_t)((int32_t)max_steps - 1 - budget);
   if (w >= 0 && (!PIECES || (w & 0x3fffffff) < a_hi) && lane0) atomicOr(wp.fault, 1u);
   if (wp.trace && lane0) {
     const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1472,9 +1482,9 @@ __global__ void __launch_bounds__(WALK_TPB)
   }
   int32_t wcost = (int32_t)(steps + leaf_rounds);
   if (PIECES) {
-    if (wp.ck && lane0) {  // the group's cost in this walk (split: summed over its pieces)
-      if (pslot < 0) wp.ck[gidx * (CK_N + 1)] = wcost;
-      else atomicAdd(&wp.ck[gidx * (CK_N + 1)], wcost);
+    if (ckrow && lane0) {  // the group's cost in this walk (split: summed over its pieces)
+      if (pslot < 0) ckrow[0] = wcost;
+      else atomicAdd(ckrow, wcost);
     }
     if (pslot >= 0) {  // a piece of a split group: partial sums, the last piece adds them
       double *pb = wp.pbuf + ((int64_t)pslot * 64 + (threadIdx.x & 63)) * 4;
@@ -1625,7 +1635,7 @@ __global__ void __launch_bounds__(1024)
     piece_table_kernel(int32_t *__restrict__ ck, int64_t gfirst, int64_t m, int32_t nn, int permille,
                        int kmax, uint32_t cap, uint8_t *__restrict__ kbuf,
                        WavePiece *__restrict__ ptab, uint32_t *__restrict__ wtab_n,
-                       unsigned *__restrict__ pctr) {
+                       unsigned *__restrict__ pctr, int gorder) {
   __shared__ int32_t red[16];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t bcnt[PT_NB], bcur[PT_NB];
@@ -1704,13 +1714,37 @@ __global__ void __launch_bounds__(1024)
     *wtab_n = run;
   }
   __syncthreads();
-  // pass 2: the entries
-  for (int64_t g = tid; g < G; g += 1024) {
-    const int K = kbuf[g];
+  // pass 2: the entries (gorder: in group order — the pieces of neighbouring
+  // groups, which walk much the same nodes, run on the same XCD like the
+  // plain walk's waves; else longest first)
+  uint32_t gbase_run = 0;
+  for (int64_t g0 = 0; g0 < G; g0 += 1024) {
+    const int64_t g = g0 + tid;
+    const int K = g < G ? (int)kbuf[g] : 0;
+    uint32_t pos = 0;
+    if (gorder) {
+      uint32_t x = (uint32_t)K;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[wv] = x;
+      __syncthreads();
+      uint32_t off = 0, tot = 0;
+      for (int k = 0; k < 16; ++k) {
+        off += k < wv ? wsum[k] : 0u;
+        tot += wsum[k];
+      }
+      __syncthreads();
+      pos = gbase_run + off + x - (uint32_t)K;
+      gbase_run += tot;
+    }
+    if (g >= G) continue;
     const int32_t S = steps_of(g);
     const int64_t L = S / K;
     const int b = (int)min<int64_t>(PT_NB - 1, (L * PT_NB) / ((int64_t)mx + 1));
-    const uint32_t pos = atomicAdd(&bcur[b], (uint32_t)K);
+    if (!gorder) pos = atomicAdd(&bcur[b], (uint32_t)K);
     const int cnt = (int)min<int64_t>(64, m - g * 64);
     if (K == 1) {
       ptab[pos] = WavePiece{(int32_t)(g * 64), cnt, 0, 0x3fffffff, -1, 0, 1, 0};
@@ -2805,7 +2839,14 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
       PBX_HIP(hipMemsetAsync(T.ck.get(4 * ckw * (size_t)gtot), 0, 4 * ckw * (size_t)gtot, st));
       T.ck_groups = gtot;
     }
-    const int64_t cap = G;
+    // extra waves: unbounded, or (PBX_PIECE_CAP=round) only as many as keep
+    // the grid one resident round of 8 waves per SIMD
+    static const int piece_env = [] {
+      const char *o = std::getenv("PBX_PIECE_ORDER"), *c = std::getenv("PBX_PIECE_CAP");
+      return ((o && o[0] == 'g') ? 1 : 0) | ((c && c[0] == 'r') ? 2 : 0);
+    }();
+    const int64_t slots8 = 8 * (int64_t)kNumSimd;
+    const int64_t cap = (piece_env & 2) ? std::max<int64_t>(0, slots8 - G) : G;
     nwt_max = (unsigned)(G + cap);
     const int64_t slots = 2 * cap;
     if (T.p_slots < slots) {
@@ -2828,7 +2869,7 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
     hipLaunchKernelGGL(piece_table_kernel, dim3(1), dim3(1024), 0, st, T.ck.as<int32_t>(),
                        (int64_t)(first >> 6), m, (int32_t)T.nn, T.piece_permille, T.piece_kmax,
                        (uint32_t)cap, (uint8_t *)T.kbuf.get((size_t)G), (WavePiece *)(wb + 64),
-                       (uint32_t *)wb, T.pctr.as<unsigned>());
+                       (uint32_t *)wb, T.pctr.as<unsigned>(), piece_env & 1);
   } else if (T.split_cost && d_tgt == nullptr && walk_tpb() == 64 && m > 0 && T.n > 0) {
     // heavy 64-target groups of the earlier walk split in two, dispatched first
     const int64_t G = (m + 63) / 64;

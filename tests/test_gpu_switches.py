@@ -7,7 +7,8 @@ under each group of switches; the results are compared with the defaults'
 
 * profiles: edges, counts and CSR bit-identical, per-bin sums to 1e-12;
 * octree walk: the same tree and the same per-target walks — bit-identical;
-* direct sum: other summation orders — 1e-12 relative.
+* direct sum: the ordered-pair kernel in place of the pairwise-symmetric one
+  (another use of the fast reciprocal square root) — the fast-mode 1e-6.
 """
 import os
 import subprocess
@@ -55,7 +56,7 @@ def test_runtime_switches_same_results(defaults, tmp_path, group):
     for k, ref in defaults.items():
         v = got[k]
         if k.startswith("direct/"):
-            np.testing.assert_allclose(v, ref, rtol=1e-12, atol=0, err_msg=k)
+            np.testing.assert_allclose(v, ref, rtol=1e-6, atol=0, err_msg=k)
         elif "/m" in k:
             np.testing.assert_allclose(v, ref, rtol=1e-12, atol=1e-300, err_msg=k)
         else:  # edges, counts, CSR, tree outputs
