@@ -1136,9 +1136,9 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   // the grid's waves at once: the same-line hot spot fused_hist0 had)
   __shared__ SelHint shh;
   __shared__ uint8_t sdt[SPEC ? MS0_DIG : 1];      // the table's digit -> bin
-  __shared__ double sacc[SPEC ? SPEC_MACC : 1];    // per-bin sums
+  __shared__ double sacc[SPEC ? SPEC_MACC + 1 : 1];  // per-bin sums (+ a trash slot)
   // per-(tile, bin) counts of the current SH_TMAX tiles (flushed with the u16 rows)
-  __shared__ uint32_t tcs[SPEC ? SH_TMAX * ((SPEC_MAXB + 1) | 1) : 1];
+  __shared__ uint32_t tcs[SPEC ? SH_TMAX * ((SPEC_MAXB + 2) | 1) : 1];  // (+ a trash slot)
   __shared__ uint32_t sdk;                         // deferred keys listed
   __shared__ int s_spec, s_edge, s_enc;
   // edge speculation: the table's edges (and their keys), groups, and per
@@ -1189,7 +1189,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
     }
     mmode = (sa.fs.nm == 2 && mfl == 0x54u) ? 1 : (sa.fs.nm == 1 && mfl == 0x4u) ? 2 : 0;
   }
-  const int nrs = (nb + 1) | 1;
+  const int nrs = (nb + 2) | 1;  // bins 0 .. nb, the trash slot nb + 1; odd
   // the block's deferred list: 1 / SPEC_LIST of its slots (an overflow fails the speculation)
   const uint64_t lbase = (uint64_t)ta * TILE / SPEC_LIST;
   const uint32_t lcap = (uint32_t)((uint64_t)(tb - ta) * TILE / SPEC_LIST);
@@ -1235,7 +1235,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
     double m[SPEC ? SH_HALF : 1];  // SPEC: the masses (loaded with the positions)
     uint32_t in;
   };
-  auto ld = [&](uint32_t tile, int h, Half &H) {
+  auto ld = [&](uint32_t tile, int h, Half &H, auto sp) {  // sp: the speculating loop (masses)
     const int64_t wbase = p.base + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW) + h * SH_HALF * 64;
     H.in = 0;
 #pragma unroll
@@ -1247,7 +1247,7 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       H.x[k] = q[0];
       H.y[k] = q[1];
       H.z[k] = q[2];
-      if constexpr (SPEC) H.m[k] = (spec && sa.mass) ? sa.mass[in ? i : 0] : 1.0;
+      if constexpr (SPEC && decltype(sp)::value) H.m[k] = sa.mass ? sa.mass[in ? i : 0] : 1.0;
     }
   };
   uint32_t run = 0;
@@ -1294,82 +1294,104 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       for (int k = 0; k < SH_HALF; ++k)
         c8[k] = ((in4 >> k) & 1u) ? (uint32_t)sdt[(uint32_t)((kk[k] - hlo) >> hsh)] : (uint32_t)nb;
       uint32_t *trow = tcs + ((tile - ta) % SH_TMAX) * nrs;
-      const bool edge = s_edge != 0;
       const uint32_t gmin = s_enc ? 128u : (uint32_t)SPEC_DEFER;  // bytes >= gmin: edge-holding digit
-#pragma unroll
-      for (int k = 0; k < SH_HALF; ++k) {
-        const bool keep = (kb4 >> k) & 1u;
-        uint32_t code = c8[k];
-        if (((in4 >> k) & 1u) && code >= gmin) code = SPEC_DEFER;  // (out of the window: nb)
-        if (edge && keep && code == SPEC_DEFER) {
-          // an edge-holding digit: the bin among its group's edges (the
-          // table's), and per edge the keys below / equal to it (the
-          // edges are checked against this call's ranks by fused_resolve)
-          int g;
-          if (c8[k] != SPEC_DEFER) {
-            g = (int)c8[k] - 128;  // (the byte carries the group)
-          } else {  // search the group by its digit
-            const uint32_t dd = (uint32_t)((kk[k] - hlo) >> hsh);
-            int lo = 0, hi = sa.tab->ng - 1;
-            while (lo < hi) {
-              const int mid = (lo + hi) >> 1;
-              if (sgd[mid] < dd) lo = mid + 1; else hi = mid;
-            }
-            g = lo;
-          }
-          const int qa = (int)sgq[g], qb = (int)sgq[g + 1];
-          code = bin_of_in(xk[k], sedg, nb, qa, qb);
-          for (int q = qa; q < qb; ++q) {
-            if (kk[k] < sek[q]) atomicAdd(&slt[2 * q], 1u);
-            else if (kk[k] == sek[q]) atomicAdd(&slt[2 * q + 1], 1u);
-          }
-        }
-        const bool def = keep && code == SPEC_DEFER;
-        if (keep && !def) {  // (kept, outside the window: c8 = nb, the dropped bin)
-          sa.bins[slot0 + 64u * k] = (uint8_t)code;
-          atomicAdd(&trow[code], 1u);
-          if (code < (uint32_t)nb) {
-            if (mmode == 1) {  // Σw, Σx·w (mass / mean profiles)
-              atomicAdd(&sacc[code], H.m[k]);
-              atomicAdd(&sacc[nb + code], xk[k] * H.m[k]);
-            } else if (mmode == 2) {  // Σw
-              atomicAdd(&sacc[code], H.m[k]);
-            } else if (macc) {
-              // the dedicated monomials only (the host checks): (a1 a2)(b1 b2)
-              // with a = x or 1, b = w or 1 — mom_add's products (x * 1.0 is
-              // exact); monomial q's factors are bits 4q .. 4q + 3 of mfl
+      // a kept key's common effects — its byte, its tile's count of its bin,
+      // its bin's sums; a lane without one counts in the trash slots with
+      // the same instructions (no branch per key: the divergent regions,
+      // their exec-mask bookkeeping and the code copies they need had made
+      // this the kernel's largest cost after the loads)
+      auto common = [&](bool on, bool every, uint32_t code, double xv, double mv, uint32_t slot) {
+        // every: the byte of every lane's slot (the readers take the kept
+        // slots' only; a deferred key's is stored later by fix_deferred)
+        if (every || on) sa.bins[slot] = (uint8_t)code;
+        atomicAdd(&trow[on ? code : (uint32_t)nb + 1u], 1u);
+        const bool sum = on && code < (uint32_t)nb;
+        if (mmode == 1) {  // Σw, Σx·w (mass / mean profiles)
+          atomicAdd(&sacc[sum ? code : (uint32_t)SPEC_MACC], mv);
+          atomicAdd(&sacc[sum ? (uint32_t)nb + code : (uint32_t)SPEC_MACC], xv * mv);
+        } else if (mmode == 2) {  // Σw
+          atomicAdd(&sacc[sum ? code : (uint32_t)SPEC_MACC], mv);
+        } else if (macc) {
+          // the dedicated monomials only (the host checks): (a1 a2)(b1 b2)
+          // with a = x or 1, b = w or 1 — mom_add's products (x * 1.0 is
+          // exact); monomial q's factors are bits 4q .. 4q + 3 of mfl
 #pragma unroll 1
-              for (int q = 0; q < sa.fs.nm; ++q) {
-                const uint32_t f = mfl >> (4 * q);
-                const double a = ((f & 1u) ? xk[k] : 1.0) * ((f & 2u) ? xk[k] : 1.0);
-                const double b = ((f & 4u) ? H.m[k] : 1.0) * ((f & 8u) ? H.m[k] : 1.0);
-                atomicAdd(&sacc[q * nb + code], a * b);
-              }
-            }
+          for (int q = 0; q < sa.fs.nm; ++q) {
+            const uint32_t f = mfl >> (4 * q);
+            const double a = ((f & 1u) ? xv : 1.0) * ((f & 2u) ? xv : 1.0);
+            const double b = ((f & 4u) ? mv : 1.0) * ((f & 8u) ? mv : 1.0);
+            atomicAdd(&sacc[sum ? (uint32_t)q * nb + code : (uint32_t)SPEC_MACC], a * b);
           }
         }
-        const uint64_t bd = __ballot(def);
-        if (bd) {  // rare: keys of edge-holding digits, into the block's list
-          uint32_t b0 = 0;
-          if (lane == 0) b0 = atomicAdd(&sdk, (uint32_t)__popcll(bd));
-          b0 = __shfl(b0, 0, 64);
-          if (def) {
-            const uint32_t idx = b0 + rank_below(bd);
-            // (the group: filled in by assign_gather from the key — a global
-            // table lookup here stalled almost every wave step)
-            if (idx < lcap) sa.rec[lbase + idx] = AgRec{kk[k] - hlo, H.m[k], slot0 + 64u * k, tile};
+      };
+      // rare: kept window keys of an edge-holding digit
+      uint32_t rare = 0;
+#pragma unroll
+      for (int k = 0; k < SH_HALF; ++k) rare |= (((in4 >> k) & 1u) && c8[k] >= gmin) ? 1u << k : 0u;
+#pragma unroll
+      for (int k = 0; k < SH_HALF; ++k)  // (kept outside the window: c8 = nb, the dropped bin)
+        common(((kb4 & ~rare) >> k) & 1u, true, c8[k], xk[k], H.m[k], slot0 + 64u * k);
+      if (__ballot(rare != 0u)) {  // (wave-uniform, rare) one key per lane and round
+        const bool edge = s_edge != 0;
+        uint32_t todo = rare;
+        while (__ballot(todo != 0u)) {  // at most SH_HALF rounds
+          const int k = todo ? __builtin_ctz(todo) : 0;
+          double xv = xk[0], mv = H.m[0];
+          uint64_t kv = kk[0];
+          uint32_t cv = c8[0];
+#pragma unroll
+          for (int u = 1; u < SH_HALF; ++u) {
+            xv = k == u ? xk[u] : xv;
+            mv = k == u ? H.m[u] : mv;
+            kv = k == u ? kk[u] : kv;
+            cv = k == u ? c8[u] : cv;
           }
+          const uint32_t slot = slot0 + 64u * (uint32_t)k;
+          const bool act = todo != 0u;
+          bool def = act;
+          if (edge && act) {
+            // the bin among its group's edges (the table's), and per edge the
+            // keys below / equal to it (the edges are checked against this
+            // call's ranks by fused_resolve)
+            int g;
+            if (cv != SPEC_DEFER) {
+              g = (int)cv - 128;  // (the byte carries the group)
+            } else {  // search the group by its digit
+              const uint32_t dd = (uint32_t)((kv - hlo) >> hsh);
+              int lo = 0, hi = sa.tab->ng - 1;
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (sgd[mid] < dd) lo = mid + 1; else hi = mid;
+              }
+              g = lo;
+            }
+            const int qa = (int)sgq[g], qb = (int)sgq[g + 1];
+            cv = bin_of_in(xv, sedg, nb, qa, qb);
+            for (int q = qa; q < qb; ++q) {
+              if (kv < sek[q]) atomicAdd(&slt[2 * q], 1u);
+              else if (kv == sek[q]) atomicAdd(&slt[2 * q + 1], 1u);
+            }
+            def = false;
+          }
+          if (edge) common(act, false, cv, xv, mv, slot);
+          const uint64_t bd = __ballot(def);
+          if (bd) {  // keys of edge-holding digits, into the block's list
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&sdk, (uint32_t)__popcll(bd));
+            b0 = __shfl(b0, 0, 64);
+            if (def) {
+              const uint32_t idx = b0 + rank_below(bd);
+              // (the group: filled in by assign_gather from the key — a global
+              // table lookup here stalled almost every wave step)
+              if (idx < lcap) sa.rec[lbase + idx] = AgRec{kv - hlo, mv, slot, tile};
+            }
+          }
+          todo &= todo - 1u;
         }
       }
     }
   };
   auto sel = [&](uint32_t tile, int h, const Half &H) {
-    if constexpr (SPEC) {
-      if (spec) {
-        sel_spec(tile, h, H);
-        return;
-      }
-    }
     double *xt = xo + (int64_t)tile * TILE + (int64_t)w * (TILE / SH_NW) + h * SH_HALF * 64;
     const int64_t wj = (int64_t)tile * (TILE / 64) + w * SI + h * SH_HALF;
 #pragma unroll
@@ -1433,16 +1455,22 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       __syncthreads();
     }
   };
-  Half A, B;
-  if (ta < tb) ld(ta, 0, A);
-  for (uint32_t tile = ta; tile < tb; ++tile) {
-    ld(tile, 1, B);
-    run = 0;
-    sel(tile, 0, A);
-    ld(tile + 1 < tb ? tile + 1 : tile, 0, A);
-    sel(tile, 1, B);
-    tile_end(tile);
-  }
+  // the tile loop, once per kind of block: speculating or not (one loop
+  // choosing per half had both bodies' registers live: spills)
+  auto tiles = [&](auto sp) {
+    Half A, B;
+    if (ta < tb) ld(ta, 0, A, sp);
+    for (uint32_t tile = ta; tile < tb; ++tile) {
+      ld(tile, 1, B, sp);
+      run = 0;
+      if constexpr (decltype(sp)::value) sel_spec(tile, 0, A); else sel(tile, 0, A);
+      ld(tile + 1 < tb ? tile + 1 : tile, 0, A, sp);
+      if constexpr (decltype(sp)::value) sel_spec(tile, 1, B); else sel(tile, 1, B);
+      tile_end(tile);
+    }
+  };
+  if (SPEC && spec) tiles(std::integral_constant<bool, SPEC>{});
+  else tiles(std::false_type{});
   // (three half buffers with two halves in flight, at the same 2 blocks per
   // CU: 273 -> 275 us — the loads in flight are not what bounds it: dropped)
   // the block's key range: one atomic pair per block
