@@ -328,9 +328,9 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                 # time that too
                 row["level0_hinted_calls"] = lv
                 row["speculated_calls"] = dev.spec_stats()
-                dev.set_level0_hint(False)
                 ct, cd = [], []
                 for _ in range(max(20, steps // 10)):
+                    dev.forget_history()  # the next call runs as the handle's first
                     t0 = time.perf_counter()
                     e0.record()
                     step()
@@ -338,13 +338,11 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                     nat.synchronize()
                     ct.append(time.perf_counter() - t0)
                     cd.append(e0.elapsed_ms(e1))
-                dev.set_level0_hint(True)
                 row["cold_ms"] = float(np.median(ct)) * 1e3
                 row["cold_stream_ms"] = float(np.median(cd))
-                row["cold_note"] = ("level-0 geometry hint off (pbx_profile_set_level0_hint 0): "
-                                    "every call re-reads x for its level-0 histogram and runs the "
-                                    "assignment pass (no speculation), as a first call / new "
-                                    "snapshot does")
+                row["cold_note"] = ("every call a handle's first (forget_history: no earlier "
+                                    "geometry or speculation state): the level-0 geometry sampled "
+                                    "from the keys (sample_hint), the full assignment pass")
         out.append(row)
         if cpu and world == 1:
             from oracle import profile_ref as pr

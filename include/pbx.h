@@ -446,10 +446,12 @@ int pbx_profile_level0_stats(void *handle, int64_t *out);
  * miss re-runs the assignment; results are identical either way.
  * PBX_SPEC=0 disables the speculation. */
 int pbx_profile_spec_stats(void *handle, int64_t *out);
-/* enabled = 0: this handle's tiled calls never use the previous call's
- * level-0 digit geometry (every call re-reads x for its level-0 histogram:
- * the cost of a first call / a new snapshot); 1 (default): use it when it
- * holds.  Results are identical either way. */
+/* enabled = 0: this handle's tiled calls never use a level-0 digit
+ * geometry they did not derive themselves (every call re-reads x for its
+ * level-0 histogram); 1 (default): use the previous call's when it holds,
+ * and on a first call one from a sample of the keys (sample_hint); 2:
+ * forget the earlier calls (geometries, speculation state) — the next call
+ * runs as a handle's first.  Results are identical in every mode. */
 int pbx_profile_set_level0_hint(void *handle, int enabled);
 /* Per-bin percentiles of the last assignment — replaces the per-bin loop of
  * ProfileArray._compute for Percentile / Median / Abs_pXX

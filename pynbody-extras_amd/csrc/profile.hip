@@ -855,7 +855,8 @@ constexpr int32_t SPEC_MATCH = 1, SPEC_HIT = 2, SPEC_NOX = 4, SPEC_EDGE = 8;
 struct SelHint {
   uint64_t lo;
   int32_t s, w;
-  int32_t valid, pad;
+  int32_t valid;
+  int32_t sampled;  // a first call's geometry from a sample of the keys (sample_hint), not kept
 };
 constexpr int AS_MAXM = 8;
 struct FusedStats {
@@ -1550,6 +1551,102 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
   }
 }
 
+// A first tiled call has no previous geometry for its level-0 histogram, so
+// fused_hist0 would read x a second time.  sample_hint gives it one: the
+// kept window keys of S (<= 32768) evenly spaced particles of the span, their range
+// widened below by 2^-6 in value and above by 2^5 (a power-law tail) or up
+// to the Sphere's bound (|c| + R: no key beyond it), clipped to the window.
+// The sampled minimum of S of N particles in an r^3 core (Plummer) is the
+// whole set's times (N/S)^(1/3) E^(1/3), E the ratio of two unit
+// exponentials: it stays within 2^6 but for a fraction 1 / (1 + 2^18 S/N)
+// of the sets (0.4 % at 38M; an r^2 core escapes more often).  A key
+// outside it escapes the hint as any other's would (select_tiles sets
+// hflag): the call re-reads x, the results are the same.  The last block
+// writes the hint and re-arms the scratch (mm2 = [~min, max], done).
+constexpr int SMP_BT = 256, SMP_PER = 4;  // samples per thread, their loads in flight together
+template <bool FAM>
+__global__ void __launch_bounds__(SMP_BT)
+    sample_hint(const double *__restrict__ pos, int64_t n, SelectParams p, int64_t span,
+                uint32_t S, uint64_t ka, uint64_t kb, uint64_t kub,
+                unsigned long long *__restrict__ mm2, unsigned *__restrict__ done,
+                SelHint *__restrict__ out) {
+  __shared__ unsigned long long wmin[SMP_BT / 64], wmax[SMP_BT / 64];
+  __shared__ int s_last;
+  unsigned long long kmin = ~0ull, kmax = 0ull;
+  double px[SMP_PER], py[SMP_PER], pz[SMP_PER];
+  bool in[SMP_PER];
+#pragma unroll
+  for (int u = 0; u < SMP_PER; ++u) {
+    const uint32_t j = (blockIdx.x * SMP_PER + u) * SMP_BT + threadIdx.x;
+    const int64_t i = p.base + (int64_t)(((uint64_t)j * (uint64_t)span) / S);
+    in[u] = j < S && i < n && (!FAM || in_family(i, p));
+    const double *q = pos + 3 * (in[u] ? i : 0);
+    px[u] = q[0];
+    py[u] = q[1];
+    pz[u] = q[2];
+  }
+#pragma unroll
+  for (int u = 0; u < SMP_PER; ++u) {
+    double xv = 0.0;
+    if (in[u] && select_xyz(px[u], py[u], pz[u], p, xv)) {
+      const uint64_t k = dkey(xv);
+      if (k >= ka && k <= kb) {
+        kmin = k < kmin ? k : kmin;
+        kmax = k > kmax ? k : kmax;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(kmin, o, 64), b = __shfl_xor(kmax, o, 64);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    wmin[w] = kmin;
+    wmax[w] = kmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < SMP_BT / 64; ++q) {
+      kmin = wmin[q] < kmin ? wmin[q] : kmin;
+      kmax = wmax[q] > kmax ? wmax[q] : kmax;
+    }
+    if (kmin != ~0ull) atomicMax(&mm2[0], ~kmin);
+    if (kmax != 0ull) atomicMax(&mm2[1], kmax);
+    __threadfence();
+    s_last = atomicAdd(done, 1u) + 1 == gridDim.x;
+  }
+  __syncthreads();
+  if (!s_last || threadIdx.x != 0) return;
+  __threadfence();
+  const unsigned long long a = ~__hip_atomic_load(&mm2[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b = __hip_atomic_load(&mm2[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  mm2[0] = 0ull;
+  mm2[1] = 0ull;
+  *done = 0u;
+  SelHint h{};
+  if (b >= a && a != ~0ull) {
+    // keys of non-negative doubles: one binary order of magnitude = 1 << 52
+    constexpr uint64_t OCT = 1ull << 52, KZERO = 0x8000000000000000ull;  // dkey(+0.0)
+    uint64_t lo = a >= KZERO + 6 * OCT ? a - 6 * OCT : (a >= KZERO ? KZERO : a);
+    uint64_t hi = kub ? kub : (b + 5 * OCT < b ? ~0ull : b + 5 * OCT);
+    lo = lo > ka ? lo : ka;
+    hi = hi < kb ? hi : kb;
+    if (hi >= lo) {
+      const uint64_t sp = hi - lo;
+      const int B = sp ? 64 - __builtin_clzll(sp) : 1;
+      h.w = B < MS0_BITS ? B : MS0_BITS;
+      h.s = B - h.w;
+      h.lo = lo;
+      h.valid = 1;
+      h.sampled = 1;
+    }
+  }
+  *out = h;
+}
+
 // A speculating select_tiles stores no x (SPEC_NOX): a hit never reads it.
 // When a call does need it after all — a key escaped the level-0 hint
 // (fused_hist0 counts x again) or the digits missed the table (assign_gather
@@ -1725,7 +1822,7 @@ __global__ void __launch_bounds__(MS0_TPB)
       // the fresh one has the same digit width, keep it — the level-0 digits
       // (and the stored bin table's, SpecTab) stay comparable from call to
       // call of a slowly changing snapshot
-      if (ctl.hint && fsu.hint->s == h.s && fsu.hint->w == h.w) h = *fsu.hint;
+      if (ctl.hint && !fsu.hint->sampled && fsu.hint->s == h.s && fsu.hint->w == h.w) h = *fsu.hint;
     }
     *fsu.hint_out = h;
   }
@@ -4488,7 +4585,7 @@ struct Profile {
   Buf kw, toff, mstage, xc, kpre;
   // tiled radial calls: level-0 geometry hints (two SelHint slots, by call
   // parity) and select_tiles' digit rows
-  Buf shint, srows, swc, sbt;  // + select_tiles' per-(tile, wave) counts and block totals
+  Buf shint, shs, srows, swc, sbt;  // (shs: sample_hint scratch) + select_tiles' per-(tile, wave) counts and block totals
   // speculative assignment: the stored bin table, select_tiles' deferred
   // lists, their [start, length] per select block, per-block sums
   Buf stab, srec, sspec, sslab, sflag;
@@ -4920,6 +5017,7 @@ static int fused_grid(int64_t n_sel) {
 
 struct TileHist {  // select_tiles' hinted level-0 histogram (null hint: none)
   const SelHint *hint = nullptr;
+  bool cold = false;  // the hint slot holds no geometry yet (a first call): sample one
   uint64_t ka = 0, kb = ~0ull;
   // the speculative assignment (tab non-null: wanted); select_launch fills
   // the rest and sets `spec` when it launched select_tiles<FAM, true>, and
@@ -5029,6 +5127,24 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
         if (spec) {  // (x missing until the call's pack says it missed: x rebuilt)
           P.x_missing = true;
           P.xsrc = th->xs;
+        }
+        if (th && th->hint && th->cold && rows16) {  // a first call: a sampled geometry
+          if (!P.shs.p) {
+            P.shs.get(sizeof(uint64_t) * 3);
+            PBX_HIP(hipMemsetAsync(P.shs.p, 0, sizeof(uint64_t) * 3, st));
+          }
+          const uint32_t S = (uint32_t)std::min<int64_t>(32768, std::max<int64_t>(1, span / 64));
+          uint64_t kub = 0;  // the Sphere's bound on every kept x (|c| + R, a few ulps up)
+          if (sp.use_sphere || sp.sphere_origin) {
+            const double c = std::sqrt(sp.cx * sp.cx + sp.cy * sp.cy + sp.cz * sp.cz);
+            const double ub = (c + std::sqrt(sp.r2max)) * (1.0 + 1e-12);
+            if (std::isfinite(ub)) kub = dkey(ub);
+          }
+          unsigned long long *smm = (unsigned long long *)P.shs.p;
+          auto sk = sp.nfam > 1 ? sample_hint<true> : sample_hint<false>;
+          hipLaunchKernelGGL(sk, dim3(ceil_div(S, SMP_BT * SMP_PER)), dim3(SMP_BT), 0, st, (const double *)d_pos,
+                             hi, sp, span, S, th->ka, th->kb, kub, smm, (unsigned *)(smm + 2),
+                             (SelHint *)th->hint);
         }
         auto kern = spec ? (sp.nfam > 1 ? select_tiles<true, true> : select_tiles<false, true>)
                          : (sp.nfam > 1 ? select_tiles<true, false> : select_tiles<false, false>);
@@ -5504,7 +5620,7 @@ int pbx_profile_destroy(void *handle) {
                   &p->msNg, &p->msM, &p->msRows, &p->msL0, &p->msL1, &p->msCnt, &p->csrh, &p->slabp, &p->selst, &p->accs,
                   &p->pk0, &p->pk1, &p->pv0, &p->pv1, &p->pbk, &p->pcdf, &p->poff, &p->pq, &p->pout,
                   &p->fctl, &p->fseg, &p->fgrp, &p->fslab, &p->fpack, &p->frec, &p->fblk,
-                  &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->shint, &p->srows,
+                  &p->bins8, &p->kw, &p->toff, &p->mstage, &p->xc, &p->kpre, &p->shint, &p->shs, &p->srows,
                   &p->swc, &p->sbt, &p->mono, &p->bar,
                   &p->mono_trace, &p->dscal, &p->dlc, &p->pdone, &p->pstage, &p->mH,
                   &p->mhint, &p->stab, &p->srec, &p->sspec, &p->sslab, &p->sflag, &p->posst,
@@ -5538,6 +5654,19 @@ int pbx_profile_spec_stats(void *handle, int64_t *out) {
 int pbx_profile_set_level0_hint(void *handle, int enabled) {
   return guard([&] {
     Profile &P = as_profile(handle);
+    if (enabled == 2) {  // forget the earlier calls: the next call is a first call
+      Device &d = current_device();
+      std::lock_guard<std::mutex> lk(d.mu);
+      P.hint_off = false;
+      P.n_tiled = 0;
+      P.n_mhint = 0;
+      P.spec_next = P.edge_next = P.medge_next = false;
+      P.last_edges.clear();
+      P.mono_last_edges.clear();
+      if (P.shint.p) PBX_HIP(hipMemsetAsync(P.shint.p, 0, P.shint.bytes, d.stream));
+      if (P.mhint.p) PBX_HIP(hipMemsetAsync(P.mhint.p, 0, P.mhint.bytes, d.stream));
+      return;
+    }
     P.hint_off = enabled == 0;
   });
 }
@@ -6127,6 +6256,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       }
       TileHist thist;
       thist.hint = hints ? hints + (P.n_tiled & 1) : nullptr;
+      thist.cold = hints && P.n_tiled == 0;  // (no earlier tiled call left a geometry)
       thist.ka = ka;
       thist.kb = empty_bounds ? 0ull : kb;
       // the speculative assignment: when the last tiled call's level-0 ranks

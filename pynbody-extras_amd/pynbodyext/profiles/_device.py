@@ -268,10 +268,17 @@ class DeviceBins:
 
     def set_level0_hint(self, enabled: bool) -> None:
         """False: every tiled radial_equaln call on this handle re-reads x for
-        its level-0 histogram (what a first call or a new snapshot costs);
-        True (default): reuse the previous call's digit geometry when it
-        holds.  Same results either way (pbx_profile_set_level0_hint)."""
+        its level-0 histogram (no geometry it did not derive itself); True
+        (default): reuse the previous call's digit geometry when it holds,
+        and on a first call one sampled from the keys.  Same results either
+        way (pbx_profile_set_level0_hint)."""
         nat.call("pbx_profile_set_level0_hint", self._h, 1 if enabled else 0)
+
+    def forget_history(self) -> None:
+        """The next call runs as this handle's first: no earlier level-0
+        geometry (a first tiled call samples one), no speculation state
+        (pbx_profile_set_level0_hint mode 2).  Same results."""
+        nat.call("pbx_profile_set_level0_hint", self._h, 2)
 
     def selection(self, idx=True, x=True, w=True):
         """(original indices int64, x, weights) of the fused selection."""

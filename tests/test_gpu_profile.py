@@ -655,12 +655,13 @@ def test_radial_equaln_one_sync_matches_stepwise(gpu, case):
                 # the same call again on the handle: select_tiles counts the
                 # level-0 histogram with this call's digit geometry (no second
                 # read of x) — same edges, counts, CSR; sums to float-add order
+                # (the first call's geometry was sampled: hinted if it held)
                 st0 = a.level0_stats()
-                assert st0 == {"tiled": 1, "hinted": 0}, st0
+                assert st0["tiled"] == 1 and st0["hinted"] in (0, 1), st0
                 _, e3, c3, m3 = DeviceBins.radial_equaln(pos, mass, nbins=nb, sphere=sphere,
                                                          families=fams, bin_min=lo, bin_max=hi,
                                                          stats=stats, into=a)
-                assert a.level0_stats() == {"tiled": 2, "hinted": 1}, a.level0_stats()
+                assert a.level0_stats() == {"tiled": 2, "hinted": st0["hinted"] + 1}, a.level0_stats()
                 assert np.array_equal(e3, e1, equal_nan=True) and np.array_equal(c3, c1)
                 for u, v in zip(m3, m1):
                     np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300)
@@ -691,7 +692,7 @@ def test_radial_equaln_tiled_level0_hint_transitions(gpu):
     nanpos[::997] = np.nan
     # (positions, bin_min, bin_max, level-0 histogram from the selection?
     # None: either — the digits are valid both ways, only coarser or finer)
-    calls = [(base, None, None, False),          # first tiled call: no geometry yet
+    calls = [(base, None, None, True),           # first tiled call: a sampled geometry
              (base, None, None, True),           # the same keys
              (base * 0.999, None, None, True),   # within the range's 1/64 margins
              (base * 1e6, None, None, False),    # 20 octaves above it
@@ -728,6 +729,63 @@ def test_radial_equaln_tiled_level0_hint_transitions(gpu):
                                                    atol=1e-12 * np.nanmax(np.abs(want[ne])))
     finally:
         h.close()
+
+
+def test_radial_equaln_first_call_sampled_geometry(gpu):
+    """A handle's first tiled call has no earlier level-0 geometry: it
+    samples one from 32,768 evenly spaced particles (sample_hint) and counts
+    its level-0 histogram in the selection pass.  With the keys inside it
+    (the usual case), and with one key far below it (an escape: the call
+    re-reads x), every result equals the same call on a handle that never
+    takes a geometry it did not derive itself (hint off) — edges, counts and
+    CSR bit-identical, sums to 1e-12; with a Sphere off the origin and a
+    family slice (the FAM sampler) too.  forget_history() makes the next
+    call a first one again."""
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    rng = np.random.default_rng(61)
+    n = 4_400_000
+    base = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11)]
+    low = base.copy()
+    low[1234567] = (1e-200, 0.0, 0.0)  # 600 octaves below any sample
+    cases = [(base, {}, 1),
+             (base, {"sphere": ((1.0, -0.5, 0.2), 6.0), "families": [(100_000, 4_300_000)]}, 1),
+             (base, {"bin_min": 0.5, "bin_max": 6.0}, 1),
+             (low, {}, 0)]
+    ref = DeviceBins()
+    ref.set_level0_hint(False)
+    try:
+        for pos, kw, want in cases:
+            for fresh in (True, False):
+                h = DeviceBins()
+                try:
+                    if not fresh:  # a used handle told to forget
+                        DeviceBins.radial_equaln(pos * 1.5, mass, nbins=64, stats=stats, into=h)
+                        h.forget_history()
+                    t0 = h.level0_stats()
+                    _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats,
+                                                          into=h, **kw)
+                    st = h.level0_stats()
+                    assert st["hinted"] - t0["hinted"] == want, (kw, fresh, st)
+                    assert h.spec_stats()["speculated"] == 0
+                    pp, o = h.csr()
+                    _, e0, c0, m0 = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats,
+                                                             into=ref, **kw)
+                    pp0, o0 = ref.csr()
+                    assert np.array_equal(e, e0, equal_nan=True) and np.array_equal(c, c0), kw
+                    assert np.array_equal(o, o0) and np.array_equal(pp, pp0), kw
+                    for u, v in zip(m, m0):
+                        np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300, err_msg=str(kw))
+                    # the next call takes the first call's own range (no sampled geometry kept)
+                    DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h, **kw)
+                    assert h.level0_stats()["hinted"] == st["hinted"] + 1, (kw, h.level0_stats())
+                finally:
+                    h.close()
+        assert ref.level0_stats()["hinted"] == 0
+    finally:
+        ref.close()
 
 
 @pytest.mark.parametrize("n", [400_000, 1_000_000])
@@ -850,9 +908,9 @@ def test_radial_equaln_one_launch_edge_speculation(gpu):
 def test_radial_equaln_level0_hint_many_tiles_per_block(gpu):
     """A span above 765 select blocks x 15 tiles x 4096 (~47M particles):
     each select_tiles block flushes its u16 level-0 counts to a new row every
-    15 tiles, so the repeated call still takes the hinted
-    histogram — edges, counts and CSR identical to the first (re-read) call,
-    the first call's edges and counts equal to the oracle's."""
+    15 tiles, so the calls take the hinted histogram (the
+    first with a sampled geometry) — edges, counts and CSR identical from
+    call to call, the first call's edges and counts equal to the oracle's."""
     from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
 
     rng = np.random.default_rng(47)
@@ -864,9 +922,9 @@ def test_radial_equaln_level0_hint_many_tiles_per_block(gpu):
     try:
         _, e1, c1, m1 = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h)
         p1, o1 = h.csr()
-        assert h.level0_stats() == {"tiled": 1, "hinted": 0}, h.level0_stats()
+        assert h.level0_stats() == {"tiled": 1, "hinted": 1}, h.level0_stats()  # (sampled)
         _, e2, c2, m2 = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h)
-        assert h.level0_stats() == {"tiled": 2, "hinted": 1}, h.level0_stats()
+        assert h.level0_stats() == {"tiled": 2, "hinted": 2}, h.level0_stats()
         p2, o2 = h.csr()
         assert np.array_equal(e2, e1) and np.array_equal(c2, c1)
         assert np.array_equal(o2, o1) and np.array_equal(p2, p1)
@@ -928,7 +986,7 @@ def test_radial_equaln_speculative_assignment(gpu):
 
     try:
         got = [call(pos, {}) for _ in range(5)]
-        # calls 0, 1: no table / the table in call 0's unhinted geometry; call
+        # calls 0, 1: no table / the table in call 0's sampled geometry; call
         # 2 matches (no speculation yet; its edges repeat call 1's); calls 3, 4
         # speculate on the digits and the edges, and hit on both
         assert got == [(0, 0, 0), (0, 0, 0), (0, 0, 0), (1, 1, 1), (2, 2, 2)], got
@@ -959,9 +1017,10 @@ def test_radial_equaln_speculative_assignment(gpu):
 
 
 def test_radial_equaln_level0_hint_switch(gpu):
-    """set_level0_hint(False) (the bench's cold-handle timing): repeated
-    tiled calls on one handle re-read x every time — no call hinted — and
-    return what the hinted calls return (edges, counts, CSR identical)."""
+    """set_level0_hint(False): repeated tiled calls on one handle re-read x
+    every time — no call hinted — and return what the hinted calls return
+    (edges, counts, CSR identical); the first call takes a sampled
+    geometry."""
     from pynbodyext.profiles._device import SRC_NONE, SRC_W
 
     rng = np.random.default_rng(35)
@@ -975,7 +1034,7 @@ def test_radial_equaln_level0_hint_switch(gpu):
             h.set_level0_hint(enabled)
             _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=128, stats=stats, into=h)
             out.append((e, c, m[0], *h.csr(), h.level0_stats()["hinted"]))
-        assert [o[5] for o in out] == [0, 1, 1, 1, 2]
+        assert [o[5] for o in out] == [1, 2, 2, 2, 3]
         for o in out[1:]:
             assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
             assert np.array_equal(o[3], out[0][3]) and np.array_equal(o[4], out[0][4])
