@@ -1016,6 +1016,44 @@ def test_radial_equaln_speculative_assignment(gpu):
         ref.close()
 
 
+@pytest.mark.parametrize("nbins,stats,fams", [
+    (200, [(1, -1, 1 << 3)], None),                      # {Σw}: the dedicated single add, 201 bins
+    (64, [(0, 1, 0b111)], None),                         # Σw, Σx·w, Σx²·w: the factor loop
+    (128, [(1, -1, 1 << 3), (0, 1, 0b11)],
+     [(100_000, 2_000_000), (2_500_000, 4_300_000)]),    # two family slices (FAM)
+])
+def test_radial_equaln_speculation_sum_modes(gpu, nbins, stats, fams):
+    """The speculating selection's three ways of adding the per-bin sums
+    (one dedicated add, two, or the general monomial factor loop) and its
+    family-slice variant, with the trash slots of keys that add nothing:
+    repeated calls reach digit and edge hits, and every call equals the same
+    call on a handle that never speculates (edges, counts, CSR
+    bit-identical, sums to 1e-12)."""
+    rng = np.random.default_rng(71)
+    n = 4_400_000
+    pos = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    kw = {"families": fams} if fams else {}
+    h, ref = DeviceBins(), DeviceBins()
+    ref.set_level0_hint(False)
+    try:
+        for _ in range(5):
+            _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=nbins, stats=stats, into=h, **kw)
+            pp, o = h.csr()
+            _, e0, c0, m0 = DeviceBins.radial_equaln(pos, mass, nbins=nbins, stats=stats, into=ref,
+                                                     **kw)
+            pp0, o0 = ref.csr()
+            assert np.array_equal(e, e0) and np.array_equal(c, c0)
+            assert np.array_equal(o, o0) and np.array_equal(pp, pp0)
+            for u, v in zip(m, m0):
+                np.testing.assert_allclose(u, v, rtol=1e-12, atol=1e-300)
+        st = h.spec_stats()
+        assert st["hits"] >= 2 and st["edge_hits"] >= 1, st
+    finally:
+        h.close()
+        ref.close()
+
+
 def test_radial_equaln_level0_hint_switch(gpu):
     """set_level0_hint(False): repeated tiled calls on one handle re-read x
     every time — no call hinted — and return what the hinted calls return
