@@ -4,9 +4,9 @@ tools/run_leg.py profile N STEPS (FETCH_SIZE and WRITE_SIZE passes, csv):
 reads = 2 x FETCH_SIZE (gfx950: FETCH_SIZE counts half the bytes of wide
 streaming reads, MI355X_MICROARCH.md), writes = WRITE_SIZE, both KiB per
 dispatch, summed over the profile kernels.  A run_leg profile run makes
-2 warm-up + STEPS hinted calls and then max(20, STEPS // 10) cold-handle
-calls (level-0 hint off); the calls are told apart by their selection
-kernel (see main).
+2 warm-up + STEPS hinted calls and then max(20, STEPS // 10) first calls
+(forget_history); the calls are told apart by their selection kernel (see
+main).
 
 usage: python tools/pmc_profile.py FETCH_DIR WRITE_DIR N STEPS COMMIT OUT_JSON
 Writes OUT_JSON and, for bench.py's roofline "traffic", a copy at
@@ -51,12 +51,15 @@ def main():
     disp.sort()
     calls = []
     for d in disp:
-        if "select_tiles" in d[1] or not calls:
+        # a call starts at its selection, or at the sampled level-0 geometry
+        # launched just before a first call's selection
+        sampled_before = calls and calls[-1] and "sample_hint" in calls[-1][-1][1]
+        if "sample_hint" in d[1] or ("select_tiles" in d[1] and not sampled_before) or not calls:
             calls.append([])
         calls[-1].append(d)
     kinds = {"spec": [], "warm": [], "cold": []}
     for i, c in enumerate(calls):
-        sel = c[0][1]
+        sel = next((k for _, k, *_ in c if "select_tiles" in k), c[0][1])
         kind = "cold" if i >= 2 + steps else ("spec" if "true>" in sel.split("(")[0] else "warm")
         kinds[kind].append(c)
 
@@ -82,7 +85,8 @@ def main():
                        f"sum m + mean r, CSR (tools/run_leg.py profile {n} {steps})",
            "note": "per call: sum over the profile kernels of 2 x FETCH_SIZE + WRITE_SIZE; "
                    "spec = the steady state of a repeated call (the selection bins with the "
-                   "stored table), warm = hinted calls before that, cold = level-0 hint off",
+                   "stored table), warm = hinted calls before that, cold = a handle's first call "
+                   "(forget_history: its level-0 geometry sampled, the full assignment)",
            "spec": summary(kinds["spec"]), "warm": summary(kinds["warm"]),
            "cold": summary(kinds["cold"]), "source": str(Path(out))}
     steady = res["spec"] or res["warm"]
