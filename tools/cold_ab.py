@@ -4,8 +4,9 @@ device-resident positions, each timed call made a handle's first.
 mode "forget": forget_history() before every call (the sampled level-0
 geometry of a first call); mode "off": set_level0_hint(False) (every call
 re-reads x for its level-0 histogram — a first call before the sampler).
-usage: python tools/cold_ab.py N mode [reps]"""
+usage: python tools/cold_ab.py N mode [reps]   (COLD_STATS=none|w: fewer sums)"""
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -27,6 +28,8 @@ pos, mass = plummer(n, seed=1002)
 dm = family_slices(n)["dm"]
 d_pos, d_mass = nat.DeviceArray.from_host(pos), nat.DeviceArray.from_host(mass)
 stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, (1 << 0) | (1 << 1))]
+# COLD_STATS (diagnostic): "none" (counts only) or "w" (the mass sum only)
+stats = {"none": [], "w": [(SRC_W, SRC_NONE, 1 << 3)]}.get(os.environ.get("COLD_STATS", ""), stats)
 h = DeviceBins()
 e0, e1 = nat.Event(), nat.Event()
 
