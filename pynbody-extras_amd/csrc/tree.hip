@@ -2694,12 +2694,16 @@ static unsigned walk_xcd_chunk() {
   return c;
 }
 
-// small walk grids at 8 waves per SIMD (PBX_WALK_W8=0: off; =2: every grid)
+// fast order-3 walks at 8 waves per SIMD (walk_kernel<..., W8>): every grid
+// by default — the full 4M walk 31.15-31.20 -> 30.48-30.50 ms same box,
+// A/B/A/B (profiles/r5/r5z6/) although W8 parks 36 B in scratch outside the
+// loop; PBX_WALK_W8=1: only grids of at most one resident round (range
+// walks, the round-4 default), =0: never
 constexpr unsigned kNumSimd = 1024;  // 256 CUs x 4
 static int walk_w8() {
   static const int c = [] {
     const char *v = std::getenv("PBX_WALK_W8");
-    return v ? (v[0] == '0' ? 0 : v[0] == '2' ? 2 : 1) : 1;
+    return v ? (v[0] == '0' ? 0 : v[0] == '1' ? 1 : 2) : 2;
   }();
   return c;
 }

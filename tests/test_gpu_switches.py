@@ -29,7 +29,7 @@ GROUPS = {
                   "PBX_WALK_XCD_CHUNK": "0", "PBX_DIRECT_T": "1", "PBX_DIRECT_SYM": "0"},
     "profile_b": {"PBX_AGATHER": "0", "PBX_SEL_BT": "256", "PBX_RADIAL_MONO": "0",
                   "PBX_WALK_TPB": "256", "PBX_WALK_W8": "0", "PBX_DIRECT_T": "2"},
-    "profile_c": {"PBX_SEL_HINT": "0", "PBX_WALK_W8": "2"},
+    "profile_c": {"PBX_SEL_HINT": "0", "PBX_WALK_W8": "1"},
     "profile_d": {"PBX_RADIAL_EAGER": "1", "PBX_EQUALN": "sort"},
 }
 
