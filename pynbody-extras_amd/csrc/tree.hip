@@ -1833,6 +1833,131 @@ __global__ void __launch_bounds__(TPB)
   win[k] = (uint8_t)l;
 }
 
+// Range ends without path compares.  For sorted paths, path_lcp(i, j) =
+// min(eq[i+1 .. j]), so a node's range end is the first j > i with eq[j] < d
+// and its parent's start the last q <= i with eq[q] < d - 1.  eq_mins keeps
+// the minimum of every 64-byte line of eq (b1) and of every 64 lines (b2);
+// a search reads one line per level (eq, b1, b2, b1, eq: five dependent
+// 64-byte reads at most, plus a walk over b2 for the few nodes near the
+// root) instead of galloping plus bisection over the paths (~2 log2 of the
+// range dependent key loads: ~44 for the root at 4M).
+constexpr int EQ_LINE = 64;
+__global__ void __launch_bounds__(64)
+    eq_mins(const uint8_t *__restrict__ eq, int64_t n, uint8_t *__restrict__ b1,
+            uint8_t *__restrict__ b2) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;  // line of eq
+  const int64_t nb1 = (n + EQ_LINE - 1) / EQ_LINE;
+  uint32_t m = 255;
+  if (b < nb1) {
+    const int64_t j1 = (b + 1) * EQ_LINE < n ? (b + 1) * EQ_LINE : n;
+    for (int64_t j = b * EQ_LINE; j < j1; ++j) m = m < eq[j] ? m : eq[j];
+    b1[b] = (uint8_t)m;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t y = (uint32_t)__shfl_xor((int)m, o, 64);
+    m = m < y ? m : y;
+  }
+  if (threadIdx.x == 0) b2[blockIdx.x] = (uint8_t)m;
+}
+
+// the bytes of w below t (t <= 128), as their high bits: per byte
+// (x | 0x80) - t cannot borrow, and its high bit is clear iff x < t for x < 128
+__device__ __forceinline__ uint64_t bytes_lt(uint64_t w, uint64_t tt) {
+  constexpr uint64_t H = 0x8080808080808080ull;
+  return ~((w | H) - tt) & ~w & H;
+}
+// byte positions [lo, hi) of word k of a line (0 <= lo, hi <= 64)
+__device__ __forceinline__ uint64_t line_word_mask(int k, int lo, int hi) {
+  const int a = lo - 8 * k, b = hi - 8 * k;
+  const uint64_t up = b >= 8 ? ~0ull : (b <= 0 ? 0ull : (~0ull >> (64 - 8 * b)));
+  const uint64_t dn = a <= 0 ? ~0ull : (a >= 8 ? 0ull : (~0ull << (8 * a)));
+  return up & dn;
+}
+// the first (FWD) or last position j in [lo, hi) of the 64-byte line p
+// (16-byte aligned) whose byte is < t, or -1
+template <bool FWD>
+__device__ __forceinline__ int line_find_lt(const uint8_t *__restrict__ p, int lo, int hi,
+                                            uint64_t tt) {
+  const uint4 *q = (const uint4 *)p;
+  uint64_t w[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 v = q[k];
+    w[2 * k] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    w[2 * k + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
+  int r = -1;
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = FWD ? kk : 7 - kk;
+    const uint64_t f = bytes_lt(w[k], tt) & line_word_mask(k, lo, hi);
+    if (r < 0 && f)
+      r = 8 * k + (FWD ? __builtin_ctzll(f) : 63 - __builtin_clzll(f)) / 8;
+  }
+  return r;
+}
+// first j in [j0, n) with eq[j] < t (t <= 128), or n
+__device__ int64_t eq_next_lt(const uint8_t *__restrict__ eq, const uint8_t *__restrict__ b1,
+                              const uint8_t *__restrict__ b2, int64_t n, int64_t j0, int t) {
+  if (j0 >= n) return n;
+  const uint64_t tt = 0x0101010101010101ull * (uint64_t)t;
+  const int64_t nb1 = (n + EQ_LINE - 1) / EQ_LINE, nb2 = (nb1 + EQ_LINE - 1) / EQ_LINE;
+  auto lim = [](int64_t a, int64_t base) { return (int)(a - base < EQ_LINE ? a - base : EQ_LINE); };
+  int64_t b = j0 / EQ_LINE;
+  int r = line_find_lt<true>(eq + EQ_LINE * b, (int)(j0 - EQ_LINE * b), lim(n, EQ_LINE * b), tt);
+  if (r >= 0) return EQ_LINE * b + r;
+  int64_t c = b / EQ_LINE;  // the later lines of b's group of 64
+  r = line_find_lt<true>(b1 + EQ_LINE * c, (int)(b + 1 - EQ_LINE * c), lim(nb1, EQ_LINE * c), tt);
+  if (r < 0) {  // the later groups
+    int64_t g = c + 1, found = -1;
+    while (g < nb2) {
+      const int64_t L = g / EQ_LINE;
+      const int rr = line_find_lt<true>(b2 + EQ_LINE * L, (int)(g - EQ_LINE * L), lim(nb2, EQ_LINE * L), tt);
+      if (rr >= 0) {
+        found = EQ_LINE * L + rr;
+        break;
+      }
+      g = EQ_LINE * (L + 1);
+    }
+    if (found < 0) return n;
+    c = found;
+    r = line_find_lt<true>(b1 + EQ_LINE * c, 0, lim(nb1, EQ_LINE * c), tt);
+  }
+  b = EQ_LINE * c + r;
+  return EQ_LINE * b + line_find_lt<true>(eq + EQ_LINE * b, 0, lim(n, EQ_LINE * b), tt);
+}
+// last q in [0, i] with eq[q] < t (t <= 128), or -1
+__device__ int64_t eq_prev_lt(const uint8_t *__restrict__ eq, const uint8_t *__restrict__ b1,
+                              const uint8_t *__restrict__ b2, int64_t n, int64_t i, int t) {
+  if (i < 0) return -1;
+  const uint64_t tt = 0x0101010101010101ull * (uint64_t)t;
+  const int64_t nb1 = (n + EQ_LINE - 1) / EQ_LINE;
+  auto lim = [](int64_t a, int64_t base) { return (int)(a - base < EQ_LINE ? a - base : EQ_LINE); };
+  int64_t b = i / EQ_LINE;
+  int r = line_find_lt<false>(eq + EQ_LINE * b, 0, (int)(i - EQ_LINE * b + 1), tt);
+  if (r >= 0) return EQ_LINE * b + r;
+  int64_t c = b / EQ_LINE;  // the earlier lines of b's group
+  r = line_find_lt<false>(b1 + EQ_LINE * c, 0, (int)(b - EQ_LINE * c), tt);
+  if (r < 0) {  // the earlier groups
+    int64_t g = c - 1, found = -1;
+    while (g >= 0) {
+      const int64_t L = g / EQ_LINE;
+      const int rr = line_find_lt<false>(b2 + EQ_LINE * L, 0, (int)(g - EQ_LINE * L + 1), tt);
+      if (rr >= 0) {
+        found = EQ_LINE * L + rr;
+        break;
+      }
+      g = EQ_LINE * L - 1;
+    }
+    if (found < 0) return -1;
+    c = found;
+    r = line_find_lt<false>(b1 + EQ_LINE * c, 0, lim(nb1, EQ_LINE * c), tt);
+  }
+  b = EQ_LINE * c + r;
+  return EQ_LINE * b + line_find_lt<false>(eq + EQ_LINE * b, 0, lim(n, EQ_LINE * b), tt);
+}
+
 // fd(i), L(i) and the node count of every sorted position; level
 // histogram (LDS per block, one global add per level and block: the grid
 // is bounded, so those adds stay few — every block adds to the same words)
@@ -1916,6 +2041,7 @@ __global__ void bp_inverse(const int32_t *__restrict__ b2p, int64_t nn, int32_t 
 // slot); its parent's child count
 __global__ void __launch_bounds__(TPB)
     bp_nodes_bfs(const uint64_t *__restrict__ keys, int64_t n, int nw, const uint8_t *__restrict__ eq,
+                 const uint8_t *__restrict__ eb1, const uint8_t *__restrict__ eb2,
                  const uint8_t *__restrict__ fd,
                  const uint8_t *__restrict__ lv, const uint32_t *__restrict__ S,
                  const uint32_t *__restrict__ level, const int32_t *__restrict__ start,
@@ -1946,6 +2072,9 @@ __global__ void __launch_bounds__(TPB)
       if ((int)e[q] < d) q0 = q;
     if (q0 < 16 || i + 17 >= n) hi = lo = (i + 1 + q0 < n) ? i + 1 + q0 : n;
     else lo = i + 17;
+  }
+  if (lo < hi && eb1 && d <= 128) {  // the first eq < d at or after lo (eq_next_lt)
+    lo = hi = eq_next_lt(eq, eb1, eb2, n, lo, d);
   }
   for (int64_t step = 1; lo < hi;) {
     const int64_t probe = lo + step - 1 < hi ? lo + step - 1 : hi - 1;
@@ -1998,6 +2127,10 @@ __global__ void __launch_bounds__(TPB)
           if ((int)e[q] < d - 1) q0 = q;
         if (q0 < 16) a = b = (i - q0 > 0) ? i - q0 : 0;
         else b = i - 16;
+      }
+      if (a < b && eb1 && d - 1 <= 128) {  // the last eq < d - 1 at or before b (eq_prev_lt)
+        const int64_t q = eq_prev_lt(eq, eb1, eb2, n, b, d - 1);
+        a = b = q > 0 ? q : 0;
       }
       for (int64_t step = 1; a < b;) {  // galloping back
         const int64_t probe = b - step > a ? b - step : a;
@@ -2194,6 +2327,7 @@ struct Octree {
   Buf ck, kbuf, pbuf, pcost, pctr;          // their checkpoints, scratch, partial sums, counters
   int64_t ck_groups = 0, p_slots = 0;
   Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
+  Buf bp_emin;  // eq's line / group minima (eq_mins)
   Buf rec0;                  // {x, y, z, m} in original order (path_keys)
   bool rec0_valid = false;   // rec0 holds the current masses
   prim::HostBuf rm_pin;      // radial_moments readback staging
@@ -2201,7 +2335,7 @@ struct Octree {
     Buf *bufs[] = {&pos, &mass, &soft, &perm, &rec, &soft_s, &nstart, &ncount, &nfirst, &nnext,
                    &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &leaf_dfs, &keys, &ktmp0,
                    &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
-                   &counters, &trace, &bal, &iscan, &ilist, &iws, &bp_fl, &bp_eq, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
+                   &counters, &trace, &bal, &iscan, &ilist, &iws, &bp_fl, &bp_eq, &bp_emin, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
                    &bp_p2b, &wtab, &ck, &kbuf, &pbuf, &pcost, &pctr};
     for (Buf *b : bufs) b->release();
     rm_pin.release();
@@ -2332,7 +2466,8 @@ static bool split_parallel(Octree &T, hipStream_t st, int sorted_levels) {
   const size_t nctl = 3 + 2 * (size_t)BP_MAX_LEVEL + 1;
   unsigned int *ctl = (unsigned int *)T.bp_ctl.get(4 * nctl);
   PBX_HIP(hipMemsetAsync(ctl, 0, 4 * nctl, st));
-  uint8_t *eq = (uint8_t *)T.bp_eq.get(2 * (size_t)n + 16), *win = eq + n;
+  // (+128: eq_next_lt / eq_prev_lt read eq's last line whole)
+  uint8_t *eq = (uint8_t *)T.bp_eq.get(2 * (size_t)n + 128), *win = eq + n;
   hipLaunchKernelGGL(bp_lcp, dim3(nblk(n)), dim3(TPB), 0, st, keys, n, T.nwords, T.leaf_capacity,
                      eq, win);
   hipLaunchKernelGGL(bp_depth, dim3(std::min<unsigned>(BP_DEPTH_BLOCKS, nblk(n))), dim3(TPB), 0,
@@ -2388,8 +2523,12 @@ static bool split_parallel(Octree &T, hipStream_t st, int sorted_levels) {
   v.nchild = T.nchild.as<int32_t>();
   v.ncen = T.ncen.as<double4>();
   int32_t *size = (int32_t *)T.size.get(4 * (size_t)nn);
+  const int64_t nb1 = (n + EQ_LINE - 1) / EQ_LINE, nb2 = (nb1 + EQ_LINE - 1) / EQ_LINE;
+  const size_t l1 = (size_t)nb2 * EQ_LINE, l2 = ((size_t)nb2 + EQ_LINE - 1) / EQ_LINE * EQ_LINE;
+  uint8_t *eb1 = (uint8_t *)T.bp_emin.get(l1 + l2 + 64), *eb2 = eb1 + l1;
+  hipLaunchKernelGGL(eq_mins, dim3((unsigned)nb2), dim3(64), 0, st, (const uint8_t *)eq, n, eb1, eb2);
   hipLaunchKernelGGL(bp_nodes_bfs, dim3(nblk(nn)), dim3(TPB), 0, st, keys, n, T.nwords,
-                     (const uint8_t *)eq, (const uint8_t *)fd, (const uint8_t *)lv, (const uint32_t *)S,
+                     (const uint8_t *)eq, (const uint8_t *)eb1, (const uint8_t *)eb2, (const uint8_t *)fd, (const uint8_t *)lv, (const uint32_t *)S,
                      (const uint32_t *)level, (const int32_t *)startp, (const int32_t *)b2p,
                      (const int32_t *)p2b, nn,
                      make_double4(T.root[0], T.root[1], T.root[2], T.root[3]), v, size);
