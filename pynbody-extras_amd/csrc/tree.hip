@@ -1995,13 +1995,18 @@ __global__ void __launch_bounds__(TPB)
       cnt[i] = (uint32_t)(L >= f ? L - f + 1 : 0);
     }
     // nodes per level and of them internal ones (all but the deepest node
-    // starting at i): ballots per level and wave
+    // starting at i): ballots per level and wave, over the levels at which
+    // some lane of the wave starts a node (sorted paths: most start only
+    // their leaf, so [wave min f, wave max L] is a few levels, not 0 .. L)
     int dmax = ok ? L : -1;
+    int dmin = (ok && f <= L) ? f : BP_MAX_LEVEL + 1;
     for (int o = 32; o > 0; o >>= 1) {
       const int y = __shfl_xor(dmax, o, 64);
       dmax = y > dmax ? y : dmax;
+      const int z = __shfl_xor(dmin, o, 64);
+      dmin = z < dmin ? z : dmin;
     }
-    for (int d = 0; d <= dmax; ++d) {
+    for (int d = dmin; d <= dmax; ++d) {
       const uint32_t c = (uint32_t)__popcll(__ballot(ok && f <= d && d <= L));
       const uint32_t ci = (uint32_t)__popcll(__ballot(ok && f <= d && d < L));
       if ((threadIdx.x & 63) == 0 && c) atomicAdd(&h[d], c);
