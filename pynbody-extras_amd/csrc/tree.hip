@@ -2914,6 +2914,10 @@ static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
     hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
   else if (lcost)
     hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, true>), dim3(grid), dim3(tpb), 0, st, wp);
+  else if (P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC) && tpb == 64 &&
+           ((waves <= 8u * kNumSimd && walk_w8()) || walk_w8() == 2))  // precise, 8 waves per SIMD
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false, true>), dim3(grid), dim3(tpb), 0,
+                       st, wp);
   else
     hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false>), dim3(grid), dim3(tpb), 0, st, wp);
 }
