@@ -497,6 +497,29 @@ __global__ void leaf_sort(const int32_t *__restrict__ nchild, const int32_t *__r
   int64_t k = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (k >= nn || nchild[k] != 0) return;
   const int32_t s = nstart[k], c = ncount[k];
+  if (c <= 8) {  // in registers: a fixed sorting network (odd-even merge, 19
+                 // compare-exchanges) — not an insertion sort whose every
+                 // step is a dependent global read (~28 of them in a full leaf)
+    constexpr int32_t PAD = 0x7fffffff;  // (original indices are < 2^31 - 1)
+    int32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = q < c ? perm[s + q] : PAD;
+    auto cx = [&](int a, int b) {
+      const int32_t lo = v[a] < v[b] ? v[a] : v[b], hi = v[a] < v[b] ? v[b] : v[a];
+      v[a] = lo;
+      v[b] = hi;
+    };
+    cx(0, 1); cx(2, 3); cx(4, 5); cx(6, 7);
+    cx(0, 2); cx(1, 3); cx(4, 6); cx(5, 7);
+    cx(1, 2); cx(5, 6);
+    cx(0, 4); cx(1, 5); cx(2, 6); cx(3, 7);
+    cx(2, 4); cx(3, 5);
+    cx(1, 2); cx(3, 4); cx(5, 6);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < c) perm[s + q] = v[q];
+    return;
+  }
   for (int32_t i = s + 1; i < s + c; ++i) {
     int32_t v = perm[i];
     int32_t j = i - 1;
