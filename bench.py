@@ -147,8 +147,8 @@ def cpu_baseline(pos, mass, seconds: float, cores: int | None = None):
         "unit": "pairs/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{k} random targets x {n} sources (all-particles Newtonian force+potential, "
-                  f"oracle/gravity_ref.c, OpenMP {cores} threads, {dt:.1f} s)",
+        "sample": f"{k} random targets x {n} sources, oracle/gravity_ref.c, {cores} OpenMP "
+                  f"threads, {dt:.1f} s",
         **cpu_host(),
     }
 
@@ -163,9 +163,11 @@ def cpu_rows(many: dict, one: dict) -> dict:
     the harness's rule for worker pools), so the all-cores row is the
     16-thread rate scaled linearly to the affinity count — an upper bound
     on what rayon could reach there (perfect scaling), not a run."""
-    many["single_core"] = {k: one[k] for k in ("value", "cores", "sample")}
     aff = len(os.sched_getaffinity(0))
+    many["single_core_value"] = one["value"]
     many["threads_scaling_efficiency"] = many["value"] / (many["cores"] * one["value"])
+    many["all_affinity_cores_bound_value"] = many["value"] * aff / many["cores"]
+    many["single_core"] = {k: one[k] for k in ("value", "cores", "sample")}
     many["all_affinity_cores_bound"] = {
         "value": many["value"] * aff / many["cores"], "cores": aff,
         "kind": "linear extrapolation (upper bound), not run",
@@ -230,6 +232,93 @@ def dist_profile_parity(rank: int, world: int, n: int, res, counts):
             "mass_sum_max_rel": float(np.nanmax(rel))}
 
 
+N_CHANGING = 4  # distinct snapshots one handle cycles through (the base one + 3)
+
+
+def _stats_delta(a: dict, b: dict) -> dict:
+    return {k: b[k] - a[k] for k in a}
+
+
+def changing_snapshots(n: int, steps: int, single, dev, d_pos, d_mass, e0, e1, cpu: bool) -> dict:
+    """The profile step on inputs that change between calls: one handle
+    cycles through N_CHANGING distinct snapshots of the same workload (the
+    base snapshot and 3 more Plummer spheres of other seeds, drawn by
+    synthetic.plummer_chunked), every call a different particle set than the
+    previous one, as a user profiling successive outputs of a simulation
+    would.  The reference recomputes the bins on every BinsSet.__call__
+    (bins.py:397-457).  Reports the median stream / wall time per call and
+    the hit rates of the handle's speculation; the last snapshot's results
+    are checked bit-exact against a fresh handle's first call on it (and, at
+    n <= 16M with the CPU legs on, against the oracle)."""
+    from pynbodyext.profiles._device import DeviceBins
+    from pynbodyext.synthetic import family_slices, plummer_chunked
+
+    snaps = [(d_pos, d_mass, None)]
+    for k in range(1, N_CHANGING):
+        p, m = plummer_chunked(n, seed=SEEDS.get(n, 1002) + 104729 * k,
+                               threads=min(16, host_cores()))
+        snaps.append((nat.DeviceArray.from_host(p), nat.DeviceArray.from_host(m),
+                      p if (cpu and n <= 16_000_000) else None))
+        del m
+    calls = max(8 * N_CHANGING, steps)
+    calls -= calls % N_CHANGING
+    s0 = (dev.spec_stats(), dev.level0_stats(), dev.mono_stats(), dev.path_stats())
+    for k in range(N_CHANGING):  # every snapshot once before the timed calls
+        single(snaps[k][0].ptr, snaps[k][1].ptr, dev)
+    nat.synchronize()
+    s1 = (dev.spec_stats(), dev.level0_stats(), dev.mono_stats(), dev.path_stats())
+    ct, cd = [], []
+    res = None
+    for i in range(calls):
+        pp, mp, _ = snaps[i % N_CHANGING]
+        t0 = time.perf_counter()
+        e0.record()
+        res = single(pp.ptr, mp.ptr, dev)
+        e1.record()
+        nat.synchronize()
+        ct.append(time.perf_counter() - t0)
+        cd.append(e0.elapsed_ms(e1))
+    s2 = (dev.spec_stats(), dev.level0_stats(), dev.mono_stats(), dev.path_stats())
+    last = snaps[(calls - 1) % N_CHANGING]
+    fresh = DeviceBins()
+    fr = single(last[0].ptr, last[1].ptr, fresh)
+    perm_a, offs_a = dev.csr()
+    perm_b, offs_b = fresh.csr()
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ms = np.abs(res[1] - fr[1]) / np.abs(fr[1])
+    check = {"vs": "a fresh handle's first call on the same snapshot (no speculation)",
+             "edges_bit_exact": bool(np.array_equal(res[0], fr[0])),
+             "counts_bit_exact": bool(np.array_equal(dev.counts, fresh.counts)),
+             "csr_bit_exact": bool(np.array_equal(perm_a, perm_b) and np.array_equal(offs_a, offs_b)),
+             "mass_sum_max_rel": float(np.nanmax(ms))}
+    if last[2] is not None:
+        from oracle import profile_ref as pr
+
+        dm = family_slices(n)["dm"]
+        mask = pr.sphere_mask(last[2], 10.0)
+        mask[dm.stop:] = False
+        ref = pr.radial_profile(last[2], np.full(n, 1.0 / n), mask, "equaln", 128)
+        check["vs_oracle"] = profile_parity(dev, res, ref)
+    fresh.close()
+    for pp, mp, _ in snaps[1:]:
+        pp.free()
+        mp.free()
+    td = float(np.median(cd))
+    delta = [dict(zip(("speculation", "level0", "one_launch", "path"),
+                      [_stats_delta(a, b) for a, b in zip(x, y)])) for x, y in ((s0, s1), (s1, s2))]
+    return {"snapshots": N_CHANGING, "calls": calls, "stream_ms": td,
+            "stream_ms_p90": float(np.percentile(cd, 90)),
+            "ms": float(np.median(ct)) * 1e3,
+            "particles_per_s_stream": n / (td * 1e-3),
+            "particles_per_s_wall": n / (float(np.median(ct))),
+            "hbm_gbs_algorithmic": n * PROFILE_BYTES_PER_PARTICLE / (td * 1e-3) / 1e9,
+            "frac": n * PROFILE_BYTES_PER_PARTICLE / (td * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "handle_stats_timed_calls": delta[1], "handle_stats_first_pass": delta[0],
+            "parity": check,
+            "seeds": [SEEDS.get(n, 1002)] + [SEEDS.get(n, 1002) + 104729 * k
+                                             for k in range(1, N_CHANGING)]}
+
+
 def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
     """Config 3: RadialProfileBuilder(ndim=3, weight='mass', equaln, 128 bins)
     behind Sphere(R=10) & FamilyFilter('dm'), positions / masses resident in
@@ -268,13 +357,16 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
 
         staged = os.environ.get("PBX_BENCH_STAGED") == "1"
 
+        def single(pp, mp, into):  # selection, edges, counts, CSR and sums: one host round trip
+            _, edges, _, (msum, rmean) = DeviceBins.radial_equaln(
+                pp, mp, nbins=128, sphere=((0.0, 0.0, 0.0), 10.0),
+                families=[(dm.start, dm.stop)], ndim=3, stats=stats, csr=True,
+                on_device=True, n=n, into=into)
+            return edges, msum[:, 3], rmean
+
         def step():
-            if comm is None:  # selection, edges, counts, CSR and sums: one host round trip
-                _, edges, _, (msum, rmean) = DeviceBins.radial_equaln(
-                    d_pos.ptr, d_mass.ptr, nbins=128, sphere=((0.0, 0.0, 0.0), 10.0),
-                    families=[(dm.start, dm.stop)], ndim=3, stats=stats, csr=True,
-                    on_device=True, n=n, into=dev)
-                return edges, msum[:, 3], rmean
+            if comm is None:
+                return single(d_pos.ptr, d_mass.ptr, dev)
             if not staged:  # the same pipeline with device all-reduces between its kernels
                 edges, counts, (msum, rmean) = sp.radial_equaln(
                     d_pos.ptr, d_mass.ptr, nbins=128, sphere=((0.0, 0.0, 0.0), 10.0),
@@ -317,32 +409,32 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                "hbm_gbs_algorithmic_per_gpu": n * PROFILE_BYTES_PER_PARTICLE / td / 1e9,
                "stream_ms": td * 1e3}
         if dist is None:
-            row["path"] = dev.path_stats()  # one-launch / discarded / multi-kernel calls
-            lv = dev.level0_stats()
-            if lv["tiled"]:
-                # the steps above reuse the previous call's level-0 digit
-                # geometry and, once two calls in a row had the same level-0
-                # digits, bin with the stored table inside the selection (same
-                # snapshot every call); a first call or a new snapshot re-reads
-                # x for its level-0 histogram and takes the assignment pass:
-                # time that too
-                row["level0_hinted_calls"] = lv
-                row["speculated_calls"] = dev.spec_stats()
-                ct, cd = [], []
-                for _ in range(max(20, steps // 10)):
-                    dev.forget_history()  # the next call runs as the handle's first
-                    t0 = time.perf_counter()
-                    e0.record()
-                    step()
-                    e1.record()
-                    nat.synchronize()
-                    ct.append(time.perf_counter() - t0)
-                    cd.append(e0.elapsed_ms(e1))
-                row["cold_ms"] = float(np.median(ct)) * 1e3
-                row["cold_stream_ms"] = float(np.median(cd))
-                row["cold_note"] = ("every call a handle's first (forget_history: no earlier "
-                                    "geometry or speculation state): the level-0 geometry sampled "
-                                    "from the keys (sample_hint), the full assignment pass")
+            # the rows above are ONE snapshot called again and again (a profile
+            # per statistic): the handle reuses the previous call's level-0
+            # geometry and speculates on its bin table and edges
+            row["identical_snapshot"] = {"stream_ms": row["stream_ms"], "ms": row["ms"],
+                                         "path": dev.path_stats(), "mono": dev.mono_stats(),
+                                         "level0_hinted_calls": dev.level0_stats(),
+                                         "speculated_calls": dev.spec_stats()}
+            # a first call on every step: no earlier geometry or speculation state
+            ct, cd = [], []
+            for _ in range(max(20, steps // 10)):
+                dev.forget_history()  # the next call runs as the handle's first
+                t0 = time.perf_counter()
+                e0.record()
+                step()
+                e1.record()
+                nat.synchronize()
+                ct.append(time.perf_counter() - t0)
+                cd.append(e0.elapsed_ms(e1))
+            row["cold_ms"] = float(np.median(ct)) * 1e3
+            row["cold_stream_ms"] = float(np.median(cd))
+            row["cold_note"] = ("every call a handle's first (forget_history: no earlier "
+                                "geometry or speculation state)")
+            row["changing"] = changing_snapshots(n, steps, single, dev, d_pos, d_mass, e0, e1,
+                                                 cpu)
+            # the handle's CSR of the base snapshot again (the parity check below)
+            res = single(d_pos.ptr, d_mass.ptr, dev)
         out.append(row)
         if cpu and world == 1:
             from oracle import profile_ref as pr
@@ -377,12 +469,32 @@ TREE_FLOP_NODE = 94   # order-3 force+potential node interaction incl. opening t
 TREE_FLOP_PP = 22     # leaf pair, same algorithmic count as the direct sum
 
 
-def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc,
+def tree_outputs(solver, n: int):
+    """(potential, acceleration) of the solver's last walk in original
+    particle order (the walk writes them in leaf order)."""
+    pot = np.empty(n)
+    acc = np.empty((n, 3))
+    idx = nat.DeviceArray(8 * n)
+    solver.tree._leaf_particles_device(0, n, None, None, idx.ptr)
+    order = np.empty(n, dtype=np.int64)
+    idx.download(order)
+    tmp = np.empty(n)
+    solver.d_pot.download(tmp)
+    pot[order] = tmp
+    tmp3 = np.empty((n, 3))
+    solver.d_acc.download(tmp3)
+    acc[order] = tmp3
+    idx.free()
+    return pot, acc
+
+
+def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu: dict,
                       cores: int | None = None):
     """Oracle restatement of tree.rs (serial build + payload like the
     reference, OpenMP walk over a bounded random target sample); returns the
-    extrapolated full-solve rate in effective pairs/s and the parity of the
-    GPU values on the sampled targets."""
+    extrapolated full-solve rate in effective pairs/s and, for every
+    (potential, acceleration) pair in ``gpu``, the parity of the GPU values on
+    the sampled targets."""
     from oracle import gravity as og
     from oracle import tree as ot
 
@@ -403,8 +515,12 @@ def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc,
     pot, acc, _, _ = ref.compute_subset(idx, theta)
     t_walk = time.perf_counter() - t0
     t_full = t_build + t_walk * n / k
-    rp = float(np.max(np.abs(gpu_pot[idx] - pot) / np.abs(pot)))
-    ra = float(np.max(np.linalg.norm(gpu_acc[idx] - acc, axis=1) / np.linalg.norm(acc, axis=1)))
+    par = {}
+    for name, (gpu_pot, gpu_acc) in gpu.items():
+        par[name] = {"targets_checked": k,
+                     "pot_max_rel": float(np.max(np.abs(gpu_pot[idx] - pot) / np.abs(pot))),
+                     "acc_max_rel": float(np.max(np.linalg.norm(gpu_acc[idx] - acc, axis=1) /
+                                                 np.linalg.norm(acc, axis=1)))}
     return {
         "value": float(n) * float(n - 1) / t_full,
         "unit": "effective pairs/s",
@@ -414,7 +530,7 @@ def tree_cpu_baseline(pos, mass, seconds: float, theta: float, gpu_pot, gpu_acc,
                   f"walk of {k} random targets on {cores} OpenMP threads ({t_walk:.1f} s), "
                   f"full solve extrapolated to {t_full:.1f} s",
         **cpu_host(),
-    }, {"targets_checked": k, "pot_max_rel": rp, "acc_max_rel": ra}
+    }, par
 
 
 def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: float):
@@ -478,6 +594,10 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
     build_ms, bal_ms, walk_ms, share_ms, prof_ms = (float(np.median([p[i] for p in parts]))
                                                     for i in range(5))
     info = solver.info
+    check = cpu and dist.world == 1 and dist.rank == 0
+    # the outputs of the last timed (fast-mode, headline) step, before the
+    # precise-mode steps below overwrite them
+    fast_out = tree_outputs(solver, n) if check else None
     solver.set_walk_counters(True)
     with nat.precise_mode(True):  # the walk in precise mode, beside the fast headline
         pw = []
@@ -526,23 +646,15 @@ def bench_tree(dist, n: int, steps: int, warmup: int, cpu: bool, cpu_seconds: fl
                           "phi_innermost_bin": float(phi_profile[mom[:, 0] > 0][0]),
                           "phi_outermost_bin": float(phi_profile[mom[:, 0] > 0][-1])},
     }
-    if cpu and dist.world == 1 and dist.rank == 0:
-        pot = np.empty(n)
-        acc = np.empty((n, 3))
-        # compact leaf-order outputs -> original order
-        idx = nat.DeviceArray(8 * n)
-        solver.tree._leaf_particles_device(0, n, None, None, idx.ptr)
-        order = np.empty(n, dtype=np.int64)
-        idx.download(order)
-        tmp = np.empty(n)
-        solver.d_pot.download(tmp)
-        pot[order] = tmp
-        tmp3 = np.empty((n, 3))
-        solver.d_acc.download(tmp3)
-        acc[order] = tmp3
-        idx.free()
-        many, out["parity_vs_oracle"] = tree_cpu_baseline(pos, mass, cpu_seconds, theta, pot, acc)
-        one, _ = tree_cpu_baseline(pos, mass, cpu_seconds / 2, theta, pot, acc, cores=1)
+    if check:
+        precise_out = tree_outputs(solver, n)  # the last precise-mode step's
+        many, par = tree_cpu_baseline(pos, mass, cpu_seconds, theta,
+                                      {"fast": fast_out, "precise": precise_out})
+        # the headline (fast-mode) walk's outputs; the precise walk's beside them
+        out["parity_vs_oracle"] = {**par["fast"], "mode": "fast (the timed walk)",
+                                   "precise_pot_max_rel": par["precise"]["pot_max_rel"],
+                                   "precise_acc_max_rel": par["precise"]["acc_max_rel"]}
+        one, _ = tree_cpu_baseline(pos, mass, cpu_seconds / 2, theta, {}, cores=1)
         out["cpu_baseline"] = cpu_rows(many, one)
     solver.close()
     prof.close()
@@ -654,9 +766,11 @@ def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
                     "PCIe-inclusive user-facing times, not the bench value"}
 
 
-def pmc_profile_step_bytes(n: int):
-    """HBM bytes of one n-particle profile step from the committed PMC
-    summary (profiles/pmc_profile_latest.json, collected at its "n")."""
+def pmc_profile_step_bytes(n: int, inputs: str = "identical"):
+    """HBM bytes of one n-particle profile call from the committed PMC
+    summary (profiles/pmc_profile_<N>M.json, collected at its "n"): a call on
+    a changing snapshot ("changing": hbm_bytes_per_step_changing) or a
+    repeated one ("identical": hbm_bytes_per_step)."""
     for f in (ROOT / "profiles" / f"pmc_profile_{n // 1_000_000}M.json",
               ROOT / "profiles" / "pmc_profile_latest.json"):
         if not f.exists():
@@ -664,7 +778,8 @@ def pmc_profile_step_bytes(n: int):
         try:
             d = json.loads(f.read_text())
             if int(d.get("n", 64_000_000)) == n:
-                return d.get("hbm_bytes_per_step"), str(f.relative_to(ROOT))
+                key = "hbm_bytes_per_step_changing" if inputs == "changing" else "hbm_bytes_per_step"
+                return d.get(key), str(f.relative_to(ROOT))
         except Exception:
             continue
     return None, None
@@ -738,9 +853,7 @@ def executed_issue(symmetric: bool, pairs_launch: float, kern_ms: float) -> dict
     instr = pairs_launch / 2 * SYM_INSTR_PER_UNORDERED_PAIR
     rate = instr / (kern_ms * 1e-3)
     return {"executed_fp64_instr_per_unordered_pair": SYM_INSTR_PER_UNORDERED_PAIR,
-            "executed_issue_frac": rate / FP64_LANE_INSTR_PEAK,
-            "executed_issue_note": "FP64 lane-instructions the kernel actually issues / the "
-                                   "FP64 VALU issue peak (39.3e12/s)"}
+            "executed_issue_frac": rate / FP64_LANE_INSTR_PEAK}
 
 
 def main():
@@ -876,39 +989,59 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved_tf / FP64_VECTOR_PEAK_TFLOPS,
             "traffic": traffic,
+            **{f"precise_{k}": v for k, v in precise_row(pairs_launch * FLOP_PER_PAIR,
+                                                          precise_ms).items()
+               if k in ("kernel_ms", "achieved", "frac")},
             "traffic_source": traffic_src,
             "kernel": "sym_kernel<pot+acc> (each unordered pair once)" if solver.symmetric else "direct_kernel<Newtonian, pot+acc, self-skip>",
             "mode": "precise" if nat.get_precise() else "fast",
-            "mode_note": "fast: v_rsq_f64 unrefined (~5e-8 per pair, <= 1e-7 vs the oracle); "
-                         "precise: + one Newton step (pbx_set_precise)",
             "flop_per_pair": FLOP_PER_PAIR,
             "kernel_ms": kern_avg_ms,
-            "frac_is": "algorithmic: 22 flop per ORDERED pair delivered (SURVEY.md §8d)",
             **executed_issue(solver.symmetric, pairs_launch, kern_avg_ms),
-            "precise": precise_row(pairs_launch * FLOP_PER_PAIR, precise_ms),
         },
+        "roofline_notes": {
+            "mode": "fast: v_rsq_f64 unrefined (~5e-8 per pair, <= 1e-7 vs the oracle); "
+                    "precise: + one Newton step (pbx_set_precise); precise_* = the same launch "
+                    "in precise mode, not the headline",
+            "frac": "algorithmic: 22 flop per ORDERED pair delivered (SURVEY.md §8d)",
+            "executed_issue": "FP64 lane-instructions the kernel actually issues / the FP64 VALU "
+                              "issue peak (39.3e12/s)"},
         "cpu_baseline": cpu,
         "api_level": api,
     }
     if sweep is not None:
         head = sweep[0]
-        big = max(sweep, key=lambda r: r["hbm_gbs_algorithmic_per_gpu"])
+
+        def chg(r):  # the changing-input figures of a sweep row (single rank)
+            return r.get("changing") or {}
+
+        def rate(r):  # the credited rate: changing inputs where measured
+            return chg(r).get("hbm_gbs_algorithmic", r["hbm_gbs_algorithmic_per_gpu"])
+
+        big = max(sweep, key=rate)
+        credited = "changing" if chg(big) else "identical"
         # counter-based: the PMC run's HBM bytes per step over this run's stream time
         counter = None
         for r in sweep:
-            b, bsrc = pmc_profile_step_bytes(r["n_per_gpu"])
+            b, bsrc = pmc_profile_step_bytes(r["n_per_gpu"], credited)
             if b:
-                gbs = b / (r["stream_ms"] * 1e-3) / 1e9
-                counter = {"n_per_gpu": r["n_per_gpu"], "hbm_bytes_per_step": b,
+                sm = chg(r).get("stream_ms", r["stream_ms"])
+                gbs = b / (sm * 1e-3) / 1e9
+                counter = {"n_per_gpu": r["n_per_gpu"], "inputs": credited,
+                           "hbm_bytes_per_step": b,
                            "achieved_gbs": gbs, "frac_of_spec": gbs / HBM_PEAK_GBS,
                            "frac_of_measured_copy_6290": gbs / 6290.0,
                            "source": f"{bsrc} (2 x FETCH_SIZE + WRITE_SIZE of every profile "
-                                     "kernel, steady-state calls) / this run's stream_ms"}
+                                     "kernel, per call) / this run's stream_ms"}
+        value = chg(head).get("particles_per_s_wall", head["particles_per_s"])
         out["profile"] = {
             "metric": "particles/sec (RadialProfileBuilder equaln 128, Sphere&FamilyFilter, "
                       "weight=mass)",
-            "value": head["particles_per_s"],
+            "value": value,
             "unit": "particles/s",
+            "inputs": ("a different snapshot every call (one handle cycling through "
+                       f"{N_CHANGING} snapshots)" if chg(head) else "one snapshot, repeated"),
+            "identical_snapshot_value": head["particles_per_s"],
             "config": {"workload": f"{head['n_per_gpu']}-particle Plummer sphere per GPU "
                                    f"(x{world}), Sphere(R=10) & FamilyFilter('dm'), equaln 128 "
                                    "bins, mass sum + mean r"
@@ -916,22 +1049,31 @@ def main():
                                       if world > 1 else ""),
                        "kept_rank0": head["n_kept_rank0"]},
             "scaling": "weak",
-            "roofline": {"bound": "hbm", "achieved": big["hbm_gbs_algorithmic_per_gpu"],
+            "roofline": {"bound": "hbm", "achieved": rate(big),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": big["hbm_gbs_algorithmic_per_gpu"] / HBM_PEAK_GBS,
+                         "frac": rate(big) / HBM_PEAK_GBS,
+                         "inputs": credited,
                          "at_n_per_gpu": big["n_per_gpu"],
+                         "stream_ms": chg(big).get("stream_ms", big["stream_ms"]),
+                         "identical_snapshot_frac": big["hbm_gbs_algorithmic_per_gpu"] / HBM_PEAK_GBS,
+                         "identical_snapshot_stream_ms": big["stream_ms"],
+                         "cold_frac": (big["n_per_gpu"] * PROFILE_BYTES_PER_PARTICLE /
+                                       (big["cold_stream_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                                      if big.get("cold_stream_ms") else None,
+                         "cold_stream_ms": big.get("cold_stream_ms"),
                          "bytes_per_particle": PROFILE_BYTES_PER_PARTICLE,
-                         "traffic": pmc_profile_step_bytes(big["n_per_gpu"])[0],
-                         "traffic_note": "HBM bytes per step at at_n_per_gpu (all profile "
+                         "traffic": pmc_profile_step_bytes(big["n_per_gpu"], credited)[0],
+                         "traffic_note": "HBM bytes per call at at_n_per_gpu (all profile "
                                          "kernels: 2 x FETCH_SIZE + WRITE_SIZE, PMC runs "
                                          "committed as profiles/pmc_profile_<N>M.json)"},
             "counter_roofline": counter,
-            "cold_handle": {"n_per_gpu": big["n_per_gpu"], "stream_ms": big.get("cold_stream_ms"),
-                            "ms": big.get("cold_ms"), "warm_stream_ms": big["stream_ms"],
-                            "frac_cold": (big["n_per_gpu"] * PROFILE_BYTES_PER_PARTICLE /
-                                          (big["cold_stream_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
-                            if big.get("cold_stream_ms") else None},
+            "by_size": [{"n_per_gpu": r["n_per_gpu"],
+                         "changing_stream_ms": chg(r).get("stream_ms"),
+                         "changing_frac": chg(r).get("frac"),
+                         "cold_stream_ms": r.get("cold_stream_ms"),
+                         "identical_stream_ms": r["stream_ms"]} for r in sweep],
             "parity_at_roofline_point": big.get("parity_vs_oracle"),
+            "changing_parity_at_roofline_point": chg(big).get("parity"),
             "api_level": prof_api,
             "one_launch_discards": (head.get("path") or {}).get("mono_discarded"),
             "sweep": sweep,

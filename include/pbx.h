@@ -239,29 +239,6 @@ int pbx_octree_balance(pbx_octree *tree, const int32_t *d_cost_orig, int world, 
  * 4-record leaf rounds, the same for the 64 targets of one wave), which is
  * what a walk's time follows — ShardedTree balances on it. */
 int pbx_octree_set_cost_kind(pbx_octree *tree, int kind);
-/* Wave split for range walks (speed only, every target's result unchanged):
- * d_cost_orig = device array of n per-particle costs in ORIGINAL particle
- * order from an earlier walk (cost kind 1: the wave's work, e.g. after
- * pbx_octree_cost_to_orig — what ShardedTree all-gathers).  Every later
- * self-mode walk (64-thread walk blocks) splits the 64-target groups whose
- * cost is >= permille/1000 of the largest into two 32-target waves,
- * dispatched first (at most 1/8 of the groups): a range walk ends with its
- * longest wave, and a smaller wave walks a shorter union of its targets'
- * walks.  NULL disables it; the array must stay valid while it is set. */
-int pbx_octree_set_wave_split(pbx_octree *tree, const int32_t *d_cost_orig, int permille);
-/* Preorder pieces (config 5's critical path; no reference counterpart — the
- * reference parallelises over targets only, tree.rs:1443-1450): self-mode
- * walks of order 3 without softening, potential + acceleration, run their
- * 64-target waves from a table, and a wave whose previous walk took more than
- * permille / 1000 of the longest one's steps is cut into up to kmax pieces by
- * DFS preorder id interval at its previous walk's node checkpoints
- * (tree.rs:736-776: the walk visits nodes in preorder, so each piece is the
- * lane's own walk restricted to an id interval; opening decisions and
- * interaction counts are those of the whole walk, the sums of a split wave
- * are added in piece order).  Pieces are listed longest first.  permille 0:
- * the table and checkpoints only (no split); -1: off (default).  Per-group
- * state is keyed by leaf-order position / 64. */
-int pbx_octree_set_walk_pieces(pbx_octree *tree, int permille, int kmax);
 /* Walk statistics on (1, default) or off (0) for this tree's later walks of
  * order 3 with potential + acceleration, no softening, in fast mode (no
  * reference counterpart: instrumentation).  Off, pbx_octree_info reports zero

@@ -233,38 +233,17 @@ __global__ void __launch_bounds__(kBlock)
                         mass ? mass[i] : 1.0);
 }
 
-// Targets per lane.  4 is the default (measured +2% over 2, +6% over 1);
-// PBX_DIRECT_T=1|2 selects the other instantiations (tuning experiments).
-static int targets_per_lane() {
-  static int t = [] {
-    const char *v = std::getenv("PBX_DIRECT_T");
-    int x = v ? std::atoi(v) : 4;
-    return (x == 1 || x == 2) ? x : 4;
-  }();
-  return t;
-}
+// Targets per lane: 4 (measured +2 % over 2, +6 % over 1).
+constexpr int kTargetsPerLane = 4;
 
 template <int KERN, int WANT, bool SELF>
 static void launch_variant(hipStream_t st, dim3 grid, const double4 *src, const double *src_h,
                            int has_h, int64_t n_src, int64_t chunk, const double *tgt,
                            const double *tgt_h, int64_t n_tgt, int64_t self_offset,
                            double *pot, double *acc, int64_t stride) {
-  switch (targets_per_lane()) {
-    case 1:
-      hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, 1>), grid, dim3(kBlock), 0, st, src,
-                         src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
-                         stride);
-      break;
-    case 4:
-      hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, 4>), grid, dim3(kBlock), 0, st, src,
-                         src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
-                         stride);
-      break;
-    default:
-      hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, 2>), grid, dim3(kBlock), 0, st, src,
-                         src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
-                         stride);
-  }
+  hipLaunchKernelGGL((direct_kernel<KERN, WANT, SELF, kTargetsPerLane>), grid, dim3(kBlock), 0,
+                     st, src, src_h, has_h, n_src, chunk, tgt, tgt_h, n_tgt, self_offset, pot, acc,
+                     stride);
 }
 
 template <int KERN, int WANT>
@@ -310,15 +289,8 @@ void sym_finish(Device &d, const double *acc4, int64_t lo, int64_t hi, int want,
                 double *acc);
 
 // All-particles Newtonian sums of at least this many particles evaluate each
-// unordered pair once (direct_sym.hip); PBX_DIRECT_SYM=0 disables it.
+// unordered pair once (direct_sym.hip).
 static constexpr int64_t kSymMinN = 8192;
-static bool sym_enabled() {
-  static bool on = [] {
-    const char *v = std::getenv("PBX_DIRECT_SYM");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
 
 // Launch the direct sum on device-resident data (all pointers device).
 void direct_device(Device &d, const double *src, const double *src_h, int64_t n_src,
@@ -326,8 +298,7 @@ void direct_device(Device &d, const double *src, const double *src_h, int64_t n_
                    int kernel, int want, double *pot, double *acc) {
   if (n_tgt <= 0) return;
   hipStream_t st = d.stream;
-  if (kernel == PBX_KERNEL_NONE && self_offset == 0 && n_tgt == n_src && n_src >= kSymMinN &&
-      sym_enabled()) {
+  if (kernel == PBX_KERNEL_NONE && self_offset == 0 && n_tgt == n_src && n_src >= kSymMinN) {
     const int64_t npad = sym_padded(n_src);
     double4 *rec = (double4 *)d.slot(kSlotSymRec).ensure(sizeof(double4) * npad);
     double *acc4 = (double *)d.slot(kSlotSymAcc).ensure(sizeof(double) * 4 * npad);
@@ -342,7 +313,7 @@ void direct_device(Device &d, const double *src, const double *src_h, int64_t n_
     if (want & PBX_WANT_ACC) PBX_HIP(hipMemsetAsync(acc, 0, sizeof(double) * 3 * n_tgt, st));
     return;
   }
-  const int64_t per_block = (int64_t)kBlock * targets_per_lane();
+  const int64_t per_block = (int64_t)kBlock * kTargetsPerLane;
   const int64_t bx = (n_tgt + per_block - 1) / per_block;
   // Aim for >= 2048 blocks (8 per CU) but keep >= 4096 sources per split.
   int64_t nsplit = (2048 + bx - 1) / bx;

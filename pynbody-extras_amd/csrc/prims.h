@@ -559,10 +559,6 @@ static inline void scan_u32(Buf &ws, hipStream_t st, uint32_t *a, int64_t len) {
     ws.epoch = 1;
   }
   uint64_t *w = (uint64_t *)ws.p;
-  static const int ticket_env = [] {  // A/B: PBX_SCAN_TICKET=1 always draws tickets
-    const char *v = std::getenv("PBX_SCAN_TICKET");
-    return v ? std::atoi(v) : -1;
-  }();
   static const int64_t resident = [] {  // blocks resident at once on this device
     int dev = 0, cus = 0, per = 0;
     PBX_HIP(hipGetDevice(&dev));
@@ -571,7 +567,9 @@ static inline void scan_u32(Buf &ws, hipStream_t st, uint32_t *a, int64_t len) {
         &per, reinterpret_cast<const void *>(&scan_onepass), TPB, 0));
     return (int64_t)cus * per;
   }();
-  const int ticket = ticket_env >= 0 ? ticket_env : (nt > resident ? 1 : 0);
+  // tickets only when the grid is not resident at once (a resident grid
+  // waits only for running tiles: tile = workgroup id, no ticket atomic)
+  const int ticket = nt > resident ? 1 : 0;
   hipLaunchKernelGGL(scan_onepass, dim3((unsigned)nt), dim3(TPB), 0, st, a, len, w + 2,
                      (unsigned long long *)w, ws.epoch, ticket);
   PBX_HIP(hipGetLastError());

@@ -4690,15 +4690,6 @@ static void minmax_of(Profile &P, hipStream_t st, uint64_t out[2]) {
   out[1] = P.mm[1];
 }
 
-// PBX_EQUALN=sort selects the radix-sort path (kept for large nbins / A/B)
-static bool select_enabled() {
-  static bool on = [] {
-    const char *v = std::getenv("PBX_EQUALN");
-    return !(v && std::strcmp(v, "sort") == 0);
-  }();
-  return on;
-}
-
 // equaln edges by multi-rank radix select (see msel_* kernels).  Window and
 // rank semantics are those of the sort path: sorted_x[sorted_x >= bin_min],
 // then [sorted_x <= bin_max] (bins.py:734-737; NaN fails both and a NaN
@@ -5047,11 +5038,7 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
   // only the tail needs zeros, and it already holds them when the previous
   // tiled call cleared it at this address (same buffer, same nt)
   const bool persist = span && !pos_f32 && nt >= 1024 && lazy && P.x_tiled;
-  static const bool tail_fill = [] {  // A/B: PBX_SEL_TAILFILL=1 fills the tail every call
-    const char *v = std::getenv("PBX_SEL_TAILFILL");
-    return v && v[0] == '1';
-  }();
-  const bool tail_zero = persist && !tail_fill && P.selst.bytes == sbytes0 &&
+  const bool tail_zero = persist && P.selst.bytes == sbytes0 &&
                          P.sel_tail_zero == stat + nt;
   P.sel_tail_zero = nullptr;
   uint32_t *ctrl = (uint32_t *)(stat + nt);
@@ -5080,13 +5067,8 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
       if (lazy) go(select_onepass<1024, true, double>, 1024, 0.0);
       else go(select_onepass<1024, false, double>, 1024, 0.0);
     } else {
-      // 512-thread tiles (8 particles per lane, 64 VGPRs: 8 waves per SIMD)
-      // for the lazy selection: 244 -> 233 us at 64M against 256 threads
-      // (16 per lane, 136 VGPRs, 3 waves); PBX_SEL_BT=256 for the A/B
-      static const bool sel512 = [] {
-        const char *v = std::getenv("PBX_SEL_BT");
-        return !(v && std::strcmp(v, "256") == 0);
-      }();
+      // 512-thread tiles (8 particles per lane, 64 VGPRs: 8 waves per SIMD):
+      // 244 -> 233 us at 64M against 256 threads (16 per lane, 136 VGPRs, 3 waves)
       if (lazy && P.x_tiled) {  // persistent tiles (+ the hinted level-0 histogram)
         const int G0 = fused_grid(span);
         const unsigned G1 = (unsigned)(SH_K * (G0 - 1));
@@ -5153,10 +5135,8 @@ static uint32_t select_launch(Profile &P, hipStream_t st, const void *pos, const
                            sp, nt, (uint32_t)G0, xo, kw, r.kpre, wc, toff, bt, mm,
                            th ? th->hint : nullptr, th ? th->ka : 0ull, th ? th->kb : ~0ull, rows16, rsub,
                            (uint32_t *)(mm + 2 * MM_SLOTS), sa);
-      } else if (lazy && sel512) go(select_onepass<512, true, double>, 512, 0.0);
-      else if (lazy) go(select_onepass<TPB, true, double>, TPB, 0.0);
-      else if (sel512) go(select_onepass<512, false, double>, 512, 0.0);
-      else go(select_onepass<TPB, false, double>, TPB, 0.0);
+      } else if (lazy) go(select_onepass<512, true, double>, 512, 0.0);
+      else go(select_onepass<512, false, double>, 512, 0.0);
     }
     PBX_HIP(hipGetLastError());
   }
@@ -5350,65 +5330,23 @@ static void percentiles_device(Profile &P, hipStream_t st, int f_src, const doub
 }
 
 // ---- one-launch radial path (radial_mono) -------------------------------
-// PBX_RADIAL_MONO=0 turns it off (A/B: the multi-kernel path)
-// PBX_AGATHER=0: tiled selections take fused_gather + assign_sel (A/B)
-static bool agather_off() {
-  static const bool off = [] {
-    const char *v = std::getenv("PBX_AGATHER");
-    return v && v[0] == '0';
-  }();
-  return off;
-}
-
-static bool mono_edge_env() {  // A/B: PBX_MONO_EDGE=0 never speculates on the edges
-  static const bool on = [] {
-    const char *v = std::getenv("PBX_MONO_EDGE");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
-static bool mono_hint_env() {  // A/B: PBX_MONO_HINT=0 counts level 0 in phase 2 always
-  static const bool on = [] {
-    const char *v = std::getenv("PBX_MONO_HINT");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
-static bool mono_enabled() {
-  static const bool on = [] {
-    const char *v = std::getenv("PBX_RADIAL_MONO");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 // Completion of a call whose last kernel stores a tag into mapped host
 // memory (radial_mono, fused_pack): the tag is polled (a stream sync wakes
 // the host several microseconds after the kernel ends); the stream is
 // queried now and then, so a call that ends without its tag (a discarded
 // radial_mono, a fault) ends the wait too.  Returns whether the tag arrived.
-// PBX_MONO_SPIN=0: a plain stream sync (A/B).
+// (The spin beats a stream sync by 1-2 us of wall time per call.)
 static bool wait_tag(hipStream_t st, const double *word, uint64_t want) {
-  static const bool spin = [] {
-    const char *v = std::getenv("PBX_MONO_SPIN");
-    return !(v && v[0] == '0');
-  }();
   volatile const uint64_t *tag = (volatile const uint64_t *)word;
-  if (spin) {
-    for (uint32_t k = 1; *tag == ~0ull; ++k) {
-      if ((k & 1023u) == 0) {
-        const hipError_t q = hipStreamQuery(st);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) PBX_HIP(q);
-      }
-      __builtin_ia32_pause();
+  for (uint32_t k = 1; *tag == ~0ull; ++k) {
+    if ((k & 1023u) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) PBX_HIP(q);
     }
-    if (*tag != want) PBX_HIP(hipStreamSynchronize(st));
-  } else {
-    PBX_HIP(hipStreamSynchronize(st));
+    __builtin_ia32_pause();
   }
+  if (*tag != want) PBX_HIP(hipStreamSynchronize(st));
   const bool ok = *tag == want;
   __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the pack's words are read after the tag
   return ok;
@@ -5488,7 +5426,7 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
     PBX_HIP(hipMemsetAsync(P.mhint.p, 0, 2 * sizeof(SelHint), st));
   }
   SelHint *mh = (SelHint *)P.mhint.p;
-  a.hin = (P.hint_off || !mono_hint_env()) ? nullptr : mh + (P.n_mhint & 1);
+  a.hin = P.hint_off ? nullptr : mh + (P.n_mhint & 1);
   a.hout = mh + ((P.n_mhint + 1) & 1);
   a.seg = (uint64_t *)P.fseg.get(sizeof(uint64_t) * (size_t)ns);
   a.x = r.xo;
@@ -5537,7 +5475,7 @@ static double *radial_mono_run(Profile &P, hipStream_t st, const void *pos, cons
   a.pedges = (double *)P.mpedges.p;
   a.eU = (uint32_t *)P.meue.p;
   a.eE = a.eU + RADIX + 1;
-  a.eg = (P.medge_next && nq == P.medge_nq && mono_edge_env()) ? 1 : 0;
+  a.eg = (P.medge_next && nq == P.medge_nq) ? 1 : 0;
   hipLaunchKernelGGL(radial_mono, dim3(nt), dim3(MONO_BT), 0, st, a);
   PBX_HIP(hipGetLastError());
   P.bar_done += nt;
@@ -5868,7 +5806,7 @@ int pbx_profile_edges_equaln(void *handle, int64_t nbins, int has_min, double bi
     ScopedTimer tm("pbx.profile.equaln");
     const int64_t n = P.n;
     if (n == 0) fail(PBX_ERR_VALUE, "Cannot create bins: input array is empty");
-    if (nbins + 1 <= MS_MAXQ && select_enabled()) {
+    if (nbins + 1 <= MS_MAXQ) {  // (more bins: the radix-sort path below)
       equaln_select(P, st, nbins, has_min, bin_min, has_max, bin_max, h_edges, n_edges);
       return;
     }
@@ -6166,11 +6104,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
     hipStream_t st = d.stream;
     ScopedTimer tm("pbx.profile.radial_equaln");
     // bins < 256: the lazy selection + tile-walking assignment / CSR passes
-    static const bool eager_env = [] {  // A/B diagnostic: the eager selection path
-      const char *v = std::getenv("PBX_RADIAL_EAGER");
-      return v && v[0] == '1';
-    }();
-    const bool lazy = nbins < RADIX && !eager_env;
+    const bool lazy = nbins < RADIX;
     const int nq = (int)nbins + 1;
     // the window of bins.py:734-737 as key bounds (msel_begin)
     bool empty_bounds = false;
@@ -6234,7 +6168,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
     bool tiled_call = false;  // the multi-kernel path over a tiled selection
     int nsum = 0;
     int64_t n_global = 0;  // dist: kept particles over all ranks
-    if (lazy && mono_enabled() && !dist)
+    if (lazy && !dist)
       hp = radial_mono_run(P, st, pos, mass, n, on_device, use_sphere, sphere, fam, nfam, ndim,
                            nbins, ka, kb, empty_bounds, fs, &nsum);
     if (!hp) {  // the multi-kernel path
@@ -6243,11 +6177,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       // select_tiles with the previous tiled call's geometry (slot n_tiled & 1;
       // fused_hist0 writes this call's into the other slot)
       SelHint *hints = nullptr;
-      static const bool hint_env = [] {  // A/B: PBX_SEL_HINT=0 always re-reads x for level 0
-        const char *v = std::getenv("PBX_SEL_HINT");
-        return !(v && v[0] == '0');
-      }();
-      if (!dist && lazy && hint_env && !P.hint_off) {
+      if (!dist && lazy && !P.hint_off) {
         if (!P.shint.p) {
           P.shint.get(2 * sizeof(SelHint));
           PBX_HIP(hipMemsetAsync(P.shint.p, 0, 2 * sizeof(SelHint), st));
@@ -6262,14 +6192,10 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       // the speculative assignment: when the last tiled call's level-0 ranks
       // matched the stored table (a repeated or similar call), select_tiles
       // bins with it (checked by fused_resolve; a miss takes assign_gather)
-      static const bool spec_env = [] {  // A/B: PBX_SPEC=0 never speculates
-        const char *v = std::getenv("PBX_SPEC");
-        return !(v && v[0] == '0');
-      }();
       bool spec_ops = true;  // select_tiles' sums take the dedicated monomials only
       for (int q = 0; q < fs.nm; ++q) spec_ops = spec_ops && fs.op[q] != MO_GEN;
-      if (hints && spec_env && P.spec_next && P.stab.p && nb <= SPEC_MAXB &&
-          fs.nm * nb <= SPEC_MACC && spec_ops && !agather_off()) {
+      if (hints && P.spec_next && P.stab.p && nb <= SPEC_MAXB && fs.nm * nb <= SPEC_MACC &&
+          spec_ops) {
         thist.sa.tab = (const SpecTab *)P.stab.p;
         thist.sa.fs = fs;
         thist.sa.nb = (int)nb;
@@ -6303,7 +6229,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
       // tiled selections: assignment fused with the gather (assign_gather),
       // the deferred keys binned block by block by fix_deferred
-      const bool agath = tiled && lazy && n_sel && !agather_off();
+      const bool agath = tiled && lazy && n_sel;
       uint32_t *bcnt = agath ? (uint32_t *)P.fblk.get(sizeof(uint32_t) * 3 * (size_t)g0) : nullptr;
       const uint32_t *hflag = (const uint32_t *)(stat + nt + 1 + 2 * MM_SLOTS);
       const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
@@ -6556,11 +6482,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       const uint32_t npk = (uint32_t)(nhead + nsum);
       // one rank: the pack lands in mapped host memory with a completion tag
       // (no D2H copy, no stream sync); dist: all-reduced on the device, copied
-      // PBX_PACK_MAPPED=0: the copy + sync protocol (read per call: the
-      // mapped-vs-copied test switches it between calls)
-      const char *map_v = std::getenv("PBX_PACK_MAPPED");
-      const bool map_env = !(map_v && map_v[0] == '0');
-      const bool mapped = !dist && map_env;
+      const bool mapped = !dist;
       uint64_t *pdone = nullptr;
       if (mapped) {
         if (!P.pdone.p) {

@@ -58,7 +58,7 @@ using namespace prim;
 static constexpr double kR2Tiny = 2.2250738585072014e-308;  // tree.rs:36
 constexpr int LPW = 21;                                      // octree levels per key word
 constexpr int MAX_WORDS = 53;  // 1113 levels: half underflows to 0 before that
-constexpr int WALK_TPB = 256;  // max threads per walk block (waves are independent)
+constexpr int WALK_TPB = 256;  // walk kernels' launch bound (the grids use one wave per block)
 
 // --------------------------------------------------------------- moments
 // Cartesian slots in graded order (the field order of MultipoleMoment,
@@ -1002,33 +1002,7 @@ struct WalkParams {
   unsigned int *fault;           // set when a wave exceeds max_steps
   unsigned xcd_chunk;            // blocks per XCD chunk (0: launch order)
   unsigned long long *trace;     // diagnostic (PBX_WALK_TRACE): per block start, end, steps
-  const int2 *wtab;              // optional wave table (64-thread blocks): block -> {first t, count}
-  const uint32_t *wtab_n;        // its length (blocks past it exit; also the piece table's)
-  unsigned nwt_max;              // host: the table's capacity (the grid)
-  // preorder pieces (walk_kernel<..., PIECES>, piece_table_kernel): block ->
-  // one piece of a 64-target group's walk, the nodes of DFS preorder ids
-  // [a_lo, a_hi); a group split into npc pieces adds its pieces' partial sums
-  // in piece order (the last piece to finish does it)
-  const struct WavePiece *ptab;
-  int32_t *ck;                   // per global group g = gfirst + t0 / 64: [CK_N + 1] ints,
-                                 // [0] the walk's cost (node steps + leaf rounds), [1 + j]
-                                 // its node at cost j * CK_STEP
-  int64_t gfirst;
-  double *pbuf;                  // [slot][64 lanes][pot, ax, ay, az] partial sums
-  int32_t *pcost;                // [slot] the piece's wave cost (steps + leaf rounds)
-  unsigned *pctr;                // [first slot of a group] pieces finished (reset by the last)
 };
-
-// One entry of a piece table: targets t0 .. t0 + cnt - 1 (t0 a multiple of
-// 64) walked over the nodes of preorder ids [a_lo, a_hi); pslot < 0: the
-// group's whole walk (outputs written directly), else its partial-sum slot,
-// gbase .. gbase + npc - 1 the group's slots; ck0: the checkpoint index of
-// a_lo in the group's previous walk (where this piece records its own).
-struct WavePiece {
-  int32_t t0, cnt, a_lo, a_hi, pslot, gbase, npc, ck0;
-};
-constexpr int CK_STEP = 64;   // checkpoint spacing in wave cost units (node steps + leaf rounds)
-constexpr int CK_N = 160;     // checkpoints per group (walks of up to 10240 cost units)
 
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 
@@ -1159,47 +1133,15 @@ __device__ __forceinline__ void leaf_sum(const WalkParams &wp, int32_t s, int32_
 // scratch, 20 v_readlane, walk 44.5 -> 44.2 ms same-box A/B).
 // LCOST: per-lane interaction counts are wanted (cost kind 0 with a cost
 // array); otherwise their per-step VALU updates are compiled out
-// W8: 8 waves per SIMD (range walks of <= 8 x 1024 waves: every wave of the
-// grid resident at once, none waits for a slot; the register squeeze costs
-// the full walk, which keeps 7)
-// The reference's opening decision (tree.rs:1117-1126, node_soft_ok
-// tree.rs:56-71) of one node record chunk for this lane's target — the same
-// expressions as the walk loop's (the piece entry below decides the
-// ancestors of its first node with it).
-template <bool SOFT>
-__device__ __forceinline__ bool node_accept(const WalkParams &wp, const u32x16 &c0, double tx,
-                                            double ty, double tz, double th, bool has_th,
-                                            double theta2) {
-  const double dx = chunk_d(c0, 0) - tx, dy = chunk_d(c0, 1) - ty, dz = chunk_d(c0, 2) - tz;
-  const double dist2 = dist2_fma(dx, dy, dz) + kR2Tiny;
-  bool soft_ok = true;
-  if (SOFT && wp.has_hmax) {
-    double h = __builtin_fmax(chunk_d(c0, 5), 0.0);
-    if (has_th) h = __builtin_fmax(h, th);
-    if (h > 0.0) {
-      const double ch = wp.sep * h;
-      soft_ok = dist2 > ch * ch;
-    }
-  }
-  return soft_ok && chunk_d(c0, 4) < theta2 * dist2;
-}
-
-// PIECES: the blocks walk the entries of a piece table (ptab, *wtab_n of
-// them): entry = a 64-target group's walk restricted to the nodes of DFS
-// preorder ids [a_lo, a_hi).  A lane's reference walk visits nodes in
-// increasing id order, so its nodes split into the pieces without overlap:
-// the piece's first node for the lane is found by replaying the lane's
-// decisions at a_lo's ancestors (an accepted ancestor A sends it to A's
-// next, beyond a_lo; a lane that opens them all starts at a_lo), the wave
-// starts at its lanes' lowest first node and stops at a_hi.  Every node is
-// decided and evaluated exactly as in the whole walk; only the sums are
-// split (added in piece order).
+// W8: 8 waves per SIMD (the order-3 force + potential walks without
+// softening: 56 VGPRs, ~78 SGPRs, 36 B of scratch outside the loop; the
+// 4M walk 31.1-31.2 -> 30.4-30.5 ms against 7 waves, profiles/r5/r5z6/)
 // CNT: the walk statistics (interaction counts, SIMD-efficiency counters:
 // pbx_octree_info) are accumulated; a walk whose caller turned them off
 // (pbx_octree_set_walk_counters) runs without their ~7 scalar operations per
 // wave step — the same decisions and sums, only the instrumentation is gone.
 template <int P, int WANT, bool SOFT, bool RAW, bool LCOST = true, bool W8 = false,
-          bool PIECES = false, bool CNT = true>
+          bool CNT = true>
 __global__ void __launch_bounds__(WALK_TPB)
     __attribute__((amdgpu_waves_per_eu(W8 ? 8 : ((P <= 3 && !SOFT) ? 7 : 1), W8 ? 8 : 7)))
     walk_kernel(WalkParams wp) {
@@ -1208,51 +1150,8 @@ __global__ void __launch_bounds__(WALK_TPB)
   const unsigned long long t_start = wp.trace ? (unsigned long long)wall_clock64() : 0ull;  // (100 MHz)
   const unsigned lb = wp.xcd_chunk ? xcd_chunk_swizzle(blockIdx.x, wp.xcd_chunk) : blockIdx.x;
   const bool lane0 = (threadIdx.x & 63) == 0;
-  int64_t t = (int64_t)lb * blockDim.x + threadIdx.x;
-  bool valid = t < wp.m;
-  int32_t a_lo = 0, a_hi = 0x3fffffff, pslot = -1, gbase = 0, npc = 1, ck0 = 0;
-  int32_t *ckrow = nullptr;  // PIECES: the group's checkpoint row (null: none recorded)
-  if (PIECES) {  // (one wave per block) this wave's piece from the table
-    const uint32_t nwt = *wp.wtab_n;
-    if (lb >= nwt) {
-      if (wp.trace && lane0) {
-        wp.trace[3 * (int64_t)blockIdx.x] = 0;
-        wp.trace[3 * (int64_t)blockIdx.x + 1] = 0;
-        wp.trace[3 * (int64_t)blockIdx.x + 2] = 0;
-      }
-      return;
-    }
-    const WavePiece e = wp.ptab[lb];
-    const int ln = (int)(threadIdx.x & 63);
-    t = (int64_t)__builtin_amdgcn_readfirstlane(e.t0) + ln;
-    valid = ln < __builtin_amdgcn_readfirstlane(e.cnt);
-    a_lo = __builtin_amdgcn_readfirstlane(e.a_lo);
-    a_hi = __builtin_amdgcn_readfirstlane(e.a_hi);
-    // the values used only at a checkpoint or after the loop are kept in
-    // VGPRs (uniform all the same): at 8 waves per SIMD the SGPR budget is
-    // full, and as SGPRs they were spilled to VGPR lanes — ~200 v_readlane
-    // and ~80 v_writelane in the kernel, ~20 % slower per wave than the
-    // plain range walk
-    pslot = e.pslot | (int32_t)vgpr_zero();
-    gbase = e.gbase | (int32_t)vgpr_zero();
-    npc = e.npc | (int32_t)vgpr_zero();
-    ck0 = e.ck0 | (int32_t)vgpr_zero();
-    if (wp.ck) ckrow = wp.ck + (wp.gfirst + ((e.t0 | (int32_t)vgpr_zero()) >> 6)) * (CK_N + 1);
-  } else if (wp.wtab) {  // (one wave per block) this wave's targets from the table
-    const uint32_t nwt = *wp.wtab_n;
-    if (lb >= nwt) {
-      if (wp.trace && lane0) {
-        wp.trace[3 * (int64_t)blockIdx.x] = 0;
-        wp.trace[3 * (int64_t)blockIdx.x + 1] = 0;
-        wp.trace[3 * (int64_t)blockIdx.x + 2] = 0;
-      }
-      return;
-    }
-    const int2 e = wp.wtab[lb];
-    const int ln = (int)(threadIdx.x & 63);
-    t = (int64_t)e.x + ln;
-    valid = ln < e.y;
-  }
+  const int64_t t = (int64_t)lb * blockDim.x + threadIdx.x;
+  const bool valid = t < wp.m;
   const bool self_mode = wp.tgt == nullptr;
   double tx = 0.0, ty = 0.0, tz = 0.0, th = 0.0;
   int32_t self32 = -1;  // this target's own record (self mode)
@@ -1294,57 +1193,18 @@ __global__ void __launch_bounds__(WALK_TPB)
   // opening test itself).
   const uint32_t max_steps = (uint32_t)wp.max_steps;
   int32_t budget = (int32_t)max_steps - 1;  // (max_steps < 2^31: nodes + 16)
-  uint32_t ck_next = wp.ck ? 0u : ~0u;  // PIECES: cost of the next checkpoint (~0: none)
   // theta^2 in a VGPR pair: left a kernel argument, it was reloaded from the
   // kernarg segment every step (a scalar load and its wait; SGPRs are full)
   const uint64_t th2b = __builtin_bit_cast(uint64_t, wp.theta2);
   const double theta2 = __builtin_bit_cast(
       double, ((uint64_t)((uint32_t)(th2b >> 32) | vgpr_zero()) << 32) |
                   (uint64_t)((uint32_t)th2b | vgpr_zero()));
-  if (PIECES && a_lo > 0) {
-    // the piece's entry: down from the root to a_lo (wave-uniform), every
-    // lane replaying its own decisions at a_lo's ancestors.  A node whose
-    // subtree ends at or before a_lo is passed over (a lane at it continues
-    // at its next node whether it would accept or open it); at an ancestor
-    // the lanes standing on it decide: accept -> next (past a_lo), open ->
-    // first child.  The loop ends on a_lo itself (ids are contiguous).
-    int32_t u = 0;
-    uint32_t guard = 0;
-    while (u < a_lo && guard++ < max_steps) {
-      u = __builtin_amdgcn_readfirstlane(u);
-      u32x16 c0[1];
-      load_chunks<1>(wp.walk + (int64_t)u * RS, c0);
-      const int32_t nx = chunk_i(c0[0], 12), fi = chunk_i(c0[0], 13);
-      if (nx >= 0 && nx <= a_lo) {
-        p = (p == u) ? nx : p;
-        u = nx;
-      } else {
-        if (fi < 0) break;  // (a_lo past the tree: not from a valid table)
-        const bool acc = node_accept<SOFT>(wp, c0[0], tx, ty, tz, th, has_th, theta2);
-        p = (p == u) ? (acc ? nx : fi) : p;
-        u = fi;
-      }
-    }
-    // the wave starts at the lowest node any lane still needs
-    int32_t mn = p >= 0 ? p : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mn = min(mn, __shfl_xor(mn, o, 64));
-    w = mn == 0x7fffffff ? -1 : mn;
-  }
-  while ((w | budget) >= 0 &&
-         (!PIECES || (w & 0x3fffffff) < a_hi)) {  // corrupted links: stop instead of hanging
+  while ((w | budget) >= 0) {  // corrupted links: stop instead of hanging
     --budget;
     w = __builtin_amdgcn_readfirstlane(w);  // uniform: keep it (and the address math) scalar
     // bit 30 of w: the node is a leaf (walk-record flags; set only below)
     const uint32_t wleaf = ((uint32_t)w >> 30) & 1u;
     w &= 0x3fffffff;
-    if (PIECES && (uint32_t)((int32_t)max_steps - 2 - budget) + leaf_rounds >= ck_next) {  // checkpoint (uniform)
-      // the wave's node at every CK_STEP units of its cost (node steps + leaf
-      // rounds, what its time follows): the next walk's piece boundaries
-      const uint32_t j = (uint32_t)ck0 + ck_next / CK_STEP;
-      if (j < (uint32_t)CK_N && lane0) ckrow[1 + j] = w;
-      ck_next += CK_STEP;
-    }
     u32x16 c[NCH];
     load_chunks_node<NCH>(wp.walk + (int64_t)w * RS, c, wleaf);
     const double mass = chunk_d(c[0], 3);
@@ -1466,7 +1326,7 @@ __global__ void __launch_bounds__(WALK_TPB)
         leaf_active += na;
         n_pp += (unsigned long long)na * (unsigned long long)(e - s);
       }
-      if (CNT || PIECES || wp.cost_kind) leaf_rounds += (uint32_t)(e - s + 3) >> 2;
+      if (CNT || wp.cost_kind) leaf_rounds += (uint32_t)(e - s + 3) >> 2;
       if (act) {
         if (LCOST) cost += e - s;
         // only a target's own leaf needs the self-pair mask (an int compare
@@ -1484,14 +1344,13 @@ __global__ void __launch_bounds__(WALK_TPB)
     w = nw | (int32_t)nleaf;
   }
   const uint32_t steps = (uint32_t)((int32_t)max_steps - 1 - budget);
-  if (w >= 0 && (!PIECES || (w & 0x3fffffff) < a_hi) && lane0) atomicOr(wp.fault, 1u);
+  if (w >= 0 && lane0) atomicOr(wp.fault, 1u);
   if (wp.trace && lane0) {
     const int64_t wv = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     wp.trace[3 * wv] = t_start;
     wp.trace[3 * wv + 1] = (unsigned long long)wall_clock64();
     wp.trace[3 * wv + 2] = (unsigned long long)steps;
   }
-  // (before the pieces' early exits: every piece's counts are added)
   if (CNT && wp.counters) {
     if (lane0) {
       atomicAdd(&wp.counters[0], (unsigned long long)n_node);
@@ -1503,38 +1362,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       atomicAdd(&wp.counters[7], (unsigned long long)open_steps);
     }
   }
-  int32_t wcost = (int32_t)(steps + leaf_rounds);
-  if (PIECES) {
-    if (ckrow && lane0) {  // the group's cost in this walk (split: summed over its pieces)
-      if (pslot < 0) ckrow[0] = wcost;
-      else atomicAdd(ckrow, wcost);
-    }
-    if (pslot >= 0) {  // a piece of a split group: partial sums, the last piece adds them
-      double *pb = wp.pbuf + ((int64_t)pslot * 64 + (threadIdx.x & 63)) * 4;
-      pb[0] = ph;
-      pb[1] = ax;
-      pb[2] = ay;
-      pb[3] = az;
-      if (lane0) wp.pcost[pslot] = wcost;
-      __threadfence();  // (release: the partials before the arrival count)
-      unsigned old = 0;
-      if (lane0) old = atomicAdd(&wp.pctr[gbase], 1u);
-      old = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)old, 0, 64));
-      if (old + 1 != (unsigned)npc) return;
-      __threadfence();  // (acquire: every piece's partials)
-      ph = ax = ay = az = 0.0;
-      wcost = 0;
-      for (int k = 0; k < npc; ++k) {  // fixed piece order
-        const double *q = wp.pbuf + ((int64_t)(gbase + k) * 64 + (threadIdx.x & 63)) * 4;
-        ph += __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ax += __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ay += __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        az += __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        wcost += __hip_atomic_load(&wp.pcost[gbase + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (lane0) wp.pctr[gbase] = 0u;  // re-armed for the next walk
-    }
-  }
+  const int32_t wcost = (int32_t)(steps + leaf_rounds);
   if (!valid) return;
   const int64_t o = (self_mode && !wp.compact) ? (int64_t)wp.perm[wp.first + t] : t;
   if (wp.cost) wp.cost[t] = wp.cost_kind ? wcost : cost;
@@ -1543,250 +1371,6 @@ __global__ void __launch_bounds__(WALK_TPB)
     wp.acc[3 * o] = ax;
     wp.acc[3 * o + 1] = ay;
     wp.acc[3 * o + 2] = az;
-  }
-}
-
-// Wave table of a self-mode walk of targets [first, first + m) (leaf order),
-// one 1024-thread block: group g = targets 64g .. 64g + 63, its cost c_g =
-// the larger earlier wave cost (original order, cost kind 1) of its two
-// halves' first targets.  Groups with c_g >= permille/1000 of the largest
-// (at most cap of them, and only groups of > 32 targets) become two 32-target
-// waves, listed first (their blocks dispatch first); the other groups follow
-// in order.  A wave walks the union of its targets' walks, and a 32-target
-// union takes ~0.85 of the steps of a 64-target one, so the
-// range walk's longest chains get shorter; every target's result is the
-// same whatever wave it is in (each lane sees exactly its own walk).
-__global__ void __launch_bounds__(1024)
-    wave_table_kernel(const int32_t *__restrict__ cost, const int32_t *__restrict__ perm,
-                      int64_t first, int64_t m, int permille, int2 *__restrict__ wtab,
-                      uint32_t *__restrict__ wtab_n, uint32_t cap) {
-  __shared__ int32_t red[16];
-  __shared__ uint32_t wsum[16];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t G = (m + 63) / 64;
-  auto gcost = [&](int64_t g) {
-    const int64_t a = g * 64, b = a + 32;
-    int32_t c = cost[perm[first + a]];
-    if (b < m) c = max(c, cost[perm[first + b]]);
-    return c;
-  };
-  int32_t mx = 0;
-  for (int64_t g = tid; g < G; g += 1024) mx = max(mx, gcost(g));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-  if (lane == 0) red[wv] = mx;
-  __syncthreads();
-  mx = 0;
-  for (int k = 0; k < 16; ++k) mx = max(mx, red[k]);
-  const int64_t thr = max<int64_t>(1, ((int64_t)mx * permille + 999) / 1000);
-  // heavy flag of group g (a group of > 32 targets at or above the threshold)
-  auto heavy0 = [&](int64_t g) { return g < G && g * 64 + 32 < m && gcost(g) >= thr; };
-  // pass 1: how many groups split (capped)
-  uint32_t nh = 0;
-  for (int64_t g = tid; g < G; g += 1024) nh += heavy0(g) ? 1u : 0u;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nh += __shfl_xor(nh, o, 64);
-  __syncthreads();
-  if (lane == 0) wsum[wv] = nh;
-  __syncthreads();
-  uint32_t H = 0;
-  for (int k = 0; k < 16; ++k) H += wsum[k];
-  H = min(H, cap);
-  __syncthreads();
-  // pass 2: positions (block scans of 1024 groups in order)
-  uint32_t hbase = 0;
-  for (int64_t g0 = 0; g0 < G; g0 += 1024) {
-    const int64_t g = g0 + tid;
-    const bool h0 = heavy0(g);
-    uint32_t x = h0 ? 1u : 0u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int k = 0; k < 16; ++k) {
-      off += k < wv ? wsum[k] : 0u;
-      tot += wsum[k];
-    }
-    __syncthreads();
-    const uint32_t hi = hbase + off + x - (h0 ? 1u : 0u);  // heavy flags before g
-    if (g < G) {
-      const int cnt = (int)min<int64_t>(64, m - g * 64);
-      if (h0 && hi < cap) {  // split: two 32-target waves, first in the table
-        wtab[2 * hi] = make_int2((int)(g * 64), 32);
-        wtab[2 * hi + 1] = make_int2((int)(g * 64 + 32), cnt - 32);
-      } else {  // after the 2 H halves, in group order
-        wtab[2 * H + (uint32_t)(g - min(hi, cap))] = make_int2((int)(g * 64), cnt);
-      }
-    }
-    hbase += tot;
-  }
-  if (tid == 0) *wtab_n = (uint32_t)G + H;
-}
-
-// Piece table of a self-mode walk of targets [first, first + m) (leaf order),
-// one block of 1024 threads.  Group g = targets 64g .. 64g + 63 of the walk,
-// global group gg = gfirst + g; S = ck[gg][0], its cost (node steps + leaf
-// rounds) in the previous walk (0: none recorded).  With permille > 0 a group whose S exceeds
-// T = permille / 1000 of the largest is cut into K = min(kmax, ceil(S / T))
-// pieces at its previous walk's checkpoints nearest to the cost k S / K
-// (strictly increasing node ids inside the tree; a split that would not be
-// is dropped), at most `cap` extra waves in all (groups in order).  The
-// entries are listed longest piece first (32 buckets of S / K), so the
-// longest chains start first; a split group's counter slots are handed out
-// here and its cost is zeroed (its pieces add theirs).  kbuf: one
-// byte per group (its piece count), scratch.
-constexpr int PT_NB = 32;
-__device__ __forceinline__ int pt_split(const int32_t *__restrict__ ckg, int32_t S, int K, int k,
-                                        int32_t nn, int32_t prev, int32_t *j_out) {
-  // node id at the checkpoint nearest to step k S / K, or -1
-  const int64_t st = ((int64_t)k * S) / K;
-  int64_t j = (st + CK_STEP / 2) / CK_STEP;
-  const int64_t jmax = min<int64_t>(CK_N - 1, (S - 1) / CK_STEP);
-  j = min(j, jmax);
-  if (j < 1) return -1;
-  const int32_t a = ckg[1 + j];
-  if (a <= prev || a <= 0 || a >= nn) return -1;
-  *j_out = (int32_t)j;
-  return a;
-}
-
-__global__ void __launch_bounds__(1024)
-    piece_table_kernel(int32_t *__restrict__ ck, int64_t gfirst, int64_t m, int32_t nn, int permille,
-                       int kmax, uint32_t cap, uint8_t *__restrict__ kbuf,
-                       WavePiece *__restrict__ ptab, uint32_t *__restrict__ wtab_n,
-                       unsigned *__restrict__ pctr, int gorder) {
-  __shared__ int32_t red[16];
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t bcnt[PT_NB], bcur[PT_NB];
-  __shared__ uint32_t slot_ctr;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t G = (m + 63) / 64;
-  auto steps_of = [&](int64_t g) { return max(ck[(gfirst + g) * (CK_N + 1)], 0); };
-  int32_t mx = 0;
-  for (int64_t g = tid; g < G; g += 1024) mx = max(mx, steps_of(g));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-  if (lane == 0) red[wv] = mx;
-  if (tid < PT_NB) bcnt[tid] = 0;
-  if (tid == 0) slot_ctr = 0;
-  __syncthreads();
-  mx = 0;
-  for (int k = 0; k < 16; ++k) mx = max(mx, red[k]);
-  const int64_t thr = permille > 0 ? max<int64_t>(2 * CK_STEP, ((int64_t)mx * permille + 999) / 1000)
-                                   : INT64_MAX;
-  // pieces of group g before the cap: the splits that are valid
-  auto pieces0 = [&](int64_t g) -> int {
-    if (g >= G || m - g * 64 <= 0) return 0;
-    const int32_t S = steps_of(g);
-    if (S <= thr) return 1;
-    const int K = (int)min<int64_t>(kmax, (S + thr - 1) / thr);
-    const int32_t *ckg = ck + (gfirst + g) * (CK_N + 1);
-    int n = 1;
-    int32_t prev = 0, j;
-    for (int k = 1; k < K; ++k) {
-      const int32_t a = pt_split(ckg, S, K, k, nn, prev, &j);
-      if (a > 0) {
-        prev = a;
-        ++n;
-      }
-    }
-    return n;
-  };
-  // pass 1 (groups in order, chunks of 1024): the cap on extra waves -> kbuf
-  uint32_t base = 0;
-  for (int64_t g0 = 0; g0 < G; g0 += 1024) {
-    const int64_t g = g0 + tid;
-    const int K0 = pieces0(g);
-    uint32_t x = K0 > 1 ? (uint32_t)(K0 - 1) : 0u;
-    const uint32_t mine = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int k = 0; k < 16; ++k) {
-      off += k < wv ? wsum[k] : 0u;
-      tot += wsum[k];
-    }
-    __syncthreads();
-    const uint32_t before = base + off + x - mine;  // extra waves of the groups before g
-    if (g < G) {
-      const int K = (K0 > 1 && before + mine <= cap) ? K0 : 1;
-      kbuf[g] = (uint8_t)K;
-      const int32_t S = steps_of(g);
-      const int64_t L = S / K;  // the group's piece length
-      const int b = (int)min<int64_t>(PT_NB - 1, (L * PT_NB) / ((int64_t)mx + 1));
-      atomicAdd(&bcnt[b], (uint32_t)K);
-    }
-    base += tot;
-  }
-  __syncthreads();
-  if (tid == 0) {  // bucket starts, longest pieces first
-    uint32_t run = 0;
-    for (int b = PT_NB - 1; b >= 0; --b) {
-      bcur[b] = run;
-      run += bcnt[b];
-    }
-    *wtab_n = run;
-  }
-  __syncthreads();
-  // pass 2: the entries (gorder: in group order — the pieces of neighbouring
-  // groups, which walk much the same nodes, run on the same XCD like the
-  // plain walk's waves; else longest first)
-  uint32_t gbase_run = 0;
-  for (int64_t g0 = 0; g0 < G; g0 += 1024) {
-    const int64_t g = g0 + tid;
-    const int K = g < G ? (int)kbuf[g] : 0;
-    uint32_t pos = 0;
-    if (gorder) {
-      uint32_t x = (uint32_t)K;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      if (lane == 63) wsum[wv] = x;
-      __syncthreads();
-      uint32_t off = 0, tot = 0;
-      for (int k = 0; k < 16; ++k) {
-        off += k < wv ? wsum[k] : 0u;
-        tot += wsum[k];
-      }
-      __syncthreads();
-      pos = gbase_run + off + x - (uint32_t)K;
-      gbase_run += tot;
-    }
-    if (g >= G) continue;
-    const int32_t S = steps_of(g);
-    const int64_t L = S / K;
-    const int b = (int)min<int64_t>(PT_NB - 1, (L * PT_NB) / ((int64_t)mx + 1));
-    if (!gorder) pos = atomicAdd(&bcur[b], (uint32_t)K);
-    const int cnt = (int)min<int64_t>(64, m - g * 64);
-    if (K == 1) {
-      ptab[pos] = WavePiece{(int32_t)(g * 64), cnt, 0, 0x3fffffff, -1, 0, 1, 0};
-      continue;
-    }
-    int32_t *ckg = ck + (gfirst + g) * (CK_N + 1);
-    const int K0 = (int)min<int64_t>(kmax, (S + thr - 1) / thr);  // the K the splits were cut for
-    const int32_t gb = (int32_t)atomicAdd(&slot_ctr, (uint32_t)K);
-    pctr[gb] = 0u;  // (also re-armed by the group's last piece; a walk cut short leaves no count)
-    int32_t prev = 0, jprev = 0, j = 0, q = 0;
-    for (int k = 1; k <= K0 && q < K; ++k) {
-      const int32_t a = k < K0 ? pt_split(ckg, S, K0, k, nn, prev, &j) : 0x3fffffff;
-      if (k < K0 && a <= 0) continue;
-      ptab[pos + q] = WavePiece{(int32_t)(g * 64), cnt, prev, a, gb + q, gb, K, jprev};
-      ++q;
-      prev = a;
-      jprev = j;
-    }
-    ckg[0] = 0;  // the pieces add their steps
   }
 }
 
@@ -2347,13 +1931,7 @@ struct Octree {
   Buf bal;                   // cost-balanced ranges: chunk sums + cuts
   Buf iscan, ilist, iws;     // payload: internal-node flags / scan, list, scan state
   int cost_kind = 0;                   // d_cost contents (WalkParams::cost_kind)
-  const int32_t *split_cost = nullptr;  // wave split: original-order wave costs (caller's memory)
-  int32_t split_permille = 0;
-  Buf wtab;                             // the wave table + its length
-  int piece_permille = -1, piece_kmax = 2;  // preorder pieces (pbx_octree_set_walk_pieces), -1 off
-  bool walk_counts = true;                  // pbx_octree_set_walk_counters
-  Buf ck, kbuf, pbuf, pcost, pctr;          // their checkpoints, scratch, partial sums, counters
-  int64_t ck_groups = 0, p_slots = 0;
+  bool walk_counts = true;             // pbx_octree_set_walk_counters
   Buf bp_fl, bp_eq, bp_s, bp_ctl, bp_level, bp_start, bp_p2b;  // parallel structure build
   Buf bp_emin;  // eq's line / group minima (eq_mins)
   Buf rec0;                  // {x, y, z, m} in original order (path_keys)
@@ -2364,7 +1942,7 @@ struct Octree {
                    &nchild, &ncen, &pre, &size, &com, &hmax, &mom, &coef, &walk, &leaf_dfs, &keys, &ktmp0,
                    &ktmp1, &vtmp, &hist, &tsum, &front0, &front1, &lb, &cnt, &flags, &small,
                    &counters, &trace, &bal, &iscan, &ilist, &iws, &bp_fl, &bp_eq, &bp_emin, &bp_s, &rec0, &bp_ctl, &bp_level, &bp_start,
-                   &bp_p2b, &wtab, &ck, &kbuf, &pbuf, &pcost, &pctr};
+                   &bp_p2b};
     for (Buf *b : bufs) b->release();
     rm_pin.release();
   }
@@ -2481,11 +2059,6 @@ static bool split_parallel(Octree &T, hipStream_t st, int sorted_levels) {
   const int64_t n = T.n;
   if (n <= 0 || T.leaf_capacity > 64 || !(T.root[3] > 1e-290) || n >= ((int64_t)1 << 31) - 1)
     return false;
-  static const bool off = [] {  // A/B diagnostic: the level-synchronous builder
-    const char *e = std::getenv("PBX_TREE_LEVEL_BUILD");
-    return e && e[0] == '1';
-  }();
-  if (off) return false;
   const uint64_t *keys = T.keys.as<uint64_t>();
   uint8_t *fd = (uint8_t *)T.bp_fl.get(2 * (size_t)n + 16);
   uint8_t *lv = fd + n;
@@ -2852,97 +2425,52 @@ static void build_payload(Octree &T, hipStream_t st) {
   T.has_bh = true;
 }
 
-// blocks per XCD chunk of the walk grid (PBX_WALK_XCD_CHUNK, 0 = launch order)
-static unsigned walk_xcd_chunk() {
-  static const unsigned c = [] {
-    const char *v = std::getenv("PBX_WALK_XCD_CHUNK");
-    return v ? (unsigned)std::strtoul(v, nullptr, 10) : 128u;
-  }();
-  return c;
-}
-
-// fast order-3 walks at 8 waves per SIMD (walk_kernel<..., W8>): every grid
-// by default — the full 4M walk 31.15-31.20 -> 30.48-30.50 ms same box,
-// A/B/A/B (profiles/r5/r5z6/) although W8 parks 36 B in scratch outside the
-// loop; PBX_WALK_W8=1: only grids of at most one resident round (range
-// walks, the round-4 default), =0: never
-constexpr unsigned kNumSimd = 1024;  // 256 CUs x 4
-static int walk_w8() {
-  static const int c = [] {
-    const char *v = std::getenv("PBX_WALK_W8");
-    return v ? (v[0] == '0' ? 0 : v[0] == '1' ? 1 : 2) : 2;
-  }();
-  return c;
-}
-
-// threads per walk block (PBX_WALK_TPB: 64, 128 or 256)
-static unsigned walk_tpb() {
-  static const unsigned c = [] {
-    const char *v = std::getenv("PBX_WALK_TPB");
-    const unsigned t = v ? (unsigned)std::strtoul(v, nullptr, 10) : 64u;
-    return (t == 128 || t == 256) ? t : 64u;
-  }();
-  return c;
-}
+// Walk grids: one wave (64 targets) per block, blocks handed out to the XCDs
+// in chunks of WALK_XCD_CHUNK consecutive blocks (xcd_chunk_swizzle: the
+// waves of neighbouring targets, which walk much the same nodes, share an
+// XCD's L2).  Chunks of 16 / 32 / 64 / 128 / 256 blocks: 34.14 / 34.06 /
+// 33.95 / 33.67 / 33.76 ms at 4M (profiles/r3/walk_xcd_sweep/), 64 and 256
+// re-measured slower again at 8 waves per SIMD (round 5).
+constexpr unsigned WALK_XCD_CHUNK = 128;
+constexpr unsigned WALK_BT = 64;
 
 template <int P, int WANT>
 static void launch_walk_pw(WalkParams wp, bool soft, hipStream_t st) {
-  const unsigned tpb = walk_tpb();
-  unsigned grid = (wp.wtab || wp.ptab) ? wp.nwt_max : (unsigned)((wp.m + tpb - 1) / tpb);
-  const unsigned waves = grid;  // (before the rounding: blocks past the work exit at once)
-  wp.xcd_chunk = walk_xcd_chunk();
-  if (wp.xcd_chunk) {  // whole rounds of kNumXcd chunks; the extra blocks find no targets
+  unsigned grid = (unsigned)((wp.m + WALK_BT - 1) / WALK_BT);
+  wp.xcd_chunk = WALK_XCD_CHUNK;
+  {  // whole rounds of kNumXcd chunks (a bijection); the extra blocks find no targets
     const unsigned round = kNumXcd * wp.xcd_chunk;
     grid = (grid + round - 1) / round * round;
   }
   const bool raw = !precise_mode();
   const bool lcost = wp.cost && !wp.cost_kind;  // per-lane counts wanted
   const bool cnt = wp.counters != nullptr;  // (walk() clears it only where a CNT=false variant exists)
-  if (wp.ptab) {  // preorder pieces (walk() enables them for this configuration only)
-    if constexpr (P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC)) {
-      if (raw && cnt)
-        hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true, true>), dim3(grid),
-                           dim3(tpb), 0, st, wp);
-      else if (raw)
-        hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true, true, false>),
-                           dim3(grid), dim3(tpb), 0, st, wp);
-      else
-        hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false, true, true>), dim3(grid),
-                           dim3(tpb), 0, st, wp);
-    }
-    return;
-  }
-  if (!cnt) {  // order 3, potential + acceleration, no softening, fast mode (walk())
-    if constexpr (P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC)) {
-      if (tpb == 64 && ((waves <= 8u * kNumSimd && walk_w8()) || walk_w8() == 2))
-        hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true, false, false>),
-                           dim3(grid), dim3(tpb), 0, st, wp);
-      else
-        hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, false, false, false>),
-                           dim3(grid), dim3(tpb), 0, st, wp);
-    }
+  // order 3, potential + acceleration, no softening, no per-lane counts: 8 waves per SIMD
+  constexpr bool w8 = P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC);
+  if (!cnt) {  // ... fast mode, the statistics off (walk())
+    if constexpr (w8)
+      hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true, false>), dim3(grid),
+                         dim3(WALK_BT), 0, st, wp);
     return;
   }
   if (soft && raw)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, true, true>), dim3(grid), dim3(tpb), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, true, true>), dim3(grid), dim3(WALK_BT), 0, st, wp);
   else if (soft)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, true, false>), dim3(grid), dim3(WALK_BT), 0, st, wp);
   else if (raw && lcost)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, true>), dim3(grid), dim3(tpb), 0, st, wp);
-  else if (raw && P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC) && tpb == 64 &&
-           ((waves <= 8u * kNumSimd && walk_w8()) || walk_w8() == 2))  // a range walk (config 5, >= 8 ranks)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true>), dim3(grid), dim3(tpb), 0,
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, true>), dim3(grid), dim3(WALK_BT), 0, st, wp);
+  else if (raw && w8)
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false, true>), dim3(grid), dim3(WALK_BT), 0,
                        st, wp);
   else if (raw)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false>), dim3(grid), dim3(tpb), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, true, false>), dim3(grid), dim3(WALK_BT), 0, st, wp);
   else if (lcost)
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, true>), dim3(grid), dim3(tpb), 0, st, wp);
-  else if (P == 3 && WANT == (PBX_WANT_POT | PBX_WANT_ACC) && tpb == 64 &&
-           ((waves <= 8u * kNumSimd && walk_w8()) || walk_w8() == 2))  // precise, 8 waves per SIMD
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false, true>), dim3(grid), dim3(tpb), 0,
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, true>), dim3(grid), dim3(WALK_BT), 0, st, wp);
+  else if (w8)  // precise, 8 waves per SIMD
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false, true>), dim3(grid), dim3(WALK_BT), 0,
                        st, wp);
   else
-    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false>), dim3(grid), dim3(tpb), 0, st, wp);
+    hipLaunchKernelGGL((walk_kernel<P, WANT, false, false, false>), dim3(grid), dim3(WALK_BT), 0, st, wp);
 }
 
 template <int P>
@@ -2990,85 +2518,13 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   wp.max_steps = T.nn + 16;
   wp.fault = (unsigned int *)(ctr + 2);
   wp.cost_kind = T.cost_kind;
-  wp.wtab = nullptr;
-  wp.wtab_n = nullptr;
-  wp.ptab = nullptr;
-  wp.ck = nullptr;
-  wp.gfirst = 0;
-  wp.pbuf = nullptr;
-  wp.pcost = nullptr;
-  wp.pctr = nullptr;
-  unsigned nwt_max = 0;  // wave table: at most this many waves
-  const bool pieces = T.piece_permille >= 0 && d_tgt == nullptr && walk_tpb() == 64 && m > 0 &&
-                      T.n > 0 && T.moment_order() == 3 && !(T.has_hmax || T.soft_set) &&
-                      want == (PBX_WANT_POT | PBX_WANT_ACC) && !(d_cost && T.cost_kind == 0);
-  if (pieces) {
-    // preorder pieces: the groups' previous steps and checkpoints (by global
-    // group first / 64 + g; ShardedTree aligns its cuts to 64), the table,
-    // at most G extra waves
-    const int64_t G = (m + 63) / 64;
-    const int64_t gtot = T.n / 64 + 2;
-    const size_t ckw = (size_t)(CK_N + 1);
-    if (T.ck_groups < gtot) {
-      T.ck.release();
-      PBX_HIP(hipMemsetAsync(T.ck.get(4 * ckw * (size_t)gtot), 0, 4 * ckw * (size_t)gtot, st));
-      T.ck_groups = gtot;
-    }
-    // extra waves: unbounded, or (PBX_PIECE_CAP=round) only as many as keep
-    // the grid one resident round of 8 waves per SIMD
-    static const int piece_env = [] {
-      const char *o = std::getenv("PBX_PIECE_ORDER"), *c = std::getenv("PBX_PIECE_CAP");
-      return ((o && o[0] == 'g') ? 1 : 0) | ((c && c[0] == 'r') ? 2 : 0);
-    }();
-    const int64_t slots8 = 8 * (int64_t)kNumSimd;
-    const int64_t cap = (piece_env & 2) ? std::max<int64_t>(0, slots8 - G) : G;
-    nwt_max = (unsigned)(G + cap);
-    const int64_t slots = 2 * cap;
-    if (T.p_slots < slots) {
-      T.pbuf.release();
-      T.pcost.release();
-      T.pctr.release();
-      T.pbuf.get(sizeof(double) * 256 * (size_t)slots);
-      T.pcost.get(4 * (size_t)slots);
-      PBX_HIP(hipMemsetAsync(T.pctr.get(4 * (size_t)slots), 0, 4 * (size_t)slots, st));
-      T.p_slots = slots;
-    }
-    char *wb = (char *)T.wtab.get(64 + sizeof(WavePiece) * (size_t)nwt_max);
-    wp.ptab = (const WavePiece *)(wb + 64);
-    wp.wtab_n = (const uint32_t *)wb;
-    wp.ck = T.ck.as<int32_t>();
-    wp.gfirst = first >> 6;
-    wp.pbuf = T.pbuf.as<double>();
-    wp.pcost = T.pcost.as<int32_t>();
-    wp.pctr = T.pctr.as<unsigned>();
-    hipLaunchKernelGGL(piece_table_kernel, dim3(1), dim3(1024), 0, st, T.ck.as<int32_t>(),
-                       (int64_t)(first >> 6), m, (int32_t)T.nn, T.piece_permille, T.piece_kmax,
-                       (uint32_t)cap, (uint8_t *)T.kbuf.get((size_t)G), (WavePiece *)(wb + 64),
-                       (uint32_t *)wb, T.pctr.as<unsigned>(), piece_env & 1);
-  } else if (T.split_cost && d_tgt == nullptr && walk_tpb() == 64 && m > 0 && T.n > 0) {
-    // heavy 64-target groups of the earlier walk split in two, dispatched first
-    const int64_t G = (m + 63) / 64;
-    // at most 1/8 of the groups split; a grid that fits the 8-waves-per-SIMD
-    // slots (launch_walk_pw's W8) keeps fitting
-    const int64_t slots = 8 * (int64_t)kNumSimd;
-    const int64_t cap = G <= slots ? std::min<int64_t>(G / 8, slots - G) : G / 8;
-    nwt_max = (unsigned)(G + cap);
-    char *wb = (char *)T.wtab.get(sizeof(int2) * (size_t)nwt_max + 64);
-    wp.wtab = (const int2 *)(wb + 64);
-    wp.wtab_n = (const uint32_t *)wb;
-    hipLaunchKernelGGL(wave_table_kernel, dim3(1), dim3(1024), 0, st, T.split_cost,
-                       T.perm.as<int32_t>(), first, m, T.split_permille, (int2 *)(wb + 64),
-                       (uint32_t *)wb, (uint32_t)cap);
-  }
-  wp.nwt_max = nwt_max;
   wp.trace = nullptr;
   const char *trace_path = std::getenv("PBX_WALK_TRACE");  // diagnostic only
   unsigned tgrid = 0;
   if (trace_path) {
-    tgrid = nwt_max ? nwt_max : (unsigned)((m + walk_tpb() - 1) / walk_tpb());
-    const unsigned c = walk_xcd_chunk();
-    if (c) tgrid = (tgrid + kNumXcd * c - 1) / (kNumXcd * c) * (kNumXcd * c);
-    tgrid *= walk_tpb() / 64;  // one trace record per wave
+    tgrid = (unsigned)((m + WALK_BT - 1) / WALK_BT);  // one trace record per wave (block)
+    const unsigned c = WALK_XCD_CHUNK;
+    tgrid = (tgrid + kNumXcd * c - 1) / (kNumXcd * c) * (kNumXcd * c);
     wp.trace = (unsigned long long *)T.trace.get(24 * (size_t)tgrid);
   }
   // softened leaves need softenings; the guard needs h_max; at query points
@@ -3543,26 +2999,6 @@ int pbx_octree_cost_to_orig(pbx_octree *t, const int32_t *d_cost_leaf, int32_t *
       hipLaunchKernelGGL(cost_to_orig, dim3(nblk(T.n)), dim3(TPB), 0, dev.stream, d_cost_leaf,
                          T.perm.as<int32_t>(), T.n, d_cost_orig);
     PBX_HIP(hipGetLastError());
-  });
-}
-
-int pbx_octree_set_wave_split(pbx_octree *t, const int32_t *d_cost_orig, int permille) {
-  return guard([&] {
-    Octree &T = as_tree(t);
-    if (d_cost_orig && (permille < 1 || permille > 1000))
-      fail(PBX_ERR_VALUE, "permille must be in [1, 1000]");
-    T.split_cost = d_cost_orig;
-    T.split_permille = permille;
-  });
-}
-
-int pbx_octree_set_walk_pieces(pbx_octree *t, int permille, int kmax) {
-  return guard([&] {
-    Octree &T = as_tree(t);
-    if (permille > 1000) fail(PBX_ERR_VALUE, "permille must be <= 1000");
-    if (permille >= 0 && (kmax < 2 || kmax > 8)) fail(PBX_ERR_VALUE, "kmax must be in [2, 8]");
-    T.piece_permille = permille < 0 ? -1 : permille;
-    T.piece_kmax = kmax;
   });
 }
 

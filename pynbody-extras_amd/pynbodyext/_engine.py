@@ -317,16 +317,6 @@ class Octree:
         """Per-target costs in this build's leaf order -> original order."""
         nat.call("pbx_octree_cost_to_orig", self._h, d_cost_leaf, d_cost_orig)
 
-    def _set_wave_split(self, d_cost_orig, permille: int = 750) -> None:
-        """Range walks split the 64-target groups whose earlier wave cost
-        (original order, cost kind 1) is >= permille/1000 of the largest into
-        two 32-target waves dispatched first (speed only); None: off."""
-        nat.call("pbx_octree_set_wave_split", self._h, d_cost_orig or None, int(permille))
-
-    def _set_walk_pieces(self, permille: int = -1, kmax: int = 2) -> None:
-        """Preorder pieces of the heaviest waves in self-mode walks
-        (pbx_octree_set_walk_pieces; -1 = off)."""
-        nat.call("pbx_octree_set_walk_pieces", self._h, int(permille), int(kmax))
 
     def _set_walk_counters(self, enabled: bool = True) -> None:
         """Walk statistics (info()'s interaction / step counts) on or off for

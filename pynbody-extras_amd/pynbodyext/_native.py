@@ -112,8 +112,6 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_octree_cost_to_orig": (c_int, [c_void_p, c_void_p, c_void_p]),
     "pbx_octree_balance": (c_int, [c_void_p, c_void_p, c_int, _i64p]),
     "pbx_octree_set_cost_kind": (c_int, [c_void_p, c_int]),
-    "pbx_octree_set_wave_split": (c_int, [c_void_p, c_void_p, c_int]),
-    "pbx_octree_set_walk_pieces": (c_int, [c_void_p, c_int, c_int]),
     "pbx_octree_set_walk_counters": (c_int, [c_void_p, c_int]),
     "pbx_octree_info": (c_int, [c_void_p, _i64p]),
     "pbx_octree_export": (c_int, [c_void_p, _dp, _dp, _dp, _i64p, _i64p, _i64p, _dp]),

@@ -399,23 +399,6 @@ def balanced_ranges(cost: np.ndarray, world: int) -> list[tuple[int, int]]:
     return [(int(cuts[r]), int(cuts[r + 1] - cuts[r])) for r in range(world)]
 
 
-PIECES_DEFAULT = "off"
-
-
-def parse_pieces(spec):
-    """"permille[,kmax]" -> (permille, kmax), or None for "off" / negative."""
-    if spec is None or str(spec).strip().lower() in ("", "off", "none"):
-        return None
-    parts = [int(v) for v in str(spec).split(",")]
-    permille = parts[0]
-    kmax = parts[1] if len(parts) > 1 else 2
-    if permille < 0:
-        return None
-    if permille > 1000 or not 2 <= kmax <= 8:
-        raise ValueError(f"PBX_WALK_PIECES: permille <= 1000 and 2 <= kmax <= 8, got {spec!r}")
-    return permille, kmax
-
-
 def align_ranges(ranges, n: int, q: int):
     """Contiguous (first, count) ranges with every inner cut rounded to a
     multiple of q (monotone, the last range ending at n)."""
@@ -468,16 +451,6 @@ class ShardedTree:
         self.d_cost = nat.DeviceArray(4 * max(cap, 1))       # leaf order, last walk
         self.d_cost_orig = nat.DeviceArray(4 * max(cap, 1))  # original order, carried
         self.have_costs = False
-        # range walks: split 64-target groups whose earlier wave cost is >=
-        # this fraction (per mille) of the largest into two 32-target waves
-        # (PBX_WAVE_SPLIT=900, say).  Off by default: at 8 ranks of 4M it
-        # moved the longest range walk by noise only
-        self.split_permille = int(os.environ.get("PBX_WAVE_SPLIT", "0"))
-        # range walks: preorder pieces (pbx_octree_set_walk_pieces) — the
-        # waves whose previous walk took more than permille / 1000 of the
-        # longest one's steps cut into up to kmax DFS-preorder id intervals
-        # (PBX_WALK_PIECES="permille,kmax"; "off" or -1 disables)
-        self.pieces = parse_pieces(os.environ.get("PBX_WALK_PIECES", PIECES_DEFAULT))
         self.info = None
         self.count_walks = True  # walk statistics (set_walk_counters)
         self.d_prof = None  # [counts | moments] of the profile all-reduce
@@ -489,8 +462,7 @@ class ShardedTree:
             self.tree = Octree._from_device(self.d_pos.ptr, self.n, self.d_mass.ptr, self.leaf,
                                             self.order)
             self.tree._set_cost_kind(1)
-            if self.pieces is not None and self.world > 1:
-                self.tree._set_walk_pieces(*self.pieces)
+            self.tree._set_walk_counters(self.count_walks)
         else:  # next step / snapshot: same handle, HBM buffers reused
             self.tree._rebuild_device(self.d_pos.ptr, self.n, self.d_mass.ptr)
 
@@ -507,8 +479,6 @@ class ShardedTree:
             self.ranges = [(0, self.n)]
         elif self.have_costs:
             self.ranges = self.tree._balance_device(self.d_cost_orig.ptr, self.world)
-            if self.pieces is not None:  # whole 64-target groups (the pieces' per-group state)
-                self.ranges = align_ranges(self.ranges, self.n, 64)
         else:
             self.ranges = [(lo, hi - lo) for lo, hi in all_shards(self.n, self.world)]
         return self.ranges
@@ -537,10 +507,6 @@ class ShardedTree:
             self.comm.allgatherv(self.d_cost.ptr, [4 * c for _, c in self.ranges],
                                  [4 * f for f, _ in self.ranges])
         self.tree._cost_to_orig_device(self.d_cost.ptr, self.d_cost_orig.ptr)
-        if not self.have_costs and self.split_permille:
-            # later range walks split their heaviest 64-target groups into two
-            # 32-target waves dispatched first (the costs stay in d_cost_orig)
-            self.tree._set_wave_split(self.d_cost_orig.ptr, self.split_permille)
         self.have_costs = True
 
     def profile(self, dev_bins, edges) -> np.ndarray:

@@ -41,6 +41,37 @@ def plummer(n: int, seed: int = 1002, rmax: float = 50.0):
     return pos, mass
 
 
+def plummer_chunked(n: int, seed: int, chunk: int = 1 << 22, threads: int = 16,
+                    rmax: float = 50.0):
+    """A Plummer sphere drawn in independent chunks on a thread pool (numpy
+    releases the GIL in its kernels): chunk k holds particles
+    [k·chunk, (k+1)·chunk) drawn by plummer()'s rule from the k-th child of
+    SeedSequence(seed).  A different particle set than plummer(n, seed) —
+    used where many large snapshots are needed (the bench's changing-input
+    rows), ~10x faster than one stream."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    nch = max(1, -(-n // chunk))
+    seqs = np.random.SeedSequence(seed).spawn(nch)
+    pos = np.empty((n, 3), dtype=np.float64)
+
+    def fill(k):
+        lo, hi = k * chunk, min(n, (k + 1) * chunk)
+        rng = np.random.default_rng(seqs[k])
+        m = hi - lo
+        r = plummer_radii(m, rng, rmax)
+        cost = rng.uniform(-1.0, 1.0, m)
+        phi = rng.uniform(0.0, 2.0 * np.pi, m)
+        sint = np.sqrt(1.0 - cost * cost)
+        pos[lo:hi, 0] = r * sint * np.cos(phi)
+        pos[lo:hi, 1] = r * sint * np.sin(phi)
+        pos[lo:hi, 2] = r * cost
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        list(ex.map(fill, range(nch)))
+    return pos, np.full(n, 1.0 / n, dtype=np.float64)
+
+
 def family_slices(n: int) -> dict:
     out, start = {}, 0
     for i, (name, frac) in enumerate(FAMILY_FRACTIONS):

@@ -189,9 +189,9 @@ class MockOctree:
     def _set_cost_kind(self, kind):
         self.kind = kind
 
-    def _set_wave_split(self, d_cost_orig, permille=750):
-        # speed only on the device (every target's result unchanged): recorded
-        self.split = (d_cost_orig, permille)
+    def _set_walk_counters(self, enabled=True):
+        # instrumentation only on the device: recorded
+        self.counters = bool(enabled)
 
     def _rebuild_device(self, d_pos, n, d_mass):
         self.__init__(view(d_pos, 24 * n, np.float64).reshape(n, 3).copy(),

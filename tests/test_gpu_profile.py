@@ -1239,40 +1239,38 @@ def test_lazy_selection_reads_device_mass_at_use(gpu):
 
 
 @pytest.mark.parametrize("n,nb", [(4_400_000, 255), (300_000, 1000)])
-def test_results_pack_mapped_equals_copied(gpu, monkeypatch, n, nb):
+def test_results_pack_mapped_many_blocks(gpu, n, nb):
     """the results pack written into coherent mapped host memory
-    behind a completion tag (fused_pack, PBX_PACK_MAPPED default) against the
-    copy + stream-sync protocol (PBX_PACK_MAPPED=0), over thousands of pack
-    blocks (8 fused monomials x nb bins: 2040 at the tiled 255-bin size,
-    8000 on the 1000-bin eager path), with two inputs alternating on one
-    handle so a stale pack would show the other input's values: control
-    record, edges and counts bit-identical, sums to LDS-atomic rounding."""
+    behind a completion tag (fused_pack / csr_slots' pack blocks), over
+    thousands of pack blocks (8 fused monomials x nb bins: 2040 at the tiled
+    255-bin size, 8000 on the 1000-bin eager path), with two inputs
+    alternating on one handle so a stale pack would show the other input's
+    values: edges and counts bit-exact against the oracle, the per-bin Σw
+    against numpy's sums (LDS-atomic rounding)."""
     from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
 
     rng = np.random.default_rng(31)
     inputs = []
     for scale in (3.0, 5.0):
         pos = rng.normal(scale=scale, size=(n, 3))
-        inputs.append((pos, rng.uniform(0.5, 1.5, n)))
+        mass = rng.uniform(0.5, 1.5, n)
+        x = pr.radial_r(pos)
+        edges = pr.edges_equaln(x, nb)
+        perm, offs, cnt = pr.assign(x, edges)
+        wsum = np.bincount(np.repeat(np.arange(nb), cnt), weights=mass[perm], minlength=nb)
+        inputs.append((pos, mass, edges, cnt, wsum))
     # 8 distinct monomials: w, xw, x^2 w, x, x^2, |x| w, |x| and w^2
     stats = [(SRC_X, SRC_W, 0x7F), (SRC_W, SRC_NONE, 0x18)]
     h = DeviceBins()
-    out = {}
     try:
-        for mode in ("1", "0", "1"):
-            monkeypatch.setenv("PBX_PACK_MAPPED", mode)
-            for k, (pos, mass) in enumerate(inputs):
+        for _ in range(3):
+            for pos, mass, edges, cnt, wsum in inputs:
                 _, e, c, m = DeviceBins.radial_equaln(pos, mass, nbins=nb, stats=stats, csr=False,
                                                       into=h)
-                out.setdefault(k, []).append((e, c, m))
+                assert np.array_equal(e.view(np.uint64), edges.view(np.uint64))
+                assert np.array_equal(c, cnt)
+                np.testing.assert_allclose(m[0][:, 0], wsum, rtol=1e-12, atol=0)
     finally:
         h.close()
-    for k in out:
-        (e0, c0, m0), *rest = out[k]
-        for e, c, m in rest:
-            assert np.array_equal(e.view(np.uint64), e0.view(np.uint64))
-            assert np.array_equal(c, c0)
-            for a, b in zip(m, m0):
-                np.testing.assert_allclose(a, b, rtol=1e-12, atol=0)
     # the two inputs differ, so a pack left from the other call would be seen
-    assert not np.array_equal(out[0][0][0], out[1][0][0])
+    assert not np.array_equal(inputs[0][3], inputs[1][3])

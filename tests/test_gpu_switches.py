@@ -1,15 +1,15 @@
-"""The library's runtime A/B switches (INTEGRATION.md "Runtime variables")
-select alternatives that were measured slower; each must still compute the
-same results.  tests/_switch_child.py runs one fixed workload in a child
-process (the switches are read once per process) with the defaults and
-under each group of switches; the results are compared with the defaults'
-(which the other GPU tests check against the oracle):
+"""The library's remaining runtime variables (INTEGRATION.md "Runtime
+variables") — PBX_PRECISE (the precise arithmetic for every call of the
+process), GRAVITY_TIMING (per-call timing lines on stderr) and the
+diagnostic traces PBX_MONO_TRACE / PBX_WALK_TRACE — are read once per
+process.  tests/_switch_child.py runs one fixed workload in a child process
+with the defaults and under each of them; the results are compared with the
+defaults' (which the other GPU tests check against the oracle):
 
-* profiles: edges, counts and CSR bit-identical, per-bin sums to 1e-12;
-* octree walk: the same tree and the same per-target walks — bit-identical;
-* direct sum: the ordered-pair kernel in place of the pairwise-symmetric one
-  (another use of the fast reciprocal square root) — the fast-mode 1e-6
-  relative per particle (vector norm for the accelerations).
+* timing and traces: every result bit-identical (profiles: sums to 1e-12);
+* PBX_PRECISE=1: profiles bit-identical; the walk and the direct sum move by
+  the fast reciprocal square root's rounding only — within the fast mode's
+  1e-6 relative per particle (vector norm for the accelerations).
 """
 import os
 import subprocess
@@ -23,44 +23,45 @@ pytestmark = pytest.mark.gpu
 CHILD = Path(__file__).resolve().parent / "_switch_child.py"
 
 GROUPS = {
-    "profile_a": {"PBX_SPEC": "0", "PBX_MONO_EDGE": "0", "PBX_MONO_HINT": "0",
-                  "PBX_MONO_SPIN": "0", "PBX_SEL_TAILFILL": "1", "PBX_SCAN_TICKET": "1",
-                  "PBX_PACK_MAPPED": "0", "PBX_TREE_LEVEL_BUILD": "1",
-                  "PBX_WALK_XCD_CHUNK": "0", "PBX_DIRECT_T": "1", "PBX_DIRECT_SYM": "0"},
-    "profile_b": {"PBX_AGATHER": "0", "PBX_SEL_BT": "256", "PBX_RADIAL_MONO": "0",
-                  "PBX_WALK_TPB": "256", "PBX_WALK_W8": "0", "PBX_DIRECT_T": "2"},
-    "profile_c": {"PBX_SEL_HINT": "0", "PBX_WALK_W8": "1"},
-    "profile_d": {"PBX_RADIAL_EAGER": "1", "PBX_EQUALN": "sort"},
+    "timing": ({"GRAVITY_TIMING": "1"}, True),
+    "traces": ({"PBX_MONO_TRACE": "1", "PBX_WALK_TRACE": "{tmp}/walk_trace.bin"}, True),
+    "precise": ({"PBX_PRECISE": "1"}, False),
 }
 
 
 def run_child(tmp_path, tag, env_extra):
     out = tmp_path / f"{tag}.npz"
-    env = {k: v for k, v in os.environ.items() if not k.startswith("PBX_") or k == "PBX_LIBRARY"}
-    env.update(env_extra)
+    env = {k: v for k, v in os.environ.items()
+           if not (k.startswith("PBX_") or k == "GRAVITY_TIMING") or k == "PBX_LIBRARY"}
+    env.update({k: v.format(tmp=tmp_path) for k, v in env_extra.items()})
     r = subprocess.run([sys.executable, str(CHILD), str(out)], env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0, f"{tag}: rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-4000:]}"
     with np.load(out) as z:
-        return {k: z[k] for k in z.files}
+        return {k: z[k] for k in z.files}, r.stderr
 
 
 @pytest.fixture(scope="module")
 def defaults(gpu, tmp_path_factory):
-    return run_child(tmp_path_factory.mktemp("sw"), "defaults", {})
+    return run_child(tmp_path_factory.mktemp("sw"), "defaults", {})[0]
 
 
 @pytest.mark.parametrize("group", sorted(GROUPS))
-def test_runtime_switches_same_results(defaults, tmp_path, group):
-    got = run_child(tmp_path, group, GROUPS[group])
+def test_runtime_variables_same_results(defaults, tmp_path, group):
+    env, exact = GROUPS[group]
+    got, err = run_child(tmp_path, group, env)
     assert sorted(got) == sorted(defaults)
+    if group == "timing":
+        assert "pbx." in err  # ScopedTimer lines
+    if group == "traces":
+        assert "[mono]" in err and (tmp_path / "walk_trace.bin").stat().st_size > 0
     for k, ref in defaults.items():
         v = got[k]
-        if k.startswith("direct/"):  # per particle, the vector norm for accelerations
+        if (k.startswith("direct/") or k.startswith("tree/")) and not exact:
             d = np.abs(v - ref) if v.ndim == 1 else np.linalg.norm(v - ref, axis=1)
             nrm = np.abs(ref) if ref.ndim == 1 else np.linalg.norm(ref, axis=1)
             assert float(np.max(d / nrm)) < 1e-6, k
         elif "/m" in k:
             np.testing.assert_allclose(v, ref, rtol=1e-12, atol=1e-300, err_msg=k)
-        else:  # edges, counts, CSR, tree outputs
+        else:  # edges, counts, CSR, tree and direct outputs
             assert np.array_equal(v, ref, equal_nan=True), k

@@ -425,33 +425,7 @@ def test_range_walk_wave_costs(gpu):
     wave = cost[:, 0].astype(np.int64)
     assert wave.min() > 0
     assert info["wave_steps"] + info["leaf_wave_steps"] <= wave.sum()
-    # wave split (speed only): the heaviest 64-target groups walk as two
-    # 32-target waves, dispatched first — every target of the full walk and
-    # of range walks bit-identical, every output written (NaN-filled first)
-    d_orig = nat.DeviceArray(4 * n)
-    dev._cost_to_orig_device(d_cost.ptr, d_orig.ptr)
-
-    def walk_fresh(first, count):
-        d_pot.upload(np.full(n, np.nan))
-        d_acc.upload(np.full((n, 3), np.nan))
-        return walk(first, count)
-
-    for permille in (1000, 750, 1):  # the largest group(s) only / the top / every group (capped)
-        dev._set_wave_split(d_orig.ptr, permille)
-        try:
-            p2, a2 = walk_fresh(0, n)
-            assert np.array_equal(p2, p0) and np.array_equal(a2, a0), permille
-            for first, count in ((0, 1000), (12_345, 64 * 700 + 5), (n - 77, 77), (5, 31)):
-                p3, a3 = walk_fresh(first, count)
-                assert np.array_equal(p3, p0[first:first + count]), (permille, first)
-                assert np.array_equal(a3, a0[first:first + count]), (permille, first)
-        finally:
-            dev._set_wave_split(None, 0)
-    with pytest.raises(ValueError, match="permille"):
-        dev._set_wave_split(d_orig.ptr, 0)
-    p4, a4 = walk_fresh(0, n)
-    assert np.array_equal(p4, p0) and np.array_equal(a4, a0)
-    for a in (d_pot, d_acc, d_cost, d_orig):
+    for a in (d_pot, d_acc, d_cost):
         a.free()
 
 
@@ -527,72 +501,6 @@ def test_fast_mode_softened_at_points(gpu):
     assert rel_pot(dev.compute_potentials(0.5), ref.compute_potentials(0.5)) < FAST
     pts = np.random.default_rng(3).normal(size=(500, 3))
     assert rel_acc(dev.accelerations_at_points(pts, 0.5), ref.accelerations_at_points(pts, 0.5)) < FAST
-
-
-@pytest.mark.parametrize("mode", ["precise", pytest.param("fast", marks=pytest.mark.fast)])
-def test_walk_pieces(gpu, mode):
-    """Preorder pieces (pbx_octree_set_walk_pieces): a wave's walk cut by DFS
-    preorder id interval, each piece entering by its lanes' own decisions at
-    the ancestors of its first node.  Without splits (permille 0: the table
-    and the checkpoints only) every target is bit-identical to the plain
-    walk; with splits (a walk records the checkpoints, the next one is cut)
-    the interaction counts are identical — every lane made the same
-    decisions at the same nodes — and the values equal to rounding (partial
-    sums added in piece order), for full and range walks, aligned to 64 or
-    not, every output written (NaN-filled first)."""
-    from pynbodyext import _native as nat
-
-    n = 64 * 4688
-    pos, mass = plummer(n, seed=101)
-    dev = _engine.Octree(pos, mass, 8, 3)
-    want = nat.WANT_POT | nat.WANT_ACC
-    d_pot, d_acc = nat.DeviceArray(8 * n), nat.DeviceArray(24 * n)
-    d_cost = nat.DeviceArray(4 * n)
-
-    def walk(first, count, cost=None):
-        d_pot.upload(np.full(n, np.nan))
-        d_acc.upload(np.full((n, 3), np.nan))
-        dev._compute_range_device(0.5, want, first, count, 1, d_pot.ptr, d_acc.ptr, cost)
-        p, a = np.empty(count), np.empty((count, 3))
-        d_pot.download(p)
-        d_acc.download(a)
-        info = dev.info()
-        return p, a, (info["node_interactions"], info["leaf_pairs"])
-
-    p0, a0, k0 = walk(0, n)
-    dev._set_cost_kind(1)
-    with pytest.raises(ValueError, match="kmax"):
-        dev._set_walk_pieces(500, 1)
-    ranges = ((0, n), (0, 64 * 1000), (64 * 1000, 64 * 2500), (12_345, 64 * 700 + 5), (n - 77, 77))
-    try:
-        dev._set_walk_pieces(0, 2)
-        for first, count in ranges:
-            p1, a1, _ = walk(first, count, d_cost.offset(4 * first))
-            assert np.array_equal(p1, p0[first:first + count]), first
-            assert np.array_equal(a1, a0[first:first + count]), first
-        _, _, k1 = walk(0, n, d_cost.ptr)
-        assert k1 == k0
-        split_seen = False
-        for permille, kmax in ((500, 2), (250, 4), (1, 8)):
-            dev._set_walk_pieces(permille, kmax)
-            for first, count in ranges:
-                for rep in range(2):  # the second walk is cut at the first's checkpoints
-                    p2, a2, _ = walk(first, count, d_cost.offset(4 * first))
-                    pr_, ar_ = p0[first:first + count], a0[first:first + count]
-                    assert not np.isnan(p2).any() and not np.isnan(a2).any()
-                    np.testing.assert_allclose(p2, pr_, rtol=1e-12, atol=0)
-                    err = np.linalg.norm(a2 - ar_, axis=1) / np.linalg.norm(ar_, axis=1)
-                    assert err.max() < 1e-12, (permille, first, err.max())
-                    split_seen |= not (np.array_equal(p2, pr_) and np.array_equal(a2, ar_))
-            _, _, k2 = walk(0, n, d_cost.ptr)
-            assert k2 == k0, (permille, k2, k0)
-        assert split_seen  # some wave was cut (its sums rounded differently)
-    finally:
-        dev._set_walk_pieces(-1, 2)
-    p4, a4, _ = walk(0, n)
-    assert np.array_equal(p4, p0) and np.array_equal(a4, a0)
-    for a in (d_pot, d_acc, d_cost):
-        a.free()
 
 
 @pytest.mark.fast

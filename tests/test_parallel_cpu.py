@@ -1,19 +1,8 @@
-"""Host logic of pynbodyext.parallel that needs no device: the walk-pieces
-option and the 64-aligned range cuts ShardedTree uses with it."""
+"""Host logic of pynbodyext.parallel that needs no device: 64-aligned range
+cuts (whole walk waves per rank)."""
 import pytest
 
-from pynbodyext.parallel import align_ranges, parse_pieces
-
-
-def test_parse_pieces():
-    assert parse_pieces("off") is None and parse_pieces(None) is None and parse_pieces("-1") is None
-    assert parse_pieces("500") == (500, 2)
-    assert parse_pieces("250,4") == (250, 4)
-    assert parse_pieces("0,2") == (0, 2)  # table + checkpoints, no split
-    with pytest.raises(ValueError):
-        parse_pieces("1001,2")
-    with pytest.raises(ValueError):
-        parse_pieces("500,9")
+from pynbodyext.parallel import align_ranges
 
 
 @pytest.mark.parametrize("n", [1000, 64 * 4688, 4_000_000])

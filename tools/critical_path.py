@@ -5,9 +5,7 @@ leaf-order ranges exactly as ShardedTree.balance does, and every range
 walked alone with the per-wave timeline (PBX_WALK_TRACE: start, end and
 node steps of every wave, s_memrealtime at 100 MHz).
 
-Then the same ranges with the heaviest 64-target groups split into two
-32-target waves dispatched first (pbx_octree_set_wave_split at several
-thresholds).  walk_ms includes the trace read-back (host
+walk_ms includes the trace read-back (host
 fwrite between the events); span_us (first wave start to last wave end) is
 the kernel's own critical path.
 
@@ -85,30 +83,11 @@ for first, count in ranges:
     walk(first, count)  # warm
     ms, info = walk(first, count)
     rows.append({"first": first, "count": count, "walk_ms": ms, **info})
-# the same ranges with the heaviest 64-target groups (by the full walk's wave
-# costs, cost kind 1) split into two 32-target waves dispatched first
-# (pbx_octree_set_wave_split); every target's result is unchanged
-split = {}
-for pm in (900, 800, 700):
-    tree._set_wave_split(d_cost_orig.ptr, pm)
-    pr = []
-    for first, count in ranges:
-        walk(first, count)  # warm
-        ms, info = walk(first, count)
-        pr.append({"walk_ms": ms, "span_us": info["span_us"], "wave_us_max": info["wave_us_max"],
-                   "waves": info["waves"], "steps_of_longest": info["steps_of_longest"]})
-    split[f"permille_{pm}"] = {"max_range_ms": max(r["walk_ms"] for r in pr),
-                               "max_span_us": max(r["span_us"] for r in pr),
-                               "max_wave_us": max(r["wave_us_max"] for r in pr),
-                               "bound_speedup_spans": (build_ms + full["span_us"] / 1e3)
-                               / (build_ms + max(r["span_us"] for r in pr) / 1e3),
-                               "ranges": pr}
-tree._set_wave_split(None, 0)
 mx = max(r["walk_ms"] for r in rows)
 out = {"n": n, "world": world, "build_ms": build_ms, "full_walk_ms": full_ms, "full": full,
        "ranges": rows, "max_range_ms": mx,
        "max_range_over_longest_wave": mx / (max(r["wave_us_max"] for r in rows) / 1e3),
-       "max_span_us": max(r["span_us"] for r in rows), "split": split,
+       "max_span_us": max(r["span_us"] for r in rows),
        "bound_speedup_spans": (build_ms + full["span_us"] / 1e3)
        / (build_ms + max(r["span_us"] for r in rows) / 1e3),
        "bound_speedup_excl_profile": (build_ms + full_ms) / (build_ms + mx),
