@@ -348,6 +348,10 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
         d_pos = nat.DeviceArray.from_host(pos)
         d_mass = nat.DeviceArray.from_host(mass)
         dev = DeviceBins()
+        # the positions / masses stay resident and unchanged for the whole
+        # leg: a repeated call may speculate and keep no copy of x
+        # (pbx_profile_set_source_stable)
+        dev.set_source_stable(True)
         sp = ShardedProfile(comm, dev, offset=rank * n)
         e0, e1 = nat.Event(), nat.Event()
 

@@ -421,8 +421,19 @@ int pbx_profile_level0_stats(void *handle, int64_t *out);
  * (launched when the last two calls' edges were identical) and found every
  * edge at its rank: no deferred keys and no order-statistic finish}.  A
  * miss re-runs the assignment; results are identical either way.
- * PBX_SPEC=0 disables the speculation. */
+ * A speculating call stores no x: it is rebuilt from the positions when a
+ * later call reads it, so with on-device inputs the speculation runs only
+ * after pbx_profile_set_source_stable(handle, 1) (host inputs are staged
+ * into the handle and always qualify). */
 int pbx_profile_spec_stats(void *handle, int64_t *out);
+/* stable = 1: the caller's DEVICE positions (and masses) given to this
+ * handle's radial_equaln calls stay alive and unchanged until the next
+ * selection on the handle — a speculating call may then keep no copy of x
+ * and rebuild it from them for a later reader (selection(x), statistics or
+ * percentiles of x).  0 (default): on-device calls do not speculate, x is
+ * stored (no lifetime contract on the positions beyond the call).  No
+ * reference counterpart (numpy has no such hazard). */
+int pbx_profile_set_source_stable(void *handle, int stable);
 /* enabled = 0: this handle's tiled calls never use a level-0 digit
  * geometry they did not derive themselves (every call re-reads x for its
  * level-0 histogram); 1 (default): use the previous call's when it holds,

@@ -10,11 +10,13 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pbx.h"
@@ -73,6 +75,10 @@ struct Device {
   std::mutex mu;                      // serialises host-array entry points
   std::vector<DevBuf *> slots;        // workspace slots, indexed by enum
   DevBuf &slot(int k);
+  // h2d_staged / d2h_staged: pinned chunks and the events of their last DMA
+  std::vector<void *> ring;
+  std::vector<hipEvent_t> ring_ev;
+  std::vector<bool> ring_used;
 };
 
 // Workspace slot ids (one namespace for every module).
@@ -104,6 +110,16 @@ enum Slot {
 // Device of the calling thread (initialised on first use; fails with
 // PBX_ERR_NODEV when there is no GPU).
 Device &current_device();
+
+// Copies between PAGEABLE host memory and the device through a ring of
+// pinned chunks: a few host threads memcpy chunk i + 1 while the DMA engine
+// moves chunk i (a pageable hipMemcpy stages through the runtime's own
+// buffers one copy at a time).  Queued on `st`; h2d_staged returns once the
+// last chunk's DMA is queued (the source may be reused then), d2h_staged
+// once the data is in `dst`.  Small copies take a plain hipMemcpyAsync.
+// The caller holds the device's lock (the ring is per device).
+void h2d_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st);
+void d2h_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st);
 
 bool timing_enabled();
 

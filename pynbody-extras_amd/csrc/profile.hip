@@ -984,6 +984,10 @@ struct SpecArgs {
 #define PBX_SH_K 3
 #endif
 constexpr int SH_K = PBX_SH_K;
+// the full assignment (assign_tiles) runs one workgroup per select block
+// (+ block 0, which writes the bin table): its segment offsets come from the
+// select blocks' own level-0 rows (fused_resolve)
+__host__ __device__ constexpr uint32_t at_blocks(int g0) { return 1u + (uint32_t)SH_K * (uint32_t)(g0 - 1); }
 
 
 // the inputs x is recomputed from when a speculating selection stored none (xsrc_tiles)
@@ -1400,7 +1404,10 @@ __global__ void __launch_bounds__(SH_BT) __attribute__((amdgpu_waves_per_eu(4)))
       double xv = 0.0;
       const bool keep = ((H.in >> k) & 1u) && select_xyz(H.x[k], H.y[k], H.z[k], p, xv);
       const uint64_t bal = __ballot(keep);
-      if (lane == 0) {  // (one store per half from lane k instead: csr_slots +19 us, dropped)
+      // (the wave's 8 words stored from lanes 0..7 once per tile instead:
+      // 265 vs 268 us at 64M, no gain, round 6 — and one store per half
+      // from lane k: csr_slots +19 us; both dropped)
+      if (lane == 0) {
         kw[wj + k] = bal;
         kpre[wj + k] = (uint16_t)run;  // kept particles before the word in this wave's slice
       }
@@ -2046,18 +2053,22 @@ __global__ void __launch_bounds__(FR_TPB)
     }
   }
   __syncthreads();
-  // this block's group: per-block segment offsets (one thread per level-0
-  // block; an edge hit gathers no keys)
+  // this block's group: the segment offsets of the assignment's workgroups
+  // (one thread each; an edge hit gathers no keys).  Hinted: one workgroup
+  // per select block, b = 1 + select block (its rsub u16 rows count its
+  // keys); else one per level-0 block of fused_hist0 (its row), b < g0.
+  // Either way the workgroups' slices of a group follow in index order, so
+  // the select blocks of level-0 block ab hold one contiguous run.
   const int g = blockIdx.x;
   if ((s_err & 2) || g >= ng || edge_hit) return;
   const uint32_t d = gd[g];
   uint32_t c = 0;
-  const int b = tid;  // g0 <= FR_TPB
-  if (s_hint) {  // select_tiles blocks (b - 1) SH_K .. + SH_K - 1 cover block b's tiles
-    if (b >= 1 && b < g0)
-      for (uint32_t j = 0; j < SH_K * rsub; ++j)  // the SH_K blocks' rsub rows each
-        c += (rows16[((int64_t)(b - 1) * SH_K * rsub + j) * (MS0_DIG / 2) + (d >> 1)] >>
-              (16 * (d & 1))) &
+  const int b = tid;  // nblk <= FR_TPB
+  const int nblk = s_hint ? at_blocks(g0) : g0;
+  if (s_hint) {
+    if (b >= 1 && b < nblk)
+      for (uint32_t j = 0; j < rsub; ++j)  // the select block's rsub rows
+        c += (rows16[((int64_t)(b - 1) * rsub + j) * (MS0_DIG / 2) + (d >> 1)] >> (16 * (d & 1))) &
              0xffffu;
   } else if (b < g0) {
     c = rows[(int64_t)b * MS0_DIG + d];
@@ -2076,8 +2087,8 @@ __global__ void __launch_bounds__(FR_TPB)
     ex += k < wv ? wsum[k] : 0u;
     btot += wsum[k];
   }
-  if (b < g0) boff[(int64_t)b * MS_MAXQ + g] = go[g] + ex;
-  if (bcnt && b < g0 && c) atomicAdd(&bcnt[b], c);  // keys block b gathers, all groups
+  if (b < nblk) boff[(int64_t)b * MS_MAXQ + g] = go[g] + ex;
+  if (bcnt && b < nblk && c) atomicAdd(&bcnt[b], c);  // keys workgroup b gathers, all groups
   if (lc && b == 0) lc[g] = btot;  // distributed: this rank's keys of group g
 }
 
@@ -2154,7 +2165,7 @@ __global__ void __launch_bounds__(MS0_TPB)
 // (<= FS_LDS keys), else every pass re-reads it from global memory.
 constexpr int FS_BITS = 11;
 constexpr int FS_DIG = 1 << FS_BITS;
-constexpr int FS_LDS = 8192;
+constexpr int FS_LDS = 16384;  // group keys staged in LDS (128 KB: a 64M call's groups, ~10-20k keys, fit)
 constexpr uint32_t FS_CAND = 256;  // finish_group: keys gathered for the direct rank
 
 // keys of sk[0, S) below / equal to k: 8 keys per step from four 16-B LDS
@@ -2768,12 +2779,6 @@ __global__ void __launch_bounds__(BT)
 // Per-tile counts for the CSR pass ([bin][tile], nb + 1 rows) stay in LDS
 // for up to AG_TR tiles and leave as contiguous row pieces; per-bin sums:
 // one slab row per block.
-constexpr int AG_TR = 64;
-#ifndef PBX_AG_W
-#define PBX_AG_W 4
-#endif
-constexpr int AG_W = PBX_AG_W;                // keep words of a tile per wave
-constexpr int AG_TPS = AG_W * (MS0_TPB / 64) / 64;  // tiles per step (the block's waves)
 struct GatherOut {
   uint64_t *seg;          // key - window base, by segment slot
   AgRec *rec;             // deferred keys, block by block
@@ -2795,10 +2800,12 @@ __device__ __forceinline__ uint32_t block_prefix(const uint32_t *__restrict__ v,
 }
 
 // The speculative assignment's hand-over (select_tiles<FAM, true>): on a hit
-// (ctl->spec & SPEC_HIT) assign_gather only moves the select blocks' deferred
-// keys into their groups' segments and sums their slab rows; on a miss it
-// assigns as before and (block 0) stores the table for the next call.
-constexpr int AG_HU = 4;  // assign_gather on a hit: records per thread in flight
+// (ctl->spec & SPEC_HIT) assign_hit only moves the select blocks' deferred
+// keys into their groups' segments and sums their slab rows; on a miss
+// assign_tiles assigns as below and (block 0) stores the table for the next
+// call.  The host launches both in a speculating call; each returns at once
+// unless the call is its case.
+constexpr int AG_HU = 4;  // assign_hit: records per thread in flight
 struct SpecIO {
   SpecTab *tab;            // written by block 0 of a full assignment
   AgRec *srec;             // select blocks' deferred lists (their groups filled in) ...
@@ -2806,281 +2813,344 @@ struct SpecIO {
   const double *sslab;     // ... and per-bin sums (SH_K rows per assign block)
 };
 
+// assign_tiles' decomposition: with the level-0 hint (select_tiles counted
+// the digits, rows per select block) workgroup 1 + j walks select block j's
+// tiles (part j % SH_K of level-0 block 1 + j / SH_K's range, tile_range)
+// with the segment offsets fused_resolve gave it; without (fused_hist0 read
+// x, rows per level-0 block) workgroup 1 + SH_K (ab - 1) walks level-0 block
+// ab's whole range and the others return (the rare path: a key escaped the
+// hint).  Block 0 writes the table.  Slot counters and the deferred list's
+// count in LDS, like the whole-block kernel it replaced.
+constexpr int AT_BT = 512;
+constexpr int AT_H = SH_K;
+constexpr int AT_TR = 16;                // tiles whose [tile][bin] counts stay in LDS
+constexpr int AT_SL = TILE / AT_BT;      // slots per lane of a tile (8)
+constexpr int AT_HS = AT_SL / 2;         // ... taken in two halves
+static_assert(AT_SL == 8 && TILE / 64 == 64, "a wave takes 8 keep words of a tile");
+
 template <bool MOM>
 __global__ void __launch_bounds__(MS0_TPB)
-    assign_gather(const double *__restrict__ x, const uint64_t *__restrict__ kw, int64_t base,
-                  int64_t span, uint32_t nt, const double *__restrict__ mass,
-                  const FusedCtl *__restrict__ ctl, uint64_t ka, uint64_t kb,
-                  const MsRank *__restrict__ R, int nq,
-                  const uint32_t *__restrict__ gdig, const uint32_t *__restrict__ boff, int nb,
-                  uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
-                  double *__restrict__ slab, GatherOut go, SpecIO sio, XSrc xs) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  // per level-0 digit: the bin of its keys (#{q : digit_q < d} - 1, or nb),
-  // or 0x8000 | group when the digit holds edges — one LDS read per key
+    assign_hit(const FusedCtl *__restrict__ ctl, const uint32_t *__restrict__ gdig,
+               const uint32_t *__restrict__ boff, int nb, FusedStats fs, double *__restrict__ slab,
+               GatherOut go, SpecIO sio) {
   __shared__ uint16_t dtab[MS0_DIG];
   __shared__ uint32_t sslot[RADIX];
-  __shared__ uint32_t dk;
-  __shared__ uint32_t qd[RADIX];
-  __shared__ uint32_t red[MS0_TPB / 64];
-  const int macc = MOM ? fs.nm * nb : 0;
-  double *acc = (double *)smem;
-  const int nr = nb + 1, nrs = nr | 1;  // th row stride odd: flush reads bank-conflict free
-  uint32_t *th = (uint32_t *)(acc + macc);  // [tile][bin]: a wave's atomics hit distinct banks
+  __shared__ int c_ng, c_s, c_hit;
   const int tid = threadIdx.x;
-  // the control record's fields: one load per block, broadcast through LDS
-  // (not ~4 scalar loads of one line in each of the grid's 4096 waves)
-  __shared__ uint64_t c_lo;
-  __shared__ int c_ng, c_s, c_win, c_w0, c_hit, c_xsrc;
   if (tid == 0) {
+    c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
+    c_ng = (ctl->err & 2) ? 0 : ctl->ng;
+    c_s = ctl->s0;
+  }
+  __syncthreads();
+  if (!c_hit) return;
+  const int ng = c_ng;
+  const int macc = MOM ? fs.nm * nb : 0;
+  // (a hit is hinted: the offsets are per select block, the level-0 block's
+  // SH_K select blocks' slices one contiguous run from its first one's)
+  const int64_t ob = blockIdx.x >= 1 ? 1 + (int64_t)SH_K * (blockIdx.x - 1) : 0;
+  for (int g = tid; g < ng; g += MS0_TPB) sslot[g] = boff[ob * MS_MAXQ + g];
+  // digit -> group of the edge-holding digits (the records carry key - lo)
+  for (int g = tid; g < ng; g += MS0_TPB) dtab[gdig[g]] = (uint16_t)g;
+  __syncthreads();
+  const int s = c_s;
+  if (blockIdx.x >= 1) {  // the SH_K lists as one index range, AG_HU records in flight
+    uint32_t lb[SH_K], le[SH_K], tot = 0;
+#pragma unroll
+    for (int l = 0; l < SH_K; ++l) {
+      const uint32_t j = SH_K * (blockIdx.x - 1) + l;
+      lb[l] = sio.srbase[j] - tot;  // record of list l at index i: lb[l] + i
+      tot += sio.srn[j];
+      le[l] = tot;
+    }
+    for (uint32_t i0 = 0; i0 < tot; i0 += MS0_TPB * AG_HU) {
+      AgRec *rp[AG_HU];
+      uint64_t off[AG_HU];
+#pragma unroll
+      for (int u = 0; u < AG_HU; ++u) {
+        const uint32_t i = i0 + u * MS0_TPB + tid;
+        const uint32_t ii = i < tot ? i : 0u;
+        uint32_t base = lb[SH_K - 1];
+#pragma unroll
+        for (int l = SH_K - 2; l >= 0; --l) base = ii < le[l] ? lb[l] : base;
+        rp[u] = sio.srec + base + ii;
+        off[u] = rp[u]->off;
+      }
+#pragma unroll
+      for (int u = 0; u < AG_HU; ++u) {
+        if (i0 + u * MS0_TPB + tid >= tot) break;
+        const uint32_t g = dtab[(uint32_t)(off[u] >> s)];
+        go.seg[atomicAdd(&sslot[g], 1u)] = off[u];
+        rp[u]->tg |= g << AG_TBITS;  // (fix_deferred reads the group)
+      }
+    }
+  }
+  if (MOM) {  // this block's row: its SH_K select blocks' sums; assign_tiles' extra rows zero
+    double *dst = slab + (int64_t)blockIdx.x * macc;
+    for (int k = tid; k < macc; k += MS0_TPB) {
+      double v = 0.0;
+      if (blockIdx.x >= 1)
+        for (uint32_t j = SH_K * (blockIdx.x - 1); j < SH_K * blockIdx.x; ++j)
+          v += sio.sslab[(int64_t)j * macc + k];
+      dst[k] = v;
+    }
+    if (blockIdx.x >= 1) {
+      double *ex = slab + ((int64_t)gridDim.x + (int64_t)(blockIdx.x - 1) * (AT_H - 1)) * macc;
+      for (int k = tid; k < (AT_H - 1) * macc; k += MS0_TPB) ex[k] = 0.0;
+    }
+  }
+}
+
+// The full assignment of a tiled selection (see the section comment above):
+// every kept slot's x, mass and keep bit once, each key's bin from a byte
+// per level-0 digit (the SpecTab encoding: bin, or for an edge-holding digit
+// 128 + group when nb <= 128, else 0xff and the group searched), the [tile]
+// [bin] counts of the CSR pass and the per-bin sums in LDS, the keys of
+// edge-holding digits into their group's segment and the assign block's
+// deferred list.  512-thread workgroups, four per assign block (<= 64 VGPRs,
+// ~27 KB of LDS at 128 bins: 8 waves per SIMD) — the previous kernel ran one
+// 1024-thread workgroup per assign block at 124 VGPRs (4 waves per SIMD,
+// 43 % of wave time parked on waits).  MM: the sums' form — 1 {Σw, Σx·w},
+// 2 {Σw} as dedicated adds, 0 any monomials (monomial(): the same values).
+template <bool MOM, int MM>
+__global__ void __launch_bounds__(AT_BT) __attribute__((amdgpu_waves_per_eu(8)))
+    assign_tiles(const double *__restrict__ x, const uint64_t *__restrict__ kw, int64_t base,
+                 int64_t span, uint32_t nt, const double *__restrict__ mass, const FusedCtl *__restrict__ ctl,
+                 uint64_t ka, uint64_t kb, const MsRank *__restrict__ R, int nq,
+                 const uint32_t *__restrict__ gdig, uint32_t *__restrict__ boff, int nb,
+                 uint8_t *__restrict__ bins, uint32_t *__restrict__ tile_hist, FusedStats fs,
+                 double *__restrict__ slab, GatherOut go, SpecTab *__restrict__ tab, int g0) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint8_t dtab[MS0_DIG];
+  __shared__ uint32_t sgd[RADIX];  // the edge-holding digits (groups), ascending
+  __shared__ uint32_t qd[RADIX];
+  __shared__ uint32_t red[AT_BT / 64];
+  __shared__ uint32_t sslot[RADIX];  // this workgroup's next slot in each group's segment
+  __shared__ uint32_t dk;            // deferred keys listed
+  __shared__ uint64_t c_lo;
+  __shared__ int c_ng, c_s, c_win, c_w0, c_hit, c_hint;
+  const int tid = threadIdx.x;
+  if (tid == 0) {  // the control record: one load per block, broadcast through LDS
     const bool w0 = !(ctl->err & 2);
-    // x to recompute first: a speculating selection stored none, the call
-    // missed, and fused_hist0 did not rebuild it (the hint held)
-    c_xsrc = ((ctl->spec & SPEC_NOX) && !(ctl->spec & SPEC_HIT) && ctl->hint) ? 1 : 0;
+    c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
+    c_hint = ctl->hint ? 1 : 0;
     c_win = w0;
     c_ng = w0 ? ctl->ng : 0;
     c_lo = ctl->lo;
     c_s = ctl->s0;
     c_w0 = ctl->w0;
-    c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
     dk = 0;
   }
   __syncthreads();
-  const int ng = c_ng;
-  for (int g = tid; g < ng; g += MS0_TPB) sslot[g] = boff[(int64_t)blockIdx.x * MS_MAXQ + g];
-  if (c_hit) {  // select_tiles binned the keys: its lists -> the group segments, its sums
-    // digit -> group of the edge-holding digits (the records carry key - lo)
-    for (int g = tid; g < ng; g += MS0_TPB) dtab[gdig[g]] = (uint16_t)g;
-    __syncthreads();
-    const int s = c_s;
-    if (blockIdx.x >= 1) {  // the SH_K lists as one index range, AG_HU records in flight
-      uint32_t lb[SH_K], le[SH_K], tot = 0;
-#pragma unroll
-      for (int l = 0; l < SH_K; ++l) {
-        const uint32_t j = SH_K * (blockIdx.x - 1) + l;
-        lb[l] = sio.srbase[j] - tot;  // record of list l at index i: lb[l] + i
-        tot += sio.srn[j];
-        le[l] = tot;
-      }
-      for (uint32_t i0 = 0; i0 < tot; i0 += MS0_TPB * AG_HU) {
-        AgRec *rp[AG_HU];
-        uint64_t off[AG_HU];
-#pragma unroll
-        for (int u = 0; u < AG_HU; ++u) {
-          const uint32_t i = i0 + u * MS0_TPB + tid;
-          const uint32_t ii = i < tot ? i : 0u;
-          uint32_t base = lb[SH_K - 1];
-#pragma unroll
-          for (int l = SH_K - 2; l >= 0; --l) base = ii < le[l] ? lb[l] : base;
-          rp[u] = sio.srec + base + ii;
-          off[u] = rp[u]->off;
-        }
-#pragma unroll
-        for (int u = 0; u < AG_HU; ++u) {
-          if (i0 + u * MS0_TPB + tid >= tot) break;
-          const uint32_t g = dtab[(uint32_t)(off[u] >> s)];
-          go.seg[atomicAdd(&sslot[g], 1u)] = off[u];
-          rp[u]->tg |= g << AG_TBITS;  // (fix_deferred reads the group)
-        }
-      }
-    }
-    if (MOM) {
-      double *dst = slab + (int64_t)blockIdx.x * macc;
-      for (int k = tid; k < macc; k += MS0_TPB) {
-        double v = 0.0;
-        if (blockIdx.x >= 1)
-          for (uint32_t j = SH_K * (blockIdx.x - 1); j < SH_K * blockIdx.x; ++j)
-            v += sio.sslab[(int64_t)j * macc + k];
-        dst[k] = v;
-      }
-    }
+  if (c_hit) return;  // (assign_hit)
+  const bool hinted = c_hint != 0;
+  // without the hint one workgroup per level-0 block works (see above); the
+  // others leave zero sums (the pack adds every workgroup's row)
+  if (!hinted && blockIdx.x >= 1 && (blockIdx.x - 1u) % SH_K != 0u) {
+    if (MOM)
+      for (int k = tid; k < fs.nm * nb; k += AT_BT) slab[(int64_t)blockIdx.x * fs.nm * nb + k] = 0.0;
     return;
   }
-  const uint32_t rb = block_prefix(go.bcnt, (int)blockIdx.x, red);
-  for (int q = tid; q < nq; q += MS0_TPB) qd[q] = (uint32_t)R[q].prefix;
-  for (int k = tid; k < macc; k += MS0_TPB) acc[k] = 0.0;
-  for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
+  const int ng = c_ng, macc = MOM ? fs.nm * nb : 0;
+  const int nr = nb + 1, nrs = nr | 1;  // th row stride odd
+  double *acc = (double *)smem;
+  uint32_t *th = (uint32_t *)(acc + macc);  // [tile][bin]
+  const int enc = nb <= 128 ? 1 : 0;
+  const uint32_t gmin = enc ? 128u : (uint32_t)SPEC_DEFER;  // bytes >= gmin: edge-holding digit
+  for (int q = tid; q < nq; q += AT_BT) qd[q] = (uint32_t)R[q].prefix;
+  for (int g = tid; g < ng; g += AT_BT) sgd[g] = gdig[g];
+  for (int k = tid; k < macc; k += AT_BT) acc[k] = 0.0;
+  for (int k = tid; k < nrs * AT_TR; k += AT_BT) th[k] = 0;
   __syncthreads();
-  const bool win = c_win;
-  const uint64_t lo = c_lo;
-  const int s = c_s;
-  for (int d = tid; d < MS0_DIG; d += MS0_TPB) {  // #{q : digit_q < d}, lower bound
+  for (int d = tid; d < MS0_DIG; d += AT_BT) {  // #{q : digit_q < d} - 1, lower bound
     int a = 0, len = nq;
     while (len > 0) {
-      const int h = len >> 1;
-      if (qd[a + h] < (uint32_t)d) {
-        a += h + 1;
-        len -= h + 1;
+      const int hh = len >> 1;
+      if (qd[a + hh] < (uint32_t)d) {
+        a += hh + 1;
+        len -= hh + 1;
       } else {
-        len = h;
+        len = hh;
       }
     }
     const int b = a - 1;
-    dtab[d] = (uint16_t)((b < 0 || b >= nb) ? nb : b);
+    const int e = (b < 0 || b >= nb) ? nb : b;  // (no window key has such a digit)
+    dtab[d] = (uint8_t)(enc ? (e < 128 ? e : 0) : e);
   }
   __syncthreads();
-  for (int g = tid; g < ng; g += MS0_TPB) dtab[gdig[g]] = (uint16_t)(0x8000u | (uint32_t)g);
+  for (int g = tid; g < ng; g += AT_BT)
+    dtab[sgd[g]] = enc ? (g < 127 ? (uint8_t)(128 + g) : SPEC_DEFER) : SPEC_DEFER;
   __syncthreads();
-  if (blockIdx.x == 0 && sio.tab) {  // (block 0 has no tiles) the table for the next call
-    SpecTab *T = sio.tab;
-    const bool ok = win && nb <= SPEC_MAXB && ng < 256;
-    // nb <= 128: a window key's digit outside the edges' digits cannot occur
-    // (the lowest / highest window keys ARE the first / last edge), so the
-    // bytes 128 .. 254 carry the groups 0 .. 126 of edge-holding digits
-    const int enc = nb <= 128 ? 1 : 0;
-    for (int d = tid; d < MS0_DIG; d += MS0_TPB) {
-      const uint32_t e = dtab[d];
-      uint8_t c;
-      if (e & 0x8000u) {
-        const uint32_t g = e & 0x7fffu;
-        c = enc ? (g < 127 ? (uint8_t)(128 + g) : SPEC_DEFER) : SPEC_DEFER;
-      } else {
-        c = enc ? (uint8_t)(e < 128 ? e : 0) : (uint8_t)e;
+  const uint64_t lo = c_lo;
+  const int s = c_s;
+  if (blockIdx.x == 0) {  // (no tiles) the table for the next call's speculation
+    if (tab) {
+      SpecTab *T = tab;
+      const bool ok = c_win && nb <= SPEC_MAXB && ng < 256;
+      for (int d = tid; d < MS0_DIG / 16; d += AT_BT) ((uint4 *)T->bin)[d] = ((const uint4 *)dtab)[d];
+      for (int q = tid; q < nq; q += AT_BT) T->qd[q] = qd[q];
+      for (int g = tid; g < ng; g += AT_BT) T->gdig[g] = sgd[g];
+      if (tid == 0) {
+        T->enc = enc;
+        T->edges_valid = 0;  // (fix_deferred stores this call's edges)
+        T->lo = lo;
+        T->s0 = s;
+        T->w0 = c_w0;
+        T->nb = nb;
+        T->nq = nq;
+        T->ng = ng;
+        T->valid = ok ? 1 : 0;
       }
-      T->bin[d] = c;
     }
-    if (tid == 0) T->enc = enc;
-    for (int q = tid; q < nq; q += MS0_TPB) T->qd[q] = qd[q];
-    for (int g = tid; g < ng; g += MS0_TPB) T->gdig[g] = gdig[g];
-    if (tid == 0) {
-      T->edges_valid = 0;  // (fix_deferred stores this call's edges)
-      T->lo = lo;
-      T->s0 = s;
-      T->w0 = c_w0;
-      T->nb = nb;
-      T->nq = nq;
-      T->ng = ng;
-      T->valid = ok ? 1 : 0;
-    }
+    if (MOM)
+      for (int k = tid; k < macc; k += AT_BT) slab[k] = 0.0;
+    return;
   }
-  uint32_t ta, tb;
-  tile_range(nt, ta, tb);
-  if (c_xsrc) {
-    xsrc_tiles(xs, ta, tb);
-    __threadfence();
-    __syncthreads();
-  }
-  // wave w: words [AG_W wl, AG_W (wl + 1)) of tiles ta + sub, ta + sub + AG_TPS, ...
+  // this workgroup's tiles: select block j's (part h of level-0 block ab's
+  // range, tile_range over g0 blocks), or without the hint block ab's all;
+  // bi: the index of its offsets, key count and list (fused_resolve's)
+  const uint32_t ab = 1u + (blockIdx.x - 1u) / SH_K, h = (blockIdx.x - 1u) % SH_K;
+  const uint64_t G = (uint64_t)(g0 - 1);
+  const uint32_t ta0 = (uint32_t)((uint64_t)nt * (ab - 1) / G), tb0 = (uint32_t)((uint64_t)nt * ab / G);
+  const uint32_t ta = hinted ? ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * h / SH_K) : ta0;
+  const uint32_t tb = hinted ? ta0 + (uint32_t)((uint64_t)(tb0 - ta0) * (h + 1) / SH_K) : tb0;
+  const uint32_t bi = hinted ? blockIdx.x : ab;
+  for (int g = tid; g < ng; g += AT_BT) sslot[g] = boff[(int64_t)bi * MS_MAXQ + g];
+  // the list starts after the earlier workgroups' gathered keys
+  uint32_t pre = 0;
+  for (uint32_t i = (uint32_t)tid; i < bi; i += AT_BT) pre += go.bcnt[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (lane_id() == 0) red[tid >> 6] = pre;
+  __syncthreads();
+  uint32_t rb = 0;
+  for (int q = 0; q < AT_BT / 64; ++q) rb += red[q];
+  if (tid == 0) go.rbase[bi] = rb;
+  const bool win = c_win;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wl = w % (64 / AG_W), sub = w / (64 / AG_W);
   const uint32_t lane = lane_id();
   const bool wneed = mass != nullptr;
-  // one tile's share of a wave: x, masses and keep words by particle slot,
-  // so no load address waits for anything; three buffers, loads issued two
-  // tiles ahead.  No branch around a load (a missing mass array reads x,
-  // and the weight is 1), so the in-order vmcnt waits stay exact.
-  struct Part {
-    double v[AG_W], m[AG_W];
-    uint64_t k[AG_W];
-  };
-  const double *mp = wneed ? mass + base : x;
-  // the keep words as VECTOR loads (every lane the same address: one line):
-  // a scalar load would be waited for with lgkmcnt(0) — SMEM returns out of
-  // order — at the first LDS read after it, i.e. every tile's lookups would
-  // wait for the keep words of the tiles in flight
-  const uint32_t vz = vgpr_zero();
-  auto issue = [&](uint32_t t, Part &P) {
-    const int64_t s0 = (int64_t)t * TILE + 64 * (wl * AG_W);
+  const double *mp = wneed ? mass + base : x;  // (the masses of the selection's span)
+  for (uint32_t r0 = ta; r0 < tb; r0 += AT_TR) {
+    const uint32_t r1 = min(tb, r0 + (uint32_t)AT_TR);
+    for (uint32_t t = r0; t < r1; ++t) {
+      const uint32_t tl = t - r0;
 #pragma unroll
-    for (int kk = 0; kk < AG_W; ++kk) {
-      const int64_t sl = s0 + 64 * kk + lane;
-      // streaming (nt) loads, both read once: 202 -> 180 us at 64M (A/B/A/B)
-      P.v[kk] = __builtin_nontemporal_load(x + sl);
-      P.m[kk] = __builtin_nontemporal_load(mp + (wneed ? (sl < span ? sl : span - 1) : sl));
-      P.k[kk] = kw[(s0 >> 6) + kk + vz];
-    }
-  };
-  constexpr uint32_t SKIP = 0xffffu, DEFER = 0x10000u;  // DEFER + group: a deferred key
-  auto bin = [&](uint32_t t, uint32_t tl, const Part &P) {
-    uint32_t bk[AG_W];
-    double wv[AG_W];
-    uint64_t anydef = 0;
+      for (int hf = 0; hf < 2; ++hf) {  // the wave's 8 keep words in two halves of 4
+      const int64_t s0 = (int64_t)t * TILE + (int64_t)w * (64 * AT_SL) + hf * (64 * AT_HS);
+      // the half's 4 keep words (uniform: scalar loads), 4 slots per lane
+      const uint64_t *kwp = kw + (s0 >> 6);
+      uint64_t kk[AT_HS];
+      double xv[AT_HS], mv[AT_HS];
 #pragma unroll
-    for (int kk = 0; kk < AG_W; ++kk) {
-      const bool kp = (P.k[kk] >> lane) & 1ull;
-      const uint64_t key = dkey(P.v[kk]);
-      const bool inw = win && key >= ka && key <= kb;  // fused_hist0's window
-      const uint32_t e = dtab[inw ? (uint32_t)((key - lo) >> s) : 0u];
-      // (NaN in a digit without edges: no NaN edge, dropped like the table says;
-      // NaN in a group's digit is deferred: its bin is below the first NaN edge)
-      const bool def = kp && inw && (e & 0x8000u);
-      // a deferred key carries its group: DEFER + g (no second table lookup)
-      bk[kk] = !kp ? SKIP : def ? DEFER + (e & 0x7fffu) : inw ? e : (uint32_t)nb;
-      wv[kk] = wneed ? P.m[kk] : 1.0;
-      anydef |= __ballot(def);
-    }
-    const uint32_t sbase = t * (uint32_t)TILE + 64u * (uint32_t)(wl * AG_W) + lane;
-    // (branch-free byte stores and adds — non-bins into per-lane LDS dummies —
-    // measured the same, 179 us at 64M: the branches are not the cost)
-#pragma unroll
-    for (int kk = 0; kk < AG_W; ++kk)
-      if (bk[kk] <= (uint32_t)nb) {
-        bins[sbase + 64u * kk] = (uint8_t)bk[kk];
-        atomicAdd(&th[tl * nrs + bk[kk]], 1u);
+      for (int k = 0; k < AT_HS; ++k) {
+        kk[k] = kwp[k];
+        const int64_t sl = s0 + 64 * k + lane;
+        xv[k] = __builtin_nontemporal_load(x + sl);
+        mv[k] = wneed ? __builtin_nontemporal_load(mp + (sl < span ? sl : span - 1)) : 1.0;
       }
-    if (MOM) {
+      uint32_t c[AT_HS];
+      uint64_t key[AT_HS];
+      uint32_t kp8 = 0, inw8 = 0;
 #pragma unroll
-      for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
-        if (q >= fs.nm) break;
-        mom_add<AG_W>(acc + q * nb, fs.op[q], fs.col[q], fs.f[q], fs.w[q], bk, P.v, wv,
-                      (uint32_t)nb);
+      for (int k = 0; k < AT_HS; ++k) {  // every lookup issued before any is used
+        const bool kp = (kk[k] >> lane) & 1ull;
+        key[k] = dkey(xv[k]);
+        const bool inw = kp && win && key[k] >= ka && key[k] <= kb;
+        kp8 |= (uint32_t)kp << k;
+        inw8 |= (uint32_t)inw << k;
+        c[k] = dtab[inw ? (uint32_t)((key[k] - lo) >> s) : 0u];
       }
-    }
-    if (anydef) {  // rare (edge-holding digits): the group segment + the block's deferred list
-      // (one list reservation per call for the whole wave, ballot ranks, and
-      // every segment-slot atomic issued before any is waited for: 179 -> 184
-      // us at 64M — dropped)
+      uint32_t defm = 0;
 #pragma unroll
-      for (int kk = 0; kk < AG_W; ++kk)
-        if (bk[kk] >= DEFER) {
-          const uint64_t off = dkey(P.v[kk]) - lo;
-          const uint32_t g = bk[kk] - DEFER;
-          go.seg[atomicAdd(&sslot[g], 1u)] = off;
-          go.rec[rb + atomicAdd(&dk, 1u)] = AgRec{off, wv[kk], sbase + 64u * kk, t | (g << AG_TBITS)};
+      for (int k = 0; k < AT_HS; ++k) {
+        if (!((kp8 >> k) & 1u)) continue;
+        const bool inw = (inw8 >> k) & 1u;
+        if (inw && c[k] >= gmin) {
+          defm |= 1u << k;
+          continue;
         }
-    }
-  };
-  for (uint32_t r0 = ta; r0 < tb; r0 += AG_TR) {
-    const uint32_t r1 = min(tb, r0 + (uint32_t)AG_TR);
-    Part A, B, C;
-    constexpr uint32_t S1 = AG_TPS;
-    const uint32_t t0 = r0 + sub;
-    // every issue unconditional (a tile past the range re-reads the last
-    // one): the same loads are in flight on every path, so the compiler's
-    // vmcnt waits stay exact (a conditional issue made it wait for all)
-    auto cl = [&](uint32_t t) { return t < r1 ? t : r1 - 1; };
-    if (t0 < r1) {
-      issue(t0, A);
-      issue(cl(t0 + S1), B);
-    }
-    for (uint32_t t = t0; t < r1; t += 3 * S1) {
-      issue(cl(t + 2 * S1), C);
-      bin(t, t - r0, A);
-      if (t + S1 >= r1) break;
-      issue(cl(t + 3 * S1), A);
-      bin(t + S1, t + S1 - r0, B);
-      if (t + 2 * S1 >= r1) break;
-      issue(cl(t + 4 * S1), B);
-      bin(t + 2 * S1, t + 2 * S1 - r0, C);
+        const uint32_t bk = inw ? c[k] : (uint32_t)nb;  // outside the window: dropped
+        bins[s0 + 64 * k + lane] = (uint8_t)bk;
+        atomicAdd(&th[tl * nrs + bk], 1u);
+        if (MOM && bk < (uint32_t)nb) {
+          if (MM == 1) {
+            atomicAdd(&acc[bk], mv[k]);
+            atomicAdd(&acc[nb + bk], xv[k] * mv[k]);
+          } else if (MM == 2) {
+            atomicAdd(&acc[bk], mv[k]);
+          } else {
+#pragma unroll
+            for (int q = 0; q < AS_MAXM; ++q) {  // unrolled: fs's fields are kernel-argument scalars
+              if (q >= fs.nm) break;
+              const double f = fs.f[q] == 0 ? xv[k] : mv[k];
+              const double ww = fs.w[q] == 0 ? xv[k] : mv[k];
+              atomicAdd(&acc[q * nb + bk], monomial(fs.col[q], f, ww));
+            }
+          }
+        }
+      }
+      if (__ballot(defm != 0u)) {  // rare: the keys of edge-holding digits
+#pragma unroll
+        for (int k = 0; k < AT_HS; ++k) {
+          const bool def = (defm >> k) & 1u;
+          const uint64_t bd = __ballot(def);
+          if (!bd) continue;
+          uint32_t li0 = 0;  // the list slots: one LDS atomic per wave
+          if (lane == 0) li0 = atomicAdd(&dk, (uint32_t)__popcll(bd));
+          li0 = __shfl(li0, 0, 64);
+          if (def) {
+            const uint64_t off = key[k] - lo;
+            uint32_t g;
+            if (c[k] != SPEC_DEFER) {
+              g = c[k] - 128u;
+            } else {  // search the group by its digit
+              const uint32_t dd = (uint32_t)(off >> s);
+              int l = 0, hh = ng - 1;
+              while (l < hh) {
+                const int mid = (l + hh) >> 1;
+                if (sgd[mid] < dd) l = mid + 1; else hh = mid;
+              }
+              g = (uint32_t)l;
+            }
+            go.seg[atomicAdd(&sslot[g], 1u)] = off;
+            const uint32_t slot = (uint32_t)(s0 + 64 * k) + lane;
+            go.rec[rb + li0 + rank_below(bd)] = AgRec{off, mv[k], slot, t | (g << AG_TBITS)};
+          }
+        }
+      }
+      }
     }
     __syncthreads();
     const int nrt = (int)(r1 - r0);
-    for (int k = tid; k < nr * AG_TR; k += MS0_TPB) {
-      const int b = k / AG_TR, tl = k - b * AG_TR;
-      if (tl < nrt) tile_hist[(int64_t)b * nt + r0 + tl] = th[tl * nrs + b];
+    for (int k = tid; k < nr * nrt; k += AT_BT) {
+      const int b = k / nrt, tl = k - b * nrt;
+      tile_hist[(int64_t)b * nt + r0 + tl] = th[tl * nrs + b];
     }
     __syncthreads();
-    for (int k = tid; k < nrs * AG_TR; k += MS0_TPB) th[k] = 0;
+    for (int k = tid; k < nrs * AT_TR; k += AT_BT) th[k] = 0;
     __syncthreads();
   }
-  if (tid == 0) {
-    go.rbase[blockIdx.x] = rb;
-    go.rn[blockIdx.x] = dk;
-  }
+  if (tid == 0) go.rn[bi] = dk;
   if (MOM) {
     double *dst = slab + (int64_t)blockIdx.x * macc;
-    for (int k = tid; k < macc; k += MS0_TPB) dst[k] = acc[k];
+    for (int k = tid; k < macc; k += AT_BT) dst[k] = acc[k];
   }
+}
+
+// A speculating selection stored no x and its call missed with the level-0
+// hint held (fused_hist0 did not rebuild it): x of every tile, from the
+// positions, before assign_tiles reads it (every block returns at once
+// otherwise)
+__global__ void __launch_bounds__(TPB)
+    xsrc_miss(const FusedCtl *__restrict__ ctl, XSrc xs, uint32_t nt, uint32_t tiles_per_block) {
+  __shared__ int c_x;
+  if (threadIdx.x == 0)
+    c_x = ((ctl->spec & SPEC_NOX) && !(ctl->spec & SPEC_HIT) && ctl->hint) ? 1 : 0;
+  __syncthreads();
+  if (!c_x) return;
+  const uint32_t ta = blockIdx.x * tiles_per_block;
+  xsrc_tiles(xs, ta, min(nt, ta + tiles_per_block));
 }
 
 // The deferred keys' bins once fused_finish has the edges (the ~1-3 % of
@@ -3119,13 +3189,14 @@ __global__ void __launch_bounds__(MS0_TPB)
   tile_range(nt, ta, tb);
   const uint32_t wt = (uint32_t)(FD_LDSW / nrs);  // tiles per window
   __shared__ uint64_t c_lo;  // the control record's fields, one load per block
-  __shared__ int c_ng, c_hit, c_edge;  // (c_ng -1: no window)
+  __shared__ int c_ng, c_hit, c_edge, c_hint;  // (c_ng -1: no window)
   if (tid == 0) {
     const bool ok = !(ctl->err & 2);
     c_ng = ok ? ctl->ng : -1;
     c_lo = ctl->lo;
     c_hit = (ctl->spec & SPEC_HIT) ? 1 : 0;
     c_edge = (ctl->spec & SPEC_EDGE) ? 1 : 0;
+    c_hint = ctl->hint ? 1 : 0;
   }
   __syncthreads();
   // an edge hit: no deferred keys, and the table keeps its edges (the pack
@@ -3153,10 +3224,11 @@ __global__ void __launch_bounds__(MS0_TPB)
     __syncthreads();
     if (tid == 0) T->edges_valid = s_fin;
   }
-  // this block's deferred keys: assign_gather's list of the block, or on a
-  // speculation hit the lists of its SH_K select blocks (keys of its own tiles)
+  // this block's deferred keys (keys of its own tiles): on a speculation hit
+  // the lists of its SH_K select blocks; else assign_tiles' lists — one per
+  // select block with the level-0 hint, one for the block without
   const bool hit = c_hit != 0;
-  const int nl = hit ? (blockIdx.x >= 1 ? SH_K : 0) : 1;
+  const int nl = blockIdx.x == 0 ? 0 : (hit || c_hint) ? SH_K : 1;
   int64_t lb[SH_K], lc[SH_K];
   int64_t cnt_all = 0;
 #pragma unroll
@@ -3164,7 +3236,8 @@ __global__ void __launch_bounds__(MS0_TPB)
     lb[l] = 0;
     lc[l] = 0;
     if (l < nl && ok_all) {
-      const uint32_t j = hit ? SH_K * (blockIdx.x - 1) + l : blockIdx.x;
+      const uint32_t j = hit ? SH_K * (blockIdx.x - 1) + l
+                             : (c_hint ? 1 + SH_K * (blockIdx.x - 1) + l : blockIdx.x);
       lb[l] = hit ? sio.srbase[j] : rbase[j];
       lc[l] = hit ? sio.srn[j] : rn[j];
       cnt_all += lc[l];
@@ -4053,7 +4126,7 @@ __global__ void __launch_bounds__(MONO_BT) radial_mono(MonoArgs a) {
     const int s = ctl0.s0;
     for (int g = (int)t; g < ng; g += (int)nt) {
       const int64_t o = g_off[g], S = (int64_t)g_off[g + 1] - o;
-      const bool in_lds = S <= FS_LDS;
+      const bool in_lds = S <= (int64_t)(sizeof(L0) / 8);  // (L0 holds 8192 u64 keys)
       if (in_lds)
         for (int64_t i = tid; i < S; i += MONO_BT) sk[i] = ld_sc1(&a.seg[o + i]);
       __syncthreads();
@@ -4590,6 +4663,16 @@ struct Profile {
   // lists, their [start, length] per select block, per-block sums
   Buf stab, srec, sspec, sslab, sflag;
   bool spec_next = false;  // the last tiled call's ranks matched the table: speculate
+  // a speculating call launched select_tiles<_, true> and has not finished
+  // (an error between it and fused_finish, which clears them, can leave the
+  // speculation flag word and the per-edge counts set): the next speculating
+  // call zeroes them first
+  bool spec_dirty = false;
+  // pbx_profile_set_source_stable: the caller's device positions stay alive
+  // and unchanged until the next selection on this handle, so a speculating
+  // call may keep no copy of x (ensure_x rebuilds it from them); without it
+  // only handle-owned (staged host) positions let a call speculate
+  bool src_stable = false;
   bool edge_next = false;  // ... and its edges were the call's before it: speculate on edges too
   std::vector<double> last_edges;  // the last tiled call's edges
   Buf slteq;               // edge speculation: per rank, keys below / equal to its edge
@@ -4962,15 +5045,21 @@ static SelPrep select_prep(Profile &P, hipStream_t st, const void *pos, const vo
   const void *d_pos = pos, *d_mass = mass;
   P.x_missing = false;
   if (!on_device && n) {
+    // Only the families' span [lo, hi) is read: only it crosses PCIe, at its
+    // own offset in an n-sized buffer (the kernels index particles
+    // absolutely), through pinned chunks (h2d_staged).
     // (lazy: kept for the selection's lifetime — a speculating tiled call may
     // have to recompute x from them later, ensure_x)
-    void *tp = (lazy ? P.posst : P.keys0).get(ps * 3 * (size_t)n);
-    PBX_HIP(hipMemcpyAsync(tp, pos, ps * 3 * n, hipMemcpyHostToDevice, st));
+    Device &dv = current_device();
+    char *tp = (char *)(lazy ? P.posst : P.keys0).get(ps * 3 * (size_t)n);
+    if (span) h2d_staged(dv, tp + ps * 3 * (size_t)lo, (const char *)pos + ps * 3 * (size_t)lo,
+                         ps * 3 * (size_t)span, st);
     d_pos = tp;
     if (mass) {
       Buf &mb = lazy ? P.mstage : P.keys1;  // lazy: kept for the selection's lifetime
-      void *tm2 = mb.get(ms * (size_t)n);
-      PBX_HIP(hipMemcpyAsync(tm2, mass, ms * n, hipMemcpyHostToDevice, st));
+      char *tm2 = (char *)mb.get(ms * (size_t)n);
+      if (span) h2d_staged(dv, tm2 + ms * (size_t)lo, (const char *)mass + ms * (size_t)lo,
+                           ms * (size_t)span, st);
       d_mass = tm2;
     }
   }
@@ -5589,6 +5678,13 @@ int pbx_profile_spec_stats(void *handle, int64_t *out) {
   });
 }
 
+int pbx_profile_set_source_stable(void *handle, int stable) {
+  return guard([&] {
+    Profile &P = as_profile(handle);
+    P.src_stable = stable != 0;
+  });
+}
+
 int pbx_profile_set_level0_hint(void *handle, int enabled) {
   return guard([&] {
     Profile &P = as_profile(handle);
@@ -5711,14 +5807,13 @@ int pbx_profile_get_selection(void *handle, int64_t *h_idx, double *h_x, double 
       int64_t *tmp = (int64_t *)P.vtmp.get(sizeof(int64_t) * (size_t)n);
       hipLaunchKernelGGL(widen_perm, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st,
                          (const int32_t *)P.idx.p, n, tmp);
-      PBX_HIP(hipMemcpyAsync(h_idx, tmp, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+      d2h_staged(d, h_idx, tmp, sizeof(int64_t) * n, st);  // (through pinned chunks)
     }
     if (h_x) {
       ensure_x(P, st);
-      PBX_HIP(hipMemcpyAsync(h_x, P.x.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+      d2h_staged(d, h_x, P.x.p, sizeof(double) * n, st);
     }
-    if (h_w && P.has_w)
-      PBX_HIP(hipMemcpyAsync(h_w, P.w.p, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    if (h_w && P.has_w) d2h_staged(d, h_w, P.w.p, sizeof(double) * n, st);
     PBX_HIP(hipStreamSynchronize(st));
   });
 }
@@ -6191,11 +6286,14 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       thist.kb = empty_bounds ? 0ull : kb;
       // the speculative assignment: when the last tiled call's level-0 ranks
       // matched the stored table (a repeated or similar call), select_tiles
-      // bins with it (checked by fused_resolve; a miss takes assign_gather)
+      // bins with it (checked by fused_resolve; a miss takes assign_tiles).
+      // It stores no x, which is then rebuilt from the positions on demand:
+      // only from positions the handle owns (staged host arrays) or that the
+      // caller declared stable
       bool spec_ops = true;  // select_tiles' sums take the dedicated monomials only
       for (int q = 0; q < fs.nm; ++q) spec_ops = spec_ops && fs.op[q] != MO_GEN;
       if (hints && P.spec_next && P.stab.p && nb <= SPEC_MAXB && fs.nm * nb <= SPEC_MACC &&
-          spec_ops) {
+          spec_ops && (!on_device || P.src_stable)) {
         thist.sa.tab = (const SpecTab *)P.stab.p;
         thist.sa.fs = fs;
         thist.sa.nb = (int)nb;
@@ -6205,10 +6303,18 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
           PBX_HIP(hipMemsetAsync(P.slteq.p, 0, sizeof(uint32_t) * 2 * MS_MAXQ, st));
         }
         thist.sa.lteq = (uint32_t *)P.slteq.p;
+        if (P.spec_dirty) {
+          if (P.sflag.p) PBX_HIP(hipMemsetAsync(P.sflag.p, 0, sizeof(uint32_t), st));
+          if (P.slteq.p) PBX_HIP(hipMemsetAsync(P.slteq.p, 0, sizeof(uint32_t) * 2 * MS_MAXQ, st));
+          P.spec_dirty = false;
+        }
       }
       const uint32_t nt = select_launch(P, st, pos, mass, n, on_device, use_sphere, sphere, fam,
                                         nfam, ndim, lazy, 0, 0, /*tiled=*/true, &thist);
-      if (thist.spec) ++P.n_spec;
+      if (thist.spec) {
+        ++P.n_spec;
+        P.spec_dirty = true;  // (until the call's results arrive)
+      }
       const bool hinted = hints && P.x_tiled;
       tiled_call = P.x_tiled;
       if (hinted) ++P.n_tiled;  // (the next tiled call reads the slot this one writes)
@@ -6227,13 +6333,17 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       // per-group finish -> edges
       const int g0 = fused_grid(n_sel);
       uint32_t *rows = (uint32_t *)P.msRows.get(sizeof(uint32_t) * (size_t)g0 * MS0_DIG);
-      // tiled selections: assignment fused with the gather (assign_gather),
-      // the deferred keys binned block by block by fix_deferred
+      // tiled selections: assignment fused with the gather (assign_tiles),
+      // the deferred keys binned block by block by fix_deferred; the three
+      // per-block words [bcnt | rbase | rn] zeroed by fused_hist0
       const bool agath = tiled && lazy && n_sel;
-      uint32_t *bcnt = agath ? (uint32_t *)P.fblk.get(sizeof(uint32_t) * 3 * (size_t)g0) : nullptr;
+      if (agath && g0 < 2) fail(PBX_ERR_RUNTIME, "tiled selection with one level-0 block");
+      // [bcnt | rbase | rn] per assignment workgroup (at_blocks: one per select block + 1)
+      const uint32_t nab = agath ? at_blocks(g0) : 0u;
+      uint32_t *bcnt = agath ? (uint32_t *)P.fblk.get(sizeof(uint32_t) * 3 * (size_t)nab) : nullptr;
       const uint32_t *hflag = (const uint32_t *)(stat + nt + 1 + 2 * MM_SLOTS);
       const FusedSetup fsu{(const uint64_t *)stat, nt, n_sel, ka, kb, (int)empty_bounds, (int)tiled,
-                           (uint32_t *)P.toff.p, bcnt, agath ? g0 : 0, (int)dist,
+                           (uint32_t *)P.toff.p, bcnt, agath ? 3 * (int)nab : 0, (int)dist,
                            (const uint64_t *)P.kw.p,
                            hinted ? hints + ((P.n_tiled - 1) & 1) : nullptr, hflag,
                            hinted ? hints + (P.n_tiled & 1) : nullptr, (const uint32_t *)P.sbt.p,
@@ -6258,7 +6368,9 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         comm_allreduce(comm, H, H, MS0_DIG, 3, 0, st, lk);
       }
       MsRank *R = (MsRank *)P.msR.get(sizeof(MsRank) * (size_t)nq);
-      uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)g0) * (MS_MAXQ + 1));
+      // [gdig | goff | gq | boff: a row per assignment workgroup (g0 or nab rows)]
+      uint32_t *gdig = (uint32_t *)P.fgrp.get(sizeof(uint32_t) * (3 + (size_t)std::max<uint32_t>(g0, nab)) *
+                                              (MS_MAXQ + 1));
       uint32_t *goff = gdig + (MS_MAXQ + 1), *gq = goff + (MS_MAXQ + 1);
       uint32_t *boff = gq + (MS_MAXQ + 1);
       // the stored bin table (one rank, tiled assignment): allocated zeroed (invalid)
@@ -6317,28 +6429,47 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
         const int64_t macc = (int64_t)fs.nm * nb;
         th = (uint32_t *)P.csrh.get(sizeof(uint32_t) * (size_t)nt * nr);
         bins8 = (uint8_t *)P.bins8.get((size_t)nt * TILE);  // by particle slot
-        double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)(2 * g0) * macc) : nullptr;
-        go = GatherOut{seg, (AgRec *)P.frec.get(sizeof(AgRec) * (size_t)n_sel), bcnt, bcnt + g0,
-                       bcnt + 2 * g0};
-        const size_t lds = sizeof(double) * (size_t)macc + sizeof(uint32_t) * (size_t)(nr | 1) * AG_TR;
+        // (nab: assign_tiles' workgroups = its slab rows)
+        double *slab = fs.nm ? (double *)P.fslab.get(sizeof(double) * (size_t)(nab + g0) * macc) : nullptr;
+        go = GatherOut{seg, (AgRec *)P.frec.get(sizeof(AgRec) * (size_t)n_sel), bcnt, bcnt + nab,
+                       bcnt + 2 * nab};
         sio = SpecIO{stab, thist.spec ? thist.sa.rec : nullptr,
                      thist.spec ? (const uint32_t *)thist.sa.rbase : nullptr,
                      thist.spec ? (const uint32_t *)thist.sa.rn : nullptr,
                      thist.spec ? (const double *)thist.sa.slab : nullptr};
-        auto ag = [&](auto kern) {
-          hipLaunchKernelGGL(kern, dim3(g0), dim3(MS0_TPB), lds, st, x, (const uint64_t *)P.kw.p,
-                             P.sel_base, P.sel_span, nt, P.sel_mass,
-                             (const FusedCtl *)ctl, ka, kb, (const MsRank *)R, nq,
-                             (const uint32_t *)gdig, (const uint32_t *)boff, (int)nb, bins8, th,
-                             fs, slab, go, sio, thist.xs);
+        if (thist.spec) {
+          // a speculating call: the hit's hand-over (assign_hit), and x from the
+          // positions for a miss whose selection stored none (xsrc_miss); each
+          // returns at once unless the call is its case
+          constexpr uint32_t xpb = 4;
+          hipLaunchKernelGGL(xsrc_miss, dim3(ceil_div(nt, xpb)), dim3(TPB), 0, st, (const FusedCtl *)ctl,
+                             thist.xs, nt, xpb);
+          if (fs.nm)
+            hipLaunchKernelGGL(assign_hit<true>, dim3(g0), dim3(MS0_TPB), 0, st, (const FusedCtl *)ctl,
+                               (const uint32_t *)gdig, (const uint32_t *)boff, (int)nb, fs, slab, go, sio);
+          else
+            hipLaunchKernelGGL(assign_hit<false>, dim3(g0), dim3(MS0_TPB), 0, st, (const FusedCtl *)ctl,
+                               (const uint32_t *)gdig, (const uint32_t *)boff, (int)nb, fs, slab, go, sio);
+        }
+        // the sums' form: {Σw, Σx·w} / {Σw} as dedicated adds, else any monomials
+        const int mm = (fs.nm == 2 && fs.op[0] == MO_W && fs.op[1] == MO_XW) ? 1
+                       : (fs.nm == 1 && fs.op[0] == MO_W) ? 2 : 0;
+        const size_t lds = sizeof(double) * (size_t)macc + sizeof(uint32_t) * (size_t)(nr | 1) * AT_TR;
+        auto at = [&](auto kern) {
+          hipLaunchKernelGGL(kern, dim3(nab), dim3(AT_BT), lds, st, x, (const uint64_t *)P.kw.p,
+                             P.sel_base, P.sel_span, nt, P.sel_mass, (const FusedCtl *)ctl, ka, kb,
+                             (const MsRank *)R, nq, (const uint32_t *)gdig, boff, (int)nb, bins8, th, fs,
+                             slab, go, stab, g0);
         };
-        if (fs.nm) ag(assign_gather<true>);
-        else ag(assign_gather<false>);
+        if (!fs.nm) at(assign_tiles<false, 0>);
+        else if (mm == 1) at(assign_tiles<true, 1>);
+        else if (mm == 2) at(assign_tiles<true, 2>);
+        else at(assign_tiles<true, 0>);
         PBX_HIP(hipGetLastError());
-        ablocks = (uint32_t)g0;
+        ablocks = nab;
         if (fs.nm) {
           maccs = slab;
-          maccs2 = slab + (size_t)g0 * macc;
+          maccs2 = slab + (size_t)nab * macc;
         }
       } else {
         hipLaunchKernelGGL(fused_gather, dim3(g0), dim3(MS0_TPB), 0, st, x, ka, kb,
@@ -6555,6 +6686,7 @@ static int radial_equaln_entry(void *comm, void *handle, const double *pos, cons
       P.last_edges.assign(he, he + nq);
       // a hit stored no x (ensure_x rebuilds it on demand); a miss rebuilt it
       P.x_missing = (c.spec & SPEC_NOX) && (c.spec & SPEC_HIT);
+      P.spec_dirty = false;  // fused_finish cleared the flag word and the edge counts
     }
     P.mm[0] = c.kmin;
     P.mm[1] = c.kmax;

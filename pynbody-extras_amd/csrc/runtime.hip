@@ -1,5 +1,6 @@
 // runtime.hip — device selection, HBM allocation, the library stream and
 // HIP events, thread-local error text.  No kernels live here.
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
@@ -48,6 +49,137 @@ void *DevBuf::ensure(size_t need) {
 DevBuf::~DevBuf() {
   // Device buffers of a process-lifetime context are released by the
   // driver at exit; freeing here could run after the HIP runtime is gone.
+}
+
+// ---- staged host <-> device copies (pbx_common.h) ---------------------
+// A few persistent host threads split each chunk's memcpy; the pool is a
+// leaked singleton (its threads block on a condition variable for the life
+// of the process: no joinable std::thread is ever destroyed at exit).
+namespace {
+class CopyPool {
+ public:
+  static CopyPool &get() {
+    static CopyPool *p = new CopyPool();
+    return *p;
+  }
+  // dst[0 .. len) = src[0 .. len), split over the pool and the caller
+  void copy(void *dst, const void *src, size_t len) {
+    const int nt = (int)th_.size() + 1;
+    if (len < ((size_t)1 << 20) || nt == 1) {
+      std::memcpy(dst, src, len);
+      return;
+    }
+    const size_t part = ((len + nt - 1) / nt + 63) & ~(size_t)63;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      dst_ = (char *)dst;
+      src_ = (const char *)src;
+      len_ = len;
+      part_ = part;
+      pending_ = nt - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    piece(0);  // the caller's share
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  CopyPool() {
+    unsigned hw = std::thread::hardware_concurrency();
+    const int n = (int)std::max(1u, std::min(8u, hw ? hw / 2 : 1u));
+    for (int i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  void piece(int i) {
+    const size_t a = (size_t)i * part_;
+    if (a < len_) std::memcpy(dst_ + a, src_ + a, std::min(part_, len_ - a));
+  }
+  void loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      piece(i);
+      std::lock_guard<std::mutex> lk(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  char *dst_ = nullptr;
+  const char *src_ = nullptr;
+  size_t len_ = 0, part_ = 0;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
+constexpr size_t kStageChunk = (size_t)16 << 20;  // bytes per pinned chunk
+constexpr int kStageRing = 4;                     // chunks
+constexpr size_t kStageMin = (size_t)8 << 20;     // smaller copies: plain hipMemcpyAsync
+
+void ring_init(Device &d) {
+  if (!d.ring.empty()) return;
+  d.ring.assign(kStageRing, nullptr);
+  d.ring_ev.assign(kStageRing, nullptr);
+  d.ring_used.assign(kStageRing, false);
+  for (int k = 0; k < kStageRing; ++k) {
+    PBX_HIP(hipHostMalloc(&d.ring[k], kStageChunk, hipHostMallocDefault));
+    PBX_HIP(hipEventCreateWithFlags(&d.ring_ev[k], hipEventDisableTiming));
+  }
+}
+}  // namespace
+
+void h2d_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st) {
+  if (bytes < kStageMin) {
+    PBX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+    return;
+  }
+  ring_init(d);
+  CopyPool &pool = CopyPool::get();
+  size_t off = 0;
+  for (int i = 0; off < bytes; ++i, off += kStageChunk) {
+    const int k = i % kStageRing;
+    const size_t len = std::min(kStageChunk, bytes - off);
+    if (d.ring_used[k]) PBX_HIP(hipEventSynchronize(d.ring_ev[k]));  // its last DMA is done
+    pool.copy(d.ring[k], (const char *)src + off, len);
+    PBX_HIP(hipMemcpyAsync((char *)dst + off, d.ring[k], len, hipMemcpyHostToDevice, st));
+    PBX_HIP(hipEventRecord(d.ring_ev[k], st));
+    d.ring_used[k] = true;
+  }
+}
+
+void d2h_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st) {
+  if (bytes < kStageMin) {
+    PBX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    return;
+  }
+  ring_init(d);
+  CopyPool &pool = CopyPool::get();
+  const int nc = (int)((bytes + kStageChunk - 1) / kStageChunk);
+  // chunks in flight on the DMA engine while the host copies earlier ones out
+  auto issue = [&](int i) {
+    const int k = i % kStageRing;
+    const size_t off = (size_t)i * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    if (d.ring_used[k]) PBX_HIP(hipEventSynchronize(d.ring_ev[k]));
+    PBX_HIP(hipMemcpyAsync(d.ring[k], (const char *)src + off, len, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipEventRecord(d.ring_ev[k], st));
+    d.ring_used[k] = true;
+  };
+  for (int i = 0; i < std::min(nc, kStageRing); ++i) issue(i);
+  for (int i = 0; i < nc; ++i) {
+    const int k = i % kStageRing;
+    const size_t off = (size_t)i * kStageChunk, len = std::min(kStageChunk, bytes - off);
+    PBX_HIP(hipEventSynchronize(d.ring_ev[k]));
+    pool.copy((char *)dst + off, d.ring[k], len);
+    d.ring_used[k] = false;  // (copied out: free for the next chunk)
+    if (i + kStageRing < nc) issue(i + kStageRing);
+  }
 }
 
 DevBuf &Device::slot(int k) {

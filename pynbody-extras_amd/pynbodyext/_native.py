@@ -163,6 +163,7 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_profile_level0_stats": (c_int, [c_void_p, _i64p]),
     "pbx_profile_spec_stats": (c_int, [c_void_p, _i64p]),
     "pbx_profile_set_level0_hint": (c_int, [c_void_p, c_int]),
+    "pbx_profile_set_source_stable": (c_int, [c_void_p, c_int]),
     "pbx_profile_key_range": (c_int, [c_void_p, POINTER(c_uint64), POINTER(c_uint64)]),
     "pbx_profile_msel_begin": (c_int, [c_void_p, c_int64, c_int, c_double, c_int, c_double,
                                        c_uint64, c_uint64, POINTER(c_int)]),

@@ -143,11 +143,12 @@ class DeviceBins:
         first later call that needs them (moments(), selection(w=True),
         weighted percentiles) and held by the handle from then on, so that
         array must stay alive and unchanged until that call or the next
-        selection on this handle (pbx.h, pbx_profile_radial_equaln).  So must
-        ``pos``: a repeated large call that bins with the stored table keeps
-        no copy of x, and the first later reader of x (selection(x=True),
-        statistics of x, percentiles) recomputes it from ``pos``.  Host
-        arrays are staged into the handle and carry no such contract."""
+        selection on this handle (pbx.h, pbx_profile_radial_equaln).  After
+        ``set_source_stable(True)`` so must ``pos``: a repeated large call
+        may then bin with the stored table and keep no copy of x, the first
+        later reader of x (selection(x=True), statistics of x, percentiles)
+        recomputing it from ``pos``.  Host arrays are staged into the handle
+        and carry no such contract."""
         if comm is None and not on_device and (
                 np.asarray(pos).dtype == np.float32 or
                 (mass is not None and np.asarray(mass).dtype == np.float32)):
@@ -273,6 +274,16 @@ class DeviceBins:
         and on a first call one sampled from the keys.  Same results either
         way (pbx_profile_set_level0_hint)."""
         nat.call("pbx_profile_set_level0_hint", self._h, 1 if enabled else 0)
+
+    def set_source_stable(self, stable: bool) -> None:
+        """True: the DEVICE positions (and masses) this handle's
+        radial_equaln calls are given stay alive and unchanged until the next
+        selection on it, so a repeated call may speculate and keep no copy of
+        x (rebuilt from the positions for a later reader).  False (default):
+        on-device calls do not speculate and store x
+        (pbx_profile_set_source_stable).  Host arrays are staged into the
+        handle and speculate either way."""
+        nat.call("pbx_profile_set_source_stable", self._h, 1 if stable else 0)
 
     def forget_history(self) -> None:
         """The next call runs as this handle's first: no earlier level-0

@@ -20,6 +20,7 @@ from typing import Any
 import numpy as np
 
 from ..calculate import CalculatorBase
+from ..simcore import SimSnap, SubSnap
 from ._device import DeviceBins
 from .bins import BinsSet
 from .profile import ProfileBase
@@ -104,7 +105,8 @@ class RadialProfileBuilder(ProfileBuilderBase):
             dev = DeviceBins.select(pos, mass, sphere=spec.get("sphere"),
                                     families=spec.get("families"), ndim=self.ndim)
             idx, x, _ = dev.selection(idx=True, x=True, w=False)
-        sub = source[idx]
+        # (the selection keeps index order: the view's indices increase)
+        sub = SubSnap(source, idx, increasing=True) if isinstance(source, SimSnap) else source[idx]
         key = "r" if self.ndim == 3 else "rxy"
         if hasattr(sub, "_derived"):
             # the device computed the same values (in the positions' precision)

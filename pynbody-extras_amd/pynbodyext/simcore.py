@@ -356,7 +356,7 @@ class SimSnap:
 class SubSnap(SimSnap):
     """Index-list view of a parent snapshot (pynbody IndexedSubSnap)."""
 
-    def __init__(self, base: SimSnap, index: np.ndarray):
+    def __init__(self, base: SimSnap, index: np.ndarray, increasing: bool | None = None):
         self._base = base
         self._index = np.asarray(index, dtype=np.int64)
         self._n = len(self._index)
@@ -365,10 +365,16 @@ class SubSnap(SimSnap):
         # family slices of the view: families of the root restricted to index
         self._family_slice = {}
         self._root_index = base._root_index[self._index] if isinstance(base, SubSnap) else self._index
-        for f, sl in root._family_slice.items():
-            lo = np.searchsorted(self._root_index, sl.start, side="left")
-            hi = np.searchsorted(self._root_index, sl.stop, side="left")
-            if np.all(np.diff(self._root_index) > 0):
+        # strictly increasing root indices (checked once; a caller that knows
+        # it — the device selection's compacted indices — says so)
+        if increasing is None or isinstance(base, SubSnap):
+            ri = self._root_index
+            increasing = bool(len(ri) < 2 or np.all(ri[1:] > ri[:-1]))
+        self._increasing = increasing
+        if increasing:
+            for f, sl in root._family_slice.items():
+                lo = np.searchsorted(self._root_index, sl.start, side="left")
+                hi = np.searchsorted(self._root_index, sl.stop, side="left")
                 self._family_slice[f] = slice(int(lo), int(hi))
         self._arrays = {}
         self._units = {}
@@ -378,7 +384,7 @@ class SubSnap(SimSnap):
         indices are not increasing (families need not be contiguous) the
         positions of its members as an index array."""
         fam = get_family(fam)
-        if fam in self._family_slice or np.all(np.diff(self._root_index) > 0):
+        if fam in self._family_slice or self._increasing:
             return self._family_slice.get(fam, slice(0, 0))
         sl = self.ancestor._get_family_slice(fam)
         return np.nonzero((self._root_index >= sl.start) & (self._root_index < sl.stop))[0]

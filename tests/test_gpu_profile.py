@@ -182,6 +182,31 @@ def test_device_r_and_mask_bit_exact(gpu):
     assert np.all(w2 == 1.0)
 
 
+def test_staged_copies_family_span(gpu):
+    """Host arrays cross PCIe through pinned chunks (h2d_staged / d2h_staged,
+    16 MB chunks above 8 MB) and only the families' span is uploaded, at its
+    own offset: a 6M-particle set with a family slice in the middle (span
+    3.5M: 84 MB of positions) and one with two slices, their selections
+    (indices, r, masses: 28 MB each way) equal to numpy's; the particles
+    outside the span are never read."""
+    rng = np.random.default_rng(17)
+    n = 6_000_000
+    pos = rng.normal(scale=4.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    for fams in ([(2_000_000, 5_500_000)], [(100_000, 1_900_000), (4_000_000, 5_999_999)]):
+        d = DeviceBins.select(pos, mass, sphere=((0.0, 0.0, 0.0), 9.0), families=fams, ndim=3)
+        idx, x, w = d.selection()
+        keep = pr.sphere_mask(pos, 9.0)
+        inf = np.zeros(n, dtype=bool)
+        for a, b in fams:
+            inf[a:b] = True
+        keep &= inf
+        assert np.array_equal(idx, np.nonzero(keep)[0])
+        assert np.array_equal(x, pr.radial_r(pos)[keep])
+        assert np.array_equal(w, mass[keep])
+        d.close()
+
+
 def test_fused_builder_matches_oracle_config3(gpu):
     """Config 3: 1M Plummer, Sphere(R=10) & FamilyFilter('dm'), equaln 128, weight mass."""
     n = 1_000_000
@@ -1019,6 +1044,56 @@ def test_radial_equaln_speculative_assignment(gpu):
         ref.close()
 
 
+def test_radial_equaln_device_positions_lifetime(gpu):
+    """a speculating call keeps no copy of x and rebuilds it from
+    the positions for a later reader, so with DEVICE positions it speculates
+    only after set_source_stable(True).  Without it, repeated on-device calls
+    never speculate and x is stored: overwriting the positions after the
+    calls leaves selection(x) equal to the x the bins were made from.  With
+    it, the calls speculate and hit, and every call equals a handle that
+    never speculates."""
+    from pynbodyext import _native as nat
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W
+
+    rng = np.random.default_rng(53)
+    n = 4_400_000
+    pos = rng.normal(scale=3.0, size=(n, 3))
+    mass = rng.uniform(0.5, 1.5, n)
+    stats = [(SRC_W, SRC_NONE, 1 << 3)]
+    d_pos, d_mass = nat.DeviceArray.from_host(pos), nat.DeviceArray.from_host(mass)
+    h, ref = DeviceBins(), DeviceBins()
+    ref.set_level0_hint(False)
+
+    def call(hd):
+        _, e, c, _ = DeviceBins.radial_equaln(d_pos.ptr, d_mass.ptr, nbins=128, stats=stats,
+                                              on_device=True, n=n, into=hd)
+        return e, c
+
+    try:
+        for _ in range(5):
+            call(h)
+        assert h.spec_stats()["speculated"] == 0
+        x0 = pr.radial_r(pos)
+        d_pos.upload(pos * 3.0)  # the caller reuses its array after the calls
+        _, xx, _ = h.selection(idx=False, x=True, w=False)
+        assert np.array_equal(xx, x0)
+        d_pos.upload(pos)
+        h.set_source_stable(True)
+        for _ in range(5):
+            e, c = call(h)
+            e0, c0 = call(ref)
+            assert np.array_equal(e, e0) and np.array_equal(c, c0)
+        st = h.spec_stats()
+        assert st["speculated"] >= 2 and st["hits"] >= 2, st
+        _, xx, _ = h.selection(idx=False, x=True, w=False)  # rebuilt from the (unchanged) positions
+        assert np.array_equal(xx, x0)
+    finally:
+        h.close()
+        ref.close()
+        d_pos.free()
+        d_mass.free()
+
+
 @pytest.mark.parametrize("nbins,stats,fams", [
     (200, [(1, -1, 1 << 3)], None),                      # {Σw}: the dedicated single add, 201 bins
     (64, [(0, 1, 0b111)], None),                         # Σw, Σx·w, Σx²·w: the factor loop
@@ -1273,4 +1348,5 @@ def test_results_pack_mapped_many_blocks(gpu, n, nb):
     finally:
         h.close()
     # the two inputs differ, so a pack left from the other call would be seen
-    assert not np.array_equal(inputs[0][3], inputs[1][3])
+    assert not np.array_equal(inputs[0][2], inputs[1][2])
+    assert not np.allclose(inputs[0][4], inputs[1][4], rtol=1e-12)

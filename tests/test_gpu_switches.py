@@ -6,7 +6,8 @@ process.  tests/_switch_child.py runs one fixed workload in a child process
 with the defaults and under each of them; the results are compared with the
 defaults' (which the other GPU tests check against the oracle):
 
-* timing and traces: every result bit-identical (profiles: sums to 1e-12);
+* timing and traces: every result bit-identical (profiles: sums to 1e-12;
+  the direct sum to 1e-12: its float atomics make the last bits vary);
 * PBX_PRECISE=1: profiles bit-identical; the walk and the direct sum move by
   the fast reciprocal square root's rounding only — within the fast mode's
   1e-6 relative per particle (vector norm for the accelerations).
@@ -57,10 +58,12 @@ def test_runtime_variables_same_results(defaults, tmp_path, group):
         assert "[mono]" in err and (tmp_path / "walk_trace.bin").stat().st_size > 0
     for k, ref in defaults.items():
         v = got[k]
-        if (k.startswith("direct/") or k.startswith("tree/")) and not exact:
+        if k.startswith("direct/") or (k.startswith("tree/") and not exact):
+            # (the direct sum adds its per-particle partials with float
+            # atomics: the last bits follow the arrival order, run to run)
             d = np.abs(v - ref) if v.ndim == 1 else np.linalg.norm(v - ref, axis=1)
             nrm = np.abs(ref) if ref.ndim == 1 else np.linalg.norm(ref, axis=1)
-            assert float(np.max(d / nrm)) < 1e-6, k
+            assert float(np.max(d / nrm)) < (1e-12 if exact else 1e-6), k
         elif "/m" in k:
             np.testing.assert_allclose(v, ref, rtol=1e-12, atol=1e-300, err_msg=k)
         else:  # edges, counts, CSR, tree and direct outputs

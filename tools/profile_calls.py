@@ -35,6 +35,7 @@ for k in range(bench.N_CHANGING if mode == "changing" else 1):
 dm = family_slices(n)["dm"]
 stats = [(SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, (1 << 0) | (1 << 1))]
 h = DeviceBins()
+h.set_source_stable(True)
 e0, e1 = nat.Event(), nat.Event()
 
 
