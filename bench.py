@@ -704,6 +704,7 @@ def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
     bins.py:720-746 equaln fused with :346-395 assignment + CSR read-back,
     and the Σ mass of proarray.py:272-334) on the host r of the kept
     particles, as the reference's BinsSet calls them."""
+    import ctypes
     import importlib.util
     from types import SimpleNamespace
 
@@ -759,15 +760,25 @@ def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
         same = (np.array_equal(edges, np.asarray(prof.bin_edges)) and
                 np.array_equal(counts, np.asarray(prof.npart_bins)))
         b, sm = float(np.median(tb)), float(np.median(ts))
+        # the bound: the bytes the selection reads (positions + masses of the
+        # family's span) over this box's pinned host -> device rate
+        sel_bytes = (dm.stop - dm.start) * (24 + 8)
+        pin, stg = ctypes.c_double(), ctypes.c_double()
+        nat.call("pbx_measure_h2d", sel_bytes, ctypes.byref(pin), ctypes.byref(stg))
+        bound_ms = sel_bytes / (pin.value * 1e9) * 1e3
         rows.append({"n": n, "kept": kept,
                      "builder_ms": b * 1e3, "builder_particles_per_s": n / b,
+                     "selection_bytes": sel_bytes, "pinned_h2d_gbs": pin.value,
+                     "staged_h2d_gbs": stg.value, "bound_ms": bound_ms,
+                     "builder_over_bound": b * 1e3 / bound_ms,
                      "seams_ms": sm * 1e3, "seams_kept_per_s": kept / sm,
                      "seams_equal_builder": bool(same)})
         del sim, prof
     return {"rows": rows,
-            "note": "host numpy in and out (positions / masses staged to HBM inside the call "
-                    "for the builder; r uploaded, the int64 CSR read back for the seams): "
-                    "PCIe-inclusive user-facing times, not the bench value"}
+            "note": "host numpy in and out (positions / masses of the family span staged to HBM "
+                    "through pinned chunks inside the call for the builder; r uploaded, the int64 "
+                    "CSR read back for the seams): PCIe-inclusive user-facing times, not the bench "
+                    "value; bound_ms = selection_bytes / pinned_h2d_gbs (pbx_measure_h2d)"}
 
 
 def pmc_profile_step_bytes(n: int, inputs: str = "identical"):

@@ -73,6 +73,11 @@ int pbx_device_name(char *buf, int buflen);
 int pbx_malloc(void **d_ptr, size_t bytes);
 int pbx_free(void *d_ptr);
 int pbx_memcpy_htod(void *d_dst, const void *h_src, size_t bytes);
+/* Host -> device copy rates of `bytes` (best of 3 after a warm-up, GB/s):
+ * from pinned host memory (one DMA) and from pageable memory through the
+ * library's pinned chunks (what a profile call on host arrays uses).  No
+ * reference counterpart: the bench's bound for the user-facing profile. */
+int pbx_measure_h2d(int64_t bytes, double *pinned_gbs, double *staged_gbs);
 int pbx_memcpy_dtoh(void *h_dst, const void *d_src, size_t bytes);
 int pbx_memcpy_dtod(void *d_dst, const void *d_src, size_t bytes);
 int pbx_memset(void *d_ptr, int value, size_t bytes);

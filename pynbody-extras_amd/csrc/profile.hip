@@ -2341,8 +2341,21 @@ __global__ void __launch_bounds__(FR_TPB)
   const int s = c_s;
   const int64_t o = c_o0, S = (int64_t)c_o1 - o;
   const bool in_lds = S <= FS_LDS;
-  if (in_lds) {
-    for (int64_t i = tid; i < S; i += FR_TPB) sk[i] = seg[o + i];
+  if (in_lds) {  // (FS_SU loads per thread in flight: a group of ~10-20k keys was ~15 dependent trips)
+    constexpr int FS_SU = 8;
+    for (int64_t i0 = tid; i0 < S; i0 += (int64_t)FR_TPB * FS_SU) {
+      uint64_t v[FS_SU];
+#pragma unroll
+      for (int u = 0; u < FS_SU; ++u) {
+        const int64_t i = i0 + (int64_t)u * FR_TPB;
+        v[u] = seg[o + (i < S ? i : 0)];
+      }
+#pragma unroll
+      for (int u = 0; u < FS_SU; ++u) {
+        const int64_t i = i0 + (int64_t)u * FR_TPB;
+        if (i < S) sk[i] = v[u];
+      }
+    }
     __syncthreads();
   }
   if (S <= FR_TPB) {  // small group: each key's rank by counting (one key per thread)
@@ -3042,12 +3055,16 @@ __global__ void __launch_bounds__(AT_BT) __attribute__((amdgpu_waves_per_eu(8)))
       const uint64_t *kwp = kw + (s0 >> 6);
       uint64_t kk[AT_HS];
       double xv[AT_HS], mv[AT_HS];
+      // (only the span's last slots lie past its masses: the clamp for that
+      // half alone, a uniform test, not a 64-bit select per slot)
+      const bool past = s0 + 64 * AT_HS > span;
 #pragma unroll
       for (int k = 0; k < AT_HS; ++k) {
         kk[k] = kwp[k];
         const int64_t sl = s0 + 64 * k + lane;
         xv[k] = __builtin_nontemporal_load(x + sl);
-        mv[k] = wneed ? __builtin_nontemporal_load(mp + (sl < span ? sl : span - 1)) : 1.0;
+        if (wneed) mv[k] = __builtin_nontemporal_load(mp + (past ? (sl < span ? sl : span - 1) : sl));
+        else mv[k] = 1.0;
       }
       uint32_t c[AT_HS];
       uint64_t key[AT_HS];
@@ -3090,32 +3107,49 @@ __global__ void __launch_bounds__(AT_BT) __attribute__((amdgpu_waves_per_eu(8)))
           }
         }
       }
-      if (__ballot(defm != 0u)) {  // rare: the keys of edge-holding digits
+      if (__ballot(defm != 0u)) {  // the keys of edge-holding digits (~3 % of them)
+        // the half's list slots with ONE LDS atomic, and every key's segment
+        // slot issued before any is used: two LDS round trips per half, not
+        // two per key word (a wave half almost always holds one such key)
+        uint64_t bd[AT_HS];
+        uint32_t before[AT_HS], tot = 0;
 #pragma unroll
         for (int k = 0; k < AT_HS; ++k) {
-          const bool def = (defm >> k) & 1u;
-          const uint64_t bd = __ballot(def);
-          if (!bd) continue;
-          uint32_t li0 = 0;  // the list slots: one LDS atomic per wave
-          if (lane == 0) li0 = atomicAdd(&dk, (uint32_t)__popcll(bd));
-          li0 = __shfl(li0, 0, 64);
-          if (def) {
-            const uint64_t off = key[k] - lo;
-            uint32_t g;
+          bd[k] = __ballot((defm >> k) & 1u);
+          before[k] = tot;
+          tot += (uint32_t)__popcll(bd[k]);
+        }
+        uint32_t li0 = 0;
+        if (lane == 0) li0 = atomicAdd(&dk, tot);
+        uint32_t g[AT_HS], sl[AT_HS];
+#pragma unroll
+        for (int k = 0; k < AT_HS; ++k) {
+          g[k] = 0;
+          sl[k] = 0;
+          if ((defm >> k) & 1u) {
             if (c[k] != SPEC_DEFER) {
-              g = c[k] - 128u;
+              g[k] = c[k] - 128u;
             } else {  // search the group by its digit
-              const uint32_t dd = (uint32_t)(off >> s);
+              const uint32_t dd = (uint32_t)((key[k] - lo) >> s);
               int l = 0, hh = ng - 1;
               while (l < hh) {
                 const int mid = (l + hh) >> 1;
                 if (sgd[mid] < dd) l = mid + 1; else hh = mid;
               }
-              g = (uint32_t)l;
+              g[k] = (uint32_t)l;
             }
-            go.seg[atomicAdd(&sslot[g], 1u)] = off;
+            sl[k] = atomicAdd(&sslot[g[k]], 1u);
+          }
+        }
+        li0 = __shfl(li0, 0, 64);
+#pragma unroll
+        for (int k = 0; k < AT_HS; ++k) {
+          if ((defm >> k) & 1u) {
+            const uint64_t off = key[k] - lo;
+            go.seg[sl[k]] = off;
             const uint32_t slot = (uint32_t)(s0 + 64 * k) + lane;
-            go.rec[rb + li0 + rank_below(bd)] = AgRec{off, mv[k], slot, t | (g << AG_TBITS)};
+            go.rec[rb + li0 + before[k] + rank_below(bd[k])] =
+                AgRec{off, mv[k], slot, t | (g[k] << AG_TBITS)};
           }
         }
       }
@@ -3405,18 +3439,20 @@ __global__ void __launch_bounds__(TPB)
               uint32_t ntiles, int32_t *__restrict__ perm, uint32_t nrows, PackArgs pack,
               int npk) {
   __shared__ uint32_t run[NWAVE][RADIX];
-  __shared__ uint32_t dstart[RADIX];
-  __shared__ uint32_t gofs[RADIX];
+  __shared__ uint32_t delta[RADIX];  // a digit's run: global offset - its start in the sorted tile
   __shared__ uint32_t wsum[NWAVE];
-  __shared__ uint8_t sk[TILE];
-  // sv, and during the ranking the [NWAVE][RADIX] peer words (8 KB either
-  // way); before both, the pack's reduction buffer (TPB doubles)
-  __shared__ __attribute__((aligned(16))) uint16_t sv[TILE];
-  static_assert(sizeof(uint16_t) * TILE == sizeof(uint64_t) * NWAVE * RADIX, "pmask aliases sv");
-  static_assert(sizeof(uint16_t) * TILE >= sizeof(double) * TPB, "the pack's buffer fits sv");
-  uint64_t *pmask = (uint64_t *)sv;
+  // the tile sorted by bin, one word per element: digit << 16 | in-tile
+  // position (one LDS write per element when sorting, one read when writing
+  // out — a byte array and a u16 array took two of each, and the out pass
+  // read the digit's offset and start separately: ~48 fewer LDS
+  // instructions per thread); during the ranking the [NWAVE][RADIX] peer
+  // words, before both the pack's reduction buffer (TPB doubles)
+  __shared__ __attribute__((aligned(16))) uint32_t sw[TILE];
+  static_assert(sizeof(uint32_t) * TILE >= sizeof(uint64_t) * NWAVE * RADIX, "pmask aliases sw");
+  static_assert(sizeof(uint32_t) * TILE >= sizeof(double) * TPB, "the pack's buffer fits sw");
+  uint64_t *pmask = (uint64_t *)sw;
   if ((int)blockIdx.x < npk) {
-    pack_block(pack, (int)blockIdx.x, (double *)sv);
+    pack_block(pack, (int)blockIdx.x, (double *)sw);
     __syncthreads();
   }
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // keep words: scalar loads
@@ -3473,8 +3509,7 @@ __global__ void __launch_bounds__(TPB)
 #pragma unroll
     for (int ww = 0; ww < NWAVE; ++ww) tot += run[ww][d0];
     const uint32_t st = block_excl_scan(tot, wsum, nullptr);
-    dstart[d0] = st;
-    gofs[d0] = go;
+    delta[d0] = go - st;  // (mod 2^32: + the sorted position is the CSR position)
     uint32_t a = st;  // tile-local sorted position
 #pragma unroll
     for (int ww = 0; ww < NWAVE; ++ww) {
@@ -3491,14 +3526,13 @@ __global__ void __launch_bounds__(TPB)
       const uint32_t dgt = key[k] & 255u;
       const uint32_t q = run[w][dgt] + lp[k];
       const uint32_t v = (k < 8 ? sbase0 : sbase1) + (uint32_t)kpt[k] + rank_below(wd);
-      sk[q] = (uint8_t)dgt;
-      sv[q] = (uint16_t)v;
+      sw[q] = (dgt << 16) | v;  // (v < TILE)
     }
   }
   __syncthreads();
   for (int j = threadIdx.x; j < (int)tn; j += TPB) {
-    const uint32_t dgt = sk[j];
-    perm[gofs[dgt] + ((uint32_t)j - dstart[dgt])] = (int32_t)(o + sv[j]);
+    const uint32_t e = sw[j];
+    perm[delta[e >> 16] + (uint32_t)j] = (int32_t)(o + (e & 0xffffu));
   }
 }
 

@@ -336,6 +336,43 @@ int pbx_memcpy_htod(void *d_dst, const void *h_src, size_t bytes) {
   });
 }
 
+int pbx_measure_h2d(int64_t bytes, double *pinned_gbs, double *staged_gbs) {
+  return guard([&] {
+    if (bytes <= 0) fail(PBX_ERR_VALUE, "bytes must be > 0");
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    const size_t nb = (size_t)bytes;
+    void *dev = nullptr, *pin = nullptr;
+    PBX_HIP(hipMalloc(&dev, nb));
+    std::vector<char> pageable(nb, 1);  // (touched: resident pages)
+    try {
+      PBX_HIP(hipHostMalloc(&pin, nb, hipHostMallocDefault));
+      std::memset(pin, 1, nb);
+      auto best = [&](auto copy) {
+        double t = 1e30;
+        for (int r = 0; r < 4; ++r) {  // (the first one warms the path up)
+          PBX_HIP(hipStreamSynchronize(d.stream));
+          const auto t0 = std::chrono::steady_clock::now();
+          copy();
+          PBX_HIP(hipStreamSynchronize(d.stream));
+          const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+          if (r) t = std::min(t, s);
+        }
+        return (double)nb / t / 1e9;
+      };
+      if (pinned_gbs)
+        *pinned_gbs = best([&] { PBX_HIP(hipMemcpyAsync(dev, pin, nb, hipMemcpyHostToDevice, d.stream)); });
+      if (staged_gbs) *staged_gbs = best([&] { h2d_staged(d, dev, pageable.data(), nb, d.stream); });
+    } catch (...) {
+      if (pin) (void)hipHostFree(pin);
+      (void)hipFree(dev);
+      throw;
+    }
+    (void)hipHostFree(pin);
+    (void)hipFree(dev);
+  });
+}
+
 int pbx_memcpy_dtoh(void *h_dst, const void *d_src, size_t bytes) {
   return guard([&] {
     Device &d = current_device();

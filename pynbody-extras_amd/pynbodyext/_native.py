@@ -72,6 +72,7 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
     "pbx_free": (c_int, [c_void_p]),
     "pbx_memcpy_htod": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "pbx_measure_h2d": (c_int, [c_int64, POINTER(c_double), POINTER(c_double)]),
     "pbx_memcpy_dtoh": (c_int, [c_void_p, c_void_p, c_size_t]),
     "pbx_memcpy_dtod": (c_int, [c_void_p, c_void_p, c_size_t]),
     "pbx_memset": (c_int, [c_void_p, c_int, c_size_t]),

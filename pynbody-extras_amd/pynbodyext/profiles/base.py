@@ -104,13 +104,19 @@ class RadialProfileBuilder(ProfileBuilderBase):
             mass = _native_float(source["mass"]) if "mass" in source.keys() else None
             dev = DeviceBins.select(pos, mass, sphere=spec.get("sphere"),
                                     families=spec.get("families"), ndim=self.ndim)
-            idx, x, _ = dev.selection(idx=True, x=True, w=False)
+            # the kept masses come back from the device (the same values: a
+            # copy, through pinned chunks) instead of a host gather of the
+            # sub-snapshot's column — the profile's weights read them
+            wdev = mass is not None and mass.dtype == np.float64 and isinstance(source, SimSnap)
+            idx, x, w = dev.selection(idx=True, x=True, w=wdev)
         # (the selection keeps index order: the view's indices increase)
         sub = SubSnap(source, idx, increasing=True) if isinstance(source, SimSnap) else source[idx]
         key = "r" if self.ndim == 3 else "rxy"
         if hasattr(sub, "_derived"):
             # the device computed the same values (in the positions' precision)
             sub._derived[key] = x.astype(pos.dtype) if pos.dtype != x.dtype else x
+            if wdev:
+                sub._derived["mass"] = w
         xs = sub[key]
         bins_area = "spherical_shell" if self.ndim == 3 else "annulus"
         with ctx.phase(self, "device bins"):
