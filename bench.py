@@ -734,6 +734,14 @@ def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
             prof, msum, rmean = call()
             tb.append(time.perf_counter() - t0)
         kept = len(prof.sim)
+        # the same call reading the view's r and masses onto the host too (the
+        # builder leaves them on the device until read)
+        ta = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            prof, msum, rmean = call()
+            np.asarray(prof.sim["r"]), np.asarray(prof.sim["mass"])
+            ta.append(time.perf_counter() - t0)
         # the seams on the host r of the same kept particles
         pos, mass = np.asarray(sim["pos"]), np.asarray(sim["mass"])
         dm = family_slices(n)["dm"]
@@ -759,7 +767,7 @@ def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
             ts.append(time.perf_counter() - t0)
         same = (np.array_equal(edges, np.asarray(prof.bin_edges)) and
                 np.array_equal(counts, np.asarray(prof.npart_bins)))
-        b, sm = float(np.median(tb)), float(np.median(ts))
+        b, sm, ba = float(np.median(tb)), float(np.median(ts)), float(np.median(ta))
         # the bound: the bytes the selection reads (positions + masses of the
         # family's span) over this box's pinned host -> device rate
         sel_bytes = (dm.stop - dm.start) * (24 + 8)
@@ -771,14 +779,19 @@ def bench_profile_api(sizes=(1_000_000, 16_000_000), reps: int = 5) -> dict:
                      "selection_bytes": sel_bytes, "pinned_h2d_gbs": pin.value,
                      "staged_h2d_gbs": stg.value, "bound_ms": bound_ms,
                      "builder_over_bound": b * 1e3 / bound_ms,
+                     "builder_read_all_ms": ba * 1e3,
+                     "read_all_over_bound": ba * 1e3 / bound_ms,
                      "seams_ms": sm * 1e3, "seams_kept_per_s": kept / sm,
                      "seams_equal_builder": bool(same)})
         del sim, prof
     return {"rows": rows,
             "note": "host numpy in and out (positions / masses of the family span staged to HBM "
-                    "through pinned chunks inside the call for the builder; r uploaded, the int64 "
-                    "CSR read back for the seams): PCIe-inclusive user-facing times, not the bench "
-                    "value; bound_ms = selection_bytes / pinned_h2d_gbs (pbx_measure_h2d)"}
+                    "through pinned chunks inside the call for the builder, the view's indices "
+                    "read back as int32 widened on the host, r and the kept masses left on the "
+                    "device until read — builder_read_all_ms reads both too; r uploaded, the "
+                    "int64 CSR read back for the seams): PCIe-inclusive user-facing times, not "
+                    "the bench value; bound_ms = selection_bytes / pinned_h2d_gbs "
+                    "(pbx_measure_h2d)"}
 
 
 def pmc_profile_step_bytes(n: int, inputs: str = "identical"):

@@ -120,6 +120,10 @@ Device &current_device();
 // The caller holds the device's lock (the ring is per device).
 void h2d_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st);
 void d2h_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st);
+// int32 values on the device -> int64 on the host (half the bytes cross PCIe;
+// the host threads widen them on the way out of the pinned chunks).  False
+// (nothing done) below the staging size: the caller widens on the device.
+bool d2h_staged_widen(Device &d, int64_t *dst, const int32_t *src, int64_t n, hipStream_t st);
 
 bool timing_enabled();
 

@@ -5342,7 +5342,7 @@ static const double *resolve_src(Profile &P, hipStream_t st, int which, const do
   if (which == 2) {
     if (!hp && n) fail(PBX_ERR_VALUE, "host array is NULL");
     double *dp = (double *)stage.get(sizeof(double) * (size_t)(n ? n : 1));
-    if (n) PBX_HIP(hipMemcpyAsync(dp, hp, sizeof(double) * n, hipMemcpyHostToDevice, st));
+    if (n) h2d_staged(current_device(), dp, hp, sizeof(double) * n, st);  // (pinned chunks)
     return dp;
   }
   if (which == 3) {  // device array per ORIGINAL particle (e.g. a tree potential)
@@ -5766,7 +5766,7 @@ int pbx_profile_set_x(void *handle, const double *h_x, int64_t n) {
     Device &d = current_device();
     std::lock_guard<std::mutex> lk(d.mu);
     double *x = (double *)P.x.get(sizeof(double) * (size_t)(n ? n : 1));
-    if (n) PBX_HIP(hipMemcpyAsync(x, h_x, sizeof(double) * n, hipMemcpyHostToDevice, d.stream));
+    if (n) h2d_staged(d, x, h_x, sizeof(double) * n, d.stream);  // (through pinned chunks)
     P.n = n;
     P.has_w = false;
     P.has_idx = false;
@@ -5837,11 +5837,12 @@ int pbx_profile_get_selection(void *handle, int64_t *h_idx, double *h_x, double 
     if (n == 0) return;
     if (h_idx) ensure_idx(P, st);
     if (h_w) ensure_w(P, st);
-    if (h_idx) {
+    // (int32 across PCIe, widened by the host threads; small ones on the device)
+    if (h_idx && !d2h_staged_widen(d, h_idx, (const int32_t *)P.idx.p, n, st)) {
       int64_t *tmp = (int64_t *)P.vtmp.get(sizeof(int64_t) * (size_t)n);
       hipLaunchKernelGGL(widen_perm, dim3(ceil_div(n, TPB)), dim3(TPB), 0, st,
                          (const int32_t *)P.idx.p, n, tmp);
-      d2h_staged(d, h_idx, tmp, sizeof(int64_t) * n, st);  // (through pinned chunks)
+      d2h_staged(d, h_idx, tmp, sizeof(int64_t) * n, st);
     }
     if (h_x) {
       ensure_x(P, st);
@@ -6040,7 +6041,7 @@ int pbx_profile_csr(void *handle, int64_t *h_perm, int64_t *h_offsets) {
       h_offsets[0] = 0;
       for (int64_t k = 0; k < nb; ++k) h_offsets[k + 1] = h_offsets[k] + c[(size_t)k];
     }
-    if (h_perm && P.n_valid) {
+    if (h_perm && P.n_valid && !d2h_staged_widen(d, h_perm, (const int32_t *)P.perm.p, P.n_valid, st)) {
       int64_t *tmp = (int64_t *)P.field.get(sizeof(int64_t) * (size_t)P.n_valid);
       hipLaunchKernelGGL(widen_perm, dim3(ceil_div(P.n_valid, TPB)), dim3(TPB), 0, st,
                          (const int32_t *)P.perm.p, P.n_valid, tmp);

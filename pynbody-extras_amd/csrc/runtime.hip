@@ -63,15 +63,31 @@ class CopyPool {
     return *p;
   }
   // dst[0 .. len) = src[0 .. len), split over the pool and the caller
-  void copy(void *dst, const void *src, size_t len) {
+  void copy(void *dst, const void *src, size_t len) { run(dst, src, len, false); }
+  // int64 dst[0 .. n) = int32 src[0 .. n) (a widening copy-out)
+  void widen(int64_t *dst, const int32_t *src, size_t n) { run(dst, src, n, true); }
+
+ private:
+  CopyPool() {
+    unsigned hw = std::thread::hardware_concurrency();
+    const int n = (int)std::max(1u, std::min(8u, hw ? hw / 2 : 1u));
+    for (int i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+  }
+  // len bytes (copy) or elements (widen); parts of a multiple of 64 bytes
+  void run(void *dst, const void *src, size_t len, bool widen) {
     const int nt = (int)th_.size() + 1;
-    if (len < ((size_t)1 << 20) || nt == 1) {
-      std::memcpy(dst, src, len);
+    if (len < ((size_t)1 << (widen ? 18 : 20)) || nt == 1) {
+      widen_ = widen;
+      dst_ = (char *)dst;
+      src_ = (const char *)src;
+      len_ = part_ = len;
+      piece(0);
       return;
     }
     const size_t part = ((len + nt - 1) / nt + 63) & ~(size_t)63;
     {
       std::lock_guard<std::mutex> lk(m_);
+      widen_ = widen;
       dst_ = (char *)dst;
       src_ = (const char *)src;
       len_ = len;
@@ -84,16 +100,17 @@ class CopyPool {
     std::unique_lock<std::mutex> lk(m_);
     done_.wait(lk, [&] { return pending_ == 0; });
   }
-
- private:
-  CopyPool() {
-    unsigned hw = std::thread::hardware_concurrency();
-    const int n = (int)std::max(1u, std::min(8u, hw ? hw / 2 : 1u));
-    for (int i = 1; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
-  }
   void piece(int i) {
     const size_t a = (size_t)i * part_;
-    if (a < len_) std::memcpy(dst_ + a, src_ + a, std::min(part_, len_ - a));
+    if (a >= len_) return;
+    const size_t m = std::min(part_, len_ - a);
+    if (!widen_) {
+      std::memcpy(dst_ + a, src_ + a, m);
+      return;
+    }
+    int64_t *d = (int64_t *)dst_ + a;
+    const int32_t *s = (const int32_t *)src_ + a;
+    for (size_t j = 0; j < m; ++j) d[j] = s[j];
   }
   void loop(int i) {
     uint64_t seen = 0;
@@ -114,6 +131,7 @@ class CopyPool {
   char *dst_ = nullptr;
   const char *src_ = nullptr;
   size_t len_ = 0, part_ = 0;
+  bool widen_ = false;
   int pending_ = 0;
   uint64_t gen_ = 0;
 };
@@ -153,12 +171,9 @@ void h2d_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t
   }
 }
 
-void d2h_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st) {
-  if (bytes < kStageMin) {
-    PBX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
-    PBX_HIP(hipStreamSynchronize(st));
-    return;
-  }
+// (widen: src holds bytes / 4 int32 values, dst receives them as int64)
+static void d2h_ring(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st,
+                     bool widen) {
   ring_init(d);
   CopyPool &pool = CopyPool::get();
   const int nc = (int)((bytes + kStageChunk - 1) / kStageChunk);
@@ -176,10 +191,26 @@ void d2h_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t
     const int k = i % kStageRing;
     const size_t off = (size_t)i * kStageChunk, len = std::min(kStageChunk, bytes - off);
     PBX_HIP(hipEventSynchronize(d.ring_ev[k]));
-    pool.copy((char *)dst + off, d.ring[k], len);
+    if (widen) pool.widen((int64_t *)dst + off / 4, (const int32_t *)d.ring[k], len / 4);
+    else pool.copy((char *)dst + off, d.ring[k], len);
     d.ring_used[k] = false;  // (copied out: free for the next chunk)
     if (i + kStageRing < nc) issue(i + kStageRing);
   }
+}
+
+void d2h_staged(Device &d, void *dst, const void *src, size_t bytes, hipStream_t st) {
+  if (bytes < kStageMin) {
+    PBX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    PBX_HIP(hipStreamSynchronize(st));
+    return;
+  }
+  d2h_ring(d, dst, src, bytes, st, false);
+}
+
+bool d2h_staged_widen(Device &d, int64_t *dst, const int32_t *src, int64_t n, hipStream_t st) {
+  if (sizeof(int32_t) * (size_t)n < kStageMin) return false;
+  d2h_ring(d, dst, src, sizeof(int32_t) * (size_t)n, st, true);
+  return true;
 }
 
 DevBuf &Device::slot(int k) {

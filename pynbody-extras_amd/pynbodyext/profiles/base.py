@@ -20,7 +20,7 @@ from typing import Any
 import numpy as np
 
 from ..calculate import CalculatorBase
-from ..simcore import SimSnap, SubSnap
+from ..simcore import PendingField, SimSnap, SubSnap
 from ._device import DeviceBins
 from .bins import BinsSet
 from .profile import ProfileBase
@@ -104,20 +104,28 @@ class RadialProfileBuilder(ProfileBuilderBase):
             mass = _native_float(source["mass"]) if "mass" in source.keys() else None
             dev = DeviceBins.select(pos, mass, sphere=spec.get("sphere"),
                                     families=spec.get("families"), ndim=self.ndim)
-            # the kept masses come back from the device (the same values: a
-            # copy, through pinned chunks) instead of a host gather of the
-            # sub-snapshot's column — the profile's weights read them
+            # the kept masses: read from the device (the same values: a copy,
+            # through pinned chunks) instead of a host gather of the
+            # sub-snapshot's column
             wdev = mass is not None and mass.dtype == np.float64 and isinstance(source, SimSnap)
-            idx, x, w = dev.selection(idx=True, x=True, w=wdev)
+            idx = dev.selection(idx=True, x=False, w=False)[0]
         # (the selection keeps index order: the view's indices increase)
         sub = SubSnap(source, idx, increasing=True) if isinstance(source, SimSnap) else source[idx]
         key = "r" if self.ndim == 3 else "rxy"
-        if hasattr(sub, "_derived"):
-            # the device computed the same values (in the positions' precision)
-            sub._derived[key] = x.astype(pos.dtype) if pos.dtype != x.dtype else x
+        if isinstance(sub, SubSnap):
+            # r / rxy (the same values, in the positions' precision) and the
+            # kept masses stay on the device until the host reads them (sub[key],
+            # bins.x, sub["mass"], a host-side statistic): device sums never do
+            def fetch_x(dev=dev, dt=pos.dtype):
+                x = dev.selection(idx=False, x=True, w=False)[1]
+                return x.astype(dt) if dt != x.dtype else x
+
+            sub._pending[key] = fetch_x
             if wdev:
-                sub._derived["mass"] = w
-        xs = sub[key]
+                sub._pending["mass"] = lambda dev=dev: dev.selection(idx=False, x=False, w=True)[2]
+            xs = PendingField(sub, key)
+        else:
+            xs = sub[key]
         bins_area = "spherical_shell" if self.ndim == 3 else "annulus"
         with ctx.phase(self, "device bins"):
             template = BinsSet(bins_by=key, bins_area=bins_area, bins_type=self.bins_type,

@@ -26,6 +26,7 @@ from typing import Any
 import numpy as np
 
 from .._pyn import SimArray
+from ..simcore import PendingField
 from ._device import DeviceBins
 
 __all__ = ["BinsSet", "BinIndexLists"]
@@ -82,7 +83,7 @@ class BinsSet:
         self._bin_min = bin_min
         self._bin_max = bin_max
         self._kwargs = kwargs
-        self.x = None
+        self._x = None  # x, or a PendingField (device-held, read on first use)
         self.bin_edges = None
         self.rbins = None
         self.dr = None
@@ -91,6 +92,20 @@ class BinsSet:
         self.binsize = None
         self._device: DeviceBins | None = None
         self._device_x = None
+
+    @property
+    def x(self):
+        v = self._x
+        if isinstance(v, PendingField):
+            pend, v = v, v.resolve()
+            self._x = v
+            if self._device_x is pend:
+                self._device_x = v  # (the device copy is of these values)
+        return v
+
+    @x.setter
+    def x(self, value):
+        self._x = value
 
     # ---- read-only configuration -------------------------------------------------
     @property
@@ -123,7 +138,7 @@ class BinsSet:
         raise TypeError(f"Invalid _nbins type: {type(nb)}")
 
     def is_defined(self) -> bool:
-        return all(a is not None for a in (self.bin_edges, self.rbins, self.dr, self.x,
+        return all(a is not None for a in (self.bin_edges, self.rbins, self.dr, self._x,
                                            self.binind, self.npart_bins, self.binsize))
 
     # ---- device state ------------------------------------------------------------
@@ -150,6 +165,11 @@ class BinsSet:
 
     @staticmethod
     def _coerce_edges_units(edges, x):
+        if isinstance(x, PendingField) and not isinstance(edges, SimArray):
+            out = SimArray(edges)
+            out.units = x.units
+            out.sim = x.sim
+            return out
         if isinstance(x, SimArray) and not isinstance(edges, SimArray):
             out = SimArray(edges)
             out.units = x.units
@@ -163,8 +183,9 @@ class BinsSet:
             if arr.ndim != 1 or arr.shape[0] < 2:
                 raise ValueError("Explicit bin_edges must be a 1D array of length >= 2")
             return self._coerce_edges_units(arr, x)
-        if callable(self._bins_type):
-            return self._coerce_edges_units(self._bins_type(self, x), x)
+        if callable(self._bins_type):  # (a user's algorithm reads the values)
+            xv = x.resolve() if isinstance(x, PendingField) else x
+            return self._coerce_edges_units(self._bins_type(self, xv), x)
         if isinstance(self._bins_type, str):
             return self._coerce_edges_units(self._bins_algorithm_registry[self._bins_type](self, x), x)
         raise ValueError(f"Invalid bins_type: {self._bins_type}, required callable or registry keys: "
@@ -211,13 +232,13 @@ class BinsSet:
                        bin_max=self._bin_max, **self._kwargs)
 
     def _materialise(self, x) -> None:
-        self.x = x
+        self._x = x
         self.bin_edges = self._build_edges(x)
         if self.bin_edges.ndim != 1 or self.bin_edges.shape[0] < 2:
             self.bin_edges = np.asarray([0.0, 1.0])
         self.rbins = self._calc_binmid(self.bin_edges)
         self.dr = np.gradient(self.rbins)
-        self.binind, self.npart_bins = self._assign_particles(self.x, self.bin_edges)
+        self.binind, self.npart_bins = self._assign_particles(x, self.bin_edges)
         self.binsize = self._calc_area_or_volume(self.bin_edges)
 
     def __call__(self, sim, inplace: bool = False) -> "BinsSet":
@@ -226,7 +247,9 @@ class BinsSet:
         return target
 
     def materialise_on_device(self, x, device: DeviceBins) -> "BinsSet":
-        """Materialise from x already resident on the device (fused path)."""
+        """Materialise from x already resident on the device (fused path;
+        x may be a PendingField: then the host reads it only when asked,
+        bins.x or the view's field)."""
         target = self._config_copy()
         target._adopt_device(device, x)
         target._materialise(x)
@@ -255,7 +278,7 @@ class BinsSet:
                f"nbins={self.nbins if self.is_defined() else self._nbins}, "
                f"bin_min={self._bin_min}, bin_max={self._bin_max}")
         if self.is_defined():
-            return f"BinsSet(materialized: {cfg}, x len={len(self.x)}, "
+            return f"BinsSet(materialized: {cfg}, x len={len(self._x)}, "
         return f"BinsSet(config: {cfg})"
 
     # ---- registries ------------------------------------------------------------------

@@ -25,6 +25,7 @@ from typing import Union
 import numpy as np
 
 from .._pyn import IndexedSimArray, SimArray
+from ..simcore import PendingField, is_pending
 from ._device import SRC_HOST, SRC_NONE, SRC_W, SRC_X
 
 __all__ = ["ProfileArray", "StatisticBase", "Mean", "Sum", "Sum_w", "Percentile", "RMS", "Median",
@@ -60,8 +61,13 @@ class ProfileArray(SimArray):
         if not isinstance(name, str):
             raise ValueError("name must be a string")
         src = name if array is None else array
-        arr = profile.sim[name] if array is None else array
-        if not isinstance(arr, (np.ndarray, SimArray, IndexedSimArray)):
+        if array is not None:
+            arr = array
+        elif is_pending(profile.sim, name):  # (device-held: its length, no host copy)
+            arr = PendingField(profile.sim, name)
+        else:
+            arr = profile.sim[name]
+        if not isinstance(arr, (np.ndarray, SimArray, IndexedSimArray, PendingField)):
             raise ValueError("array must be a numpy ndarray or SimArray, got " + str(type(arr)))
         n_particles, n_bins = len(profile.sim), profile.nbins
         if len(arr) == n_particles:
@@ -114,20 +120,26 @@ class ProfileArray(SimArray):
         if calc is None:
             raise ValueError(f"Statistic '{compute_mode}' not found")
         name = arr if isinstance(arr, str) else None
-        arr_pp = profile.sim[arr] if isinstance(arr, str) else arr
-        weights = profile._weight
+        # a device-held field of the view (fused selection) is not read onto
+        # the host when the device sums it (arr_pp None until a path needs it)
+        pending = name is not None and is_pending(profile.sim, name)
+        arr_pp = None if pending else (profile.sim[arr] if isinstance(arr, str) else arr)
+        weighted = profile._weighted
         fast = calc.from_moments if hasattr(calc, "from_moments") else None
         dev = getattr(profile.bins, "_device", None) if fast is not None else None
         pct = _percentile_of(calc)
         pdev = getattr(profile.bins, "_device", None) if pct is not None else None
         if dev is not None and dev.nbins == profile.nbins:
-            cols = _columns_of(fast, profile.nbins, weights is not None)
-            vals = fast(_moments_for(profile, dev, name, arr_pp, weights, cols),
-                        np.asarray(profile.npart_bins), weights is not None)
+            cols = _columns_of(fast, profile.nbins, weighted)
+            vals = fast(_moments_for(profile, dev, name, arr_pp, cols),
+                        np.asarray(profile.npart_bins), weighted)
         elif pdev is not None and pdev.nbins == profile.nbins:
-            fsrc, wsrc = _sources_for(profile, pdev, name, arr_pp, weights)
+            fsrc, wsrc = _sources_for(profile, pdev, name, arr_pp)
             vals = pdev.percentiles([pct[0] / 100], fsrc, wsrc, absval=pct[1])[:, 0]
         else:
+            if arr_pp is None:
+                arr_pp = profile.sim[arr]
+            weights = profile._weight
             vals = np.zeros(profile.nbins)
             for i, ind in enumerate(profile.binind):
                 if len(ind) == 0:
@@ -135,7 +147,10 @@ class ProfileArray(SimArray):
                     continue
                 vals[i] = calc(arr_pp[ind], None if weights is None else weights[ind])
         res = np.asarray(vals, dtype=np.float64).view(SimArray)
-        if isinstance(arr_pp, (SimArray, IndexedSimArray)):
+        if arr_pp is None:  # (what sim[arr] would carry)
+            res.units = profile.sim._unit_of(arr)
+            res.sim = profile.sim
+        elif isinstance(arr_pp, (SimArray, IndexedSimArray)):
             res.units = arr_pp.units
             res.sim = arr_pp.sim
         return res, calc.key
@@ -220,28 +235,29 @@ def _percentile_of(calc):
     return None
 
 
-def _sources_for(profile, dev, name, arr_pp, weights):
-    """Device source selectors (or host arrays) of a field and the weights."""
+def _sources_for(profile, dev, name, arr_pp):
+    """Device source selectors (or host arrays) of a field and the weights
+    (arr_pp None: the field is device-held and not on the host yet)."""
     bins = profile.bins
     if name is not None and isinstance(bins.bins_by, str) and name == bins.bins_by:
         fsrc = SRC_X
     elif name is not None and dev.has_selection and name == getattr(profile, "_device_weight_name", None):
         fsrc = SRC_W
     else:
-        fsrc = np.asarray(arr_pp, dtype=np.float64)
-    if weights is None:
+        fsrc = np.asarray(profile.sim[name] if arr_pp is None else arr_pp, dtype=np.float64)
+    if not profile._weighted:
         wsrc = SRC_NONE
     elif getattr(profile, "_device_weight_name", None) is not None and dev.has_selection:
         wsrc = SRC_W
     else:
-        wsrc = np.asarray(weights, dtype=np.float64)
+        wsrc = np.asarray(profile._weight, dtype=np.float64)
     return fsrc, wsrc
 
 
-def _moments_for(profile, dev, name, arr_pp, weights, cols=(1 << 7) - 1) -> np.ndarray:
+def _moments_for(profile, dev, name, arr_pp, cols=(1 << 7) - 1) -> np.ndarray:
     """(nbins, 7) device sums of a field, reusing device-resident arrays;
     only the columns in ``cols`` are accumulated."""
-    fsrc, wsrc = _sources_for(profile, dev, name, arr_pp, weights)
+    fsrc, wsrc = _sources_for(profile, dev, name, arr_pp)
     return dev.moments(fsrc, wsrc, cols)
 
 

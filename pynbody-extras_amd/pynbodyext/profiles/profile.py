@@ -18,6 +18,7 @@ from typing import Any
 import numpy as np
 
 from .._pyn import SimSnap
+from ..simcore import PendingField, is_pending
 from .bins import BinsSet
 from .proarray import ProfileArray
 
@@ -56,14 +57,26 @@ class ProfileBase:
         self.sim = sim
         self._bins = bins_set if bins_set.is_defined() else bins_set(sim)
         self._parent = parent
-        self._weight = weight
-        if self._weight is not None:
-            assert len(self._weight) == len(sim), "Weight array length must match simulation length."
+        # the weights, or a PendingField (device-held, read on first use)
+        self._weight_v = weight
+        if weight is not None:
+            assert len(weight) == len(sim), "Weight array length must match simulation length."
         self._data_cache: dict[str, ProfileArray] = {}
         self._stats_cache: defaultdict[str, dict[str, ProfileArray]] = defaultdict(dict)
         # name of the per-particle field whose values the device holds as the
         # selection weights (fused path), if any
         self._device_weight_name: str | None = None
+
+    @property
+    def _weight(self):
+        w = self._weight_v
+        if isinstance(w, PendingField):
+            w = self._weight_v = w.resolve()
+        return w
+
+    @property
+    def _weighted(self) -> bool:
+        return self._weight_v is not None
 
     # ---- caching -------------------------------------------------------------
     def cache(self, pro_arr: ProfileArray) -> None:
@@ -258,7 +271,7 @@ class Profile(ProfileBase):
         if weight is None:
             w = None
         elif isinstance(weight, str):
-            w = sim[weight]
+            w = PendingField(sim, weight) if is_pending(sim, weight) else sim[weight]
         elif callable(weight):
             w = weight(sim)
         else:

@@ -311,6 +311,7 @@ class SimSnap:
         if isinstance(value, SimArray) and value.units is not NoUnit:
             self._units[key] = value.units
         self._derived.pop(key, None)
+        self.__dict__.get("_pending", {}).pop(key, None)
 
     def __getitem__(self, key):
         if isinstance(key, str):
@@ -361,6 +362,9 @@ class SubSnap(SimSnap):
         self._index = np.asarray(index, dtype=np.int64)
         self._n = len(self._index)
         self._derived = {}
+        # fields a device holds for this view, read on first access
+        # (key -> fetch(): the array); see PendingField
+        self._pending = {}
         root = base.ancestor
         # family slices of the view: families of the root restricted to index
         self._family_slice = {}
@@ -397,11 +401,18 @@ class SubSnap(SimSnap):
         return self._base.keys()
 
     def _array(self, key: str) -> np.ndarray:
+        if key in self._arrays:
+            return self._arrays[key]
         if key in self._derived:
             return self._derived[key]
-        val = self._base._array(key)[self._index]
+        fetch = self._pending.pop(key, None)
+        val = fetch() if fetch is not None else self._base._array(key)[self._index]
         self._derived[key] = val
         return val
+
+    def is_pending(self, key: str) -> bool:
+        """The field is held by a device and not read onto the host yet."""
+        return key in self._pending and key not in self._arrays and key not in self._derived
 
     def _unit_of(self, key: str):
         return self._base._unit_of(key)
@@ -422,6 +433,33 @@ class SubSnap(SimSnap):
 
 
 IndexedSubSnap = SubSnap
+
+
+class PendingField:
+    """A view's field that a device holds and the host has not read yet
+    (SubSnap._pending): its length and units without the copy; resolve()
+    reads it (sim[key], the same values)."""
+
+    __slots__ = ("sim", "key")
+
+    def __init__(self, sim: SubSnap, key: str):
+        self.sim, self.key = sim, key
+
+    def __len__(self) -> int:
+        return len(self.sim)
+
+    @property
+    def units(self):
+        return self.sim._unit_of(self.key)
+
+    def resolve(self) -> SimArray:
+        return self.sim[self.key]
+
+
+def is_pending(sim, key) -> bool:
+    """``key`` of ``sim`` is a device-held field not read onto the host yet."""
+    f = getattr(sim, "is_pending", None)
+    return isinstance(key, str) and f is not None and f(key)
 
 
 def new_snapshot(pos, mass, families: dict | None = None, units_map: dict | None = None,

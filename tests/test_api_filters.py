@@ -70,3 +70,33 @@ def test_family_filter_index_subsnap():
     shuffled = sim[np.array([33, 3, 49, 7, 20])]
     assert np.array_equal(f.build_mask(shuffled), [True, False, True, False, True])
     assert f.device_spec(shuffled) is None
+
+
+def test_subsnap_pending_fields():
+    """A view's device-held field (SubSnap._pending, the fused builder's r /
+    rxy and kept masses) is fetched once, on the first host read, and gives
+    what the read returns; PendingField carries length and units without the
+    copy; assigning the field drops the pending fetch."""
+    from pynbodyext.simcore import PendingField, SubSnap, is_pending
+
+    rng = np.random.default_rng(3)
+    pos = rng.normal(size=(50, 3))
+    sim = SimSnap({"pos": pos, "mass": rng.random(50)}, families={"dm": slice(0, 50)},
+                  units_map={"pos": "kpc", "mass": "Msol"})
+    idx = np.arange(0, 50, 3)
+    sub = SubSnap(sim, idx, increasing=True)
+    calls = []
+    r_true = np.sqrt((pos[idx, 0] ** 2 + pos[idx, 1] ** 2) + pos[idx, 2] ** 2)
+    sub._pending["r"] = lambda: calls.append("r") or r_true.copy()
+    assert is_pending(sub, "r") and not is_pending(sub, "mass")
+    pf = PendingField(sub, "r")
+    assert len(pf) == len(idx) and str(pf.units) == str(sim["pos"].units) and not calls
+    r = pf.resolve()
+    assert calls == ["r"] and np.array_equal(np.asarray(r), r_true)
+    assert str(r.units) == str(sim["pos"].units) and r.sim is sub
+    assert np.array_equal(np.asarray(sub["r"]), r_true) and calls == ["r"]  # fetched once
+    assert not is_pending(sub, "r")
+    sub._pending["mass"] = lambda: calls.append("mass") or np.zeros(len(idx))
+    sub["mass"] = np.ones(len(idx))  # an assignment wins over the pending fetch
+    assert not is_pending(sub, "mass") and np.array_equal(np.asarray(sub["mass"]), np.ones(len(idx)))
+    assert calls == ["r"]

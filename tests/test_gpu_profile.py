@@ -229,6 +229,43 @@ def test_fused_builder_matches_oracle_config3(gpu):
                                rtol=1e-12)
 
 
+def test_fused_builder_device_held_fields(gpu):
+    """The fused builder leaves r and the kept masses on the device: the
+    profile's device sums (sum, mean, density, median) read none of them
+    onto the host; the view's indices, sub['r'], bins.x, sub['mass'] and the
+    profile weights then read back bit-exact (4M: 2.4M kept, so the indices
+    and the CSR cross PCIe as int32 widened by the host threads)."""
+    from pynbodyext.simcore import is_pending
+
+    n = 4_000_000
+    sim = plummer_snapshot(n, seed=1006)
+    prof = RadialProfileBuilder(ndim=3, weight="mass", bins_type="equaln", nbins=128).filter(
+        Sphere(10.0) & FamilyFilter("dm"))(sim)
+    pos, mass = plummer(n, seed=1006)
+    mask = pr.sphere_mask(pos, 10.0)
+    mask[family_slices(n)["dm"].stop:] = False
+    ref = pr.radial_profile(pos, mass, mask, "equaln", 128)
+    sub = prof.sim
+    assert is_pending(sub, "r") and is_pending(sub, "mass")
+    np.testing.assert_allclose(np.asarray(prof["mass"]["sum"]), ref["mass_sum"], rtol=1e-12)
+    np.testing.assert_allclose(np.asarray(prof["r"]), ref["r_mean"], rtol=1e-12)
+    np.testing.assert_allclose(np.asarray(prof["density"]),
+                               ref["mass_sum"] / pr.area_spherical_shell(ref["edges"]), rtol=1e-12)
+    med = np.asarray(prof["r"]["median"])
+    assert np.isfinite(med).all()
+    assert str(prof["mass"]["sum"].units) == str(sim["mass"].units)
+    assert is_pending(sub, "r") and is_pending(sub, "mass")  # device sums fetched nothing
+    assert np.array_equal(sub.get_index_list(sim), np.nonzero(mask)[0])
+    perm, offsets = prof.bins.binind.csr
+    assert np.array_equal(perm, ref["perm"]) and np.array_equal(offsets, ref["offsets"])
+    r = np.asarray(sub["r"])
+    assert np.array_equal(r, pr.radial_r(pos)[mask])
+    assert np.array_equal(np.asarray(prof.bins.x), r)
+    assert np.array_equal(np.asarray(prof._weight), mass[mask])
+    assert np.array_equal(np.asarray(sub["mass"]), mass[mask])
+    assert not is_pending(sub, "r") and not is_pending(sub, "mass")
+
+
 @pytest.mark.parametrize("n", [8_000_000, 32_000_000])
 def test_fused_config3_large_input_path(gpu, n):
     """Config 3 on the tiled path (>= 1024 selection tiles of the dm span:
