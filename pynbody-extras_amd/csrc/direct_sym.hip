@@ -12,18 +12,18 @@
 // v_rsq_f64 itself (1/r to ~5e-8 relative, measured), 18 FP64 instructions
 // per pair, results within ~1e-7 of the reference (contract: 1e-5).
 //
-// Decomposition: particles padded to a multiple of 1024 (pads: zero mass,
-// far away, distinct).  I-block = 256 targets of one wave (4 per lane),
+// Decomposition: particles padded to a multiple of 2048 (pads: zero mass,
+// far away, distinct).  I-block = 512 targets of one wave (8 per lane),
 // J-chunk = 256 sources.  A workgroup (4 waves) owns a superblock of 4
 // consecutive I-blocks and walks a range of J-chunks; for each J-chunk a wave
-// evaluates the 256 x 256 pairs with its targets in registers while the
+// evaluates the 512 x 256 pairs with its targets in registers while the
 // chunk's sources — and their accumulators — rotate one lane per step around
 // the wave (sources and the potential / x-force partials by DPP wave_rol:1
 // on the VALU, the y / z partials by ds_bpermute on the LDS crossbar, see
 // PBX_SYM_DPP_MASK): after 64 steps every source
 // met every target, so neither side needs a cross-lane reduction.  Chunk
-// j > block b: both sides accumulate; j == b: target side only (each
-// ordered pair exactly once, self pair masked); j < b: skipped (done by the
+// j past block b: both sides accumulate; b's own two chunks: target side only (each
+// ordered pair exactly once, self pair masked); chunks before b: skipped (done by the
 // other block).  The source side of the 4 waves is summed in LDS and added
 // to a per-particle accumulator with coalesced f64 atomics; the target side
 // is added once per work unit.  Atomic bytes ~ 16 N^2 / 1024 (3 % of the
@@ -39,11 +39,13 @@ namespace sym {
 
 static constexpr double kR2Tiny = 2.2250738585072014e-308;  // direct.rs:7
 constexpr int kWaves = 4;
-constexpr int kT = 4;                  // targets per lane
+constexpr int kT = 8;                  // targets per lane
 constexpr int kS = 4;                  // source slots per lane
-constexpr int kBlk = 64 * kT;          // particles per I-block / J-chunk
+constexpr int kBlk = 64 * kT;          // targets per I-block (one wave)
+constexpr int kChunk = 64 * kS;        // sources per J-chunk
+constexpr int kJPerI = kBlk / kChunk;  // J-chunks per I-block
 constexpr int kSuper = kWaves * kBlk;  // particles per superblock (workgroup)
-static_assert(64 * kS == kBlk, "I-block and J-chunk must match for the diagonal");
+static_assert(kJPerI * kChunk == kBlk, "an I-block is a whole number of J-chunks");
 
 struct Unit {
   int32_t sb;  // superblock
@@ -85,9 +87,10 @@ __device__ __forceinline__ double rot_dpp(double v) {
 #define PBX_SYM_DPP_MASK 0x3F
 #endif
 
-// One J-chunk for one wave.  SYMM: both sides; else the diagonal chunk
-// (target side only, self pair masked at rotation 0).
-template <int WANT, bool SYMM, bool RAW>
+// One J-chunk for one wave.  SYMM: both sides; else chunk DOFF of the
+// wave's own I-block (target side only, self pair masked at rotation 0:
+// source slot ks of that chunk is target kt = DOFF * kS + ks).
+template <int WANT, bool SYMM, bool RAW, int DOFF = 0>
 __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t jbase, int lane,
                                       const double (&tx)[kT], const double (&ty)[kT],
                                       const double (&tz)[kT], const double (&tm)[kT],
@@ -112,7 +115,7 @@ __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t j
       for (int kt = 0; kt < kT; ++kt) {
         double dx = sx[ks] - tx[kt], dy = sy[ks] - ty[kt], dz = sz[ks] - tz[kt];
         double ms = sm[ks];
-        if (!SYMM && kt == ks) {
+        if (!SYMM && kt == DOFF * kS + ks) {
           const bool self = (r == 0);
           ms = self ? 0.0 : ms;
           dx = self ? 1.0 : dx;
@@ -166,7 +169,7 @@ template <int WANT, bool RAW>
 __global__ void __launch_bounds__(kWaves * 64)
     sym_kernel(const double4 *__restrict__ rec, const Unit *__restrict__ units,
                double *__restrict__ acc4) {
-  __shared__ double jl[kWaves][4][kBlk];  // source-side partials of one chunk, per wave
+  __shared__ double jl[kWaves][4][kChunk];  // source-side partials of one chunk, per wave
   const Unit u = units[blockIdx.x];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t iblk = (int64_t)u.sb * kWaves + w;
@@ -180,16 +183,21 @@ __global__ void __launch_bounds__(kWaves * 64)
     tm[k] = r.w;
     tp[k] = ta[k] = tb[k] = tc[k] = 0.0;
   }
+  const int64_t jdiag = iblk * kJPerI;  // this wave's first own chunk
   for (int32_t j = u.j0; j < u.j1; ++j) {
     double sp[kS], sa[kS], sb[kS], sc[kS];
 #pragma unroll
     for (int k = 0; k < kS; ++k) sp[k] = sa[k] = sb[k] = sc[k] = 0.0;
-    if (j > iblk)
-      chunk<WANT, true, RAW>(rec, (int64_t)j * kBlk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa, sb,
-                        sc);
-    else if (j == iblk)
-      chunk<WANT, false, RAW>(rec, (int64_t)j * kBlk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa,
-                         sb, sc);
+    static_assert(kJPerI == 2, "two diagonal chunk kinds");
+    if (j >= jdiag + kJPerI)
+      chunk<WANT, true, RAW>(rec, (int64_t)j * kChunk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa,
+                             sb, sc);
+    else if (j == jdiag)
+      chunk<WANT, false, RAW, 0>(rec, (int64_t)j * kChunk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp,
+                                 sa, sb, sc);
+    else if (j == jdiag + 1)
+      chunk<WANT, false, RAW, 1>(rec, (int64_t)j * kChunk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp,
+                                 sa, sb, sc);
 #pragma unroll
     for (int k = 0; k < kS; ++k) {
       jl[w][0][k * 64 + lane] = sp[k];
@@ -198,9 +206,10 @@ __global__ void __launch_bounds__(kWaves * 64)
       jl[w][3][k * 64 + lane] = sc[k];
     }
     __syncthreads();
-    // chunk j can only have source-side partials from blocks below it
-    if ((int64_t)j > (int64_t)u.sb * kWaves) {
-      double *dst = acc4 + (int64_t)j * kBlk * 4;
+    // chunk j has source-side partials only past the superblock's first I-block
+    if ((int64_t)j >= ((int64_t)u.sb * kWaves + 1) * kJPerI) {
+      double *dst = acc4 + (int64_t)j * kChunk * 4;
+      static_assert(kWaves * 64 * 4 == kChunk * 4, "four (source, quantity) words per thread");
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int idx = threadIdx.x + i * kWaves * 64;  // 0 .. 1023 = (source, quantity)
@@ -254,14 +263,18 @@ int64_t sym_padded(int64_t n) {
 }
 
 // Work units over the upper triangle of (superblock, J-chunk): superblock sb
-// covers chunks [4 sb, nchunks) split into pieces of at most kChunksPerUnit.
+// covers chunks [kWaves kJPerI sb, nchunks) split into pieces of at most
+// kChunksPerUnit.
+#ifndef PBX_SYM_CHUNKS_PER_UNIT
+#define PBX_SYM_CHUNKS_PER_UNIT 32
+#endif
 static std::vector<sym::Unit> sym_units(int64_t npad) {
-  constexpr int kChunksPerUnit = 32;
-  const int32_t nch = (int32_t)(npad / sym::kBlk);
+  constexpr int kChunksPerUnit = PBX_SYM_CHUNKS_PER_UNIT;
+  const int32_t nch = (int32_t)(npad / sym::kChunk);
   const int32_t nsb = (int32_t)(npad / sym::kSuper);
   std::vector<sym::Unit> u;
   for (int32_t sb = 0; sb < nsb; ++sb)
-    for (int32_t j = sb * sym::kWaves; j < nch; j += kChunksPerUnit)
+    for (int32_t j = sb * sym::kWaves * sym::kJPerI; j < nch; j += kChunksPerUnit)
       u.push_back({sb, j, std::min(nch, j + kChunksPerUnit), 0});
   return u;
 }
