@@ -51,7 +51,8 @@ def main():
 
     root = Path(__file__).resolve().parent.parent / "profiles"
     src = str((out / "pmc_summary.csv").relative_to(root.parent))
-    d = [] if only_profile else (pick("sym_kernel") or pick("direct_kernel"))  # all-particles kernel
+    # the all-particles kernel, fast mode (the timed one) first
+    d = [] if only_profile else (pick("sym_kernel<3, true>") or pick("sym_kernel") or pick("direct_kernel"))
     if d:
         r = d[0]
         (root / "pmc_direct_latest.json").write_text(json.dumps({
