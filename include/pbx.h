@@ -78,6 +78,14 @@ int pbx_memcpy_htod(void *d_dst, const void *h_src, size_t bytes);
  * library's pinned chunks (what a profile call on host arrays uses).  No
  * reference counterpart: the bench's bound for the user-facing profile. */
 int pbx_measure_h2d(int64_t bytes, double *pinned_gbs, double *staged_gbs);
+/* The current device's cache of engine buffers (profile / octree handles
+ * take freed blocks instead of hipMalloc): out[0] cached bytes, out[1]
+ * cached blocks, out[2] allocations served from the cache, out[3]
+ * allocations that called hipMalloc.  pbx_device_pool_trim frees every
+ * cached block (memory back to the device for other users).  No reference
+ * counterpart (runtime). */
+int pbx_device_pool_stats(int64_t *out);
+int pbx_device_pool_trim(void);
 int pbx_memcpy_dtoh(void *h_dst, const void *d_src, size_t bytes);
 int pbx_memcpy_dtod(void *d_dst, const void *d_src, size_t bytes);
 int pbx_memset(void *d_ptr, int value, size_t bytes);

@@ -68,6 +68,12 @@ struct DevBuf {
   ~DevBuf();
 };
 
+// Caching device allocator (runtime.hip) behind the engines' Buf: a block
+// of at least `need` bytes (*got: its size, *dev: the current device), and
+// its return to that device's cache (or hipFree when the cache is full).
+void *dev_alloc(size_t need, size_t *got, int *dev);
+void dev_release(void *p, size_t bytes, int dev);
+
 // Per-device state.  All library kernels of a device run on `stream`.
 struct Device {
   int id = -1;

@@ -473,24 +473,22 @@ __global__ void __launch_bounds__(TPB)
 }
 
 // ------------------------------------------------------------------ host
-// A grow-only device allocation owned by one engine object.
+// A grow-only device allocation owned by one engine object; its blocks come
+// from (and go back to) the device's allocation cache (dev_alloc).
 struct Buf {
   void *p = nullptr;
   size_t bytes = 0;
   uint32_t epoch = 0;  // scan workspaces: the current call's status tag
+  int dev = 0;
   void *get(size_t need) {
     if (need <= bytes) return p;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-    size_t want = need < 256 ? 256 : need;
-    PBX_HIP(hipMalloc(&p, want));
-    bytes = want;
+    release();
+    p = dev_alloc(need, &bytes, &dev);
     return p;
   }
   template <typename T> T *as() const { return (T *)p; }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) dev_release(p, bytes, dev);
     p = nullptr;
     bytes = 0;
   }

@@ -4,6 +4,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <strings.h>
 
 #include "pbx_common.h"
@@ -44,6 +45,97 @@ void *DevBuf::ensure(size_t need) {
   PBX_HIP(hipMalloc(&ptr, want));
   bytes = want;
   return ptr;
+}
+
+// ---- caching allocator for the engines' grow-only buffers (Buf) --------
+// A Buf's block goes back to a per-device cache when the buffer grows or its
+// handle is destroyed, and the next Buf of about that size takes it instead
+// of a hipMalloc (a handle per profile / BinsSet made every call allocate and
+// free its ~30 buffers: hipMalloc maps pages, hipFree synchronises the
+// device).  Every library kernel of a device runs on its one stream, so a
+// block handed to a new owner is only touched by work queued after the old
+// owner's.  Cached bytes per device are capped; a failed hipMalloc empties
+// the cache and tries again.
+namespace {
+struct DevPool {
+  std::mutex mu;
+  std::multimap<size_t, void *> free;  // cached blocks by size
+  size_t cached = 0;
+  int64_t hits = 0, misses = 0;
+};
+DevPool g_pools[64];
+constexpr size_t kPoolCap = (size_t)8 << 30;        // cached bytes per device
+constexpr size_t kPoolMaxBlock = (size_t)2 << 30;   // larger blocks are freed
+size_t pool_class(size_t need) {
+  if (need <= 256) return 256;
+  if (need <= ((size_t)1 << 20)) {
+    size_t c = 512;
+    while (c < need) c <<= 1;
+    return c;
+  }
+  const size_t g = (size_t)2 << 20;  // 2 MiB granules
+  return (need + g - 1) / g * g;
+}
+void pool_trim(DevPool &P) {
+  std::lock_guard<std::mutex> lk(P.mu);
+  for (auto &b : P.free) (void)hipFree(b.second);
+  P.free.clear();
+  P.cached = 0;
+}
+}  // namespace
+
+void *dev_alloc(size_t need, size_t *got, int *dev_out) {
+  int dev = 0;
+  PBX_HIP(hipGetDevice(&dev));
+  DevPool &P = g_pools[dev & 63];
+  const size_t want = pool_class(need);
+  *dev_out = dev;
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.free.lower_bound(want);
+    if (it != P.free.end() && it->first <= 2 * want) {  // (not a much larger block)
+      void *p = it->second;
+      *got = it->first;
+      P.cached -= it->first;
+      P.free.erase(it);
+      ++P.hits;
+#ifdef PBX_POOL_POISON  // test builds: a reused block holds garbage, not zeros
+      // (on the device's stream: after the old owner's work, before the new one's)
+      PBX_HIP(hipMemsetAsync(p, 0xA5, *got, current_device().stream));
+#endif
+      return p;
+    }
+  }
+  void *p = nullptr;
+  if (hipMalloc(&p, want) != hipSuccess) {
+    (void)hipGetLastError();
+    pool_trim(P);
+    PBX_HIP(hipMalloc(&p, want));
+  }
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    ++P.misses;
+  }
+  *got = want;
+  return p;
+}
+
+void dev_release(void *p, size_t bytes, int dev) {
+  if (!p) return;
+  DevPool &P = g_pools[dev & 63];
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (bytes <= kPoolMaxBlock && P.cached + bytes <= kPoolCap) {
+      P.free.emplace(bytes, p);
+      P.cached += bytes;
+      return;
+    }
+  }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != dev) (void)hipSetDevice(dev);
+  (void)hipFree(p);
+  if (cur != dev) (void)hipSetDevice(cur);
 }
 
 DevBuf::~DevBuf() {
@@ -364,6 +456,28 @@ int pbx_memcpy_htod(void *d_dst, const void *h_src, size_t bytes) {
     Device &d = current_device();
     PBX_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, d.stream));
     PBX_HIP(hipStreamSynchronize(d.stream));
+  });
+}
+
+int pbx_device_pool_stats(int64_t *out) {
+  return guard([&] {
+    if (!out) fail(PBX_ERR_VALUE, "null output");
+    Device &d = current_device();
+    DevPool &P = g_pools[d.id & 63];
+    std::lock_guard<std::mutex> lk(P.mu);
+    out[0] = (int64_t)P.cached;
+    out[1] = (int64_t)P.free.size();
+    out[2] = P.hits;
+    out[3] = P.misses;
+  });
+}
+
+int pbx_device_pool_trim(void) {
+  return guard([&] {
+    Device &d = current_device();
+    std::lock_guard<std::mutex> lk(d.mu);
+    PBX_HIP(hipStreamSynchronize(d.stream));
+    pool_trim(g_pools[d.id & 63]);
   });
 }
 

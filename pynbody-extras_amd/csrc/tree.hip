@@ -1958,15 +1958,14 @@ static inline unsigned nblk(int64_t n) { return (unsigned)((n + TPB - 1) / TPB);
 static void grow_keep(Buf &b, size_t esize, int64_t ncap, int64_t keep, hipStream_t st) {
   size_t need = esize * (size_t)ncap;
   if (need <= b.bytes) return;
-  void *np = nullptr;
-  PBX_HIP(hipMalloc(&np, need));
+  size_t got = 0;
+  int dev = 0;
+  void *np = dev_alloc(need, &got, &dev);
   if (keep > 0 && b.p) PBX_HIP(hipMemcpyAsync(np, b.p, esize * (size_t)keep, hipMemcpyDeviceToDevice, st));
-  if (b.p) {
-    PBX_HIP(hipStreamSynchronize(st));
-    (void)hipFree(b.p);
-  }
+  b.release();  // (the copy is queued before any later owner's work on st)
   b.p = np;
-  b.bytes = need;
+  b.bytes = got;
+  b.dev = dev;
 }
 
 static void ensure_nodes(Octree &T, int64_t need, hipStream_t st) {

@@ -73,6 +73,8 @@ _SIGNATURES: dict[str, tuple] = {
     "pbx_free": (c_int, [c_void_p]),
     "pbx_memcpy_htod": (c_int, [c_void_p, c_void_p, c_size_t]),
     "pbx_measure_h2d": (c_int, [c_int64, POINTER(c_double), POINTER(c_double)]),
+    "pbx_device_pool_stats": (c_int, [POINTER(c_int64)]),
+    "pbx_device_pool_trim": (c_int, []),
     "pbx_memcpy_dtoh": (c_int, [c_void_p, c_void_p, c_size_t]),
     "pbx_memcpy_dtod": (c_int, [c_void_p, c_void_p, c_size_t]),
     "pbx_memset": (c_int, [c_void_p, c_int, c_size_t]),

@@ -207,6 +207,43 @@ def test_staged_copies_family_span(gpu):
         d.close()
 
 
+def test_device_buffer_cache_reuse(gpu):
+    """Engine buffers come from the device's cache (dev_alloc): a second
+    builder call's new handle takes the blocks the first one's handle gave
+    back (cache hits, no new hipMalloc) and returns the same profile bit for
+    bit; pbx_device_pool_trim empties the cache."""
+    import ctypes
+
+    from pynbodyext import _native as nat
+
+    def stats():
+        out = (ctypes.c_int64 * 4)()
+        nat.call("pbx_device_pool_stats", out)
+        return list(out)
+
+    sim = plummer_snapshot(2_000_000, seed=1008)
+    builder = RadialProfileBuilder(ndim=3, weight="mass", bins_type="equaln", nbins=64).filter(
+        Sphere(10.0) & FamilyFilter("dm"))
+    outs = []
+    for k in range(3):
+        prof = builder(sim)
+        outs.append((np.asarray(prof.bin_edges).copy(), np.asarray(prof.npart_bins).copy(),
+                     np.asarray(prof["mass"]["sum"]).copy(), prof.bins.binind.csr[0].copy()))
+        if k == 0:
+            s1 = stats()
+        del prof
+        import gc
+        gc.collect()
+    s3 = stats()
+    for o in outs[1:]:
+        assert all(np.array_equal(a, b) for a, b in zip(o, outs[0]))
+    assert s3[2] > s1[2]            # later handles were served from the cache
+    assert s3[3] - s1[3] <= 2       # ... without (almost) any new hipMalloc
+    nat.call("pbx_device_pool_trim")
+    s4 = stats()
+    assert s4[0] == 0 and s4[1] == 0
+
+
 def test_fused_builder_matches_oracle_config3(gpu):
     """Config 3: 1M Plummer, Sphere(R=10) & FamilyFilter('dm'), equaln 128, weight mass."""
     n = 1_000_000
