@@ -26,6 +26,16 @@ def _i64(a: np.ndarray):
     return a.ctypes.data_as(_i64p)
 
 
+_REQ_CACHE = 8  # argument sets kept per handle (radial_equaln on device pointers)
+
+
+def _addr(p):
+    """A device pointer argument as a hashable address (None stays None)."""
+    if p is None:
+        return None
+    v = getattr(p, "value", p)  # (ctypes pointers)
+    return int(v) if v is not None else 0
+
 class DeviceBins:
     """One binned quantity on the GPU and the results derived from it."""
 
@@ -168,15 +178,18 @@ class DeviceBins:
         # returned arrays are fresh copies every call.
         key = None
         if on_device:
-            key = (d._h.value if d._h is not None else None, pos, mass,
+            key = (d._h.value if d._h is not None else None, _addr(pos), _addr(mass),
                    None if sphere is None else (tuple(sphere[0]), float(sphere[1])),
                    None if families is None else tuple(map(tuple, families)), ndim, n,
                    tuple(map(tuple, stats)), nbins, bin_min, bin_max, bool(csr),
                    None if comm is None else comm.handle.value)
-        cached = getattr(d, "_req", None)
+        # (a few argument sets per handle: a handle cycling through several
+        # snapshots' device arrays keeps each one's)
+        reqs = d.__dict__.setdefault("_reqs", {})
+        cached = reqs.get(key) if key is not None else None
         prep = None
-        if key is not None and cached is not None and cached[0] == key:
-            args, keep, fs, ws, cs, head, refs, outs, prep = cached[1]
+        if cached is not None:
+            args, keep, fs, ws, cs, head, refs, outs, prep = cached
         else:
             args, keep = cls._select_args(pos, mass, sphere, families, ndim, on_device, n)
             fs = (c_int * max(k, 1))(*[int(s[0]) for s in stats])
@@ -202,7 +215,9 @@ class DeviceBins:
                     if comm is None else \
                     nat.Prepared("pbx_profile_radial_equaln_comm", comm.handle, d._h, *args, *head,
                                  *optrs_)
-                d._req = (key, (args, keep, fs, ws, cs, head, refs, outs, prep))
+                if len(reqs) >= _REQ_CACHE:
+                    reqs.pop(next(iter(reqs)))  # (the oldest)
+                reqs[key] = (args, keep, fs, ws, cs, head, refs, outs, prep)
         kept, ne, nv = refs
         edges, counts, mom, optrs, local = outs
         try:
