@@ -61,7 +61,8 @@ def main():
             "note": "2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction); memory-side requests "
                     "incl. Infinity-Cache hits and the f64 accumulator atomics", "source": src},
             indent=1))
-    t = [] if only_profile else pick("walk_kernel<3, 3")
+    # the timed walk (fast mode) first
+    t = [] if only_profile else (pick("walk_kernel<3, 3, false, true") or pick("walk_kernel<3, 3"))
     if t:
         r = t[0]
         (root / "pmc_tree_latest.json").write_text(json.dumps({
