@@ -328,6 +328,47 @@ def test_fused_config3_large_input_path(gpu, n):
     np.testing.assert_allclose(np.asarray(prof["r"]), ref["r_mean"], rtol=1e-12)
 
 
+@pytest.mark.parametrize("n", [1_000_000, 8_000_000])
+def test_radial_equaln_changing_snapshots(gpu, n):
+    """The bench's changing-input mode (bench.changing_snapshots): one handle
+    on device arrays cycling through three different Plummer snapshots, two
+    rounds, every call bit-exact against the oracle on its own snapshot —
+    edges, counts and CSR; sums to 1e-12 (1M: the one-launch path, whose
+    level-0 hint comes from the previous snapshot; 8M: the tiled path, the
+    hint held or escaped, no speculation: the positions are not declared
+    stable)."""
+    from pynbodyext import _native as nat
+    from pynbodyext.profiles._device import SRC_NONE, SRC_W, SRC_X
+
+    dm = family_slices(n)["dm"]
+    snaps, refs = [], []
+    for k in range(3):
+        pos, mass = plummer(n, seed=2000 + 7 * k)
+        mask = pr.sphere_mask(pos, 10.0)
+        mask[dm.stop:] = False
+        refs.append(pr.radial_profile(pos, mass, mask, "equaln", 128))
+        snaps.append((nat.DeviceArray.from_host(pos), nat.DeviceArray.from_host(mass)))
+    stats = ((SRC_W, SRC_NONE, 1 << 3), (SRC_X, SRC_W, 0b11))
+    h = DeviceBins()
+    try:
+        for i in range(6):
+            p, m = snaps[i % 3]
+            ref = refs[i % 3]
+            _, edges, counts, (msum, rmean) = DeviceBins.radial_equaln(
+                p.ptr, m.ptr, nbins=128, sphere=((0.0, 0.0, 0.0), 10.0),
+                families=[(dm.start, dm.stop)], ndim=3, stats=stats, csr=True,
+                on_device=True, n=n, into=h)
+            assert np.array_equal(edges, ref["edges"]), i
+            assert np.array_equal(counts, ref["counts"]), i
+            perm, offs = h.csr()
+            assert np.array_equal(offs, ref["offsets"]) and np.array_equal(perm, ref["perm"]), i
+            np.testing.assert_allclose(msum[:, 3], ref["mass_sum"], rtol=1e-12)
+            np.testing.assert_allclose(rmean[:, 1] / rmean[:, 0], ref["r_mean"], rtol=1e-12)
+        assert h.spec_stats()["speculated"] == 0
+    finally:
+        h.close()
+
+
 def test_fused_equals_unfused(gpu):
     sim = plummer_snapshot(50_000, seed=9)
     filt = Sphere(5.0, cen=(0.1, 0.0, -0.2)) & FamilyFilter("gas")
