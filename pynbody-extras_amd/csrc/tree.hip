@@ -1270,7 +1270,7 @@ __global__ void __launch_bounds__(WALK_TPB)
       if (LCOST) cost += accept ? 1 : 0;
       if (accept) {
         if constexpr (P == 0) {  // monopole without multipoles (tree.rs:1126-1129, 1284-1291)
-          const double y = rsq_walk<RAW>(dist2 + kR2Tiny);
+          const double y = rsq_walk<RAW>(RAW ? dist2 : dist2 + kR2Tiny);  // (see inv_r)
           if (WANT & PBX_WANT_POT) ph = __builtin_fma(-mass, y, ph);
           if (WANT & PBX_WANT_ACC) {
             const double g = mass * (y * y * y);
@@ -1280,8 +1280,10 @@ __global__ void __launch_bounds__(WALK_TPB)
           }
         } else {
           // derivative builders add eps2 = R2_TINY and R2_TINY again
-          // (multipole.rs:594, tree.rs:1429)
-          const double inv_r = rsq_walk<RAW>(dist2 + kR2Tiny);
+          // (multipole.rs:594, tree.rs:1429); the fast walk's second add is
+          // dropped: dist2 (>= R2_TINY) + R2_TINY is dist2 itself unless the
+          // node lies within ~1e-146 of the target
+          const double inv_r = rsq_walk<RAW>(RAW ? dist2 : dist2 + kR2Tiny);
           if constexpr (P == 1) {  // stored as O0: monopole with the D1 tensor (multipole.rs:272)
             double D[4];
             derivs<1>(dx, dy, dz, inv_r, D);
