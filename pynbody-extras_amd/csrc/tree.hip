@@ -1304,7 +1304,11 @@ __global__ void __launch_bounds__(WALK_TPB)
             const double qz = __builtin_fma(C(4), dx, __builtin_fma(C(5), dy, C(2) * dz));
             const double q2 = __builtin_fma(dx, qx, __builtin_fma(dy, qy, dz * qz));
             if (WANT & PBX_WANT_POT) {
-              double tp = __builtin_fma(-u5, q2, -mass * u);
+              // (the fast walk accumulates the terms into ph one by one: one
+              // add less; the precise walk sums the node's terms first, as
+              // the reference does)
+              double tp = RAW ? __builtin_fma(-u5, q2, __builtin_fma(-mass, u, ph))
+                              : __builtin_fma(-u5, q2, -mass * u);
               if constexpr (P == 3) {
                 const double zz = dz * dz;
                 const double A = __builtin_fma(C(6), dx, __builtin_fma(C(7), dy, C(8) * dz));
@@ -1315,7 +1319,7 @@ __global__ void __launch_bounds__(WALK_TPB)
                 const double q3 = __builtin_fma(dx, X, __builtin_fma(dy, Y, (C(15) * dz) * zz));
                 tp = __builtin_fma(u5 * u2, q3, tp);
               }
-              ph += tp;
+              ph = RAW ? tp : ph + tp;
             }
             if (WANT & PBX_WANT_ACC) {
               // the order-P force uses moments up to P-1 (multipole.rs:1408-1528):
