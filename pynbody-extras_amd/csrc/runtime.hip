@@ -432,7 +432,8 @@ int pbx_device_name(char *buf, int buflen) {
     Device &d = current_device();
     hipDeviceProp_t prop;
     PBX_HIP(hipGetDeviceProperties(&prop, d.id));
-    std::snprintf(buf, (size_t)buflen, "%s (%s, %d CUs)", prop.name,
+    // (the marketing name can be empty on some driver stacks)
+    std::snprintf(buf, (size_t)buflen, "%s (%s, %d CUs)", prop.name[0] ? prop.name : "gfx950 device",
                   prop.gcnArchName, prop.multiProcessorCount);
   });
 }
