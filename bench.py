@@ -267,6 +267,10 @@ def changing_snapshots(n: int, steps: int, single, dev, d_pos, d_mass, e0, e1, c
         single(snaps[k][0].ptr, snaps[k][1].ptr, dev)
     nat.synchronize()
     s1 = (dev.spec_stats(), dev.level0_stats(), dev.mono_stats(), dev.path_stats())
+    # per call (an event pair and a sync around each: the distribution), then
+    # the same calls back to back between one event pair and one sync — the
+    # bench's step bracket; the per-call events and sync add ~15 us of
+    # measurement to every call, which the credited (batch) figure leaves out
     ct, cd = [], []
     res = None
     for i in range(calls):
@@ -278,6 +282,16 @@ def changing_snapshots(n: int, steps: int, single, dev, d_pos, d_mass, e0, e1, c
         nat.synchronize()
         ct.append(time.perf_counter() - t0)
         cd.append(e0.elapsed_ms(e1))
+    nat.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for i in range(calls):
+        pp, mp, _ = snaps[i % N_CHANGING]
+        res = single(pp.ptr, mp.ptr, dev)
+    e1.record()
+    nat.synchronize()
+    bt = (time.perf_counter() - t0) / calls
+    bd = e0.elapsed_ms(e1) / calls
     s2 = (dev.spec_stats(), dev.level0_stats(), dev.mono_stats(), dev.path_stats())
     last = snaps[(calls - 1) % N_CHANGING]
     fresh = DeviceBins()
@@ -303,14 +317,19 @@ def changing_snapshots(n: int, steps: int, single, dev, d_pos, d_mass, e0, e1, c
     for pp, mp, _ in snaps[1:]:
         pp.free()
         mp.free()
-    td = float(np.median(cd))
+    td = bd
     delta = [dict(zip(("speculation", "level0", "one_launch", "path"),
                       [_stats_delta(a, b) for a, b in zip(x, y)])) for x, y in ((s0, s1), (s1, s2))]
     return {"snapshots": N_CHANGING, "calls": calls, "stream_ms": td,
-            "stream_ms_p90": float(np.percentile(cd, 90)),
-            "ms": float(np.median(ct)) * 1e3,
+            "ms": bt * 1e3,
+            "timing": "stream_ms / ms: `calls` back-to-back calls between one event pair and one "
+                      "sync, per call; per_call: an event pair and a sync around every call "
+                      "(median, p90)",
+            "per_call": {"stream_ms": float(np.median(cd)),
+                         "stream_ms_p90": float(np.percentile(cd, 90)),
+                         "ms": float(np.median(ct)) * 1e3},
             "particles_per_s_stream": n / (td * 1e-3),
-            "particles_per_s_wall": n / (float(np.median(ct))),
+            "particles_per_s_wall": n / bt,
             "hbm_gbs_algorithmic": n * PROFILE_BYTES_PER_PARTICLE / (td * 1e-3) / 1e9,
             "frac": n * PROFILE_BYTES_PER_PARTICLE / (td * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "handle_stats_timed_calls": delta[1], "handle_stats_first_pass": delta[0],
@@ -404,8 +423,19 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
             dev_ms.append(e0.elapsed_ms(e1))
         t = float(np.median(times))
         td = float(np.median(dev_ms)) * 1e-3
+        per_call = {"stream_ms": td * 1e3, "ms": t * 1e3}
         if dist is not None:
             td = dist.max(td)
+        else:  # the same steps back to back in one bracket (see changing_snapshots)
+            nat.synchronize()
+            t0 = time.perf_counter()
+            e0.record()
+            for _ in range(steps):
+                res = step()
+            e1.record()
+            nat.synchronize()
+            t = (time.perf_counter() - t0) / steps
+            td = e0.elapsed_ms(e1) * 1e-3 / steps
         n_all = n * world
         row = {"n": n_all, "n_per_gpu": n, "n_kept_rank0": dev.n, "ms": t * 1e3,
                "particles_per_s": n_all / t,
@@ -417,12 +447,14 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
             # per statistic): the handle reuses the previous call's level-0
             # geometry and speculates on its bin table and edges
             row["identical_snapshot"] = {"stream_ms": row["stream_ms"], "ms": row["ms"],
+                                         "per_call": per_call,
                                          "path": dev.path_stats(), "mono": dev.mono_stats(),
                                          "level0_hinted_calls": dev.level0_stats(),
                                          "speculated_calls": dev.spec_stats()}
             # a first call on every step: no earlier geometry or speculation state
             ct, cd = [], []
-            for _ in range(max(20, steps // 10)):
+            nc = max(20, steps // 10)
+            for _ in range(nc):
                 dev.forget_history()  # the next call runs as the handle's first
                 t0 = time.perf_counter()
                 e0.record()
@@ -431,8 +463,18 @@ def bench_profile(sizes, steps: int, warmup: int, cpu: bool, dist=None):
                 nat.synchronize()
                 ct.append(time.perf_counter() - t0)
                 cd.append(e0.elapsed_ms(e1))
-            row["cold_ms"] = float(np.median(ct)) * 1e3
-            row["cold_stream_ms"] = float(np.median(cd))
+            nat.synchronize()
+            t0 = time.perf_counter()
+            e0.record()
+            for _ in range(nc):
+                dev.forget_history()
+                step()
+            e1.record()
+            nat.synchronize()
+            row["cold_ms"] = (time.perf_counter() - t0) / nc * 1e3
+            row["cold_stream_ms"] = e0.elapsed_ms(e1) / nc
+            row["cold_per_call"] = {"stream_ms": float(np.median(cd)),
+                                    "ms": float(np.median(ct)) * 1e3}
             row["cold_note"] = ("every call a handle's first (forget_history: no earlier "
                                 "geometry or speculation state)")
             row["changing"] = changing_snapshots(n, steps, single, dev, d_pos, d_mass, e0, e1,
