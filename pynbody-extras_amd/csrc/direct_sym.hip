@@ -12,17 +12,18 @@
 // v_rsq_f64 itself (1/r to ~5e-8 relative, measured), 18 FP64 instructions
 // per pair, results within ~1e-7 of the reference (contract: 1e-5).
 //
-// Decomposition: particles padded to a multiple of 2048 (pads: zero mass,
-// far away, distinct).  I-block = 512 targets of one wave (8 per lane),
-// J-chunk = 256 sources.  A workgroup (4 waves) owns a superblock of 4
-// consecutive I-blocks and walks a range of J-chunks; for each J-chunk a wave
-// evaluates the 512 x 256 pairs with its targets in registers while the
+// Decomposition: particles padded to a multiple of 4 x 64 kT (pads: zero
+// mass, far away, distinct).  I-block = 64 kT targets of one wave (kT per
+// lane), J-chunk = 64 kS sources.  A workgroup (4 waves) owns a superblock
+// of 4 consecutive I-blocks and walks a range of J-chunks; for each J-chunk a
+// wave evaluates the I-block x J-chunk pairs with its targets in registers
+// while the
 // chunk's sources — and their accumulators — rotate one lane per step around
 // the wave (sources and the potential / x-force partials by DPP wave_rol:1
 // on the VALU, the y / z partials by ds_bpermute on the LDS crossbar, see
 // PBX_SYM_DPP_MASK): after 64 steps every source
 // met every target, so neither side needs a cross-lane reduction.  Chunk
-// j past block b: both sides accumulate; b's own two chunks: target side only (each
+// j past block b: both sides accumulate; b's own chunks: target side only (each
 // ordered pair exactly once, self pair masked); chunks before b: skipped (done by the
 // other block).  The source side of the 4 waves is summed in LDS and added
 // to a per-particle accumulator with coalesced f64 atomics; the target side
@@ -39,8 +40,18 @@ namespace sym {
 
 static constexpr double kR2Tiny = 2.2250738585072014e-308;  // direct.rs:7
 constexpr int kWaves = 4;
-constexpr int kT = 8;                  // targets per lane
-constexpr int kS = 4;                  // source slots per lane
+// 12 targets x 2 source slots per lane (254 VGPRs, no scratch: 2 waves per
+// SIMD): a slot's rotation serves 12 pairs — 20.0 VALU issues per unordered
+// pair; 8 x 4 took 20.5, 10 x 2 20.2, 6 x 2 (158 VGPRs, 3 waves) 21.0 —
+// same box 337.4 / 332.0 / 338.5 against 331.1 ms (profiles/r6/r6y/)
+#ifndef PBX_SYM_KT
+#define PBX_SYM_KT 12
+#endif
+#ifndef PBX_SYM_KS
+#define PBX_SYM_KS 2
+#endif
+constexpr int kT = PBX_SYM_KT;         // targets per lane
+constexpr int kS = PBX_SYM_KS;         // source slots per lane
 constexpr int kBlk = 64 * kT;          // targets per I-block (one wave)
 constexpr int kChunk = 64 * kS;        // sources per J-chunk
 constexpr int kJPerI = kBlk / kChunk;  // J-chunks per I-block
@@ -165,6 +176,20 @@ __device__ __forceinline__ void chunk(const double4 *__restrict__ rec, int64_t j
   }
 }
 
+// chunk d of the wave's own I-block (d < kJPerI, a compile-time DOFF each)
+template <int WANT, bool RAW, int D>
+__device__ __forceinline__ void own_chunk(int d, const double4 *__restrict__ rec, int64_t jbase,
+                                          int lane, const double (&tx)[kT], const double (&ty)[kT],
+                                          const double (&tz)[kT], const double (&tm)[kT],
+                                          double (&tp)[kT], double (&ta)[kT], double (&tb)[kT],
+                                          double (&tc)[kT], double (&sp)[kS], double (&sa)[kS],
+                                          double (&sb)[kS], double (&sc)[kS]) {
+  if (d == D)
+    chunk<WANT, false, RAW, D>(rec, jbase, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa, sb, sc);
+  else if constexpr (D + 1 < kJPerI)
+    own_chunk<WANT, RAW, D + 1>(d, rec, jbase, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa, sb, sc);
+}
+
 template <int WANT, bool RAW>
 __global__ void __launch_bounds__(kWaves * 64)
     sym_kernel(const double4 *__restrict__ rec, const Unit *__restrict__ units,
@@ -188,16 +213,12 @@ __global__ void __launch_bounds__(kWaves * 64)
     double sp[kS], sa[kS], sb[kS], sc[kS];
 #pragma unroll
     for (int k = 0; k < kS; ++k) sp[k] = sa[k] = sb[k] = sc[k] = 0.0;
-    static_assert(kJPerI == 2, "two diagonal chunk kinds");
     if (j >= jdiag + kJPerI)
       chunk<WANT, true, RAW>(rec, (int64_t)j * kChunk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp, sa,
                              sb, sc);
-    else if (j == jdiag)
-      chunk<WANT, false, RAW, 0>(rec, (int64_t)j * kChunk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp,
-                                 sa, sb, sc);
-    else if (j == jdiag + 1)
-      chunk<WANT, false, RAW, 1>(rec, (int64_t)j * kChunk, lane, tx, ty, tz, tm, tp, ta, tb, tc, sp,
-                                 sa, sb, sc);
+    else if (j >= jdiag)  // one of the wave's own chunks (target side, self pair masked)
+      own_chunk<WANT, RAW, 0>((int)(j - jdiag), rec, (int64_t)j * kChunk, lane, tx, ty, tz, tm, tp,
+                              ta, tb, tc, sp, sa, sb, sc);
 #pragma unroll
     for (int k = 0; k < kS; ++k) {
       jl[w][0][k * 64 + lane] = sp[k];
@@ -209,9 +230,9 @@ __global__ void __launch_bounds__(kWaves * 64)
     // chunk j has source-side partials only past the superblock's first I-block
     if ((int64_t)j >= ((int64_t)u.sb * kWaves + 1) * kJPerI) {
       double *dst = acc4 + (int64_t)j * kChunk * 4;
-      static_assert(kWaves * 64 * 4 == kChunk * 4, "four (source, quantity) words per thread");
+      static_assert(kWaves * 64 * kS == kChunk * 4, "kS (source, quantity) words per thread");
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < kS; ++i) {
         const int idx = threadIdx.x + i * kWaves * 64;  // 0 .. 1023 = (source, quantity)
         const int s = idx >> 2, q = idx & 3;
         const double v = jl[0][q][s] + jl[1][q][s] + jl[2][q][s] + jl[3][q][s];

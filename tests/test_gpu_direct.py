@@ -172,7 +172,7 @@ def test_kernelkind_override(gpu):
 @pytest.mark.parametrize("n", [8192, 9000, 20_000])
 def test_symmetric_path(gpu, n, precise):
     """N >= 8192 all-particles Newtonian solves evaluate each unordered pair
-    once (csrc/direct_sym.hip, padded to 2048, f64 atomics), in both the fast
+    once (csrc/direct_sym.hip, padded to 4 x 64 kT, f64 atomics), in both the fast
     (raw v_rsq_f64) and the precise (Newton-refined) mode."""
     pos, mass = plummer(n, seed=300 + n)
     with nat.precise_mode(precise):
