@@ -19,9 +19,8 @@
 // wave evaluates the I-block x J-chunk pairs with its targets in registers
 // while the
 // chunk's sources — and their accumulators — rotate one lane per step around
-// the wave (sources and the potential / x-force partials by DPP wave_rol:1
-// on the VALU, the y / z partials by ds_bpermute on the LDS crossbar, see
-// PBX_SYM_DPP_MASK): after 64 steps every source
+// the wave (by DPP wave_rol:1 on the VALU; the LDS crossbar, ds_bpermute,
+// is the alternative PBX_SYM_DPP_MASK selects): after 64 steps every source
 // met every target, so neither side needs a cross-lane reduction.  Chunk
 // j past block b: both sides accumulate; b's own chunks: target side only (each
 // ordered pair exactly once, self pair masked); chunks before b: skipped (done by the
@@ -93,9 +92,11 @@ __device__ __forceinline__ double rot_dpp(double v) {
 // 376-377 ms; with the DPP result written in place (old = source) sx, sy
 // 348, the four source values 339, those and sp, sa 333-343 (the best on
 // two boxes), everything 334; before in-place DPP every rotated word cost
-// a v_mov of 0 and a copy back (sx, sy: 358 ms).
+// a v_mov of 0 and a copy back (sx, sy: 358 ms).  Round 6, 12 pairs per
+// slot rotation (profiles/r6/r6z/): everything on DPP 328.8-329.0 ms,
+// 0x3F 331.0-331.7, 0x0F 333.6-334.5, all on the crossbar 340.0-340.6.
 #ifndef PBX_SYM_DPP_MASK
-#define PBX_SYM_DPP_MASK 0x3F
+#define PBX_SYM_DPP_MASK 0xFF
 #endif
 
 // One J-chunk for one wave.  SYMM: both sides; else chunk DOFF of the
