@@ -237,7 +237,7 @@ def test_device_buffer_cache_reuse(gpu):
     s3 = stats()
     for o in outs[1:]:
         assert all(np.array_equal(a, b) for a, b in zip(o, outs[0]))
-    assert s3[2] - s1[2] >= 20      # later handles were served from the cache (~30 buffers each)
+    assert s3[2] - s1[2] >= 20      # later handles were served from the cache (25 buffers each, measured)
     assert s3[3] - s1[3] <= 8       # ... with hardly any new hipMalloc (uncached: ~60)
     nat.call("pbx_device_pool_trim")
     s4 = stats()
