@@ -1260,7 +1260,12 @@ __global__ void __launch_bounds__(WALK_TPB)
           soft_ok = dist2 > ch * ch;
         }
       }
-      const bool accept = act && soft_ok && chunk_d(c[0], 4) < theta2 * dist2;
+      // (the fast unsoftened walk: size2 / theta^2 pre-divided into the
+      // record's h_max slot per theta — open_scale — one multiply less per
+      // step; it can differ from size2 < theta^2 dist2 only within an ulp)
+      const bool accept = act && soft_ok &&
+                          ((RAW && !SOFT) ? chunk_d(c[0], 5) < dist2
+                                          : chunk_d(c[0], 4) < theta2 * dist2);
       // this lane's next node, and the lanes that open w as the ballot of ONE
       // compare (pn == first holds exactly for the lanes that opened w: a lane
       // not at w cannot have its next node inside w's subtree) — a ballot of
@@ -1951,6 +1956,9 @@ struct Octree {
   bool soft_set = false;
   bool has_bh = false;
   bool has_hmax = false;
+  // theta^2 the walk records' h_max slot holds size2 / theta^2 for (the
+  // fast unsoftened walks' opening test; -1: not scaled since the payload)
+  double open_theta2 = -1.0;
   int nwords = 1;
   double root[4] = {0, 0, 0, 0};
   int64_t nn = 0, cap = 0;
@@ -2456,6 +2464,14 @@ static void build_payload(Octree &T, hipStream_t st) {
   }
   PBX_HIP(hipGetLastError());
   T.has_bh = true;
+  T.open_theta2 = -1.0;
+}
+
+// the fast unsoftened walk's opening sizes: size2 / theta^2 into the h_max
+// slot (field 5, unused without softening) of every walk record
+__global__ void open_scale(double *__restrict__ walk, int64_t nn, int rs, double theta2) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nn) walk[k * rs + 5] = walk[k * rs + 4] / theta2;
 }
 
 // Walk grids: one wave (64 targets) per block, blocks handed out to the XCDs
@@ -2563,6 +2579,14 @@ static void walk(Octree &T, double theta, int want, const double *d_tgt, int64_t
   // softened leaves need softenings; the guard needs h_max; at query points
   // there is no target softening (tree.rs:1516,1547)
   const bool soft = T.has_hmax || T.soft_set;
+  if (!soft && !precise_mode() && T.nn > 0 && T.open_theta2 != wp.theta2) {
+    const int rs = T.moment_order() <= 1 ? rec_stride<0>() : T.moment_order() == 2 ? rec_stride<2>()
+                   : T.moment_order() == 3 ? rec_stride<3>() : T.moment_order() == 4 ? rec_stride<4>()
+                                                             : rec_stride<5>();
+    hipLaunchKernelGGL(open_scale, dim3((unsigned)((T.nn + 255) / 256)), dim3(256), 0, st,
+                       T.walk.as<double>(), (int64_t)T.nn, rs, wp.theta2);
+    T.open_theta2 = wp.theta2;
+  }
   if (T.n == 0) {
     if (d_pot) PBX_HIP(hipMemsetAsync(d_pot, 0, 8 * (size_t)m, st));
     if (d_acc) PBX_HIP(hipMemsetAsync(d_acc, 0, 24 * (size_t)m, st));
