@@ -1239,7 +1239,9 @@ __global__ void __launch_bounds__(WALK_TPB)
     const unsigned na = CNT ? (unsigned)__popcll(__ballot(act)) : 0u;
     if (CNT) n_active += na;  // SIMD efficiency counter
     uint64_t bo = 0ull;  // the lanes that open this node
-    int32_t pn = act ? next : p;  // this lane's next node (a leaf: next)
+    // this lane's next node (a leaf: next) — act ? next : p as an unsigned
+    // max (see the opening test below: p >= next(w) unless p = w)
+    int32_t pn = (int32_t)__builtin_elementwise_max((uint32_t)p, (uint32_t)next);
     int32_t nw = next;
     // tree.rs:1087-1090: empty nodes are skipped — their records say "leaf
     // of no records" (walk_record), so the sign of `first` alone decides.
@@ -1270,7 +1272,12 @@ __global__ void __launch_bounds__(WALK_TPB)
       // compare (pn == first holds exactly for the lanes that opened w: a lane
       // not at w cannot have its next node inside w's subtree) — a ballot of
       // the bool `open` is rebuilt from a VGPR copy (v_cndmask + v_cmp)
-      pn = act ? (accept ? next : first) : p;
+      // (act ? ... : p as an unsigned max: a lane not at w has its next node
+      // past w's subtree, p >= next(w) > first = w + 1, or -1 / -2 (done /
+      // no target) — the largest unsigned values; a lane at w has p = w <
+      // first.  One v_max with `first` as a scalar operand instead of a
+      // select whose two scalar operands both had to be copied to VGPRs)
+      pn = accept ? next : (int32_t)__builtin_elementwise_max((uint32_t)p, (uint32_t)first);
       bo = __ballot(pn == first);
       if (LCOST) cost += accept ? 1 : 0;
       if (accept) {
