@@ -536,3 +536,42 @@ def test_walk_counters_off(gpu):
         assert i2["node_interactions"] == i0["node_interactions"]
     d_pot.free()
     d_acc.free()
+
+
+@pytest.mark.fast
+def test_fast_mode_theta_changes(gpu):
+    """The fast unsoftened walk's opening sizes are size2 / theta^2 written
+    into the walk records once per theta (open_scale): a handle walked at
+    alternating thetas, and again after a rebuild on other particles, gives
+    the decisions of the oracle at each theta and values bit-identical to a
+    fresh handle's."""
+    from pynbodyext import _native as nat
+
+    pos, mass = plummer(12_000, seed=613)
+    pos2, mass2 = plummer(9_000, seed=614)
+    dev = _engine.Octree(pos, mass, 8, 3)
+    ref = ot.RefOctree(pos, mass, 8, 3)
+    firsts = {}
+    for theta in (0.5, 0.7, 0.5, 0.35, 0.7):
+        pot = dev.compute_potentials(theta)
+        cnt = dev.info()
+        if theta not in firsts:
+            _, _, nn_r, np_r = ref.compute_subset(np.arange(len(pos)), theta)
+            assert cnt["node_interactions"] == int(nn_r.sum()), theta
+            assert cnt["leaf_pairs"] == int(np_r.sum()), theta
+            fresh = _engine.Octree(pos, mass, 8, 3).compute_potentials(theta)
+            assert np.array_equal(pot, fresh), theta
+            firsts[theta] = pot
+        else:
+            assert np.array_equal(pot, firsts[theta]), theta
+    # a rebuild writes new records: their opening sizes are scaled again
+    d_pos, d_m = nat.DeviceArray.from_host(pos2), nat.DeviceArray.from_host(mass2)
+    dev._rebuild_device(d_pos.ptr, len(pos2), d_m.ptr)
+    pot = dev.compute_potentials(0.7)
+    assert np.array_equal(pot, _engine.Octree(pos2, mass2, 8, 3).compute_potentials(0.7))
+    ref2 = ot.RefOctree(pos2, mass2, 8, 3)
+    pot_r, _, nn_r, _ = ref2.compute_subset(np.arange(len(pos2)), 0.7)
+    assert dev.info()["node_interactions"] == int(nn_r.sum())
+    assert rel_pot(pot, pot_r) < FAST
+    d_pos.free()
+    d_m.free()
