@@ -19,7 +19,10 @@ nat.set_device(0)
 if leg == "profile":
     out = bench.bench_profile(sizes, steps=steps, warmup=2, cpu=False)
     for r in out:
-        print(json.dumps({k: r[k] for k in ("n", "ms", "stream_ms", "hbm_gbs_algorithmic")}))
+        d = {k: r[k] for k in ("n", "ms", "stream_ms", "hbm_gbs_algorithmic")}
+        d["changing_stream_ms"] = (r.get("changing") or {}).get("stream_ms")
+        d["cold_stream_ms"] = r.get("cold_stream_ms")
+        print(json.dumps(d))
 elif leg == "tree":
     d = bench.Dist()
     out = bench.bench_tree(d, sizes[0], steps=steps, warmup=1, cpu=False, cpu_seconds=0)
