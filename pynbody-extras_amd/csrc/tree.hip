@@ -2486,8 +2486,14 @@ __global__ void open_scale(double *__restrict__ walk, int64_t nn, int rs, double
 // waves of neighbouring targets, which walk much the same nodes, share an
 // XCD's L2).  Chunks of 16 / 32 / 64 / 128 / 256 blocks: 34.14 / 34.06 /
 // 33.95 / 33.67 / 33.76 ms at 4M (profiles/r3/walk_xcd_sweep/), 64 and 256
-// re-measured slower again at 8 waves per SIMD (round 5).
-constexpr unsigned WALK_XCD_CHUNK = 128;
+// re-measured slower again at 8 waves per SIMD (round 5).  Round 6, the
+// 4M walk at HEAD (profiles/r6/r7o/, r7p/, three runs each): 128 / 256 /
+// 512 28.86 / 28.83 / 28.82 ms (within the noise), 384 / 768 / 1024
+// 29.45 / 30.31 / 29.98 ms.
+#ifndef PBX_WALK_XCD_CHUNK
+#define PBX_WALK_XCD_CHUNK 128
+#endif
+constexpr unsigned WALK_XCD_CHUNK = PBX_WALK_XCD_CHUNK;
 constexpr unsigned WALK_BT = 64;
 
 template <int P, int WANT>
